@@ -1,0 +1,166 @@
+// dart_mpc_abi.hip -- the C ABI of include/dart_mpc.h (host side).
+//
+// Owns the device workspace for the host-pointer entry point and the
+// per-handle stream; validates arguments the way PMPC.__init__/solve would
+// fail (mpc_3d.py:12-138), then launches the batched kernel.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "dart_mpc.h"
+#include "pmpc_ipm.h"
+
+struct dart_mpc_handle {
+    dart_mpc_config cfg;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    double* dbuf = nullptr;        // staged inputs/outputs for the host entry
+    int32_t* ibuf = nullptr;
+    size_t nd = 0, ni = 0;
+    std::string err;
+};
+
+namespace {
+
+int fail(dart_mpc_handle* h, int code, const char* what, hipError_t e = hipSuccess) {
+    if (h) {
+        char buf[256];
+        if (e != hipSuccess) std::snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+        else std::snprintf(buf, sizeof buf, "%s", what);
+        h->err = buf;
+    }
+    return code;
+}
+
+#define HIPCHK(h, call, what)                                          \
+    do {                                                               \
+        hipError_t e_ = (call);                                        \
+        if (e_ != hipSuccess) return fail((h), DART_MPC_EHIP, (what), e_); \
+    } while (0)
+
+int check_cfg(const dart_mpc_config* c) {
+    if (!c) return 0;
+    if (c->variant != DART_MPC_PMPC) return 0;
+    if (c->N < 1 || c->N > 63) return 0;
+    if (!(c->Ts > 0.0) || !(c->tol > 0.0) || !(c->gravity == c->gravity) || c->max_iter < 1 || c->B_max < 1) return 0;
+    return 1;
+}
+
+int launch(dart_mpc_handle* h, int B, const double* x0, const double* ref, const double* prm, const double* w_warm,
+           double* u0, double* f, double* w_out, int32_t* status, int32_t* iters, hipStream_t s) {
+    dartmpc::PmpcArgs a;
+    a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter; a.g = h->cfg.gravity;
+    a.x0 = x0; a.ref = ref; a.prm = prm; a.w_warm = w_warm;
+    a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
+    HIPCHK(h, dartmpc_launch_pmpc(&a, s), "kernel launch");
+    return DART_MPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void dart_mpc_config_default(dart_mpc_config* c) {
+    if (!c) return;
+    c->variant = DART_MPC_PMPC;
+    c->N = 20;
+    c->Ts = 0.002;
+    c->tol = 1e-8;
+    c->max_iter = 3000;
+    c->B_max = 1024;
+    c->gravity = -9.81;
+}
+
+int dart_mpc_nw(int N) { return 6 * (N + 1) + 2 * N; }
+
+int dart_mpc_abi_version(void) { return DART_MPC_ABI_VERSION; }
+
+int dart_mpc_create(const dart_mpc_config* cfg, int device, dart_mpc_handle** out) {
+    if (!out || !check_cfg(cfg)) return DART_MPC_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) return DART_MPC_ENODEV;
+    dart_mpc_handle* h = new dart_mpc_handle();
+    h->cfg = *cfg;
+    h->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    const size_t B = (size_t)cfg->B_max, nw = (size_t)dart_mpc_nw(cfg->N);
+    h->nd = B * (6 + 6 + 6 + nw + 2 + 1 + nw);
+    h->ni = B * 2;
+    if (e == hipSuccess) e = hipMalloc(&h->dbuf, h->nd * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&h->ibuf, h->ni * sizeof(int32_t));
+    if (e != hipSuccess) {
+        dart_mpc_destroy(h);
+        return DART_MPC_EHIP;
+    }
+    *out = h;
+    return DART_MPC_OK;
+}
+
+int dart_mpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* x0, const double* ref, const double* prm,
+                             const double* w_warm, double* u0, double* f, double* w_out, int32_t* status,
+                             int32_t* iters, void* stream) {
+    if (!h) return DART_MPC_EINVAL;
+    if (B < 0 || (B > 0 && (!x0 || !ref || !prm || !u0 || !f || !status || !iters)))
+        return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
+    if (B == 0) return DART_MPC_OK;
+    HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    return launch(h, B, x0, ref, prm, w_warm, u0, f, w_out, status, iters, s);
+}
+
+int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const double* ref, const double* prm,
+                         const double* w_warm, double* u0, double* f, double* w_out, int32_t* status,
+                         int32_t* iters, void* stream) {
+    if (!h) return DART_MPC_EINVAL;
+    if (B < 0 || (B > 0 && (!x0 || !ref || !prm || !u0 || !f || !status || !iters)))
+        return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
+    if (B > h->cfg.B_max) return fail(h, DART_MPC_EINVAL, "batch larger than B_max");
+    if (B == 0) return DART_MPC_OK;
+    HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    const size_t nw = (size_t)dart_mpc_nw(h->cfg.N), Bm = (size_t)h->cfg.B_max;
+    double* d_x0 = h->dbuf;
+    double* d_ref = d_x0 + Bm * 6;
+    double* d_prm = d_ref + Bm * 6;
+    double* d_ww = d_prm + Bm * 6;
+    double* d_u0 = d_ww + Bm * nw;
+    double* d_f = d_u0 + Bm * 2;
+    double* d_wo = d_f + Bm;
+    int32_t* d_st = h->ibuf;
+    int32_t* d_it = d_st + Bm;
+    HIPCHK(h, hipMemcpyAsync(d_x0, x0, sizeof(double) * 6 * B, hipMemcpyHostToDevice, s), "copy x0");
+    HIPCHK(h, hipMemcpyAsync(d_ref, ref, sizeof(double) * 6 * B, hipMemcpyHostToDevice, s), "copy ref");
+    HIPCHK(h, hipMemcpyAsync(d_prm, prm, sizeof(double) * 6 * B, hipMemcpyHostToDevice, s), "copy prm");
+    if (w_warm) HIPCHK(h, hipMemcpyAsync(d_ww, w_warm, sizeof(double) * nw * B, hipMemcpyHostToDevice, s), "copy w_warm");
+    int rc = launch(h, B, d_x0, d_ref, d_prm, w_warm ? d_ww : nullptr, d_u0, d_f, w_out ? d_wo : nullptr, d_st, d_it, s);
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpyAsync(u0, d_u0, sizeof(double) * 2 * B, hipMemcpyDeviceToHost, s), "copy u0");
+    HIPCHK(h, hipMemcpyAsync(f, d_f, sizeof(double) * B, hipMemcpyDeviceToHost, s), "copy f");
+    if (w_out) HIPCHK(h, hipMemcpyAsync(w_out, d_wo, sizeof(double) * nw * B, hipMemcpyDeviceToHost, s), "copy w_out");
+    HIPCHK(h, hipMemcpyAsync(status, d_st, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s), "copy status");
+    HIPCHK(h, hipMemcpyAsync(iters, d_it, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s), "copy iters");
+    HIPCHK(h, hipStreamSynchronize(s), "hipStreamSynchronize");
+    return DART_MPC_OK;
+}
+
+int dart_mpc_sync(dart_mpc_handle* h) {
+    if (!h) return DART_MPC_EINVAL;
+    HIPCHK(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+    return DART_MPC_OK;
+}
+
+const char* dart_mpc_last_error(const dart_mpc_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+void dart_mpc_destroy(dart_mpc_handle* h) {
+    if (!h) return;
+    if (h->dbuf) (void)hipFree(h->dbuf);
+    if (h->ibuf) (void)hipFree(h->ibuf);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+}  // extern "C"

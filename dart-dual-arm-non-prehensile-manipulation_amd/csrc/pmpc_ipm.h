@@ -1,0 +1,25 @@
+// pmpc_ipm.h -- launch arguments of the batched PMPC interior-point kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dartmpc {
+
+struct PmpcArgs {
+    int B, N;
+    double Ts, tol, g;      // g = model.opt.gravity[2]
+    int max_iter;
+    const double* x0;       // [B][6]   device
+    const double* ref;      // [B][6]
+    const double* prm;      // [B][6]  mu, Qp, Qv, R, u_lo, u_hi
+    const double* w_warm;   // [B][nw] or nullptr
+    double* u0;             // [B][2]
+    double* f;              // [B]
+    double* w_out;          // [B][nw] or nullptr
+    int32_t* status;        // [B]
+    int32_t* iters;         // [B]
+};
+
+}  // namespace dartmpc
+
+extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStream_t stream);

@@ -1,0 +1,13 @@
+"""dart_mpc -- MI355X-native batched tray-tilt NMPC solver for DART.
+
+Drop-in for the reference's MPC hot path:
+  - ``PMPC``            <- PMPC/src/controller/mpc_3d.py:11-138
+  - ``mpc_worker``      <- PMPC/main_parallel_enhanced.py:22-55
+  - ``Solver``          the C ABI of include/dart_mpc.h (libdartmpc.so)
+"""
+from ._lib import DartMPCError, Solver, build, lib, STATUS_NAMES  # noqa: F401
+from .pmpc import PMPC, tilt_to_quat  # noqa: F401
+from .worker import mpc_worker  # noqa: F401
+from . import workload  # noqa: F401
+
+__all__ = ["PMPC", "mpc_worker", "Solver", "DartMPCError", "build", "lib", "tilt_to_quat", "workload"]

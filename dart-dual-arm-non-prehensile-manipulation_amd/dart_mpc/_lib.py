@@ -1,0 +1,153 @@
+"""ctypes binding of libdartmpc.so (the C ABI declared in include/dart_mpc.h).
+
+The product path has exactly one implementation: the HIP kernel in this
+library.  There is no CPU fallback -- if the library or a GPU is missing,
+every solve raises ``DartMPCError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "libdartmpc.so")
+
+SOLVED, MAXITER, LS_FAIL, INERTIA_FAIL = 0, -1, -2, -3
+STATUS_NAMES = {SOLVED: "Solve_Succeeded", MAXITER: "Maximum_Iterations_Exceeded",
+                LS_FAIL: "Restoration_Failed", INERTIA_FAIL: "Error_In_Step_Computation"}
+
+# exported symbols of include/dart_mpc.h (tests check every one is present)
+EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch", "dart_mpc_solve_batch_dev",
+           "dart_mpc_sync", "dart_mpc_last_error", "dart_mpc_destroy", "dart_mpc_nw", "dart_mpc_abi_version")
+ABI_VERSION = 1
+
+
+class DartMPCError(RuntimeError):
+    pass
+
+
+class Config(ctypes.Structure):
+    """Mirror of ``struct dart_mpc_config``."""
+    _fields_ = [("variant", ctypes.c_int32), ("N", ctypes.c_int32), ("Ts", ctypes.c_double),
+                ("tol", ctypes.c_double), ("max_iter", ctypes.c_int32), ("B_max", ctypes.c_int32),
+                ("gravity", ctypes.c_double)]
+
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int32)
+_lib = None
+
+
+def build(verbose: bool = False) -> str:
+    """Compile libdartmpc.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    r = subprocess.run(["make", "-C", CSRC_DIR], capture_output=not verbose, text=True)
+    if r.returncode != 0:
+        raise DartMPCError("building libdartmpc.so failed:\n" + (r.stdout or "") + (r.stderr or ""))
+    return LIB_PATH
+
+
+def lib():
+    """Load the library (no compute).  Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DartMPCError(f"{LIB_PATH} not built: run __graft_entry__.build() or `make -C {CSRC_DIR}`")
+    L = ctypes.CDLL(LIB_PATH)
+    L.dart_mpc_config_default.argtypes = [ctypes.POINTER(Config)]
+    L.dart_mpc_config_default.restype = None
+    L.dart_mpc_create.argtypes = [ctypes.POINTER(Config), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    L.dart_mpc_create.restype = ctypes.c_int
+    sig = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.dart_mpc_solve_batch.argtypes = sig
+    L.dart_mpc_solve_batch.restype = ctypes.c_int
+    L.dart_mpc_solve_batch_dev.argtypes = sig
+    L.dart_mpc_solve_batch_dev.restype = ctypes.c_int
+    L.dart_mpc_sync.argtypes = [ctypes.c_void_p]
+    L.dart_mpc_sync.restype = ctypes.c_int
+    L.dart_mpc_last_error.argtypes = [ctypes.c_void_p]
+    L.dart_mpc_last_error.restype = ctypes.c_char_p
+    L.dart_mpc_destroy.argtypes = [ctypes.c_void_p]
+    L.dart_mpc_destroy.restype = None
+    L.dart_mpc_nw.argtypes = [ctypes.c_int]
+    L.dart_mpc_nw.restype = ctypes.c_int
+    L.dart_mpc_abi_version.argtypes = []
+    L.dart_mpc_abi_version.restype = ctypes.c_int
+    if L.dart_mpc_abi_version() != ABI_VERSION:
+        raise DartMPCError("libdartmpc.so ABI version mismatch")
+    _lib = L
+    return L
+
+
+def default_config(**over) -> Config:
+    c = Config()
+    lib().dart_mpc_config_default(ctypes.byref(c))
+    for k, v in over.items():
+        setattr(c, k, v)
+    return c
+
+
+def _ptr(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+class Solver:
+    """Owns one ``dart_mpc_handle`` (device workspace + stream) for a fixed N/Ts/tol."""
+
+    def __init__(self, N=20, Ts=0.002, tol=1e-8, max_iter=3000, B_max=1024, device=0, gravity=-9.81):
+        self._h = ctypes.c_void_p()
+        self.cfg = default_config(N=int(N), Ts=float(Ts), tol=float(tol), max_iter=int(max_iter), B_max=int(B_max),
+                                  gravity=float(gravity))
+        rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
+        if rc != 0:
+            raise DartMPCError(f"dart_mpc_create failed with code {rc} (no gfx950 device or bad config)")
+        self.N = int(N)
+        self.nw = lib().dart_mpc_nw(self.N)
+
+    def _err(self, rc, what):
+        msg = lib().dart_mpc_last_error(self._h)
+        raise DartMPCError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def solve_batch(self, x0, ref, prm, w_warm=None, want_w=False):
+        """Host arrays in, host arrays out (blocking).  Returns dict(u0, f, w, status, iters)."""
+        x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 6)
+        B = x0.shape[0]
+        ref = np.ascontiguousarray(ref, np.float64).reshape(B, 6)
+        prm = np.ascontiguousarray(prm, np.float64).reshape(B, 6)
+        ww = None if w_warm is None else np.ascontiguousarray(w_warm, np.float64).reshape(B, self.nw)
+        u0 = np.empty((B, 2)); f = np.empty(B)
+        w = np.empty((B, self.nw)) if want_w else None
+        st = np.empty(B, np.int32); it = np.empty(B, np.int32)
+        rc = lib().dart_mpc_solve_batch(self._h, B, _ptr(x0), _ptr(ref), _ptr(prm), _ptr(ww), _ptr(u0), _ptr(f),
+                                        _ptr(w), _ptr(st), _ptr(it), None)
+        if rc != 0:
+            self._err(rc, "dart_mpc_solve_batch")
+        return dict(u0=u0, f=f, w=w, status=st, iters=it)
+
+    def solve_batch_dev(self, B, x0, ref, prm, u0, f, status, iters, w_warm=0, w_out=0, stream=0):
+        """Device pointers (ints) in/out, asynchronous on ``stream`` (an int hipStream_t, 0 = own)."""
+        rc = lib().dart_mpc_solve_batch_dev(self._h, int(B), x0, ref, prm, w_warm or None, u0, f, w_out or None,
+                                            status, iters, stream or None)
+        if rc != 0:
+            self._err(rc, "dart_mpc_solve_batch_dev")
+
+    def sync(self):
+        rc = lib().dart_mpc_sync(self._h)
+        if rc != 0:
+            self._err(rc, "dart_mpc_sync")
+
+    def close(self):
+        if self._h:
+            lib().dart_mpc_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

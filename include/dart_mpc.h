@@ -1,0 +1,119 @@
+/*
+ * dart_mpc.h -- C ABI of the MI355X-native batched tray-tilt NMPC solver.
+ *
+ * This is the drop-in boundary for DART's per-timestep MPC solve.  Each entry
+ * point replaces one reference interface (paths relative to the reference root):
+ *
+ *   dart_mpc_create        <- PMPC.__init__ building the CasADi NLP and
+ *                             ca.nlpsol('solver','ipopt',...)
+ *                             PMPC/src/controller/mpc_3d.py:12-85 (:82)
+ *   dart_mpc_solve_batch   <- PMPC.solve(target) -> (U_opt[0], loss), one call
+ *                             per instance today: mpc_3d.py:115-138, called from
+ *                             the worker loop PMPC/main_parallel_enhanced.py:51-53
+ *   dart_mpc_solve_batch_dev  same, with device-resident inputs/outputs
+ *   dart_mpc_sync / dart_mpc_last_error / dart_mpc_destroy
+ *                           <- process-lifetime handling of the solver object in
+ *                             mpc_worker (main_parallel_enhanced.py:22-55)
+ *
+ * Plain C types only: no torch, no HIP types in signatures (streams are void*).
+ *
+ * Layouts (row-major, fp64):
+ *   x0  [B][6]  state  [px, vx, py, vy, pz, vz]             (mpc_3d.py:106-113)
+ *   ref [B][6]  target [px, vx, py, vy, pz, vz]             (mpc_3d.py:34, P[nx:])
+ *   prm [B][6]  [mu, Qp, Qv, R, u_lo, u_hi]                 (mpc_3d.py:12 ctor args)
+ *   w   [B][nw] decision vector in the reference order: x_0..x_N (6 each) then
+ *               u_0..u_{N-1} (2 each), nw = 6(N+1) + 2N     (mpc_3d.py:69)
+ *   u0  [B][2]  first control U_opt[0] = [theta_x, theta_y] (mpc_3d.py:137-138)
+ *   f   [B]     objective value at the solution ("loss")    (mpc_3d.py:134)
+ *   status[B]   DART_MPC_SOLVED (0), DART_MPC_MAXITER (-1), DART_MPC_LS_FAIL (-2),
+ *               DART_MPC_INERTIA_FAIL (-3).  As in the reference (which never
+ *               checks IPOPT's status, mpc_3d.py:133-138) u0 is written anyway.
+ *   iters[B]    interior-point iterations taken.
+ *
+ * Errors: every int-returning call returns 0 on success or a negative
+ * DART_MPC_E* code; dart_mpc_last_error() describes the last failure.
+ * Threading: a handle is not thread-safe; use one handle per host thread.
+ */
+#ifndef DART_MPC_H
+#define DART_MPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DART_MPC_ABI_VERSION 1
+
+enum dart_mpc_variant { DART_MPC_PMPC = 0 };
+
+enum dart_mpc_status {
+    DART_MPC_SOLVED = 0,
+    DART_MPC_MAXITER = -1,
+    DART_MPC_LS_FAIL = -2,
+    DART_MPC_INERTIA_FAIL = -3
+};
+
+enum dart_mpc_error {
+    DART_MPC_OK = 0,
+    DART_MPC_EINVAL = -1,     /* bad argument (null pointer, N out of range, B > B_max) */
+    DART_MPC_EHIP = -2,       /* HIP runtime error (message in dart_mpc_last_error) */
+    DART_MPC_ENODEV = -3      /* no usable gfx950 device */
+};
+
+/* Solver configuration.  Defaults (dart_mpc_config_default) follow the
+ * reference: N = 20 (mpc_3d.py:12), Ts = 0.002 (MuJoCo default timestep),
+ * IPOPT tol = 1e-8 and max_iter = 3000 (IPOPT defaults; mpc_3d.py:82 sets
+ * neither), gravity = -9.81 (world xml line 5). */
+typedef struct dart_mpc_config {
+    int32_t variant;    /* enum dart_mpc_variant */
+    int32_t N;          /* horizon, 1 <= N <= 63 */
+    double Ts;          /* sampling time [s] */
+    double tol;         /* IPOPT-style scaled optimality tolerance */
+    int32_t max_iter;   /* interior-point iteration cap */
+    int32_t B_max;      /* largest batch the handle's device workspace serves */
+    double gravity;     /* model.opt.gravity[2] (mpc_3d.py:23), default -9.81 */
+} dart_mpc_config;
+
+typedef struct dart_mpc_handle dart_mpc_handle;
+
+void dart_mpc_config_default(dart_mpc_config *cfg);
+
+int dart_mpc_create(const dart_mpc_config *cfg, int device, dart_mpc_handle **out);
+
+/* Host-pointer entry: stages inputs to HBM, solves, copies results back and
+ * blocks until they are in host memory.  w_warm (nullable) is an initial
+ * guess in the w layout; NULL = the reference's cold start (mpc_3d.py:123).
+ * w_out is nullable. */
+int dart_mpc_solve_batch(dart_mpc_handle *h, int B,
+                         const double *x0, const double *ref, const double *prm,
+                         const double *w_warm,
+                         double *u0, double *f, double *w_out,
+                         int32_t *status, int32_t *iters, void *hip_stream);
+
+/* Device-pointer entry: all pointers are device memory; asynchronous on
+ * hip_stream (NULL = the handle's own stream).  Call dart_mpc_sync or
+ * synchronise the stream before reading results. */
+int dart_mpc_solve_batch_dev(dart_mpc_handle *h, int B,
+                             const double *x0, const double *ref, const double *prm,
+                             const double *w_warm,
+                             double *u0, double *f, double *w_out,
+                             int32_t *status, int32_t *iters, void *hip_stream);
+
+int dart_mpc_sync(dart_mpc_handle *h);
+
+const char *dart_mpc_last_error(const dart_mpc_handle *h);
+
+void dart_mpc_destroy(dart_mpc_handle *h);
+
+/* Number of fp64 entries of w for horizon N: 6(N+1) + 2N. */
+int dart_mpc_nw(int N);
+
+/* ABI version (DART_MPC_ABI_VERSION) of the loaded library. */
+int dart_mpc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DART_MPC_H */

@@ -1,0 +1,67 @@
+"""ctypes loader for the C oracle (liboracle_pmpc.so) -- TEST INFRASTRUCTURE ONLY.
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  See pmpc_ipm.c for what is restated and where from.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle_pmpc.so")
+_lib = None
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int32)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oracle_pmpc_solve_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, _dp, _dp, _dp,
+                                              ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                              _dp, _dp, _dp, _ip, _ip]
+        L.oracle_pmpc_solve_batch.restype = ctypes.c_int
+        L.oracle_pmpc_rk4.argtypes = [ctypes.c_double, ctypes.c_double, _dp, _dp, _dp]
+        L.oracle_pmpc_rk4.restype = None
+        _lib = L
+    return _lib
+
+
+def _p(a, t=_dp):
+    return a.ctypes.data_as(t)
+
+
+def solve_batch(states, targets, params, N=20, Ts=0.002, max_iter=200, tol=1e-9, nthreads=1, want_w=True):
+    states = np.ascontiguousarray(states, np.float64)
+    targets = np.ascontiguousarray(targets, np.float64)
+    params = np.ascontiguousarray(params, np.float64)
+    B = states.shape[0]
+    nw = 6 * (N + 1) + 2 * N
+    u0 = np.zeros((B, 2))
+    f = np.zeros(B)
+    w = np.zeros((B, nw)) if want_w else None
+    st = np.zeros(B, np.int32)
+    it = np.zeros(B, np.int32)
+    lib().oracle_pmpc_solve_batch(B, N, Ts, _p(states), _p(targets), _p(params), max_iter, tol, nthreads,
+                                  _p(u0), _p(f), _p(w) if want_w else None, _p(st, _ip), _p(it, _ip))
+    return dict(u0=u0, f=f, w=w, status=st, iters=it)
+
+
+def rk4(Ts, mu, x, u):
+    x = np.ascontiguousarray(x, np.float64)
+    u = np.ascontiguousarray(u, np.float64)
+    out = np.zeros(6)
+    lib().oracle_pmpc_rk4(Ts, mu, _p(x), _p(u), _p(out))
+    return out

@@ -1,0 +1,63 @@
+"""The C-ABI library loads and exports every symbol include/dart_mpc.h declares (no compute)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    src = open(os.path.join(ROOT, "include", "dart_mpc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dart_mpc_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from dart_mpc import _lib
+    L = _lib.lib()
+    names = _declared_functions()
+    assert len(names) >= 9
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(_lib.EXPORTS)
+
+
+def test_defaults_follow_reference():
+    from dart_mpc import _lib
+    c = _lib.default_config()
+    assert (c.variant, c.N, c.Ts, c.tol, c.max_iter, c.gravity) == (0, 20, 0.002, 1e-8, 3000, -9.81)
+    assert _lib.lib().dart_mpc_nw(20) == 166 and _lib.lib().dart_mpc_nw(15) == 126
+    assert _lib.lib().dart_mpc_abi_version() == 1
+
+
+def test_create_rejects_bad_config_without_touching_a_gpu():
+    from dart_mpc import _lib
+    h = ctypes.c_void_p()
+    for over in (dict(N=0), dict(N=64), dict(Ts=0.0), dict(tol=-1.0), dict(B_max=0), dict(variant=7)):
+        c = _lib.default_config(**over)
+        assert _lib.lib().dart_mpc_create(ctypes.byref(c), 0, ctypes.byref(h)) == -1
+    assert _lib.lib().dart_mpc_solve_batch(None, 1, *([None] * 10)) == -1
+
+
+def test_pmpc_shim_validates_like_reference():
+    import dart_mpc
+    with pytest.raises(ValueError):
+        dart_mpc.PMPC(None, None, nx=4)
+    with pytest.raises(ValueError):
+        dart_mpc.PMPC(None, None, N=0)
+    c = dart_mpc.PMPC(None, None, Ts=0.002, N=15, Qp=600, Qv=5, R=0.1, mu=0.1, u_bounds=(-0.6, 0.6))
+    assert c.target_body == "cube" and c.w0.shape == (126,) and len(c.lbx) == 126
+    np.testing.assert_array_equal(c.params(), [0.1, 600, 5, 0.1, -0.6, 0.6])
+    with pytest.raises(RuntimeError):
+        c.get_state()
+
+
+def test_tilt_to_quat_matches_reference_formula():
+    from scipy.spatial.transform import Rotation as Rot
+    from dart_mpc import tilt_to_quat
+    for u in ([0.1, -0.2], [0.6, 0.6], [0.0, 0.0]):
+        q = Rot.from_euler("xyz", [u[1], -u[0], 0.0]).as_quat()          # main.py:107-116
+        np.testing.assert_allclose(tilt_to_quat(u), [q[3], q[0], q[1], q[2]], atol=1e-15)
