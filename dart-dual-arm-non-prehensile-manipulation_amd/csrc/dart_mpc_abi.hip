@@ -153,6 +153,16 @@ int dart_mpc_sync(dart_mpc_handle* h) {
     return DART_MPC_OK;
 }
 
+// internal self-test of the wave primitives (not in include/dart_mpc.h): host_out[195]
+int dartmpc_selftest(double* host_out) {
+    double* d = nullptr;
+    if (hipMalloc(&d, 195 * sizeof(double)) != hipSuccess) return DART_MPC_EHIP;
+    hipError_t e = dartmpc_wave_selftest(d, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(host_out, d, 195 * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return e == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
+}
+
 const char* dart_mpc_last_error(const dart_mpc_handle* h) { return h ? h->err.c_str() : "null handle"; }
 
 void dart_mpc_destroy(dart_mpc_handle* h) {

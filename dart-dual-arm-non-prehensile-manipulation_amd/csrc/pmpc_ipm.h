@@ -23,3 +23,4 @@ struct PmpcArgs {
 }  // namespace dartmpc
 
 extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStream_t stream);
+extern "C" hipError_t dartmpc_wave_selftest(double* d_out, hipStream_t stream);

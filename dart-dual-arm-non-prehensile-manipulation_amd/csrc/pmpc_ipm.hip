@@ -4,7 +4,7 @@
 // PMPC.solve (PMPC/src/controller/mpc_3d.py:115-138) for a whole batch of
 // independent tray-tilt NMPC instances.
 //
-// Structure exploited (see DESIGN.md §2): the reference NLP (mpc_3d.py:28-85)
+// Structure exploited (DESIGN.md §3): the reference NLP (mpc_3d.py:28-85)
 // splits into two independent scalar-input optimal-control problems -- the x
 // axis (px, vx; theta_x) and the y axis (py, vy; theta_y) -- plus the cost-free
 // z sub-state (pz, vz), which only follows the controls (its multipliers are
@@ -16,10 +16,11 @@
 // trajectory by the reference's own RK4 once the controls are final.
 //
 // Mapping: one wave64 per instance, lane k <-> shooting node k (0..N, N <= 63).
-// Everything per node lives in VGPRs; the stage-coupled recursions (Riccati
-// backward sweep, forward state sweep, z rollout) pass 2x2 blocks between
-// neighbouring lanes with cross-lane shifts; norms and inner products are
-// wave reductions.  No LDS, no global traffic inside the iteration loop.
+// Everything per node lives in VGPRs.  Stage-coupled recursions (Riccati
+// backward sweep, forward state sweep, z rollout) hand 2x2 blocks to the
+// neighbouring lane with DPP wave shifts (wave_shl:1 / wave_shr:1, no LDS);
+// norms and inner products are DPP row reductions + 4 readlanes.  No LDS and
+// no global traffic inside the iteration loop.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -30,98 +31,172 @@ namespace dartmpc {
 constexpr int kWave = 64;
 
 // ---------------------------------------------------------------------------
-// wave primitives
+// wave primitives (every call site is at wave-uniform control flow: EXEC full)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double uniform(double x) {   // lane 0's value in every lane (SGPR broadcast)
-    unsigned long long b = __builtin_bit_cast(unsigned long long, x);
-    unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(b & 0xffffffffu));
-    unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ double dpp(double x) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+    const int lo = (int)(unsigned)(b & 0xffffffffu), hi = (int)(unsigned)(b >> 32);
+    const int rlo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWMASK, 0xf, false);
+    const int rhi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWMASK, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)rhi << 32) | (unsigned)rlo);
+}
+__device__ __forceinline__ double readlane(double x, int l) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)(b & 0xffffffffu), l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
-__device__ __forceinline__ double wsum(double x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    return uniform(x);
+constexpr int kWaveShl1 = 0x130;   // lane k <- lane k+1
+constexpr int kWaveShr1 = 0x138;   // lane k <- lane k-1
+__device__ __forceinline__ double from_next(double x) { return dpp<kWaveShl1>(x); }
+__device__ __forceinline__ double from_prev(double x) { return dpp<kWaveShr1>(x); }
+
+struct OpSum { __device__ double operator()(double a, double b) const { return a + b; } };
+struct OpMax { __device__ double operator()(double a, double b) const { return fmax(a, b); } };
+struct OpMin { __device__ double operator()(double a, double b) const { return fmin(a, b); } };
+
+// row reduction by quad_perm + row_ror, then the four row totals by readlane: uniform result
+template <class Op>
+__device__ __forceinline__ double wreduce(double x, Op op) {
+    x = op(x, dpp<0xB1>(x));     // quad_perm [1,0,3,2]
+    x = op(x, dpp<0x4E>(x));     // quad_perm [2,3,0,1]
+    x = op(x, dpp<0x124>(x));    // row_ror:4
+    x = op(x, dpp<0x128>(x));    // row_ror:8
+    return op(op(readlane(x, 0), readlane(x, 16)), op(readlane(x, 32), readlane(x, 48)));
 }
-__device__ __forceinline__ double wmax(double x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o));
-    return uniform(x);
+// f32 variant for error measures, scalings and step-length minima (half the DPP traffic):
+// their consumers only compare against tolerances or fractions-to-the-boundary with >= 1 % slack
+template <int CTRL>
+__device__ __forceinline__ float dppf(float x) {
+    const int r = __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(float, r);
 }
-__device__ __forceinline__ double wmin(double x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o));
-    return uniform(x);
+__device__ __forceinline__ float readlanef(float x, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
-__device__ __forceinline__ double from_next(double x) { return __shfl_down(x, 1); }  // lane k <- lane k+1
-__device__ __forceinline__ double from_prev(double x) { return __shfl_up(x, 1); }    // lane k <- lane k-1
+template <class Op>
+__device__ __forceinline__ float wreducef(float x, Op op) {
+    x = op(x, dppf<0xB1>(x));
+    x = op(x, dppf<0x4E>(x));
+    x = op(x, dppf<0x124>(x));
+    x = op(x, dppf<0x128>(x));
+    return op(op(readlanef(x, 0), readlanef(x, 16)), op(readlanef(x, 32), readlanef(x, 48)));
+}
+struct OpSumF { __device__ float operator()(float a, float b) const { return a + b; } };
+struct OpMaxF { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
+struct OpMinF { __device__ float operator()(float a, float b) const { return fminf(a, b); } };
+__device__ __forceinline__ float wsumf(float x) { return wreducef(x, OpSumF()); }
+__device__ __forceinline__ float wmaxf(float x) { return wreducef(x, OpMaxF()); }
+__device__ __forceinline__ float wminf(float x) { return wreducef(x, OpMinF()); }
+
+__device__ __forceinline__ double wsum(double x) { return wreduce(x, OpSum()); }
+__device__ __forceinline__ double wmax(double x) { return wreduce(x, OpMax()); }
+__device__ __forceinline__ double wmin(double x) { return wreduce(x, OpMin()); }
 __device__ __forceinline__ bool wany(bool p) { return __ballot(p) != 0ull; }
+
+// reciprocal: v_rcp_f64 + two Newton steps (operands are well scaled, no denormals)
+__device__ __forceinline__ double frcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+
+// log2 of a positive double to ~1e-7 relative: exponent + f32 log2 of the mantissa.  Used only in
+// the filter's switching condition / minimum step heuristics, never in a quantity that is solved for.
+__device__ __forceinline__ float lg2(double x) {
+    const int e = __builtin_amdgcn_frexp_exp(x);
+    const float m = (float)__builtin_amdgcn_frexp_mant(x);
+    return (float)e + __builtin_amdgcn_logf(m);
+}
+
+#ifdef DART_STAMPS
+__device__ unsigned long long g_stamp[16];
+#define STAMP_DECL unsigned long long t_prev_ = __builtin_amdgcn_s_memtime(), t_acc_[12] = {0};
+#define STAMP_ADD(i, n) do { t_acc_[i] += (unsigned long long)(n); } while (0)
+#define STAMP(i) do { unsigned long long t_ = __builtin_amdgcn_s_memtime(); t_acc_[i] += t_ - t_prev_; t_prev_ = t_; } while (0)
+#define STAMP_FLUSH(b) do { if ((b) == 0 && threadIdx.x == 0) for (int q_ = 0; q_ < 12; ++q_) g_stamp[q_] = t_acc_[q_]; } while (0)
+#else
+#define STAMP_DECL
+#define STAMP_ADD(i, n) do {} while (0)
+#define STAMP(i) do {} while (0)
+#define STAMP_FLUSH(b) do {} while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // model pieces
 // ---------------------------------------------------------------------------
 // mpc_3d.py:87-97, one axis:  pdot = v,  vdot = g sin(theta) - mu v
-__device__ __forceinline__ void axis_rhs(double g, double mu, double s, double p, double v, double& dp, double& dv) {
-    (void)p;
+__device__ __forceinline__ void axis_rhs(double g, double mu, double s, double v, double& dp, double& dv) {
     dp = v;
     dv = g * s - mu * v;
 }
 // mpc_3d.py:99-104 on one axis with s = sin(theta) held constant
-__device__ __forceinline__ void axis_rk4(double h, double g, double mu, double s, double p, double v, double& pn, double& vn) {
+__device__ __forceinline__ void axis_rk4(double h, double g, double mu, double s, double p, double v,
+                                         double& pn, double& vn) {
     double k1p, k1v, k2p, k2v, k3p, k3v, k4p, k4v;
-    axis_rhs(g, mu, s, p, v, k1p, k1v);
-    axis_rhs(g, mu, s, p + h / 2 * k1p, v + h / 2 * k1v, k2p, k2v);
-    axis_rhs(g, mu, s, p + h / 2 * k2p, v + h / 2 * k2v, k3p, k3v);
-    axis_rhs(g, mu, s, p + h * k3p, v + h * k3v, k4p, k4v);
+    axis_rhs(g, mu, s, v, k1p, k1v);
+    axis_rhs(g, mu, s, v + h / 2 * k1v, k2p, k2v);
+    axis_rhs(g, mu, s, v + h / 2 * k2v, k3p, k3v);
+    axis_rhs(g, mu, s, v + h * k3v, k4p, k4v);
     pn = p + h / 6 * (k1p + 2 * k2p + 2 * k3p + k4p);
     vn = v + h / 6 * (k1v + 2 * k2v + 2 * k3v + k4v);
 }
 // z sub-state (mpc_3d.py:93-97): pzdot = vz_new, vzdot = (vz_new - vz)/Ts, literal RK4
 __device__ __forceinline__ void z_rk4(double h, double w, double pz, double vz, double& pzn, double& vzn) {
-    double k1v = (w - vz) / h;
-    double k2v = (w - (vz + h / 2 * k1v)) / h;
-    double k3v = (w - (vz + h / 2 * k2v)) / h;
-    double k4v = (w - (vz + h * k3v)) / h;
+    const double k1v = (w - vz) / h;
+    const double k2v = (w - (vz + h / 2 * k1v)) / h;
+    const double k3v = (w - (vz + h / 2 * k2v)) / h;
+    const double k4v = (w - (vz + h * k3v)) / h;
     pzn = pz + h / 6 * (w + 2 * w + 2 * w + w);
     vzn = vz + h / 6 * (k1v + 2 * k2v + 2 * k3v + k4v);
 }
 
-struct Model {        // per-instance constants (wave-uniform)
-    double a12, a22, b1, b2;      // x+ = [[1,a12],[0,a22]] x + [b1,b2] sin(theta)
-    double qp2, qv2, r2;          // scaled 2*Qp, 2*Qv, 2*R
-    double Qp, Qv, R, sc;
-    double lo, hi;                // relaxed box
-};
-
-// per-node, per-axis iterate and work registers
-struct Axis {
-    double sp, sv, rp, rv;        // initial state, reference (uniform)
-    double p, v, th;              // primal
-    double lp, lv;                // multipliers of the constraint that defines x_k
-    double zl, zu;                // bound multipliers (k < N)
-    double s, c;                  // sin, cos theta
-    double g1, g2;                // defect g_k
-    double K1, K2, kff, iQ, U1, U2;
-    double P11, P12, P22, p1, p2;
-    double dp, dv, dth, dlp, dlv, dzl, dzu;
-};
-
-// defect g_k = x_k - f(x_{k-1}, u_{k-1}) (mpc_3d.py:48), g_0 = x_0 - state (:37)
-__device__ __forceinline__ void defects(const Model& M, int k, double sp, double sv, double p, double v, double s,
-                                        double& g1, double& g2) {
-    double fp = p + M.a12 * v + M.b1 * s;
-    double fv = M.a22 * v + M.b2 * s;
-    double ip = from_prev(fp), iv = from_prev(fv);
-    g1 = (k == 0) ? p - sp : p - ip;
-    g2 = (k == 0) ? v - sv : v - iv;
+// sin/cos for |x| <= 1.0 (bound-relaxed tilt range) by Taylor series to x^19 / x^20:
+// truncation < 2e-20, i.e. below fp64 rounding.  Wider boxes fall back to ocml sincos.
+__device__ __forceinline__ void sincos_small(double x, double& s, double& c) {
+    const double y = x * x;
+    double ps = -1.0 / 121645100408832000.0;                 // -1/19!
+    ps = fma(ps, y, 1.0 / 355687428096000.0);                // 1/17!
+    ps = fma(ps, y, -1.0 / 1307674368000.0);                 // -1/15!
+    ps = fma(ps, y, 1.0 / 6227020800.0);                     // 1/13!
+    ps = fma(ps, y, -1.0 / 39916800.0);                      // -1/11!
+    ps = fma(ps, y, 1.0 / 362880.0);                         // 1/9!
+    ps = fma(ps, y, -1.0 / 5040.0);                          // -1/7!
+    ps = fma(ps, y, 1.0 / 120.0);                            // 1/5!
+    ps = fma(ps, y, -1.0 / 6.0);                             // -1/3!
+    s = fma(x * y, ps, x);
+    double pc = 1.0 / 2432902008176640000.0;                 // 1/20!
+    pc = fma(pc, y, -1.0 / 6402373705728000.0);              // -1/18!
+    pc = fma(pc, y, 1.0 / 20922789888000.0);                 // 1/16!
+    pc = fma(pc, y, -1.0 / 87178291200.0);                   // -1/14!
+    pc = fma(pc, y, 1.0 / 479001600.0);                      // 1/12!
+    pc = fma(pc, y, -1.0 / 3628800.0);                       // -1/10!
+    pc = fma(pc, y, 1.0 / 40320.0);                          // 1/8!
+    pc = fma(pc, y, -1.0 / 720.0);                           // -1/6!
+    pc = fma(pc, y, 1.0 / 24.0);                             // 1/4!
+    pc = fma(pc, y, -0.5);                                   // -1/2!
+    c = fma(y, pc, 1.0);
+}
+__device__ __forceinline__ void tilt_sincos(bool poly, double x, double& s, double& c) {
+    if (poly) sincos_small(x, s, c);
+    else sincos(x, &s, &c);
 }
 
 // ---------------------------------------------------------------------------
-// the kernel: one wave64 = one instance
+// the kernel: one wave64 = one instance.
+//   NAX = 1 (N <= 31): lane = axis*32 + k, one axis per lane (x in lanes 0-31, y in 32-63)
+//   NAX = 2 (N <= 63): lane = k, both axes in every lane
 // ---------------------------------------------------------------------------
+template <int NAX>
 __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
+    STAMP_DECL
     const int b = blockIdx.x;
-    const int k = threadIdx.x;
+    const int lane = threadIdx.x;
+    const int k = NAX == 1 ? (lane & 31) : lane;            // shooting node of this lane
+    const int ax0 = NAX == 1 ? (lane >> 5) : 0;               // axis of slot 0 (NAX == 1)
     const int N = a.N;
     const bool xon = k <= N, uon = k < N;
     const double h = a.Ts;
@@ -131,254 +206,275 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
     const double* pr = a.prm + 6 * b;
     const double mu_f = pr[0], Qp = pr[1], Qv = pr[2], R = pr[3], ulo = pr[4], uhi = pr[5];
 
-    Model M;
-    {   // RK4 map of the linear axis model applied to the basis: exact Phi, Gamma
-        double pn, vn;
-        axis_rk4(h, a.g, mu_f, 0.0, 0.0, 1.0, pn, vn); M.a12 = pn; M.a22 = vn;
-        axis_rk4(h, a.g, mu_f, 1.0, 0.0, 0.0, pn, vn); M.b1 = pn; M.b2 = vn;
-    }
-    M.Qp = Qp; M.Qv = Qv; M.R = R;
-    M.lo = ulo - 1e-8 * fmax(1.0, fabs(ulo));       // IPOPT bound_relax_factor = 1e-8
-    M.hi = uhi + 1e-8 * fmax(1.0, fabs(uhi));
-    const double lo = M.lo, hi = M.hi;
+    // RK4 map of the linear axis model applied to the basis: exact Phi = [[1,a12],[0,a22]], Gamma = [b1,b2]
+    double a12, a22, b1, b2;
+    axis_rk4(h, a.g, mu_f, 0.0, 0.0, 1.0, a12, a22);
+    axis_rk4(h, a.g, mu_f, 1.0, 0.0, 0.0, b1, b2);
+    const double lo = ulo - 1e-8 * fmax(1.0, fabs(ulo));       // IPOPT bound_relax_factor = 1e-8
+    const double hi = uhi + 1e-8 * fmax(1.0, fabs(uhi));
+    const bool poly = fmax(fabs(lo), fabs(hi)) <= 1.0;
+    // per-lane stage map: the real Phi on stages k < N, zero on the terminal/idle lanes, so that the
+    // backward sweep reproduces the terminal value function there without a branch
+    const double f11 = uon ? 1.0 : 0.0, a12k = uon ? a12 : 0.0, a22k = uon ? a22 : 0.0;
+    const double A11k = a12k * a12k, A12k = 2.0 * a12k * a22k, A22k = a22k * a22k;
 
-    Axis X[2];
+    // per-lane axis slots
+    double sp[NAX], sv[NAX], rp[NAX], rv[NAX];
+    double p[NAX], v[NAX], th[NAX], lp[NAX], lv[NAX], zl[NAX], zu[NAX];
     const int nw = 6 * (N + 1) + 2 * N;
     const double* ww = a.w_warm ? a.w_warm + (size_t)nw * b : nullptr;
-    const double pushl = fmin(1e-2 * fmax(1.0, fabs(lo)), 1e-2 * (hi - lo));
+    const double pushl = fmin(1e-2 * fmax(1.0, fabs(lo)), 1e-2 * (hi - lo));   // IPOPT bound_push / frac
     const double pushu = fmin(1e-2 * fmax(1.0, fabs(hi)), 1e-2 * (hi - lo));
     double gmax = 0.0;
 #pragma unroll
-    for (int ax = 0; ax < 2; ++ax) {
-        Axis& A = X[ax];
-        A.sp = st[2 * ax]; A.sv = st[2 * ax + 1];
-        A.rp = rf[2 * ax]; A.rv = rf[2 * ax + 1];
-        A.p = xon ? (ww ? ww[6 * k + 2 * ax] : A.sp) : 0.0;       // cold start: tile(state) (mpc_3d.py:123)
-        A.v = xon ? (ww ? ww[6 * k + 2 * ax + 1] : A.sv) : 0.0;
-        double th = uon ? (ww ? ww[6 * (N + 1) + 2 * k + ax] : 0.0) : 0.0;
-        if (uon) th = fmin(fmax(th, lo + pushl), hi - pushu);
-        A.th = th;
-        A.lp = 0.0; A.lv = 0.0;
-        A.zl = uon ? 1.0 : 0.0; A.zu = uon ? 1.0 : 0.0;   // bound_mult_init_val = 1
-        if (xon) gmax = fmax(gmax, fmax(fabs(2 * Qp * (A.p - A.rp)), fabs(2 * Qv * (A.v - A.rv))));
-        if (uon) gmax = fmax(gmax, fabs(2 * R * A.th));
+    for (int j = 0; j < NAX; ++j) {
+        const int ax = NAX == 1 ? ax0 : j;
+        sp[j] = st[2 * ax]; sv[j] = st[2 * ax + 1];
+        rp[j] = rf[2 * ax]; rv[j] = rf[2 * ax + 1];
+        p[j] = xon ? (ww ? ww[6 * k + 2 * ax] : sp[j]) : 0.0;       // cold start: tile(state) (mpc_3d.py:123)
+        v[j] = xon ? (ww ? ww[6 * k + 2 * ax + 1] : sv[j]) : 0.0;
+        double t = uon ? (ww ? ww[6 * (N + 1) + 2 * k + ax] : 0.0) : 0.0;
+        if (uon) t = fmin(fmax(t, lo + pushl), hi - pushu);
+        th[j] = t;
+        lp[j] = 0.0; lv[j] = 0.0;
+        zl[j] = uon ? 1.0 : 0.0; zu[j] = uon ? 1.0 : 0.0;      // bound_mult_init_val = 1
+        if (xon) gmax = fmax(gmax, fmax(fabs(2 * Qp * (p[j] - rp[j])), fabs(2 * Qv * (v[j] - rv[j]))));
+        if (uon) gmax = fmax(gmax, fabs(2 * R * th[j]));
     }
     gmax = wmax(gmax);
     const double sc = gmax > 100.0 ? 100.0 / gmax : 1.0;     // nlp_scaling_max_gradient = 100
-    M.sc = sc; M.qp2 = sc * 2 * Qp; M.qv2 = sc * 2 * Qv; M.r2 = sc * 2 * R;
+    const double qp2 = sc * 2 * Qp, qv2 = sc * 2 * Qv, r2 = sc * 2 * R;
+    const double scQp = sc * Qp, scQv = sc * Qv, scR = sc * R;
 
     const double tol = a.tol, mu_min = tol / 10;
     const double n_eq = 6.0 * (N + 1), n_b = 4.0 * N;       // IPOPT counts on the full NLP
     const double gam_th = 1e-5, gam_ph = 1e-8, s_th = 1.1, s_ph = 2.3, eta_ph = 1e-8, gam_al = 0.05;
 
-    // constraint violation at the start (filter bounds)
+    // defect g_k = x_k - f(x_{k-1}, u_{k-1}) (mpc_3d.py:48), g_0 = x_0 - state (:37)
+    auto defects = [&](double pj, double vj, double sj, double spj, double svj, double& g1, double& g2) {
+        const double fp = fma(a12, vj, fma(b1, sj, pj));
+        const double fv = fma(a22, vj, b2 * sj);
+        const double ip = from_prev(fp), iv = from_prev(fv);
+        g1 = (k == 0) ? pj - spj : pj - ip;
+        g2 = (k == 0) ? vj - svj : vj - iv;
+    };
+
+    double g1[NAX], g2[NAX];
     double th0 = 0.0;
 #pragma unroll
-    for (int ax = 0; ax < 2; ++ax) {
-        Axis& A = X[ax];
-        A.s = uon ? sin(A.th) : 0.0;
-        defects(M, k, A.sp, A.sv, A.p, A.v, A.s, A.g1, A.g2);
-        if (xon) th0 += fabs(A.g1) + fabs(A.g2);
+    for (int j = 0; j < NAX; ++j) {
+        double s0, c0_;
+        tilt_sincos(poly, th[j], s0, c0_);
+        defects(p[j], v[j], uon ? s0 : 0.0, sp[j], sv[j], g1[j], g2[j]);
+        if (xon) th0 += fabs(g1[j]) + fabs(g2[j]);
     }
-    double theta = wsum(th0);
+    double theta = wsum(th0);                                  // filter's constraint violation
     const double th_max = 1e4 * fmax(1.0, theta), th_min = 1e-4 * fmax(1.0, theta);
 
     double fth = 0.0, fph = 0.0;      // filter entry held by lane (slot = lane id)
     int nfilt = 0;
     double mu = 0.1, delta_last = 0.0;
     int status = -1, it = 0;
+    STAMP(0);
 
     for (it = 0; it < a.max_iter; ++it) {
-        // -------- point quantities ------------------------------------------
+        // -------- point quantities and optimality error (IPOPT eq. 5) ------------
+        double sn[NAX], cs[NAX], isl[NAX], isu[NAX], lpn[NAX], lvn[NAX];
         double dinf = 0.0, pinf = 0.0, c0 = 0.0, suml = 0.0, sumz = 0.0;
 #pragma unroll
-        for (int ax = 0; ax < 2; ++ax) {
-            Axis& A = X[ax];
-            double s = 0.0, c = 1.0;
-            if (uon) sincos(A.th, &s, &c);
-            A.s = s; A.c = c;
-            defects(M, k, A.sp, A.sv, A.p, A.v, A.s, A.g1, A.g2);
-            double lpn = from_next(A.lp), lvn = from_next(A.lv);
-            if (xon) {
-                double r1 = M.qp2 * (A.p - A.rp) + A.lp - (uon ? lpn : 0.0);
-                double r2 = M.qv2 * (A.v - A.rv) + A.lv - (uon ? M.a12 * lpn + M.a22 * lvn : 0.0);
-                dinf = fmax(dinf, fmax(fabs(r1), fabs(r2)));
-                pinf = fmax(pinf, fmax(fabs(A.g1), fabs(A.g2)));
-                suml += fabs(A.lp) + fabs(A.lv);
-            }
-            if (uon) {
-                double sl = A.th - lo, su = hi - A.th;
-                double ru = M.r2 * A.th - c * (M.b1 * lpn + M.b2 * lvn) - A.zl + A.zu;
-                dinf = fmax(dinf, fabs(ru));
-                c0 = fmax(c0, fmax(A.zl * sl, A.zu * su));
-                sumz += A.zl + A.zu;
-                // keep next-lane multipliers for the Hessian term
-                A.dlp = lpn; A.dlv = lvn;
-            } else {
-                A.dlp = 0.0; A.dlv = 0.0;
-            }
+        for (int j = 0; j < NAX; ++j) {
+            double s_, c_;
+            tilt_sincos(poly, th[j], s_, c_);
+            sn[j] = uon ? s_ : 0.0; cs[j] = uon ? c_ : 0.0;
+            defects(p[j], v[j], sn[j], sp[j], sv[j], g1[j], g2[j]);
+            const double ln = from_next(lp[j]), vn = from_next(lv[j]);   // unconditional: EXEC stays full
+            lpn[j] = uon ? ln : 0.0; lvn[j] = uon ? vn : 0.0;
+            const double sl = th[j] - lo, su = hi - th[j];
+            isl[j] = uon ? frcp(sl) : 0.0; isu[j] = uon ? frcp(su) : 0.0;
+            const double r1 = fma(qp2, p[j] - rp[j], lp[j] - lpn[j]);
+            const double r2x = fma(qv2, v[j] - rv[j], lv[j] - fma(a12, lpn[j], a22 * lvn[j]));
+            const double ru = fma(r2, th[j], -cs[j] * fma(b1, lpn[j], b2 * lvn[j])) - zl[j] + zu[j];
+            dinf = fmax(dinf, xon ? fmax(fabs(r1), fabs(r2x)) : 0.0);
+            dinf = fmax(dinf, uon ? fabs(ru) : 0.0);
+            pinf = fmax(pinf, xon ? fmax(fabs(g1[j]), fabs(g2[j])) : 0.0);
+            suml += xon ? fabs(lp[j]) + fabs(lv[j]) : 0.0;
+            c0 = fmax(c0, uon ? fmax(zl[j] * sl, zu[j] * su) : 0.0);
+            sumz += zl[j] + zu[j];
         }
-        dinf = wmax(dinf); pinf = wmax(pinf); c0 = wmax(c0);
-        suml = wsum(suml); sumz = wsum(sumz);
-        const double s_d = fmax(100.0, (suml + sumz) / (n_eq + n_b)) / 100.0;
-        const double s_c = fmax(100.0, sumz / n_b) / 100.0;
+        const double dinf_w = wmaxf((float)dinf), pinf_w = wmaxf((float)pinf), c0_w = wmaxf((float)c0);
+        const double s_d = fmax(100.0, (double)(wsumf((float)suml) + wsumf((float)sumz)) / (n_eq + n_b)) / 100.0;
+        const double s_c = fmax(100.0, (double)wsumf((float)sumz) / n_b) / 100.0;
+        dinf = dinf_w; pinf = pinf_w; c0 = c0_w;
+        STAMP(1);
         if (fmax(dinf / s_d, fmax(pinf, c0 / s_c)) <= tol) { status = 0; break; }
-        // -------- monotone barrier update -----------------------------------
+        // -------- monotone barrier update (Fiacco-McCormick, may fire repeatedly) --
         for (;;) {
             double cmu = 0.0;
 #pragma unroll
-            for (int ax = 0; ax < 2; ++ax) {
-                const Axis& A = X[ax];
-                if (uon) cmu = fmax(cmu, fmax(fabs(A.zl * (A.th - lo) - mu), fabs(A.zu * (hi - A.th) - mu)));
-            }
-            cmu = wmax(cmu);
+            for (int j = 0; j < NAX; ++j)
+                cmu = fmax(cmu, uon ? fmax(fabs(zl[j] * (th[j] - lo) - mu), fabs(zu[j] * (hi - th[j]) - mu)) : 0.0);
+            cmu = wmaxf((float)cmu);
             if (fmax(dinf / s_d, fmax(pinf, cmu / s_c)) > 10.0 * mu || mu <= mu_min) break;
             mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
             nfilt = 0;
         }
         const double tau = fmax(0.99, 1.0 - mu);
+        STAMP(2);
 
-        // -------- Newton step: Riccati recursion + inertia correction ---------
+        // -------- Newton step: Riccati recursion + inertia correction ---------------
+        double be1[NAX], be2[NAX], E11[NAX], E12[NAX], E22[NAX], Rt0[NAX], rt[NAX], q1[NAX], q2[NAX], gn1[NAX], gn2[NAX];
+#pragma unroll
+        for (int j = 0; j < NAX; ++j) {
+            be1[j] = b1 * cs[j]; be2[j] = b2 * cs[j];           // B_k = Gamma cos(theta_k); 0 on idle lanes
+            E11[j] = be1[j] * be1[j]; E12[j] = 2.0 * be1[j] * be2[j]; E22[j] = be2[j] * be2[j];
+            // Hessian of the Lagrangian in theta: 2R + lam_{k+1}^T Gamma sin(theta) + Sigma
+            Rt0[j] = uon ? fma(sn[j], fma(b1, lpn[j], b2 * lvn[j]), r2 + zl[j] * isl[j] + zu[j] * isu[j]) : 1.0;
+            rt[j] = uon ? fma(r2, th[j], mu * (isu[j] - isl[j])) : 0.0;
+            q1[j] = qp2 * (p[j] - rp[j]); q2[j] = qv2 * (v[j] - rv[j]);
+            gn1[j] = from_next(g1[j]); gn2[j] = from_next(g2[j]);
+        }
+        double W1[NAX], W2[NAX], kff[NAX], P11[NAX], P12[NAX], P22[NAX], p1[NAX], p2[NAX];
         double delta = 0.0;
         bool ok = false;
-        for (int attempt = 0; attempt < 60 && !ok; ++attempt) {
+        int attempt = 0;
+        for (; attempt < 60 && !ok; ++attempt) {
             if (attempt > 0)
                 delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last / 3.0))
                                        : delta * (delta_last == 0.0 ? 100.0 : 8.0);
-            bool bad = false;
+            const double X11d = qp2 + delta, X22d = qv2 + delta;
+            double Quu[NAX], Rt[NAX];
 #pragma unroll
-            for (int ax = 0; ax < 2; ++ax) {
-                Axis& A = X[ax];
-                // terminal value function in every lane; lanes k < N are overwritten by the sweep
-                A.P11 = M.qp2 + delta; A.P12 = 0.0; A.P22 = M.qv2 + delta;
-                A.p1 = M.qp2 * (A.p - A.rp); A.p2 = M.qv2 * (A.v - A.rv);
+            for (int j = 0; j < NAX; ++j) {      // terminal value function in every lane
+                P11[j] = X11d; P12[j] = 0.0; P22[j] = X22d;
+                p1[j] = q1[j]; p2[j] = q2[j];
+                Rt[j] = Rt0[j] + delta;
             }
-            const double gn[2][2] = {{from_next(X[0].g1), from_next(X[0].g2)}, {from_next(X[1].g1), from_next(X[1].g2)}};
-            double Quu[2] = {1.0, 1.0};
+            // backward sweep: every lane maps its neighbour's value function through its own
+            // stage; after step j lane N-1-j is final.  Terminal/idle lanes have Phi = 0, B = 0.
             for (int step = 0; step < N; ++step) {
+                double n11[NAX], n12[NAX], n22[NAX], n1[NAX], n2[NAX];
 #pragma unroll
-                for (int ax = 0; ax < 2; ++ax) {
-                    Axis& A = X[ax];
-                    const double P11 = from_next(A.P11), P12 = from_next(A.P12), P22 = from_next(A.P22);
-                    const double pn1 = from_next(A.p1), pn2 = from_next(A.p2);
-                    if (uon) {
-                        const double a12 = M.a12, a22 = M.a22;
-                        const double be1 = M.b1 * A.c, be2 = M.b2 * A.c;
-                        const double sl = A.th - lo, su = hi - A.th;
-                        // Hessian of the Lagrangian in theta: 2R + lam_{k+1}^T Gamma sin(theta) + Sigma + delta
-                        const double Rt = M.r2 + A.s * (M.b1 * A.dlp + M.b2 * A.dlv) + A.zl / sl + A.zu / su + delta;
-                        const double rt = M.r2 * A.th - mu / sl + mu / su;
-                        const double q1 = M.qp2 * (A.p - A.rp), q2 = M.qv2 * (A.v - A.rv);
-                        // Phi^T P Phi with Phi = [[1,a12],[0,a22]]
-                        const double t12 = P11 * a12 + P12 * a22;
-                        const double t22 = P12 * a12 + P22 * a22;
-                        const double X11 = P11 + M.qp2 + delta;
-                        const double X12 = t12;
-                        const double X22 = a12 * t12 + a22 * t22 + M.qv2 + delta;
-                        const double PB1 = P11 * be1 + P12 * be2, PB2 = P12 * be1 + P22 * be2;
-                        const double Q = Rt + be1 * PB1 + be2 * PB2;
-                        const double U1 = PB1, U2 = PB1 * a12 + PB2 * a22;
-                        const double h1 = pn1 - (P11 * gn[ax][0] + P12 * gn[ax][1]);
-                        const double h2 = pn2 - (P12 * gn[ax][0] + P22 * gn[ax][1]);
-                        const double qx1 = q1 + h1, qx2 = q2 + a12 * h1 + a22 * h2;
-                        const double qu = rt + be1 * h1 + be2 * h2;
-                        const double iQ = 1.0 / Q;
-                        A.iQ = iQ; A.U1 = U1; A.U2 = U2;
-                        A.K1 = -iQ * U1; A.K2 = -iQ * U2; A.kff = -iQ * qu;
-                        A.P11 = X11 - iQ * U1 * U1;
-                        A.P12 = X12 - iQ * U1 * U2;
-                        A.P22 = X22 - iQ * U2 * U2;
-                        A.p1 = qx1 + U1 * A.kff;
-                        A.p2 = qx2 + U2 * A.kff;
-                        Quu[ax] = Q;
-                    }
+                for (int j = 0; j < NAX; ++j) {
+                    n11[j] = from_next(P11[j]); n12[j] = from_next(P12[j]); n22[j] = from_next(P22[j]);
+                    n1[j] = from_next(p1[j]); n2[j] = from_next(p2[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < NAX; ++j) {
+                    const double e1 = be1[j], e2 = be2[j];
+                    const double Q = fma(E11[j], n11[j], fma(E12[j], n12[j], fma(E22[j], n22[j], Rt[j])));
+                    const double PB1 = fma(n11[j], e1, n12[j] * e2), PB2 = fma(n12[j], e1, n22[j] * e2);
+                    const double U1 = PB1, U2 = fma(PB1, a12k, PB2 * a22k);
+                    const double X12 = fma(n11[j], a12k, n12[j] * a22k);
+                    const double X22 = fma(A11k, n11[j], fma(A12k, n12[j], fma(A22k, n22[j], X22d)));
+                    const double h1 = n1[j] - fma(n11[j], gn1[j], n12[j] * gn2[j]);
+                    const double h2 = n2[j] - fma(n12[j], gn1[j], n22[j] * gn2[j]);
+                    const double qu = fma(e1, h1, fma(e2, h2, rt[j]));
+                    const double iQ = frcp(Q);
+                    const double kf = -iQ * qu, w1 = iQ * U1, w2 = iQ * U2;
+                    P11[j] = fma(-w1, U1, fma(f11, n11[j], X11d));
+                    P12[j] = fma(-w1, U2, X12);
+                    P22[j] = fma(-w2, U2, X22);
+                    p1[j] = fma(U1, kf, fma(f11, h1, q1[j]));
+                    p2[j] = fma(U2, kf, q2[j] + fma(a12k, h1, a22k * h2));
+                    W1[j] = w1; W2[j] = w2; kff[j] = kf;
+                    Quu[j] = Q;
                 }
             }
-            if (uon) bad = !(Quu[0] > 0.0) || !(Quu[1] > 0.0) || !isfinite(Quu[0]) || !isfinite(Quu[1]);
+            bool bad = false;
+#pragma unroll
+            for (int j = 0; j < NAX; ++j) bad = bad || !(Quu[j] > 0.0) || !isfinite(Quu[j]);
             ok = !wany(bad);
         }
+        STAMP_ADD(9, attempt);
+        STAMP(3);
         if (!ok) { status = -3; break; }
         if (delta > 0.0) delta_last = delta;
 
-        // -------- forward sweep of the state step ------------------------------
+        // -------- forward sweep of the state step ----------------------------------
+        double dp[NAX], dv[NAX];
 #pragma unroll
-        for (int ax = 0; ax < 2; ++ax) { X[ax].dp = -X[ax].g1; X[ax].dv = -X[ax].g2; }
+        for (int j = 0; j < NAX; ++j) { dp[j] = -g1[j]; dv[j] = -g2[j]; }
         for (int step = 0; step < N; ++step) {
+            double op[NAX], ov[NAX];
 #pragma unroll
-            for (int ax = 0; ax < 2; ++ax) {
-                Axis& A = X[ax];
-                const double dth = A.K1 * A.dp + A.K2 * A.dv + A.kff;
-                const double op = A.dp + M.a12 * A.dv + M.b1 * A.c * dth;
-                const double ov = M.a22 * A.dv + M.b2 * A.c * dth;
-                const double ip = from_prev(op), iv = from_prev(ov);
-                if (k >= 1) { A.dp = ip - A.g1; A.dv = iv - A.g2; }
+            for (int j = 0; j < NAX; ++j) {
+                const double dth = fma(-W1[j], dp[j], fma(-W2[j], dv[j], kff[j]));
+                op[j] = fma(a12, dv[j], fma(be1[j], dth, dp[j]));
+                ov[j] = fma(a22, dv[j], be2[j] * dth);
+            }
+#pragma unroll
+            for (int j = 0; j < NAX; ++j) {
+                const double ip = from_prev(op[j]), iv = from_prev(ov[j]);
+                dp[j] = k >= 1 ? ip - g1[j] : dp[j];
+                dv[j] = k >= 1 ? iv - g2[j] : dv[j];
             }
         }
         double amax = 1.0, az = 1.0;
+        double dth[NAX], dlp[NAX], dlv[NAX], dzl[NAX], dzu[NAX];
 #pragma unroll
-        for (int ax = 0; ax < 2; ++ax) {
-            Axis& A = X[ax];
-            A.dth = uon ? A.K1 * A.dp + A.K2 * A.dv + A.kff : 0.0;
+        for (int j = 0; j < NAX; ++j) {
+            dth[j] = uon ? fma(-W1[j], dp[j], fma(-W2[j], dv[j], kff[j])) : 0.0;
             // new multipliers lam+ = -(P dx + p), step = lam+ - lam
-            A.dlp = xon ? -(A.P11 * A.dp + A.P12 * A.dv + A.p1) - A.lp : 0.0;
-            A.dlv = xon ? -(A.P12 * A.dp + A.P22 * A.dv + A.p2) - A.lv : 0.0;
-            if (uon) {
-                const double sl = A.th - lo, su = hi - A.th;
-                A.dzl = mu / sl - A.zl - A.zl / sl * A.dth;
-                A.dzu = mu / su - A.zu + A.zu / su * A.dth;
-                if (A.dth < 0) amax = fmin(amax, -tau * sl / A.dth);
-                if (A.dth > 0) amax = fmin(amax, tau * su / A.dth);
-                if (A.dzl < 0) az = fmin(az, -tau * A.zl / A.dzl);
-                if (A.dzu < 0) az = fmin(az, -tau * A.zu / A.dzu);
-            } else {
-                A.dzl = 0.0; A.dzu = 0.0;
-            }
+            dlp[j] = xon ? -fma(P11[j], dp[j], fma(P12[j], dv[j], p1[j])) - lp[j] : 0.0;
+            dlv[j] = xon ? -fma(P12[j], dp[j], fma(P22[j], dv[j], p2[j])) - lv[j] : 0.0;
+            const double sl = th[j] - lo, su = hi - th[j];
+            const double zlx = zl[j] * isl[j], zux = zu[j] * isu[j];
+            dzl[j] = uon ? fma(-zlx, dth[j], fma(mu, isl[j], -zl[j])) : 0.0;
+            dzu[j] = uon ? fma(zux, dth[j], fma(mu, isu[j], -zu[j])) : 0.0;
+            const double ith = frcp(dth[j]);
+            const double cand = dth[j] < 0 ? -tau * sl * ith : (dth[j] > 0 ? tau * su * ith : 1.0);
+            const double czl = dzl[j] < 0 ? -tau * zl[j] * frcp(dzl[j]) : 1.0;
+            const double czu = dzu[j] < 0 ? -tau * zu[j] * frcp(dzu[j]) : 1.0;
+            amax = fmin(amax, uon ? cand : 1.0);
+            az = fmin(az, uon ? fmin(czl, czu) : 1.0);
         }
-        amax = wmin(amax); az = wmin(az);
+        // f32 minima rounded down: tau <= 0.99 leaves far more slack than the f32 rounding
+        amax = (double)wminf((float)amax) * (1.0 - 1.0 / 1048576.0);
+        az = (double)wminf((float)az) * (1.0 - 1.0 / 1048576.0);
+        STAMP(4);
 
-        // -------- filter line search (Waechter & Biegler 2006, Alg. A) ----------
+        // -------- filter line search (Waechter & Biegler 2006, Alg. A) -------------
         double phil = 0.0, gtdl = 0.0;
 #pragma unroll
-        for (int ax = 0; ax < 2; ++ax) {
-            const Axis& A = X[ax];
-            if (xon) {
-                const double ep = A.p - A.rp, ev = A.v - A.rv;
-                phil += sc * (Qp * ep * ep + Qv * ev * ev);
-                gtdl += M.qp2 * ep * A.dp + M.qv2 * ev * A.dv;
-            }
-            if (uon) {
-                const double sl = A.th - lo, su = hi - A.th;
-                phil += sc * R * A.th * A.th - mu * (log(sl) + log(su));
-                gtdl += (M.r2 * A.th - mu / sl + mu / su) * A.dth;
-            }
+        for (int j = 0; j < NAX; ++j) {
+            const double ep = p[j] - rp[j], ev = v[j] - rv[j];
+            const double sl = th[j] - lo, su = hi - th[j];
+            phil += xon ? fma(scQp * ep, ep, scQv * ev * ev) : 0.0;
+            gtdl += xon ? fma(qp2 * ep, dp[j], qv2 * ev * dv[j]) : 0.0;
+            phil += uon ? fma(scR * th[j], th[j], -mu * log(sl * su)) : 0.0;
+            gtdl += uon ? rt[j] * dth[j] : 0.0;
         }
         const double phi = wsum(phil), gTd = wsum(gtdl);
+        // switching condition alpha (-gTd)^s_ph > delta theta^s_th, compared in log2 space
+        const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
+        const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
+        const float lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;    // log2(theta^s_th / (-gTd)^s_ph)
         double amin = gam_th;
-        if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta / (-gTd), pow(theta, s_th) / pow(-gTd, s_ph)));
+        if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta / (-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
         amin *= gam_al;
         double alpha = amax, th_t = 0.0, ph_t = 0.0;
         bool accepted = false, ftype = false;
-        for (int ls = 0; ls < 80; ++ls) {
+        STAMP(5);
+        int ls = 0;
+        for (; ls < 80; ++ls) {
             double thl = 0.0, phl = 0.0;
 #pragma unroll
-            for (int ax = 0; ax < 2; ++ax) {
-                const Axis& A = X[ax];
-                const double pt = A.p + alpha * A.dp, vt = A.v + alpha * A.dv, tt = A.th + alpha * A.dth;
-                const double s = uon ? sin(tt) : 0.0;
-                double g1, g2;
-                defects(M, k, A.sp, A.sv, pt, vt, s, g1, g2);
-                if (xon) {
-                    thl += fabs(g1) + fabs(g2);
-                    const double ep = pt - A.rp, ev = vt - A.rv;
-                    phl += sc * (Qp * ep * ep + Qv * ev * ev);
-                }
-                if (uon) phl += sc * R * tt * tt - mu * (log(tt - lo) + log(hi - tt));
+            for (int j = 0; j < NAX; ++j) {
+                const double pt = fma(alpha, dp[j], p[j]), vt = fma(alpha, dv[j], v[j]), tt = fma(alpha, dth[j], th[j]);
+                double s_, c_;
+                tilt_sincos(poly, tt, s_, c_);
+                double t1, t2;
+                defects(pt, vt, uon ? s_ : 0.0, sp[j], sv[j], t1, t2);
+                const double ep = pt - rp[j], ev = vt - rv[j];
+                thl += xon ? fabs(t1) + fabs(t2) : 0.0;
+                phl += xon ? fma(scQp * ep, ep, scQv * ev * ev) : 0.0;
+                phl += uon ? fma(scR * tt, tt, -mu * log((tt - lo) * (hi - tt))) : 0.0;
             }
             th_t = wsum(thl); ph_t = wsum(phl);
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
-            in_filter = in_filter || wany(k < nfilt && th_t >= fth && ph_t >= fph);
+            in_filter = in_filter || wany(lane < nfilt && th_t >= fth && ph_t >= fph);
             if (!in_filter) {
-                const bool sw = gTd < 0.0 && alpha * pow(-gTd, s_ph) > pow(theta, s_th);
+                const bool sw = gTd < 0.0 && lg2(alpha) > lg_sw;
                 if (theta <= th_min && sw) {
                     if (ph_t <= phi + eta_ph * alpha * gTd) { accepted = true; ftype = true; }
                 } else if (th_t <= (1 - gam_th) * theta || ph_t <= phi - gam_ph * theta) {
@@ -389,72 +485,112 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
             alpha *= 0.5;
             if (alpha < amin) break;
         }
+        STAMP_ADD(10, ls + 1);
+        STAMP(6);
         if (!accepted) { status = -2; break; }   // IPOPT would enter its restoration phase here
         if (!ftype && nfilt < kWave) {
-            if (k == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
+            if (lane == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
             ++nfilt;
         }
-        // -------- accept the step ------------------------------------------------
+        // -------- accept the step ----------------------------------------------------
 #pragma unroll
-        for (int ax = 0; ax < 2; ++ax) {
-            Axis& A = X[ax];
-            if (xon) {
-                A.p += alpha * A.dp; A.v += alpha * A.dv;
-                A.lp += alpha * A.dlp; A.lv += alpha * A.dlv;
-            }
-            if (uon) {
-                A.th += alpha * A.dth;
-                const double sl = A.th - lo, su = hi - A.th;
-                double zl = A.zl + az * A.dzl, zu = A.zu + az * A.dzu;
-                zl = fmax(fmin(zl, 1e10 * mu / sl), mu / (1e10 * sl));      // kappa_sigma = 1e10
-                zu = fmax(fmin(zu, 1e10 * mu / su), mu / (1e10 * su));
-                A.zl = zl; A.zu = zu;
-            }
+        for (int j = 0; j < NAX; ++j) {
+            p[j] = fma(alpha, dp[j], p[j]); v[j] = fma(alpha, dv[j], v[j]);
+            lp[j] = fma(alpha, dlp[j], lp[j]); lv[j] = fma(alpha, dlv[j], lv[j]);
+            th[j] = fma(alpha, dth[j], th[j]);
+            const double il = frcp(th[j] - lo), iu = frcp(hi - th[j]);
+            const double zln = fmax(fmin(fma(az, dzl[j], zl[j]), 1e10 * mu * il), 1e-10 * mu * il);   // kappa_sigma
+            const double zun = fmax(fmin(fma(az, dzu[j], zu[j]), 1e10 * mu * iu), 1e-10 * mu * iu);
+            zl[j] = uon ? zln : 0.0; zu[j] = uon ? zun : 0.0;
         }
         theta = th_t;
+        STAMP(7);
     }
 
-    // -------- outputs ---------------------------------------------------------
+    // -------- outputs ---------------------------------------------------------------
     // objective (mpc_3d.py:44-46, :63-66), unscaled
     double fl = 0.0;
 #pragma unroll
-    for (int ax = 0; ax < 2; ++ax) {
-        const Axis& A = X[ax];
-        if (xon) { const double ep = A.p - A.rp, ev = A.v - A.rv; fl += Qp * ep * ep + Qv * ev * ev; }
-        if (uon) fl += R * A.th * A.th;
+    for (int j = 0; j < NAX; ++j) {
+        const double ep = p[j] - rp[j], ev = v[j] - rv[j];
+        fl += xon ? Qp * ep * ep + Qv * ev * ev : 0.0;
+        fl += uon ? R * th[j] * th[j] : 0.0;
     }
     const double fval = wsum(fl);
-    if (k == 0) {
-        a.u0[2 * b] = X[0].th;
-        a.u0[2 * b + 1] = X[1].th;
+    // theta_x and theta_y of this lane's node
+    double tx, ty;
+    if (NAX == 1) {
+        const double other = __shfl_xor(th[0], 32);
+        tx = ax0 == 0 ? th[0] : other;
+        ty = ax0 == 0 ? other : th[0];
+    } else {
+        tx = th[0]; ty = th[NAX - 1];
+    }
+    if (lane == 0) {
+        a.u0[2 * b] = tx;
+        a.u0[2 * b + 1] = ty;
         a.f[b] = fval;
         a.status[b] = status;
         a.iters[b] = it;
     }
     if (a.w_out) {
         // z sub-state follows the final controls through the reference RK4 (mpc_3d.py:93-97, :99-104)
-        const double w = uon ? -a.g * (X[0].th * X[0].th + X[1].th * X[1].th) : 0.0;
+        const double w = uon ? -a.g * (tx * tx + ty * ty) : 0.0;
         double pz = st[4], vz = st[5];
         for (int step = 0; step < N; ++step) {
             double pzn, vzn;
             z_rk4(h, w, pz, vz, pzn, vzn);
             const double ip = from_prev(pzn), iv = from_prev(vzn);
-            if (k >= 1) { pz = ip; vz = iv; }
+            pz = k >= 1 ? ip : pz; vz = k >= 1 ? iv : vz;
         }
         double* wo = a.w_out + (size_t)nw * b;
-        if (xon) {
-            wo[6 * k + 0] = X[0].p; wo[6 * k + 1] = X[0].v;
-            wo[6 * k + 2] = X[1].p; wo[6 * k + 3] = X[1].v;
-            wo[6 * k + 4] = pz;     wo[6 * k + 5] = vz;
+#pragma unroll
+        for (int j = 0; j < NAX; ++j) {
+            const int ax = NAX == 1 ? ax0 : j;
+            if (xon) { wo[6 * k + 2 * ax] = p[j]; wo[6 * k + 2 * ax + 1] = v[j]; }
+            if (uon) wo[6 * (N + 1) + 2 * k + ax] = th[j];
         }
-        if (uon) { wo[6 * (N + 1) + 2 * k] = X[0].th; wo[6 * (N + 1) + 2 * k + 1] = X[1].th; }
+        if (xon && (NAX == 2 || ax0 == 0)) { wo[6 * k + 4] = pz; wo[6 * k + 5] = vz; }
     }
+    STAMP(8);
+    STAMP_FLUSH(b);
+}
+
+// self-test of the wave primitives: out[0..63] = from_next(lane), out[64..127] = from_prev(lane),
+// out[128] = wsum(lane), out[129] = wmax(lane), out[130] = wmin(lane + 1),
+// out[131..194] = relative error of the raw v_rcp_f64 on x_i = 1.37^(i-32)*pi (diagnostic)
+__global__ __launch_bounds__(kWave) void wave_selftest_kernel(double* out) {
+    const double x = (double)threadIdx.x;
+    const double n = from_next(x), p = from_prev(x);
+    const double s = wsum(x), mx = wmax(x), mn = wmin(x + 1.0);
+    out[threadIdx.x] = n;
+    out[64 + threadIdx.x] = p;
+    if (threadIdx.x == 0) { out[128] = s; out[129] = mx; out[130] = mn; }
+    const double y = 3.141592653589793 * pow(1.37, (double)threadIdx.x - 32.0);
+    out[131 + threadIdx.x] = fma(y, __builtin_amdgcn_rcp(y), -1.0);
 }
 
 }  // namespace dartmpc
 
 extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStream_t stream) {
     if (args->B <= 0) return hipSuccess;
-    hipLaunchKernelGGL(dartmpc::pmpc_ipm_kernel, dim3(args->B), dim3(dartmpc::kWave), 0, stream, *args);
+    if (args->N <= 31)
+        hipLaunchKernelGGL(dartmpc::pmpc_ipm_kernel<1>, dim3(args->B), dim3(dartmpc::kWave), 0, stream, *args);
+    else
+        hipLaunchKernelGGL(dartmpc::pmpc_ipm_kernel<2>, dim3(args->B), dim3(dartmpc::kWave), 0, stream, *args);
     return hipGetLastError();
 }
+
+// internal (not part of include/dart_mpc.h): runs the wave-primitive self-test into device buffer d_out[131]
+extern "C" hipError_t dartmpc_wave_selftest(double* d_out, hipStream_t stream) {
+    hipLaunchKernelGGL(dartmpc::wave_selftest_kernel, dim3(1), dim3(dartmpc::kWave), 0, stream, d_out);
+    return hipGetLastError();
+}
+
+#ifdef DART_STAMPS
+// diagnostic build only: per-phase s_memtime cycles of block 0 from the last launch
+extern "C" hipError_t dartmpc_read_stamps(unsigned long long* host_out) {
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp), sizeof(unsigned long long) * 12, 0,
+                               hipMemcpyDeviceToHost);
+}
+#endif

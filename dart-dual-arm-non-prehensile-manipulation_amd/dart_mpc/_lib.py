@@ -84,6 +84,18 @@ def lib():
     return L
 
 
+def wave_selftest():
+    """Run the internal wave-primitive self-test kernel (DPP shifts and reductions) on device 0."""
+    L = lib()
+    L.dartmpc_selftest.argtypes = [ctypes.c_void_p]
+    L.dartmpc_selftest.restype = ctypes.c_int
+    out = np.zeros(195)
+    rc = L.dartmpc_selftest(ctypes.c_void_p(out.ctypes.data))
+    if rc != 0:
+        raise DartMPCError(f"dartmpc_selftest failed ({rc})")
+    return out
+
+
 def default_config(**over) -> Config:
     c = Config()
     lib().dart_mpc_config_default(ctypes.byref(c))

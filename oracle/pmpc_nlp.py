@@ -175,7 +175,7 @@ def multipliers_from_state_rows(prob: PMPCProblem, w, p):
     return lam.reshape(-1)
 
 
-def kkt_certificate(prob: PMPCProblem, w, p, relax=1e-8):
+def kkt_certificate(prob: PMPCProblem, w, p, relax=1e-8, act_tol=1e-6):
     """Return a dict of KKT residuals for a candidate optimum ``w``.
 
     - primal: ||g(w)||_inf
@@ -184,6 +184,8 @@ def kkt_certificate(prob: PMPCProblem, w, p, relax=1e-8):
     - stat_sign: worst sign violation of grad_u L at active bounds
       (at the upper bound grad_u L <= 0, at the lower bound >= 0)
     - lam: the recovered equality multipliers
+    A control within ``act_tol`` of a bound counts as active (an interior-point
+    answer at tolerance tol sits mu/z inside a weakly active bound).
     """
     w = np.asarray(w, float)
     X, U = prob.unpack(w)
@@ -195,7 +197,6 @@ def kkt_certificate(prob: PMPCProblem, w, p, relax=1e-8):
     u = w[prob.nX:]
     lo = prob.u_lo - relax * max(1.0, abs(prob.u_lo))
     hi = prob.u_hi + relax * max(1.0, abs(prob.u_hi))
-    act_tol = 1e-6
     at_hi = u >= prob.u_hi - act_tol
     at_lo = u <= prob.u_lo + act_tol
     free = ~(at_hi | at_lo)

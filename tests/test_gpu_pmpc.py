@@ -82,7 +82,7 @@ def test_full_w_layout_and_kkt_certificate(dm, goldens):
             mu, qp, qv, r, lo, hi = G["prm"][i]
             prob = PMPCProblem(N=N, Ts=Ts, Qp=qp, Qv=qv, R=r, mu=mu, u_bounds=(lo, hi))
             p = np.concatenate([G["state"][i], G["target"][i]])
-            c = kkt_certificate(prob, out["w"][j], p)
+            c = kkt_certificate(prob, out["w"][j], p, act_tol=U_TOL)
             assert c["primal"] <= 1e-9, (i, c["primal"])
             assert c["bound"] == 0.0, i
             assert c["stat_free"] <= 1e-5 * max(1.0, c["grad_scale"]), (i, c["stat_free"])
@@ -93,18 +93,24 @@ def test_full_w_layout_and_kkt_certificate(dm, goldens):
 
 
 def test_c2_and_c4_batches_match_oracle(dm):
-    """C2 (18 configs) and C4 (18 x 64 seeds) against the C oracle on the full 6-state NLP."""
+    """C2 (18 configs) and C4 (18 x 64 seeds) against the C oracle on the full 6-state NLP.
+
+    At the reference tolerance (tol 1e-8) an interior-point answer sits up to
+    mu_final/z inside a weakly active bound; with z -> 0 (degenerate bound, seen
+    in C4) two such answers differ by up to ~1e-4 in u0 while their objectives
+    agree to 1e-7 relative.  At tol 1e-11 both are at the exact KKT point."""
     import oracle_lib
     from dart_mpc.workload import pmpc_batch
     for n_seeds in (1, 64):
         S, T, P = pmpc_batch(n_seeds)
-        s = dm.Solver(N=20, Ts=0.002, tol=1e-8, B_max=S.shape[0])
-        out = s.solve_batch(S, T, P)
-        s.close()
-        ref = oracle_lib.solve_batch(S, T, P, N=20, Ts=0.002, tol=1e-8, nthreads=8, want_w=False)
-        assert np.all(out["status"] == 0) and np.all(ref["status"] == 0)
-        assert np.max(np.abs(out["u0"] - ref["u0"])) <= U0_TOL
-        np.testing.assert_allclose(out["f"], ref["f"], rtol=1e-7, atol=1e-9)
+        for tol, utol in ((1e-8, 1e-4), (1e-11, 1e-6)):
+            s = dm.Solver(N=20, Ts=0.002, tol=tol, B_max=S.shape[0])
+            out = s.solve_batch(S, T, P)
+            s.close()
+            ref = oracle_lib.solve_batch(S, T, P, N=20, Ts=0.002, tol=tol, nthreads=8, want_w=False)
+            assert np.all(out["status"] == 0) and np.all(ref["status"] == 0)
+            assert np.max(np.abs(out["u0"] - ref["u0"])) <= utol, (n_seeds, tol)
+            np.testing.assert_allclose(out["f"], ref["f"], rtol=1e-7, atol=1e-9)
 
 
 def test_symmetry_and_rest_properties(dm):
@@ -129,12 +135,12 @@ def test_horizons_match_oracle(dm, N):
     import oracle_lib
     from dart_mpc.workload import pmpc_batch
     S, T, P = pmpc_batch(1)
-    s = dm.Solver(N=N, Ts=0.002, tol=1e-8, B_max=64)
+    s = dm.Solver(N=N, Ts=0.002, tol=1e-11, B_max=64)
     out = s.solve_batch(S, T, P)
     s.close()
-    ref = oracle_lib.solve_batch(S, T, P, N=N, Ts=0.002, tol=1e-8, nthreads=8, want_w=False)
+    ref = oracle_lib.solve_batch(S, T, P, N=N, Ts=0.002, tol=1e-11, nthreads=8, want_w=False)
     assert np.all(out["status"] == 0)
-    assert np.max(np.abs(out["u0"] - ref["u0"])) <= U0_TOL
+    assert np.max(np.abs(out["u0"] - ref["u0"])) <= 1e-6
 
 
 def test_warm_start_from_optimum(dm, goldens):
@@ -197,3 +203,14 @@ def test_worker_queue_protocol(dm):
     for i, (u, loss, t) in enumerate(replies):
         assert u.shape == (2,) and loss.shape == (1,) and t >= 0.0
         assert np.max(np.abs(u - ref["u0"][i])) <= U0_TOL
+
+
+def test_wave_primitives_selftest(dm):
+    """DPP wave shifts and row reductions used by the kernel (lane k <- k+1 / k-1, sums, max, min)."""
+    from dart_mpc import _lib
+    out = _lib.wave_selftest()
+    lanes = np.arange(64.0)
+    np.testing.assert_array_equal(out[:63], lanes[1:])        # from_next
+    np.testing.assert_array_equal(out[65:128], lanes[:63])    # from_prev
+    assert out[128] == lanes.sum() and out[129] == 63.0 and out[130] == 1.0
+    print("raw v_rcp_f64 max relative error:", np.max(np.abs(out[131:195])))
