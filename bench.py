@@ -18,6 +18,7 @@ full 6-state NLP), timed on rank 0 over a bounded sample.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -44,6 +45,7 @@ def parse():
     ap.add_argument("--tol", type=float, default=1e-8)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-calls", type=int, default=200, help="calls of the host-pointer (PCIe-inclusive) path")
     ap.add_argument("--saturation-batch", type=int, default=18 * 1024,
                     help="supplementary single-launch batch for the saturated rate (0 = skip)")
     return ap.parse_args()
@@ -124,7 +126,8 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_lib   # checker + CPU baseline only
         S, T, P = steps_in[W]
-        ref = oracle_lib.solve_batch(S, T, P, N=N, Ts=0.002, tol=args.tol, nthreads=1, want_w=False)
+        # u_ref = the exact KKT point (oracle driven to tol 1e-11 on the full 6-state NLP)
+        ref = oracle_lib.solve_batch(S, T, P, N=N, Ts=0.002, tol=1e-11, nthreads=1, want_w=False)
         max_du = float(np.max(np.abs(u0[0] - ref["u0"])))
         if not args.no_cpu_baseline:
             try:
@@ -164,6 +167,27 @@ def main():
         saturation = {"batch": Bs, "ms_per_launch": ms, "solves_per_s": Bs / (ms * 1e-3),
                       "ok_frac": float((ss == 0).float().mean()), "iters_mean": float(si.double().mean())}
 
+    # supplementary host-pointer path (dart_mpc_solve_batch): H2D copies + solve + D2H + sync per call
+    host_path = None
+    if rank == 0 and args.host_calls > 0:
+        hs = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=B, device=local)
+        S, T, P = steps_in[W]
+        for _ in range(5):
+            hs.solve_batch(S, T, P)
+        h0 = time.perf_counter()
+        for _ in range(args.host_calls):
+            hs.solve_batch(S, T, P)
+        hdt = (time.perf_counter() - h0) / args.host_calls
+        host_path = {"batch": B, "ms_per_call": hdt * 1e3, "solves_per_s": B / hdt}
+        hs.close()
+
+    # HBM traffic per launch from the committed rocprofv3 PMC passes of this build (tools/profile_round.sh)
+    traffic = None
+    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")))
+    if pmc:
+        with open(pmc[-1]) as fh:
+            traffic = json.load(fh).get("traffic_bytes_per_launch")
+
     if rank == 0:
         value = world * B * K / elapsed
         achieved_tflops = iters_sum_per_launch * F_ITER_PMPC / (kern_ms * 1e-3) / 1e12
@@ -184,15 +208,16 @@ def main():
                                    "N=20, Ts=0.002, cold start, IPOPT tol 1e-8; one rank per GPU",
                        "batch_per_gpu": B, "N": N, "parallelism": f"instance-sharded x{world}"},
             "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": None,
+                         "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "kernel": "pmpc_ipm_kernel", "kernel_ms": kern_ms,
                          "note": "FP64 compute roof (vector = matrix on gfx950); algorithmic FLOP = "
                                  "sum(iters) x 6.0e4; algorithmic HBM bytes = 176 per solve"},
             "cpu_baseline": cpu_baseline,
-            "max_abs_u0_err_vs_oracle": max_du,
+            "max_abs_u0_err_vs_exact_optimum": max_du,
             "status_ok_frac": ok_frac,
             "iters_mean": float(its.mean()),
             "saturation": saturation,
+            "host_path_pcie_inclusive": host_path,
         }
         print(json.dumps(line))
     if world > 1:
