@@ -46,9 +46,80 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-calls", type=int, default=200, help="calls of the host-pointer (PCIe-inclusive) path")
+    ap.add_argument("--rmpc-steps", type=int, default=200, help="launches of the supplementary C3 RMPC line (0 = skip)")
     ap.add_argument("--saturation-batch", type=int, default=18 * 1024,
                     help="supplementary single-launch batch for the saturated rate (0 = skip)")
     return ap.parse_args()
+
+
+def bench_rmpc(args, torch, dev, stream, dart_mpc):
+    """C3: RMPC batch=18 (N=20), fused RLS + warm-start-free solve per launch, inputs in HBM."""
+    from dart_mpc.workload import rmpc_batch
+    B, K, N = 18, args.rmpc_steps, 20
+    D = [rmpc_batch(1, seed0=9000 + i) for i in range(K + 5)]
+    T = lambda k, dt=torch.float64: torch.tensor(np.stack([d[k] for d in D]), dtype=dt, device=dev).contiguous()
+    X0, UP, TH, RR, PR, PP, PH, YY = (T("x0"), T("u_prev"), T("rls_theta"), T("Rref"), T("prm"), T("rls_P"),
+                                      T("phi_prev"), T("y"))
+    U0 = torch.empty((K + 5, B, 2), dtype=torch.float64, device=dev)
+    FV = torch.empty((K + 5, B), dtype=torch.float64, device=dev)
+    ST = torch.empty((K + 5, B), dtype=torch.int32, device=dev)
+    IT = torch.empty((K + 5, B), dtype=torch.int32, device=dev)
+    s = dart_mpc.RmpcSolver(N=N, tol=args.tol, B_max=B, device=dev.index)
+    sp = stream.cuda_stream
+
+    def launch(i):
+        s.solve_batch_dev(B, X0[i].data_ptr(), UP[i].data_ptr(), TH[i].data_ptr(), RR[i].data_ptr(), PR[i].data_ptr(),
+                          U0[i].data_ptr(), FV[i].data_ptr(), ST[i].data_ptr(), IT[i].data_ptr(),
+                          rls_P=PP[i].data_ptr(), rls_phi=PH[i].data_ptr(), rls_y=YY[i].data_ptr(), rls_lambda=0.995,
+                          stream=sp)
+
+    for i in range(5):
+        launch(i)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for j in range(K):
+            ev[j][0].record(stream)
+            launch(5 + j)
+            ev[j][1].record(stream)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    st, its = ST[5:].cpu().numpy(), IT[5:].cpu().numpy()
+    # accuracy on the first timed launch: the oracle with the same (host-updated) RLS estimate, tol 1e-11
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_lib   # checker + CPU baseline only
+    d = D[5]
+    th = np.zeros((B, 14))
+    for b in range(B):
+        for a in range(2):
+            th[b, 7 * a:7 * a + 7], _ = oracle_lib.rls_update(d["rls_theta"][b, 7 * a:7 * a + 7], d["rls_P"][b, a],
+                                                              d["phi_prev"][b], d["y"][b, a], 0.995)
+    ref = oracle_lib.rmpc_solve_batch(d["x0"], d["u_prev"], th, d["Rref"], d["prm"], N=N, tol=1e-11, max_iter=500,
+                                      nthreads=4, want_w=False)
+    max_du = float(np.max(np.abs(U0[5].cpu().numpy() - ref["u0"])))
+    out = {"workload": "C3: RMPC batch=18, N=20, Ts=0.002, RLS update (2 filters, p=7) fused, cold start, tol "
+                       f"{args.tol:g}", "solves_per_s": B * K / dt, "ms_per_step": dt / K * 1e3, "kernel_ms": kern_ms,
+           "status_ok_frac": float(np.mean(st == 0)), "iters_mean": float(its.mean()),
+           "max_abs_u0_err_vs_exact_optimum": max_du}
+    if not args.no_cpu_baseline:
+        try:
+            ncores = len(os.sched_getaffinity(0))
+        except AttributeError:
+            ncores = os.cpu_count() or 1
+        nt = max(1, min(16, ncores))
+        Db = rmpc_batch(max(1, nt // 2), seed0=4242)
+        solved, c0 = 0, time.perf_counter()
+        while time.perf_counter() - c0 < min(6.0, args.cpu_seconds):
+            oracle_lib.rmpc_solve_batch(Db["x0"], Db["u_prev"], Db["theta"], Db["Rref"], Db["prm"], N=N, tol=args.tol,
+                                        nthreads=nt, want_w=False)
+            solved += Db["x0"].shape[0]
+        cdt = time.perf_counter() - c0
+        out["cpu_baseline"] = {"value": solved / cdt, "unit": "solves/s", "cores": nt, "kind": "port",
+                               "sample": f"C oracle (oracle/rmpc_ipm.c), {solved} cold-start C3 solves in {cdt:.1f} s"}
+    s.close()
+    return out
 
 
 def main():
@@ -181,6 +252,11 @@ def main():
         host_path = {"batch": B, "ms_per_call": hdt * 1e3, "solves_per_s": B / hdt}
         hs.close()
 
+    # supplementary C3 (BASELINE.json configs[2]): RMPC batch=18 with the RLS update fused into the launch
+    rmpc = None
+    if rank == 0 and args.rmpc_steps > 0:
+        rmpc = bench_rmpc(args, torch, dev, stream, dart_mpc)
+
     # HBM traffic per launch from the committed rocprofv3 PMC passes of this build (tools/profile_round.sh)
     traffic = None
     pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")))
@@ -218,6 +294,7 @@ def main():
             "iters_mean": float(its.mean()),
             "saturation": saturation,
             "host_path_pcie_inclusive": host_path,
+            "rmpc_c3": rmpc,
         }
         print(json.dumps(line))
     if world > 1:

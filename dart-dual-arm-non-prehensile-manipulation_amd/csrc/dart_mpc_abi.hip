@@ -11,6 +11,7 @@
 
 #include "dart_mpc.h"
 #include "pmpc_ipm.h"
+#include "rmpc_ipm.h"
 
 struct dart_mpc_handle {
     dart_mpc_config cfg;
@@ -42,8 +43,8 @@ int fail(dart_mpc_handle* h, int code, const char* what, hipError_t e = hipSucce
 
 int check_cfg(const dart_mpc_config* c) {
     if (!c) return 0;
-    if (c->variant != DART_MPC_PMPC) return 0;
-    if (c->N < 1 || c->N > 63) return 0;
+    if (c->variant != DART_MPC_PMPC && c->variant != DART_MPC_RMPC) return 0;
+    if (c->N < 1 || c->N > (c->variant == DART_MPC_RMPC ? 31 : 63)) return 0;
     if (!(c->Ts > 0.0) || !(c->tol > 0.0) || !(c->gravity == c->gravity) || c->max_iter < 1 || c->B_max < 1) return 0;
     return 1;
 }
@@ -75,6 +76,8 @@ void dart_mpc_config_default(dart_mpc_config* c) {
 
 int dart_mpc_nw(int N) { return 6 * (N + 1) + 2 * N; }
 
+int dart_rmpc_nw(int N) { return 4 * (N + 1) + 2 * N; }
+
 int dart_mpc_abi_version(void) { return DART_MPC_ABI_VERSION; }
 
 int dart_mpc_create(const dart_mpc_config* cfg, int device, dart_mpc_handle** out) {
@@ -87,8 +90,14 @@ int dart_mpc_create(const dart_mpc_config* cfg, int device, dart_mpc_handle** ou
     h->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
-    const size_t B = (size_t)cfg->B_max, nw = (size_t)dart_mpc_nw(cfg->N);
-    h->nd = B * (6 + 6 + 6 + nw + 2 + 1 + nw);
+    const size_t B = (size_t)cfg->B_max;
+    if (cfg->variant == DART_MPC_RMPC) {
+        const size_t nw = (size_t)dart_rmpc_nw(cfg->N);
+        h->nd = B * (4 + 2 + 14 + 98 + 7 + 2 + 4 * (cfg->N + 1) + 10 + nw + 2 + 1 + nw);
+    } else {
+        const size_t nw = (size_t)dart_mpc_nw(cfg->N);
+        h->nd = B * (6 + 6 + 6 + nw + 2 + 1 + nw);
+    }
     h->ni = B * 2;
     if (e == hipSuccess) e = hipMalloc(&h->dbuf, h->nd * sizeof(double));
     if (e == hipSuccess) e = hipMalloc(&h->ibuf, h->ni * sizeof(int32_t));
@@ -104,6 +113,7 @@ int dart_mpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* x0, const 
                              const double* w_warm, double* u0, double* f, double* w_out, int32_t* status,
                              int32_t* iters, void* stream) {
     if (!h) return DART_MPC_EINVAL;
+    if (h->cfg.variant != DART_MPC_PMPC) return fail(h, DART_MPC_EINVAL, "handle is not a PMPC handle");
     if (B < 0 || (B > 0 && (!x0 || !ref || !prm || !u0 || !f || !status || !iters)))
         return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
     if (B == 0) return DART_MPC_OK;
@@ -116,6 +126,7 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
                          const double* w_warm, double* u0, double* f, double* w_out, int32_t* status,
                          int32_t* iters, void* stream) {
     if (!h) return DART_MPC_EINVAL;
+    if (h->cfg.variant != DART_MPC_PMPC) return fail(h, DART_MPC_EINVAL, "handle is not a PMPC handle");
     if (B < 0 || (B > 0 && (!x0 || !ref || !prm || !u0 || !f || !status || !iters)))
         return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
     if (B > h->cfg.B_max) return fail(h, DART_MPC_EINVAL, "batch larger than B_max");
@@ -145,6 +156,108 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     HIPCHK(h, hipMemcpyAsync(iters, d_it, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s), "copy iters");
     HIPCHK(h, hipStreamSynchronize(s), "hipStreamSynchronize");
     return DART_MPC_OK;
+}
+
+int dart_rmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* x0, const double* u_prev, double* theta,
+                              double* rls_P, const double* rls_phi, const double* rls_y, double rls_lambda,
+                              const double* Rref, const double* prm, const double* w_warm, double* u0, double* f,
+                              double* w_out, int32_t* status, int32_t* iters, void* stream) {
+    if (!h) return DART_MPC_EINVAL;
+    if (h->cfg.variant != DART_MPC_RMPC) return fail(h, DART_MPC_EINVAL, "handle is not an RMPC handle");
+    if (B < 0 || (B > 0 && (!x0 || !u_prev || !theta || !Rref || !prm || !u0 || !f || !status || !iters)))
+        return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
+    if (rls_P && (!rls_phi || !rls_y || !(rls_lambda > 0.0))) return fail(h, DART_MPC_EINVAL, "RLS inputs incomplete");
+    if (B == 0) return DART_MPC_OK;
+    HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    dartmpc::RmpcArgs a;
+    a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.g = h->cfg.gravity; a.max_iter = h->cfg.max_iter;
+    a.x0 = x0; a.u_prev = u_prev; a.theta = theta; a.rls_P = rls_P; a.rls_phi = rls_phi; a.rls_y = rls_y;
+    a.rls_lambda = rls_lambda; a.Rref = Rref; a.prm = prm; a.w_warm = w_warm;
+    a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
+    HIPCHK(h, dartmpc_launch_rmpc(&a, stream ? (hipStream_t)stream : h->stream), "kernel launch");
+    return DART_MPC_OK;
+}
+
+int dart_rmpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const double* u_prev, double* theta,
+                          double* rls_P, const double* rls_phi, const double* rls_y, double rls_lambda,
+                          const double* Rref, const double* prm, const double* w_warm, double* u0, double* f,
+                          double* w_out, int32_t* status, int32_t* iters, void* stream) {
+    if (!h) return DART_MPC_EINVAL;
+    if (h->cfg.variant != DART_MPC_RMPC) return fail(h, DART_MPC_EINVAL, "handle is not an RMPC handle");
+    if (B < 0 || (B > 0 && (!x0 || !u_prev || !theta || !Rref || !prm || !u0 || !f || !status || !iters)))
+        return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
+    if (rls_P && (!rls_phi || !rls_y || !(rls_lambda > 0.0))) return fail(h, DART_MPC_EINVAL, "RLS inputs incomplete");
+    if (B > h->cfg.B_max) return fail(h, DART_MPC_EINVAL, "batch larger than B_max");
+    if (B == 0) return DART_MPC_OK;
+    HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    const size_t N = (size_t)h->cfg.N, nw = (size_t)dart_rmpc_nw(h->cfg.N), Bm = (size_t)h->cfg.B_max;
+    double* p = h->dbuf;
+    double* d_x0 = p; p += Bm * 4;
+    double* d_up = p; p += Bm * 2;
+    double* d_th = p; p += Bm * 14;
+    double* d_P = p; p += Bm * 98;
+    double* d_phi = p; p += Bm * 7;
+    double* d_y = p; p += Bm * 2;
+    double* d_R = p; p += Bm * 4 * (N + 1);
+    double* d_prm = p; p += Bm * 10;
+    double* d_ww = p; p += Bm * nw;
+    double* d_u0 = p; p += Bm * 2;
+    double* d_f = p; p += Bm;
+    double* d_wo = p;
+    int32_t* d_st = h->ibuf;
+    int32_t* d_it = d_st + Bm;
+    auto up = [&](double* d, const double* hsrc, size_t n) { return hipMemcpyAsync(d, hsrc, sizeof(double) * n, hipMemcpyHostToDevice, s); };
+    HIPCHK(h, up(d_x0, x0, 4 * B), "copy x0");
+    HIPCHK(h, up(d_up, u_prev, 2 * B), "copy u_prev");
+    HIPCHK(h, up(d_th, theta, 14 * B), "copy theta");
+    if (rls_P) {
+        HIPCHK(h, up(d_P, rls_P, 98 * B), "copy rls_P");
+        HIPCHK(h, up(d_phi, rls_phi, 7 * B), "copy rls_phi");
+        HIPCHK(h, up(d_y, rls_y, 2 * B), "copy rls_y");
+    }
+    HIPCHK(h, up(d_R, Rref, 4 * (N + 1) * B), "copy Rref");
+    HIPCHK(h, up(d_prm, prm, 10 * B), "copy prm");
+    if (w_warm) HIPCHK(h, up(d_ww, w_warm, nw * B), "copy w_warm");
+    int rc = dart_rmpc_solve_batch_dev(h, B, d_x0, d_up, d_th, rls_P ? d_P : nullptr, d_phi, d_y, rls_lambda, d_R, d_prm,
+                                       w_warm ? d_ww : nullptr, d_u0, d_f, w_out ? d_wo : nullptr, d_st, d_it, s);
+    if (rc) return rc;
+    auto dn = [&](void* hdst, const void* d, size_t bytes) { return hipMemcpyAsync(hdst, d, bytes, hipMemcpyDeviceToHost, s); };
+    HIPCHK(h, dn(u0, d_u0, sizeof(double) * 2 * B), "copy u0");
+    HIPCHK(h, dn(f, d_f, sizeof(double) * B), "copy f");
+    if (w_out) HIPCHK(h, dn(w_out, d_wo, sizeof(double) * nw * B), "copy w_out");
+    if (rls_P) {
+        HIPCHK(h, dn(theta, d_th, sizeof(double) * 14 * B), "copy theta");
+        HIPCHK(h, dn(rls_P, d_P, sizeof(double) * 98 * B), "copy rls_P");
+    }
+    HIPCHK(h, dn(status, d_st, sizeof(int32_t) * B), "copy status");
+    HIPCHK(h, dn(iters, d_it, sizeof(int32_t) * B), "copy iters");
+    HIPCHK(h, hipStreamSynchronize(s), "hipStreamSynchronize");
+    return DART_MPC_OK;
+}
+
+int dart_rls_update_batch_dev(int B, double* theta, double* P, const double* phi, const double* y, double lambda,
+                              void* stream) {
+    if (B < 0 || (B > 0 && (!theta || !P || !phi || !y)) || !(lambda > 0.0)) return DART_MPC_EINVAL;
+    return dartmpc_launch_rls(B, theta, P, phi, y, lambda, (hipStream_t)stream) == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
+}
+
+int dart_rls_update_batch(int B, double* theta, double* P, const double* phi, const double* y, double lambda) {
+    if (B < 0 || (B > 0 && (!theta || !P || !phi || !y)) || !(lambda > 0.0)) return DART_MPC_EINVAL;
+    if (B == 0) return DART_MPC_OK;
+    double* d = nullptr;
+    const size_t n = (size_t)B * (7 + 49 + 7 + 1);
+    if (hipMalloc(&d, n * sizeof(double)) != hipSuccess) return DART_MPC_EHIP;
+    double *dt = d, *dP = dt + 7 * B, *dphi = dP + 49 * B, *dy = dphi + 7 * B;
+    hipError_t e = hipMemcpy(dt, theta, sizeof(double) * 7 * B, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dP, P, sizeof(double) * 49 * B, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dphi, phi, sizeof(double) * 7 * B, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dy, y, sizeof(double) * B, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = dartmpc_launch_rls(B, dt, dP, dphi, dy, lambda, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(theta, dt, sizeof(double) * 7 * B, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(P, dP, sizeof(double) * 49 * B, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return e == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
 }
 
 int dart_mpc_sync(dart_mpc_handle* h) {

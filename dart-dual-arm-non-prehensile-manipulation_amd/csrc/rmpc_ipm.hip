@@ -1,0 +1,722 @@
+// rmpc_ipm.hip -- batched RMPC (regressor NMPC + fused RLS update) interior-point solve, gfx950.
+//
+// Replaces AdaptiveNPMPCSmooth.solve (RMPC/dev_dual/controller/
+// np_mpc_adaptive_with_linear_regressor.py:212-222, NLP :35-168) and the per-step RLS
+// update of the driver (RMPC/dev_dual/rob_ctrl.py:335-343, RLS :10-30) for a batch of
+// independent instances.
+//
+// Model (np_mpc...:171-193): x = [px, vx, py, vy], u = [alpha, beta],
+//   ax = gz sin(alpha) + phi(x).theta_x,  ay = gz sin(beta) + phi(x).theta_y,
+//   phi = [px, vx, py, vy, tanh(vx/v_eps), tanh(vy/v_eps), 1],  RK4 with step Ts.
+// NLP rows (:103-127): defects; Delta-u in [du_lo, du_hi] (u_{-1} = u_prev); velocity caps
+// |vx|,|vy| <= vmax on nodes 0..N-1.  Cost (:129-140): staged reference, Ru |u|^2, Rdu |Du|^2.
+//
+// Method: IPOPT's primal-dual barrier method as in pmpc_ipm.hip (monotone mu, filter line search,
+// inertia correction, bound_relax 1e-8, gradient scaling), with IPOPT's slack formulation of the
+// inequality rows (g(w) - s = 0, bounds on s) eliminated per stage.  The Delta-u coupling is
+// carried by the augmented state x~_k = [x_k; u_{k-1}] (nx~ = 6).  Exact RK4 Jacobians (forward
+// mode, 6 directions); the dynamics part of the Lagrangian Hessian is the RK4-weighted average of
+// Ts * sum_i lambda_i f_i'' over the RK stages (error O(Ts^2) relative; it changes the Newton path
+// only, never the KKT point).
+//
+// Mapping: one wave64 per instance; lane k owns shooting node k (N <= 31) for everything that is
+// node-local (model evaluation, slacks, multipliers, line search); the node-coupled Riccati and
+// forward sweeps run through LDS with the lanes sharing each node's dense algebra (ocp_wave.h).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ocp_wave.h"
+#include "rmpc_ipm.h"
+#include "wave.h"
+
+namespace dartmpc {
+
+constexpr int RM_NMAXS = 32;      // max shooting nodes (N <= 31)
+constexpr int RM_NIQ = 6;         // inequality rows per node: du_x, du_y, vx-vmax, -vx-vmax, vy-vmax, -vy-vmax
+using RmLds = OcpLds<6, RM_NMAXS>;
+
+struct RmShared {
+    RmLds ocp;
+    double theta[14];
+    double rls_Pphi[2][7], rls_phiP[2][7];
+};
+
+struct RmModel {
+    double th[14];
+    double gz, h, ie;             // gravity, Ts, 1/v_eps
+};
+
+// continuous model (np_mpc...:178-186); also returns d f / d vx|vy of rows 1, 3 and tanh values
+__device__ __forceinline__ void rm_f(const RmModel& m, const double* y, double sa, double sb, double* f,
+                                     double& j1vx, double& j1vy, double& j3vx, double& j3vy, double& tx, double& ty) {
+    tx = tanh(y[1] * m.ie);
+    ty = tanh(y[3] * m.ie);
+    const double* a = m.th;
+    const double* c = m.th + 7;
+    f[0] = y[1];
+    f[2] = y[3];
+    f[1] = m.gz * sa + a[0] * y[0] + a[1] * y[1] + a[2] * y[2] + a[3] * y[3] + a[4] * tx + a[5] * ty + a[6];
+    f[3] = m.gz * sb + c[0] * y[0] + c[1] * y[1] + c[2] * y[2] + c[3] * y[3] + c[4] * tx + c[5] * ty + c[6];
+    const double dtx = (1.0 - tx * tx) * m.ie, dty = (1.0 - ty * ty) * m.ie;
+    j1vx = a[1] + a[4] * dtx; j1vy = a[3] + a[5] * dty;
+    j3vx = c[1] + c[4] * dtx; j3vy = c[3] + c[5] * dty;
+}
+
+// RK4 value (np_mpc...:188-193)
+__device__ __forceinline__ void rm_rk4(const RmModel& m, const double* x, double sa, double sb, double* xn) {
+    double k[4], y[4], acc[4], d0, d1, d2, d3, tx, ty;
+    rm_f(m, x, sa, sb, k, d0, d1, d2, d3, tx, ty);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { acc[i] = k[i]; y[i] = x[i] + m.h / 2 * k[i]; }
+    rm_f(m, y, sa, sb, k, d0, d1, d2, d3, tx, ty);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { acc[i] += 2 * k[i]; y[i] = x[i] + m.h / 2 * k[i]; }
+    rm_f(m, y, sa, sb, k, d0, d1, d2, d3, tx, ty);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { acc[i] += 2 * k[i]; y[i] = x[i] + m.h * k[i]; }
+    rm_f(m, y, sa, sb, k, d0, d1, d2, d3, tx, ty);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xn[i] = x[i] + m.h / 6 * (acc[i] + k[i]);
+}
+
+// RK4 value + exact Jacobian J = d x+ / d [px vx py vy alpha beta] (forward mode, 6 directions)
+// + the RK-weighted dynamics curvature diag (vx, vy, alpha, beta) contracted with -lambda_{k+1}.
+__device__ __forceinline__ void rm_rk4_jac(const RmModel& m, const double* x, double sa, double ca, double sb,
+                                           double cb, const double* lam, double* xn, double J[4][6],
+                                           double& hvx, double& hvy, double& haa, double& hbb) {
+    double yd[6][4], acc[6][4], k[4], y[4], kacc[4];
+#pragma unroll
+    for (int d = 0; d < 6; ++d)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { yd[d][i] = (i == d) ? 1.0 : 0.0; acc[d][i] = 0.0; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { y[i] = x[i]; kacc[i] = 0.0; }
+    const double wts[4] = {1.0, 2.0, 2.0, 1.0}, cst[4] = {0.5, 0.5, 1.0, 0.0};
+    hvx = 0.0; hvy = 0.0;
+    const double lx = lam[1], ly = lam[3];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        double j1vx, j1vy, j3vx, j3vy, tx, ty;
+        rm_f(m, y, sa, sb, k, j1vx, j1vy, j3vx, j3vy, tx, ty);
+        // curvature of f in vx, vy at this RK stage: T'' = -2 T (1 - T^2) / eps^2
+        const double t2x = -2.0 * tx * (1.0 - tx * tx) * m.ie * m.ie, t2y = -2.0 * ty * (1.0 - ty * ty) * m.ie * m.ie;
+        const double w = m.h * wts[s] / 6.0;
+        hvx -= w * (lx * m.th[4] + ly * m.th[11]) * t2x;
+        hvy -= w * (lx * m.th[5] + ly * m.th[12]) * t2y;
+#pragma unroll
+        for (int d = 0; d < 6; ++d) {
+            const double k0 = yd[d][1], k2 = yd[d][3];
+            const double k1 = m.th[0] * yd[d][0] + j1vx * yd[d][1] + m.th[2] * yd[d][2] + j1vy * yd[d][3] + (d == 4 ? m.gz * ca : 0.0);
+            const double k3 = m.th[7] * yd[d][0] + j3vx * yd[d][1] + m.th[9] * yd[d][2] + j3vy * yd[d][3] + (d == 5 ? m.gz * cb : 0.0);
+            acc[d][0] += wts[s] * k0; acc[d][1] += wts[s] * k1; acc[d][2] += wts[s] * k2; acc[d][3] += wts[s] * k3;
+            yd[d][0] = (d == 0 ? 1.0 : 0.0) + cst[s] * m.h * k0;
+            yd[d][1] = (d == 1 ? 1.0 : 0.0) + cst[s] * m.h * k1;
+            yd[d][2] = (d == 2 ? 1.0 : 0.0) + cst[s] * m.h * k2;
+            yd[d][3] = (d == 3 ? 1.0 : 0.0) + cst[s] * m.h * k3;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) kacc[i] += wts[s] * k[i];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = x[i] + cst[s] * m.h * k[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xn[i] = x[i] + m.h / 6 * kacc[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int d = 0; d < 6; ++d) J[i][d] = ((i == d) ? 1.0 : 0.0) + m.h / 6 * acc[d][i];
+    // alpha, beta: f'' = -gz sin, contracted with -lambda and Ts
+    haa = m.h * lx * m.gz * sa;
+    hbb = m.h * ly * m.gz * sb;
+}
+
+// z = [px vx py vy upx upy ux uy]: inequality row values C z (np_mpc...:114-127)
+__device__ __forceinline__ void rm_iq(const double* z, double vmax, double* c) {
+    c[0] = z[6] - z[4];
+    c[1] = z[7] - z[5];
+    c[2] = z[1] - vmax;
+    c[3] = -z[1] - vmax;
+    c[4] = z[3] - vmax;
+    c[5] = -z[3] - vmax;
+}
+
+__global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
+    __shared__ RmShared SH;
+    RmLds* S = &SH.ocp;
+    const int b = blockIdx.x;
+    const int k = threadIdx.x;
+    const int N = a.N;
+    const bool xon = k <= N, uon = k < N;
+    const double* pr = a.prm + 10 * b;
+    const double Qp = pr[0], Qv = pr[1], Ru = pr[2], Rdu = pr[3];
+    const double ulo = pr[4], uhi = pr[5], dulo = pr[6], duhi = pr[7], vmax = pr[8], veps = pr[9];
+
+    // ---------------- fused RLS update (np_mpc...:17-27, rob_ctrl.py:340-343) -----------------
+    if (a.rls_P) {
+        double* Pg = a.rls_P + 98 * b;
+        const double* ph = a.rls_phi + 7 * b;
+        const double lamr = a.rls_lambda;
+        if (k < 28) {
+            const int ax = (k % 14) / 7, i = k % 7;
+            double s = 0.0;
+            if (k < 14) { for (int j = 0; j < 7; ++j) s = fma(Pg[49 * ax + 7 * i + j], ph[j], s); SH.rls_Pphi[ax][i] = s; }
+            else { for (int j = 0; j < 7; ++j) s = fma(ph[j], Pg[49 * ax + 7 * j + i], s); SH.rls_phiP[ax][i] = s; }
+        }
+        __syncthreads();
+        double den[2], err[2];
+#pragma unroll
+        for (int ax = 0; ax < 2; ++ax) {
+            double dn = lamr, e = a.rls_y[2 * b + ax];
+            for (int i = 0; i < 7; ++i) { dn = fma(ph[i], SH.rls_Pphi[ax][i], dn); e = fma(-ph[i], a.theta[14 * b + 7 * ax + i], e); }
+            den[ax] = dn; err[ax] = e;
+        }
+        double pnew[2];
+        int idx[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int e = k + 64 * r;
+            idx[r] = e;
+            if (e < 98) {
+                const int ax = e / 49, i = (e % 49) / 7, j = e % 7;
+                const double Ki = SH.rls_Pphi[ax][i] / den[ax];
+                pnew[r] = (Pg[e] - Ki * SH.rls_phiP[ax][j]) / lamr;
+            }
+        }
+        double thn = 0.0;
+        if (k < 14) {
+            const int ax = k / 7, i = k % 7;
+            thn = a.theta[14 * b + k] + SH.rls_Pphi[ax][i] / den[ax] * err[ax];
+        }
+        __syncthreads();          // every lane has read P, theta before anyone writes
+#pragma unroll
+        for (int r = 0; r < 2; ++r) if (idx[r] < 98) Pg[idx[r]] = pnew[r];
+        if (k < 14) { a.theta[14 * b + k] = thn; SH.theta[k] = thn; }
+    } else if (k < 14) {
+        SH.theta[k] = a.theta[14 * b + k];
+    }
+    __syncthreads();
+
+    RmModel m;
+#pragma unroll
+    for (int i = 0; i < 14; ++i) m.th[i] = SH.theta[i];
+    m.gz = a.g; m.h = a.Ts; m.ie = 1.0 / veps;
+
+    const double lo = ulo - 1e-8 * fmax(1.0, fabs(ulo)), hi = uhi + 1e-8 * fmax(1.0, fabs(uhi));
+    double sL[RM_NIQ], sU[RM_NIQ];            // relaxed slack bounds (lower only on the du rows)
+    sL[0] = sL[1] = dulo - 1e-8 * fmax(1.0, fabs(dulo));
+    sU[0] = sU[1] = duhi + 1e-8 * fmax(1.0, fabs(duhi));
+#pragma unroll
+    for (int i = 2; i < RM_NIQ; ++i) { sL[i] = -1e300; sU[i] = 1e-8; }
+    const bool poly = fmax(fabs(lo), fabs(hi)) <= 1.0;
+
+    // ---------------- iterate (lane k = node k) -------------------------------------------------
+    const double* x0 = a.x0 + 4 * b;
+    const double* upv = a.u_prev + 2 * b;
+    const double* rr = a.Rref + 4 * (N + 1) * b + 4 * (xon ? k : 0);
+    const double r0 = rr[0], r1 = rr[1], r2 = rr[2], r3 = rr[3];
+    const int nw = 4 * (N + 1) + 2 * N;
+    const double* ww = a.w_warm ? a.w_warm + (size_t)nw * b : nullptr;
+    double x[4], up[2], u[2], lam[6], zl[2], zu[2], s[RM_NIQ], yq[RM_NIQ], vl[RM_NIQ], vu[RM_NIQ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = xon && ww ? ww[4 * k + i] : 0.0;   // reference warm start, zeros first call (:168)
+    const double pushl = fmin(1e-2 * fmax(1.0, fabs(lo)), 1e-2 * (hi - lo));
+    const double pushu = fmin(1e-2 * fmax(1.0, fabs(hi)), 1e-2 * (hi - lo));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        double t = uon && ww ? ww[4 * (N + 1) + 2 * k + j] : 0.0;
+        u[j] = uon ? fmin(fmax(t, lo + pushl), hi - pushu) : 0.0;
+        zl[j] = uon ? 1.0 : 0.0; zu[j] = uon ? 1.0 : 0.0;
+    }
+    {   // auxiliary copies up_k = u_{k-1}, up_0 = u_prev
+        const double p0 = from_prev(u[0]), p1 = from_prev(u[1]);
+        up[0] = k == 0 ? upv[0] : p0;
+        up[1] = k == 0 ? upv[1] : p1;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) lam[i] = 0.0;
+    {   // slacks: s = C z pushed into the relaxed bounds; multipliers 1
+        double z[8] = {x[0], x[1], x[2], x[3], up[0], up[1], u[0], u[1]}, c[RM_NIQ];
+        rm_iq(z, vmax, c);
+#pragma unroll
+        for (int i = 0; i < RM_NIQ; ++i) {
+            double v;
+            if (i < 2) {
+                const double pl = fmin(1e-2 * fmax(1.0, fabs(sL[i])), 1e-2 * (sU[i] - sL[i]));
+                const double pu = fmin(1e-2 * fmax(1.0, fabs(sU[i])), 1e-2 * (sU[i] - sL[i]));
+                v = fmin(fmax(c[i], sL[i] + pl), sU[i] - pu);
+            } else {
+                v = fmin(c[i], sU[i] - 1e-2 * fmax(1.0, fabs(sU[i])));
+            }
+            s[i] = uon ? v : 0.0;
+            yq[i] = 0.0;
+            vl[i] = uon && i < 2 ? 1.0 : 0.0;
+            vu[i] = uon ? 1.0 : 0.0;
+        }
+    }
+
+    // objective gradient at a node (np_mpc...:129-140), z-space, unscaled
+    auto cost_grad = [&](const double* xx, const double* uu, const double* pp, double* g) {
+        g[0] = 2 * Qp * (xx[0] - r0); g[1] = 2 * Qv * (xx[1] - r1);
+        g[2] = 2 * Qp * (xx[2] - r2); g[3] = 2 * Qv * (xx[3] - r3);
+        const double d0 = uu[0] - pp[0], d1 = uu[1] - pp[1];
+        g[4] = uon ? -2 * Rdu * d0 : 0.0; g[5] = uon ? -2 * Rdu * d1 : 0.0;
+        g[6] = uon ? 2 * Ru * uu[0] + 2 * Rdu * d0 : 0.0; g[7] = uon ? 2 * Ru * uu[1] + 2 * Rdu * d1 : 0.0;
+    };
+    auto cost_val = [&](const double* xx, const double* uu, const double* pp) {
+        double f = Qp * ((xx[0] - r0) * (xx[0] - r0) + (xx[2] - r2) * (xx[2] - r2)) +
+                   Qv * ((xx[1] - r1) * (xx[1] - r1) + (xx[3] - r3) * (xx[3] - r3));
+        const double d0 = uu[0] - pp[0], d1 = uu[1] - pp[1];
+        return xon ? f + (uon ? Ru * (uu[0] * uu[0] + uu[1] * uu[1]) + Rdu * (d0 * d0 + d1 * d1) : 0.0) : 0.0;
+    };
+    // incoming defect g_k of node k (6 rows: physical 4 + up copy 2) for a trial point
+    auto defects = [&](const double* xx, const double* pp, const double* uu, double* g) {
+        double sa, ca, sb, cb, xn[4];
+        tilt_sincos(poly, uu[0], sa, ca);
+        tilt_sincos(poly, uu[1], sb, cb);
+        rm_rk4(m, xx, sa, sb, xn);
+        double f[6];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f[i] = from_prev(xn[i]);
+        f[4] = from_prev(uu[0]); f[5] = from_prev(uu[1]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) g[i] = k == 0 ? xx[i] - x0[i] : xx[i] - f[i];
+        g[4] = k == 0 ? pp[0] - upv[0] : pp[0] - f[4];
+        g[5] = k == 0 ? pp[1] - upv[1] : pp[1] - f[5];
+    };
+
+    double gmax = 0.0;
+    {
+        double g[8];
+        cost_grad(x, u, up, g);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) gmax = fmax(gmax, xon ? fabs(g[i]) : 0.0);
+    }
+    gmax = wmax(gmax);
+    const double sc = gmax > 100.0 ? 100.0 / gmax : 1.0;
+    const double tol = a.tol, mu_min = tol / 10;
+    const double nA = 6.0 * (N + 1), nI = 6.0 * N, nb = 12.0 * N;
+    const double gam_th = 1e-5, gam_ph = 1e-8, s_th = 1.1, s_ph = 2.3, eta_ph = 1e-8, gam_al = 0.05;
+
+    double gdef[6];
+    double theta;
+    {
+        defects(x, up, u, gdef);
+        double zz[8] = {x[0], x[1], x[2], x[3], up[0], up[1], u[0], u[1]}, c[RM_NIQ], th0 = 0.0;
+        rm_iq(zz, vmax, c);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) th0 += xon ? fabs(gdef[i]) : 0.0;
+#pragma unroll
+        for (int i = 0; i < RM_NIQ; ++i) th0 += uon ? fabs(c[i] - s[i]) : 0.0;
+        theta = wsum(th0);
+    }
+    const double th_max = 1e4 * fmax(1.0, theta), th_min = 1e-4 * fmax(1.0, theta);
+    double fth = 0.0, fph = 0.0;
+    int nfilt = 0;
+    double mu = 0.1, delta_last = 0.0;
+    int status = -1, it = 0;
+
+    for (it = 0; it < a.max_iter; ++it) {
+        // ---------------- derivatives, residuals, optimality error ---------------------------
+        double sa, ca, sb, cb;
+        tilt_sincos(poly, u[0], sa, ca);
+        tilt_sincos(poly, u[1], sb, cb);
+        double lamn[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) { const double t = from_next(lam[i]); lamn[i] = uon ? t : 0.0; }
+        double xn[4], J[4][6], hvx, hvy, haa, hbb;
+        rm_rk4_jac(m, x, sa, ca, sb, cb, lamn, xn, J, hvx, hvy, haa, hbb);
+        double cdef[6];           // outgoing defect c_k = F(z_k) - x~_{k+1}
+        {
+            double nx_[6];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) nx_[i] = from_next(x[i]);
+            nx_[4] = from_next(up[0]); nx_[5] = from_next(up[1]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cdef[i] = xn[i] - nx_[i];
+            cdef[4] = u[0] - nx_[4]; cdef[5] = u[1] - nx_[5];
+        }
+        double gin[6];            // incoming defect g_k
+        {
+            double f[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) f[i] = from_prev(cdef[i]);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) gin[i] = -f[i];
+            if (k == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) gin[i] = x[i] - x0[i];
+                gin[4] = up[0] - upv[0]; gin[5] = up[1] - upv[1];
+            }
+        }
+        const double zz[8] = {x[0], x[1], x[2], x[3], up[0], up[1], u[0], u[1]};
+        double cz[RM_NIQ], rq[RM_NIQ], sig[RM_NIQ], psi[RM_NIQ];
+        rm_iq(zz, vmax, cz);
+#pragma unroll
+        for (int i = 0; i < RM_NIQ; ++i) {
+            rq[i] = uon ? cz[i] - s[i] : 0.0;
+            const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
+            sig[i] = uon ? (i < 2 ? vl[i] / dl : 0.0) + vu[i] / du_ : 0.0;
+            psi[i] = uon ? (i < 2 ? -mu / dl : 0.0) + mu / du_ : 0.0;
+        }
+        double gz_[8];
+        cost_grad(x, u, up, gz_);
+        double dinf = 0.0, pinf = 0.0, c0 = 0.0, cmin = 1e300, suml = 0.0, sumz = 0.0;
+        {
+            double gl[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gl[j] = sc * gz_[j];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) gl[i] += lam[i];
+            // - A~^T lam_{k+1} - B~^T lam_{k+1}
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) gl[j] -= J[r][j] * lamn[r];
+                gl[6] -= J[r][4] * lamn[r]; gl[7] -= J[r][5] * lamn[r];
+            }
+            gl[6] -= lamn[4]; gl[7] -= lamn[5];
+            // + C^T y
+            gl[6] += yq[0]; gl[4] -= yq[0]; gl[7] += yq[1]; gl[5] -= yq[1];
+            gl[1] += yq[2] - yq[3]; gl[3] += yq[4] - yq[5];
+            gl[6] += -zl[0] + zu[0]; gl[7] += -zl[1] + zu[1];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dinf = fmax(dinf, (j < 6 ? xon : uon) ? fabs(gl[j]) : 0.0);
+#pragma unroll
+            for (int i = 0; i < RM_NIQ; ++i) dinf = fmax(dinf, uon ? fabs(-yq[i] - vl[i] + vu[i]) : 0.0);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { pinf = fmax(pinf, xon ? fabs(gin[i]) : 0.0); suml += xon ? fabs(lam[i]) : 0.0; }
+#pragma unroll
+            for (int i = 0; i < RM_NIQ; ++i) {
+                pinf = fmax(pinf, fabs(rq[i]));
+                suml += fabs(yq[i]);
+                if (uon) {
+                    const double cu = vu[i] * (sU[i] - s[i]);
+                    c0 = fmax(c0, cu); cmin = fmin(cmin, cu); sumz += vu[i];
+                    if (i < 2) { const double cl = vl[i] * (s[i] - sL[i]); c0 = fmax(c0, cl); cmin = fmin(cmin, cl); sumz += vl[i]; }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) if (uon) {
+                const double cl = zl[j] * (u[j] - lo), cu = zu[j] * (hi - u[j]);
+                c0 = fmax(c0, fmax(cl, cu)); cmin = fmin(cmin, fmin(cl, cu)); sumz += zl[j] + zu[j];
+            }
+        }
+        dinf = wmaxf((float)dinf); pinf = wmaxf((float)pinf); c0 = wmaxf((float)c0);
+        const double cminw = wminf((float)cmin);
+        suml = wsumf((float)suml); sumz = wsumf((float)sumz);
+        const double s_d = fmax(100.0, (suml + sumz) / (nA + nI + nb)) / 100.0;
+        const double s_c = fmax(100.0, sumz / nb) / 100.0;
+        if (fmax(dinf / s_d, fmax(pinf, c0 / s_c)) <= tol) { status = 0; break; }
+        for (;;) {
+            const double cmu = fmax(c0 - mu, mu - cminw);
+            if (fmax(dinf / s_d, fmax(pinf, cmu / s_c)) > 10.0 * mu || mu <= mu_min) break;
+            mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
+            nfilt = 0;
+#pragma unroll
+            for (int i = 0; i < RM_NIQ; ++i) {
+                const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
+                psi[i] = uon ? (i < 2 ? -mu / dl : 0.0) + mu / du_ : 0.0;
+            }
+        }
+        const double tau = fmax(0.99, 1.0 - mu);
+
+        // ---------------- stage QPs into LDS ---------------------------------------------------
+        const double isl0 = uon ? frcp(u[0] - lo) : 0.0, isl1 = uon ? frcp(u[1] - lo) : 0.0;
+        const double isu0 = uon ? frcp(hi - u[0]) : 0.0, isu1 = uon ? frcp(hi - u[1]) : 0.0;
+        {
+            // gradient column (index 8): scaled cost + box barrier + C^T (Sigma r + psi)
+            double gq[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gq[j] = sc * gz_[j];
+            if (uon) {
+                gq[6] += -mu * isl0 + mu * isu0; gq[7] += -mu * isl1 + mu * isu1;
+                const double t0 = sig[0] * rq[0] + psi[0], t1 = sig[1] * rq[1] + psi[1];
+                gq[6] += t0; gq[4] -= t0; gq[7] += t1; gq[5] -= t1;
+                gq[1] += (sig[2] * rq[2] + psi[2]) - (sig[3] * rq[3] + psi[3]);
+                gq[3] += (sig[4] * rq[4] + psi[4]) - (sig[5] * rq[5] + psi[5]);
+                double* Hk = S->H[k];
+                for (int e = 0; e < tri(9); ++e) Hk[e] = 0.0;
+                Hk[hp(0, 0)] = sc * 2 * Qp; Hk[hp(2, 2)] = sc * 2 * Qp;
+                Hk[hp(1, 1)] = sc * 2 * Qv + hvx + sig[2] + sig[3];
+                Hk[hp(3, 3)] = sc * 2 * Qv + hvy + sig[4] + sig[5];
+                Hk[hp(6, 6)] = sc * 2 * (Ru + Rdu) + haa + zl[0] * isl0 + zu[0] * isu0 + sig[0];
+                Hk[hp(7, 7)] = sc * 2 * (Ru + Rdu) + hbb + zl[1] * isl1 + zu[1] * isu1 + sig[1];
+                Hk[hp(4, 4)] = sc * 2 * Rdu + sig[0]; Hk[hp(5, 5)] = sc * 2 * Rdu + sig[1];
+                Hk[hp(6, 4)] = -sc * 2 * Rdu - sig[0]; Hk[hp(7, 5)] = -sc * 2 * Rdu - sig[1];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) Hk[hp(8, j)] = gq[j];
+                // M~ columns: x (0..3), up (4,5), u (6,7), 1 (8); rows x~ (0..5), 1 (6)
+                for (int j = 0; j < 9; ++j)
+                    for (int r = 0; r < 7; ++r) S->M[k][j][r] = 0.0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) S->M[k][j][r] = J[r][j];
+                    S->M[k][6][r] = J[r][4]; S->M[k][7][r] = J[r][5];
+                }
+                S->M[k][6][4] = 1.0; S->M[k][7][5] = 1.0;
+#pragma unroll
+                for (int r = 0; r < 6; ++r) S->M[k][8][r] = cdef[r];
+                S->M[k][8][6] = 1.0;
+            }
+            if (k == N) {   // terminal value function [[Q_N, q_N], [q_N^T, 0]]
+                for (int e = 0; e < tri(7); ++e) S->P[N][e] = 0.0;
+                S->P[N][hp(0, 0)] = sc * 2 * Qp; S->P[N][hp(2, 2)] = sc * 2 * Qp;
+                S->P[N][hp(1, 1)] = sc * 2 * Qv; S->P[N][hp(3, 3)] = sc * 2 * Qv;
+#pragma unroll
+                for (int j = 0; j < 6; ++j) S->P[N][hp(6, j)] = gq[j];
+            }
+        }
+        __syncthreads();
+
+        // ---------------- Newton step: Riccati with inertia correction -----------------------
+        double delta = 0.0, dapplied = 0.0;
+        bool ok = riccati_sweep(S, N);
+        for (int attempt = 1; attempt < 60 && !ok; ++attempt) {
+            delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last / 3.0))
+                                   : delta * (delta_last == 0.0 ? 100.0 : 8.0);
+            const double dd = delta - dapplied;
+            if (uon) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) S->H[k][hp(j, j)] += dd;
+            }
+            if (k == N) {
+                // restore the terminal P (the sweep does not overwrite P[N]) and add delta on x~
+#pragma unroll
+                for (int j = 0; j < 6; ++j) S->P[N][hp(j, j)] += dd;
+            }
+            dapplied = delta;
+            __syncthreads();
+            ok = riccati_sweep(S, N);
+        }
+        if (!ok) { status = -3; break; }
+        if (delta > 0.0) delta_last = delta;
+        if (k == 0) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) S->dz[0][i] = -gin[i];
+        }
+        __syncthreads();
+        forward_sweep(S, N);
+
+        double dx[6], dU[2], lamp[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) dx[i] = S->dz[xon ? k : 0][i];
+        dU[0] = uon ? S->dz[k][6] : 0.0; dU[1] = uon ? S->dz[k][7] : 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            double t = S->P[xon ? k : 0][hp(i, 6)];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) t = fma(S->P[xon ? k : 0][hp(i, j)], dx[j], t);
+            lamp[i] = -t;
+        }
+        // slack and multiplier steps
+        double dS[RM_NIQ], dY[RM_NIQ], dvl[RM_NIQ], dvu[RM_NIQ], dzl[2], dzu[2];
+        {
+            const double dzv[8] = {dx[0], dx[1], dx[2], dx[3], dx[4], dx[5], dU[0], dU[1]};
+            double cdz[RM_NIQ];
+            rm_iq(dzv, 0.0, cdz);
+#pragma unroll
+            for (int i = 0; i < RM_NIQ; ++i) {
+                dS[i] = uon ? cdz[i] + rq[i] : 0.0;
+                dY[i] = uon ? sig[i] * dS[i] + psi[i] - yq[i] : 0.0;
+                const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
+                dvl[i] = uon && i < 2 ? mu / dl - vl[i] - vl[i] / dl * dS[i] : 0.0;
+                dvu[i] = uon ? mu / du_ - vu[i] + vu[i] / du_ * dS[i] : 0.0;
+            }
+            dzl[0] = uon ? mu * isl0 - zl[0] - zl[0] * isl0 * dU[0] : 0.0;
+            dzl[1] = uon ? mu * isl1 - zl[1] - zl[1] * isl1 * dU[1] : 0.0;
+            dzu[0] = uon ? mu * isu0 - zu[0] + zu[0] * isu0 * dU[0] : 0.0;
+            dzu[1] = uon ? mu * isu1 - zu[1] + zu[1] * isu1 * dU[1] : 0.0;
+        }
+        double amax = 1.0, az = 1.0;
+        if (uon) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (dU[j] < 0) amax = fmin(amax, -tau * (u[j] - lo) / dU[j]);
+                if (dU[j] > 0) amax = fmin(amax, tau * (hi - u[j]) / dU[j]);
+                if (dzl[j] < 0) az = fmin(az, -tau * zl[j] / dzl[j]);
+                if (dzu[j] < 0) az = fmin(az, -tau * zu[j] / dzu[j]);
+            }
+#pragma unroll
+            for (int i = 0; i < RM_NIQ; ++i) {
+                if (i < 2 && dS[i] < 0) amax = fmin(amax, -tau * (s[i] - sL[i]) / dS[i]);
+                if (dS[i] > 0) amax = fmin(amax, tau * (sU[i] - s[i]) / dS[i]);
+                if (i < 2 && dvl[i] < 0) az = fmin(az, -tau * vl[i] / dvl[i]);
+                if (dvu[i] < 0) az = fmin(az, -tau * vu[i] / dvu[i]);
+            }
+        }
+        amax = (double)wminf((float)amax) * (1.0 - 1.0 / 1048576.0);
+        az = (double)wminf((float)az) * (1.0 - 1.0 / 1048576.0);
+
+        // ---------------- filter line search -------------------------------------------------
+        auto barrier_args = [&](const double* uu, const double* ss) {
+            double pa = 1.0;
+            if (uon) {
+                pa = (uu[0] - lo) * (hi - uu[0]) * (uu[1] - lo) * (hi - uu[1]);
+                pa *= (ss[0] - sL[0]) * (sU[0] - ss[0]) * (ss[1] - sL[1]) * (sU[1] - ss[1]);
+#pragma unroll
+                for (int i = 2; i < RM_NIQ; ++i) pa *= sU[i] - ss[i];
+            }
+            return pa;
+        };
+        double phil = sc * cost_val(x, u, up), gtdl = 0.0;
+        {
+            const double pa = barrier_args(u, s);
+            phil -= uon ? mu * log(pa) : 0.0;
+            double gq[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gq[j] = sc * gz_[j];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) gtdl += xon ? gq[i] * dx[i] : 0.0;
+            if (uon) {
+                gtdl += (gq[6] - mu * isl0 + mu * isu0) * dU[0] + (gq[7] - mu * isl1 + mu * isu1) * dU[1];
+#pragma unroll
+                for (int i = 0; i < RM_NIQ; ++i) gtdl += psi[i] * dS[i];
+            }
+        }
+        const double phi = wsum(phil), gTd = wsum(gtdl);
+        const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
+        const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
+        const float lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;
+        double amin = gam_th;
+        if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta / (-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
+        amin *= gam_al;
+        double alpha = amax, th_t = 0.0, ph_t = 0.0;
+        bool accepted = false, ftype = false;
+        // IPOPT's tiny-step test: max |d|/(1+|x|) < 10 eps_mach accepts the full step unfiltered
+        float tnl = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            tnl = fmaxf(tnl, xon ? fabsf((float)dx[i]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)x[i])) : 0.0f);
+        if (uon) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) tnl = fmaxf(tnl, fabsf((float)dU[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)u[j])));
+#pragma unroll
+            for (int i = 0; i < RM_NIQ; ++i) tnl = fmaxf(tnl, fabsf((float)dS[i]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)s[i])));
+        }
+        const bool tiny = wmaxf(tnl) < 2.2e-15f;
+        for (int ls = 0; ls < 80; ++ls) {
+            double xt[4], pt[2], ut[2], st_[RM_NIQ], gt[6];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xt[i] = fma(alpha, dx[i], x[i]);
+            pt[0] = fma(alpha, dx[4], up[0]); pt[1] = fma(alpha, dx[5], up[1]);
+            ut[0] = fma(alpha, dU[0], u[0]); ut[1] = fma(alpha, dU[1], u[1]);
+#pragma unroll
+            for (int i = 0; i < RM_NIQ; ++i) st_[i] = fma(alpha, dS[i], s[i]);
+            defects(xt, pt, ut, gt);
+            double zt[8] = {xt[0], xt[1], xt[2], xt[3], pt[0], pt[1], ut[0], ut[1]}, ct[RM_NIQ];
+            rm_iq(zt, vmax, ct);
+            double thl = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) thl += xon ? fabs(gt[i]) : 0.0;
+#pragma unroll
+            for (int i = 0; i < RM_NIQ; ++i) thl += uon ? fabs(ct[i] - st_[i]) : 0.0;
+            double phl = sc * cost_val(xt, ut, pt);
+            phl -= uon ? mu * log(barrier_args(ut, st_)) : 0.0;
+            th_t = wsum(thl); ph_t = wsum(phl);
+            if (tiny) { accepted = true; ftype = true; break; }
+            bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
+            in_filter = in_filter || wany(k < nfilt && th_t >= fth && ph_t >= fph);
+            if (!in_filter) {
+                const bool sw = gTd < 0.0 && lg2(alpha) > lg_sw;
+                if (theta <= th_min && sw) {
+                    if (cmp_le(ph_t, phi + eta_ph * alpha * gTd, phi)) { accepted = true; ftype = true; }
+                } else if (cmp_le(th_t, (1 - gam_th) * theta, theta) || cmp_le(ph_t - phi, -gam_ph * theta, phi)) {
+                    accepted = true;
+                }
+            }
+            if (accepted) break;
+            alpha *= 0.5;
+            if (alpha < amin) break;
+        }
+        if (!accepted) { status = -2; break; }
+        if (!ftype && nfilt < kWave) {
+            if (k == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
+            ++nfilt;
+        }
+        // ---------------- accept ------------------------------------------------------------
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = xon ? fma(alpha, dx[i], x[i]) : x[i];
+        up[0] = xon ? fma(alpha, dx[4], up[0]) : up[0];
+        up[1] = xon ? fma(alpha, dx[5], up[1]) : up[1];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) lam[i] = xon ? fma(alpha, lamp[i] - lam[i], lam[i]) : 0.0;
+        if (uon) {
+            u[0] = fma(alpha, dU[0], u[0]); u[1] = fma(alpha, dU[1], u[1]);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const double il = frcp(u[j] - lo), iu = frcp(hi - u[j]);
+                zl[j] = fmax(fmin(fma(az, dzl[j], zl[j]), 1e10 * mu * il), 1e-10 * mu * il);
+                zu[j] = fmax(fmin(fma(az, dzu[j], zu[j]), 1e10 * mu * iu), 1e-10 * mu * iu);
+            }
+#pragma unroll
+            for (int i = 0; i < RM_NIQ; ++i) {
+                s[i] = fma(alpha, dS[i], s[i]);
+                yq[i] = fma(alpha, dY[i], yq[i]);
+                const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
+                if (i < 2) vl[i] = fmax(fmin(fma(az, dvl[i], vl[i]), 1e10 * mu / dl), mu / (1e10 * dl));
+                vu[i] = fmax(fmin(fma(az, dvu[i], vu[i]), 1e10 * mu / du_), mu / (1e10 * du_));
+            }
+        }
+        theta = th_t;
+    }
+
+    // ---------------- outputs -------------------------------------------------------------
+    const double fval = wsum(cost_val(x, u, up));
+    if (k == 0) {
+        a.u0[2 * b] = u[0]; a.u0[2 * b + 1] = u[1];
+        a.f[b] = fval; a.status[b] = status; a.iters[b] = it;
+    }
+    if (a.w_out) {
+        double* wo = a.w_out + (size_t)nw * b;
+        if (xon) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) wo[4 * k + i] = x[i];
+        }
+        if (uon) { wo[4 * (N + 1) + 2 * k] = u[0]; wo[4 * (N + 1) + 2 * k + 1] = u[1]; }
+    }
+}
+
+// Standalone batched RLS.update (np_mpc...:17-27): one p = 7 filter per workgroup, lanes as entries.
+__global__ __launch_bounds__(kWave) void rls_update_kernel(int B, double* theta, double* P, const double* phi,
+                                                          const double* y, double lam) {
+    __shared__ double Pphi[7], phiP[7], ph[7], th[7];
+    const int b = blockIdx.x, l = threadIdx.x;
+    double* Pb = P + 49 * b;
+    if (l < 7) { ph[l] = phi[7 * b + l]; th[l] = theta[7 * b + l]; }
+    __syncthreads();
+    if (l < 7) {
+        double s = 0.0;
+        for (int j = 0; j < 7; ++j) s = fma(Pb[7 * l + j], ph[j], s);
+        Pphi[l] = s;
+    } else if (l < 14) {
+        const int i = l - 7;
+        double s = 0.0;
+        for (int j = 0; j < 7; ++j) s = fma(ph[j], Pb[7 * j + i], s);
+        phiP[i] = s;
+    }
+    __syncthreads();
+    double den = lam, err = y[b];
+    for (int i = 0; i < 7; ++i) { den = fma(ph[i], Pphi[i], den); err = fma(-ph[i], th[i], err); }
+    double pn = 0.0;
+    if (l < 49) pn = (Pb[l] - Pphi[l / 7] / den * phiP[l % 7]) / lam;
+    __syncthreads();
+    if (l < 49) Pb[l] = pn;
+    if (l < 7) theta[7 * b + l] = th[l] + Pphi[l] / den * err;
+}
+
+}  // namespace dartmpc
+
+extern "C" hipError_t dartmpc_launch_rls(int B, double* theta, double* P, const double* phi, const double* y,
+                                         double lam, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(dartmpc::rls_update_kernel, dim3(B), dim3(dartmpc::kWave), 0, stream, B, theta, P, phi, y, lam);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStream_t stream) {
+    if (args->B <= 0) return hipSuccess;
+    if (args->N < 1 || args->N >= dartmpc::RM_NMAXS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel, dim3(args->B), dim3(dartmpc::kWave), 0, stream, *args);
+    return hipGetLastError();
+}

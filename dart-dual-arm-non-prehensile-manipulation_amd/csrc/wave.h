@@ -1,0 +1,126 @@
+// wave.h -- wave64 primitives for gfx950 shared by the solver kernels: DPP lane shifts,
+// DPP row reductions, fast reciprocal, cheap log2 and small-angle sin/cos.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace dartmpc {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------------------
+// wave primitives (every call site is at wave-uniform control flow: EXEC full)
+// ---------------------------------------------------------------------------
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ double dpp(double x) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+    const int lo = (int)(unsigned)(b & 0xffffffffu), hi = (int)(unsigned)(b >> 32);
+    const int rlo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWMASK, 0xf, false);
+    const int rhi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWMASK, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)rhi << 32) | (unsigned)rlo);
+}
+__device__ __forceinline__ double readlane(double x, int l) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)(b & 0xffffffffu), l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+constexpr int kWaveShl1 = 0x130;   // lane k <- lane k+1
+constexpr int kWaveShr1 = 0x138;   // lane k <- lane k-1
+__device__ __forceinline__ double from_next(double x) { return dpp<kWaveShl1>(x); }
+__device__ __forceinline__ double from_prev(double x) { return dpp<kWaveShr1>(x); }
+
+struct OpSum { __device__ double operator()(double a, double b) const { return a + b; } };
+struct OpMax { __device__ double operator()(double a, double b) const { return fmax(a, b); } };
+struct OpMin { __device__ double operator()(double a, double b) const { return fmin(a, b); } };
+
+// row reduction by quad_perm + row_ror, then the four row totals by readlane: uniform result
+template <class Op>
+__device__ __forceinline__ double wreduce(double x, Op op) {
+    x = op(x, dpp<0xB1>(x));     // quad_perm [1,0,3,2]
+    x = op(x, dpp<0x4E>(x));     // quad_perm [2,3,0,1]
+    x = op(x, dpp<0x124>(x));    // row_ror:4
+    x = op(x, dpp<0x128>(x));    // row_ror:8
+    return op(op(readlane(x, 0), readlane(x, 16)), op(readlane(x, 32), readlane(x, 48)));
+}
+// f32 variant for error measures, scalings and step-length minima (half the DPP traffic):
+// their consumers only compare against tolerances or fractions-to-the-boundary with >= 1 % slack
+template <int CTRL>
+__device__ __forceinline__ float dppf(float x) {
+    const int r = __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(float, r);
+}
+__device__ __forceinline__ float readlanef(float x, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+template <class Op>
+__device__ __forceinline__ float wreducef(float x, Op op) {
+    x = op(x, dppf<0xB1>(x));
+    x = op(x, dppf<0x4E>(x));
+    x = op(x, dppf<0x124>(x));
+    x = op(x, dppf<0x128>(x));
+    return op(op(readlanef(x, 0), readlanef(x, 16)), op(readlanef(x, 32), readlanef(x, 48)));
+}
+struct OpSumF { __device__ float operator()(float a, float b) const { return a + b; } };
+struct OpMaxF { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
+struct OpMinF { __device__ float operator()(float a, float b) const { return fminf(a, b); } };
+__device__ __forceinline__ float wsumf(float x) { return wreducef(x, OpSumF()); }
+__device__ __forceinline__ float wmaxf(float x) { return wreducef(x, OpMaxF()); }
+__device__ __forceinline__ float wminf(float x) { return wreducef(x, OpMinF()); }
+
+__device__ __forceinline__ double wsum(double x) { return wreduce(x, OpSum()); }
+__device__ __forceinline__ double wmax(double x) { return wreduce(x, OpMax()); }
+__device__ __forceinline__ double wmin(double x) { return wreduce(x, OpMin()); }
+__device__ __forceinline__ bool wany(bool p) { return __ballot(p) != 0ull; }
+
+// reciprocal: v_rcp_f64 (measured max relative error 2e-8 on gfx950, tests/test_gpu_pmpc.py
+// selftest) + one Newton step -> ~4e-16 relative; operands are well scaled, no denormals
+__device__ __forceinline__ double frcp(double x) {
+    const double r = __builtin_amdgcn_rcp(x);
+    return fma(r, fma(-x, r, 1.0), r);
+}
+
+// log2 of a positive double to ~1e-7 relative: exponent + f32 log2 of the mantissa.  Used only in
+// the filter's switching condition / minimum step heuristics, never in a quantity that is solved for.
+__device__ __forceinline__ float lg2(double x) {
+    const int e = __builtin_amdgcn_frexp_exp(x);
+    const float m = (float)__builtin_amdgcn_frexp_mant(x);
+    return (float)e + __builtin_amdgcn_logf(m);
+}
+
+// sin/cos for |x| <= 1.0 (bound-relaxed tilt range) by Taylor series to x^19 / x^20:
+// truncation < 2e-20, i.e. below fp64 rounding.  Wider boxes fall back to ocml sincos.
+__device__ __forceinline__ void sincos_small(double x, double& s, double& c) {
+    const double y = x * x;
+    double ps = -1.0 / 121645100408832000.0;                 // -1/19!
+    ps = fma(ps, y, 1.0 / 355687428096000.0);                // 1/17!
+    ps = fma(ps, y, -1.0 / 1307674368000.0);                 // -1/15!
+    ps = fma(ps, y, 1.0 / 6227020800.0);                     // 1/13!
+    ps = fma(ps, y, -1.0 / 39916800.0);                      // -1/11!
+    ps = fma(ps, y, 1.0 / 362880.0);                         // 1/9!
+    ps = fma(ps, y, -1.0 / 5040.0);                          // -1/7!
+    ps = fma(ps, y, 1.0 / 120.0);                            // 1/5!
+    ps = fma(ps, y, -1.0 / 6.0);                             // -1/3!
+    s = fma(x * y, ps, x);
+    double pc = 1.0 / 2432902008176640000.0;                 // 1/20!
+    pc = fma(pc, y, -1.0 / 6402373705728000.0);              // -1/18!
+    pc = fma(pc, y, 1.0 / 20922789888000.0);                 // 1/16!
+    pc = fma(pc, y, -1.0 / 87178291200.0);                   // -1/14!
+    pc = fma(pc, y, 1.0 / 479001600.0);                      // 1/12!
+    pc = fma(pc, y, -1.0 / 3628800.0);                       // -1/10!
+    pc = fma(pc, y, 1.0 / 40320.0);                          // 1/8!
+    pc = fma(pc, y, -1.0 / 720.0);                           // -1/6!
+    pc = fma(pc, y, 1.0 / 24.0);                             // 1/4!
+    pc = fma(pc, y, -0.5);                                   // -1/2!
+    c = fma(y, pc, 1.0);
+}
+__device__ __forceinline__ void tilt_sincos(bool poly, double x, double& s, double& c) {
+    if (poly) sincos_small(x, s, c);
+    else sincos(x, &s, &c);
+}
+
+// IPOPT's Compare_le: lhs <= rhs up to 10 machine epsilons of |base| (filter acceptance tests)
+__device__ __forceinline__ bool cmp_le(double lhs, double rhs, double base) {
+    return lhs - rhs <= 10.0 * 2.220446049250313e-16 * fabs(base);
+}
+
+}  // namespace dartmpc

@@ -3,11 +3,15 @@
 Drop-in for the reference's MPC hot path:
   - ``PMPC``            <- PMPC/src/controller/mpc_3d.py:11-138
   - ``mpc_worker``      <- PMPC/main_parallel_enhanced.py:22-55
-  - ``Solver``          the C ABI of include/dart_mpc.h (libdartmpc.so)
+  - ``AdaptiveNPMPCSmooth``, ``RLS`` <- RMPC/dev_dual/controller/np_mpc_adaptive_with_linear_regressor.py
+  - ``RMPCStep``        <- RMPC/dev_dual/rob_ctrl.py:331-352 (RLS fused into the solve launch)
+  - ``Solver``, ``RmpcSolver``  the C ABI of include/dart_mpc.h (libdartmpc.so)
 """
-from ._lib import DartMPCError, Solver, build, lib, STATUS_NAMES  # noqa: F401
+from ._lib import DartMPCError, RmpcSolver, Solver, build, lib, rls_update_batch, STATUS_NAMES  # noqa: F401
 from .pmpc import PMPC, tilt_to_quat  # noqa: F401
 from .worker import mpc_worker  # noqa: F401
+from .rmpc import AdaptiveNPMPCSmooth, RLS, RMPCStep  # noqa: F401
 from . import workload  # noqa: F401
 
-__all__ = ["PMPC", "mpc_worker", "Solver", "DartMPCError", "build", "lib", "tilt_to_quat", "workload"]
+__all__ = ["PMPC", "mpc_worker", "Solver", "RmpcSolver", "AdaptiveNPMPCSmooth", "RLS", "RMPCStep", "DartMPCError",
+           "build", "lib", "rls_update_batch", "tilt_to_quat", "workload"]

@@ -22,7 +22,10 @@ STATUS_NAMES = {SOLVED: "Solve_Succeeded", MAXITER: "Maximum_Iterations_Exceeded
 
 # exported symbols of include/dart_mpc.h (tests check every one is present)
 EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch", "dart_mpc_solve_batch_dev",
-           "dart_mpc_sync", "dart_mpc_last_error", "dart_mpc_destroy", "dart_mpc_nw", "dart_mpc_abi_version")
+           "dart_mpc_sync", "dart_mpc_last_error", "dart_mpc_destroy", "dart_mpc_nw", "dart_mpc_abi_version",
+           "dart_rmpc_solve_batch", "dart_rmpc_solve_batch_dev", "dart_rmpc_nw",
+           "dart_rls_update_batch", "dart_rls_update_batch_dev")
+VARIANT_PMPC, VARIANT_RMPC = 0, 1
 ABI_VERSION = 1
 
 
@@ -78,6 +81,17 @@ def lib():
     L.dart_mpc_nw.restype = ctypes.c_int
     L.dart_mpc_abi_version.argtypes = []
     L.dart_mpc_abi_version.restype = ctypes.c_int
+    rsig = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6 + [ctypes.c_double] + [ctypes.c_void_p] * 9
+    L.dart_rmpc_solve_batch.argtypes = rsig
+    L.dart_rmpc_solve_batch.restype = ctypes.c_int
+    L.dart_rmpc_solve_batch_dev.argtypes = rsig
+    L.dart_rmpc_solve_batch_dev.restype = ctypes.c_int
+    L.dart_rmpc_nw.argtypes = [ctypes.c_int]
+    L.dart_rmpc_nw.restype = ctypes.c_int
+    L.dart_rls_update_batch.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_double]
+    L.dart_rls_update_batch.restype = ctypes.c_int
+    L.dart_rls_update_batch_dev.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_double, ctypes.c_void_p]
+    L.dart_rls_update_batch_dev.restype = ctypes.c_int
     if L.dart_mpc_abi_version() != ABI_VERSION:
         raise DartMPCError("libdartmpc.so ABI version mismatch")
     _lib = L
@@ -163,3 +177,61 @@ class Solver:
             self.close()
         except Exception:
             pass
+
+
+class RmpcSolver(Solver):
+    """``dart_mpc_handle`` of variant RMPC (regressor NMPC + fused RLS), N <= 31."""
+
+    def __init__(self, N=20, Ts=0.002, tol=1e-8, max_iter=200, B_max=1024, device=0, gravity=-9.81):
+        self._h = ctypes.c_void_p()
+        self.cfg = default_config(variant=VARIANT_RMPC, N=int(N), Ts=float(Ts), tol=float(tol),
+                                  max_iter=int(max_iter), B_max=int(B_max), gravity=float(gravity))
+        rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
+        if rc != 0:
+            raise DartMPCError(f"dart_mpc_create(RMPC) failed with code {rc} (no gfx950 device or bad config)")
+        self.N = int(N)
+        self.nw = lib().dart_rmpc_nw(self.N)
+
+    def solve_batch(self, x0, u_prev, theta, Rref, prm, w_warm=None, want_w=False, rls_P=None, rls_phi=None,
+                    rls_y=None, rls_lambda=0.995):
+        """Host arrays in/out (blocking).  With ``rls_P`` the RLS update is fused: ``theta`` and
+        ``rls_P`` are updated in place (returned in the dict as well)."""
+        c = lambda a, n: np.ascontiguousarray(a, np.float64).reshape(-1, n)
+        x0 = c(x0, 4)
+        B = x0.shape[0]
+        u_prev, theta, Rref, prm = c(u_prev, 2), c(theta, 14).copy(), c(Rref, 4 * (self.N + 1)), c(prm, 10)
+        ww = None if w_warm is None else c(w_warm, self.nw)
+        P = phi = y = None
+        if rls_P is not None:
+            P = np.ascontiguousarray(rls_P, np.float64).reshape(B, 2, 7, 7).copy()
+            phi, y = c(rls_phi, 7), c(rls_y, 2)
+        u0 = np.empty((B, 2)); f = np.empty(B)
+        w = np.empty((B, self.nw)) if want_w else None
+        st = np.empty(B, np.int32); it = np.empty(B, np.int32)
+        rc = lib().dart_rmpc_solve_batch(self._h, B, _ptr(x0), _ptr(u_prev), _ptr(theta), _ptr(P), _ptr(phi), _ptr(y),
+                                         float(rls_lambda), _ptr(Rref), _ptr(prm), _ptr(ww), _ptr(u0), _ptr(f),
+                                         _ptr(w), _ptr(st), _ptr(it), None)
+        if rc != 0:
+            self._err(rc, "dart_rmpc_solve_batch")
+        return dict(u0=u0, f=f, w=w, status=st, iters=it, theta=theta, rls_P=P)
+
+    def solve_batch_dev(self, B, x0, u_prev, theta, Rref, prm, u0, f, status, iters, w_warm=0, w_out=0,
+                        rls_P=0, rls_phi=0, rls_y=0, rls_lambda=0.995, stream=0):
+        rc = lib().dart_rmpc_solve_batch_dev(self._h, int(B), x0, u_prev, theta, rls_P or None, rls_phi or None,
+                                             rls_y or None, float(rls_lambda), Rref, prm, w_warm or None, u0, f,
+                                             w_out or None, status, iters, stream or None)
+        if rc != 0:
+            self._err(rc, "dart_rmpc_solve_batch_dev")
+
+
+def rls_update_batch(theta, P, phi, y, lam=0.995):
+    """Batched RLS.update on the GPU (B filters of p = 7).  Returns updated (theta[B,7], P[B,7,7])."""
+    th = np.ascontiguousarray(theta, np.float64).reshape(-1, 7).copy()
+    B = th.shape[0]
+    Pm = np.ascontiguousarray(P, np.float64).reshape(B, 7, 7).copy()
+    ph = np.ascontiguousarray(phi, np.float64).reshape(B, 7)
+    yy = np.ascontiguousarray(y, np.float64).reshape(B)
+    rc = lib().dart_rls_update_batch(B, _ptr(th), _ptr(Pm), _ptr(ph), _ptr(yy), float(lam))
+    if rc != 0:
+        raise DartMPCError(f"dart_rls_update_batch failed ({rc})")
+    return th, Pm

@@ -81,3 +81,77 @@ def pmpc_c1():
     target = np.array([[0.1, 0.0, 0.0, 0.0, 0.4, 0.0]])
     prm = np.array([[0.10, 600.0, 5.0, 0.1, -0.6, 0.6]])
     return state, target, prm
+
+
+# ---------------------------------------------------------------------------
+# C3: RMPC batch.  Controller weights are the rob_ctrl.py defaults
+# (RMPC/dev_dual/rob_ctrl.py:281-284); the object config enters through the
+# regressor estimate theta_hat, which is produced by 50 seeded RLS updates
+# (np_mpc...:10-30, lambda 0.995, P0 1e3) on synthetic features / accelerations.
+# ---------------------------------------------------------------------------
+RMPC_PRM = np.array([80.0, 2.0, 0.02, 1.0, -0.6, 0.6, -0.06, 0.06, 0.2, 0.1])
+N_RMPC_PRM = 10
+RMPC_PRM_NAMES = ("Qp", "Qv", "Ru", "Rdu", "u_lo", "u_hi", "du_lo", "du_hi", "vmax", "v_eps")
+
+
+def _rls_update(theta, P, phi, y, lam=0.995):
+    denom = lam + phi @ P @ phi
+    K = (P @ phi) / denom
+    err = y - phi @ theta
+    theta = theta + K * err
+    P = (P - np.outer(K, phi) @ P) / lam
+    return theta, P
+
+
+def _features(x, v_eps=0.1):
+    return np.array([x[0], x[1], x[2], x[3], np.tanh(x[1] / v_eps), np.tanh(x[3] / v_eps), 1.0])
+
+
+def rmpc_batch(n_seeds: int = 1, seed0: int = 0, N: int = 20, n_rls: int = 50):
+    """Return dict of C3 inputs for B = 18*n_seeds instances:
+    x0[B,4], u_prev[B,2], theta[B,14], Rref[B,4(N+1)], prm[B,10], and the RLS state
+    (rls_theta[B,14], rls_P[B,2,7,7], phi_prev[B,7], y[B,2]) for one more fused update."""
+    B = N_CONFIGS * n_seeds
+    out = dict(x0=np.zeros((B, 4)), u_prev=np.zeros((B, 2)), theta=np.zeros((B, 14)),
+               Rref=np.zeros((B, 4 * (N + 1))), prm=np.tile(RMPC_PRM, (B, 1)),
+               rls_theta=np.zeros((B, 14)), rls_P=np.zeros((B, 2, 7, 7)), phi_prev=np.zeros((B, 7)), y=np.zeros((B, 2)))
+    for s in range(n_seeds):
+        rng = np.random.default_rng(SEED_BASE + 7919 + seed0 + s)
+        for b in range(N_CONFIGS):
+            i = N_CONFIGS * s + b
+            shape_idx, rest = divmod(b, 6)
+            mass_idx, fric_idx = divmod(rest, 3)
+            mu, m = FRICTIONS[fric_idx], MASSES[mass_idx]
+            # synthetic ground truth of the linear-in-features acceleration model
+            tx = np.array([0.0, -mu / m, 0.0, 0.0, -0.3 * mu * (1 + 0.5 * shape_idx), 0.0, 0.0])
+            ty = np.array([0.0, 0.0, 0.0, -mu / m, 0.0, -0.3 * mu * (1 + 0.5 * shape_idx), 0.0])
+            th = [np.zeros(7), np.zeros(7)]
+            Pm = [np.eye(7) * 1e3, np.eye(7) * 1e3]
+            for _ in range(n_rls):
+                xs = np.array([rng.uniform(-0.15, 0.15), rng.uniform(-0.15, 0.15),
+                               rng.uniform(-0.12, 0.12), rng.uniform(-0.15, 0.15)])
+                ph = _features(xs)
+                for a, tt in enumerate((tx, ty)):
+                    th[a], Pm[a] = _rls_update(th[a], Pm[a], ph, ph @ tt + rng.normal(0, 0.01))
+            x0 = np.array([rng.uniform(-0.18, 0.18), rng.uniform(-0.15, 0.15),
+                           rng.uniform(-0.13, 0.13), rng.uniform(-0.15, 0.15)])
+            target = np.array([rng.uniform(-0.15, 0.15), 0.0, rng.uniform(-0.12, 0.12), 0.0])
+            r_v = np.array([x0[0], 0.0, x0[2], 0.0])
+            # reference governor step (rob_ctrl.py:346-348) then staged reference (np_mpc...:201-210)
+            err = target - r_v
+            r_v = r_v + 0.5 * np.array([np.clip(err[0], -0.01, 0.01), 0.0, np.clip(err[2], -0.01, 0.01), 0.0])
+            R = np.zeros((N + 1, 4))
+            for k in range(N + 1):
+                w = 1.0 - 0.8 ** (k + 1)
+                rk = r_v + w * (target - r_v)
+                R[k] = [rk[0], 0.0, rk[2], 0.0]
+            out["x0"][i] = x0
+            out["u_prev"][i] = rng.uniform(-0.3, 0.3, 2)
+            out["theta"][i] = np.concatenate(th)
+            out["Rref"][i] = R.reshape(-1)
+            out["rls_theta"][i] = np.concatenate(th)
+            out["rls_P"][i] = np.stack(Pm)
+            xp = x0 + rng.normal(0, 1e-3, 4)
+            out["phi_prev"][i] = _features(xp)
+            out["y"][i] = (x0[[1, 3]] - xp[[1, 3]]) / 0.002
+    return out

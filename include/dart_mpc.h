@@ -11,6 +11,9 @@
  *                             per instance today: mpc_3d.py:115-138, called from
  *                             the worker loop PMPC/main_parallel_enhanced.py:51-53
  *   dart_mpc_solve_batch_dev  same, with device-resident inputs/outputs
+ *   dart_rmpc_solve_batch(_dev) <- AdaptiveNPMPCSmooth.solve + the driver's RLS updates
+ *                             RMPC/dev_dual/controller/np_mpc_adaptive_with_linear_regressor.py
+ *                             :212-222 (RLS :10-30), RMPC/dev_dual/rob_ctrl.py:335-352
  *   dart_mpc_sync / dart_mpc_last_error / dart_mpc_destroy
  *                           <- process-lifetime handling of the solver object in
  *                             mpc_worker (main_parallel_enhanced.py:22-55)
@@ -45,7 +48,10 @@ extern "C" {
 
 #define DART_MPC_ABI_VERSION 1
 
-enum dart_mpc_variant { DART_MPC_PMPC = 0 };
+enum dart_mpc_variant {
+    DART_MPC_PMPC = 0,      /* PMPC/src/controller/mpc_3d.py, N <= 63 */
+    DART_MPC_RMPC = 1       /* RMPC/dev_dual/controller/np_mpc_adaptive_with_linear_regressor.py, N <= 31 */
+};
 
 enum dart_mpc_status {
     DART_MPC_SOLVED = 0,
@@ -99,6 +105,44 @@ int dart_mpc_solve_batch_dev(dart_mpc_handle *h, int B,
                              const double *w_warm,
                              double *u0, double *f, double *w_out,
                              int32_t *status, int32_t *iters, void *hip_stream);
+
+/* RMPC (handle created with variant DART_MPC_RMPC).  Replaces
+ * AdaptiveNPMPCSmooth.solve(x0, u_prev, theta_hat, Rref_flat)
+ * (RMPC/dev_dual/controller/np_mpc_adaptive_with_linear_regressor.py:212-222) and, when
+ * rls_P != NULL, the two RLS.update calls that precede it in the driver
+ * (RMPC/dev_dual/rob_ctrl.py:335-343; RLS :10-30), fused into the same launch.
+ *   x0 [B][4], u_prev [B][2]
+ *   theta [B][14]   theta_hat = [theta_x(7); theta_y(7)]; with rls_P != NULL it is the RLS
+ *                   estimate, updated in place before the solve
+ *   rls_P [B][2][7][7] (nullable, in/out), rls_phi [B][7] = phi(prev state), rls_y [B][2] =
+ *                   measured accelerations, rls_lambda = forgetting factor (0.995 in the driver)
+ *   Rref [B][4(N+1)] staged reference (np_mpc...:201-210)
+ *   prm [B][10] = [Qp, Qv, Ru, Rdu, u_lo, u_hi, du_lo, du_hi, vmax, v_eps]
+ *   w_warm [B][4(N+1)+2N] (nullable: zeros, the reference's first call :168), w_out same layout
+ *   (x_0..x_N then u_0..u_{N-1}, :144). */
+int dart_rmpc_solve_batch(dart_mpc_handle *h, int B,
+                          const double *x0, const double *u_prev, double *theta,
+                          double *rls_P, const double *rls_phi, const double *rls_y, double rls_lambda,
+                          const double *Rref, const double *prm, const double *w_warm,
+                          double *u0, double *f, double *w_out,
+                          int32_t *status, int32_t *iters, void *hip_stream);
+
+int dart_rmpc_solve_batch_dev(dart_mpc_handle *h, int B,
+                              const double *x0, const double *u_prev, double *theta,
+                              double *rls_P, const double *rls_phi, const double *rls_y, double rls_lambda,
+                              const double *Rref, const double *prm, const double *w_warm,
+                              double *u0, double *f, double *w_out,
+                              int32_t *status, int32_t *iters, void *hip_stream);
+
+/* Number of fp64 entries of the RMPC w for horizon N: 4(N+1) + 2N. */
+int dart_rmpc_nw(int N);
+
+/* Batched standalone RLS.update (np_mpc...:17-27) for B independent p = 7 filters:
+ * theta [B][7] and P [B][7][7] updated in place with regressors phi [B][7], targets y [B],
+ * forgetting factor lambda.  The host entry stages through device memory and blocks. */
+int dart_rls_update_batch(int B, double *theta, double *P, const double *phi, const double *y, double lambda);
+int dart_rls_update_batch_dev(int B, double *theta, double *P, const double *phi, const double *y, double lambda,
+                              void *hip_stream);
 
 int dart_mpc_sync(dart_mpc_handle *h);
 

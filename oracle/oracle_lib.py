@@ -65,3 +65,49 @@ def rk4(Ts, mu, x, u):
     out = np.zeros(6)
     lib().oracle_pmpc_rk4(Ts, mu, _p(x), _p(u), _p(out))
     return out
+
+
+# --------------------------------------------------------------------------- RMPC
+_rlib = None
+_RLIB_PATH = os.path.join(_HERE, "liboracle_rmpc.so")
+
+
+def rlib():
+    global _rlib
+    if _rlib is None:
+        if not os.path.exists(_RLIB_PATH):
+            build()
+        L = ctypes.CDLL(_RLIB_PATH)
+        L.oracle_rmpc_solve_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, _dp, _dp, _dp, _dp, _dp,
+                                              _dp, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                              _dp, _dp, _dp, _ip, _ip]
+        L.oracle_rmpc_solve_batch.restype = ctypes.c_int
+        L.oracle_rls_update.argtypes = [_dp, _dp, _dp, ctypes.c_double, ctypes.c_double]
+        L.oracle_rls_update.restype = None
+        L.oracle_rmpc_set_relax.argtypes = [ctypes.c_double]
+        L.oracle_rmpc_set_relax.restype = None
+        _rlib = L
+    return _rlib
+
+
+def rmpc_solve_batch(x0, u_prev, theta, Rref, prm, N=20, Ts=0.002, w_init=None, max_iter=200, tol=1e-8,
+                     nthreads=1, want_w=True, relax=1e-8):
+    c = lambda a: np.ascontiguousarray(a, np.float64)
+    x0, u_prev, theta, Rref, prm = c(x0), c(u_prev), c(theta), c(Rref), c(prm)
+    B = x0.shape[0]
+    nw = 4 * (N + 1) + 2 * N
+    wi = None if w_init is None else c(w_init)
+    u0 = np.zeros((B, 2)); f = np.zeros(B); w = np.zeros((B, nw)) if want_w else None
+    st = np.zeros(B, np.int32); it = np.zeros(B, np.int32)
+    rlib().oracle_rmpc_set_relax(float(relax))
+    rlib().oracle_rmpc_solve_batch(B, N, Ts, _p(x0), _p(u_prev), _p(theta), _p(Rref), _p(prm),
+                                   _p(wi) if wi is not None else None, max_iter, tol, nthreads,
+                                   _p(u0), _p(f), _p(w) if want_w else None, _p(st, _ip), _p(it, _ip))
+    return dict(u0=u0, f=f, w=w, status=st, iters=it)
+
+
+def rls_update(theta, P, phi, y, lam=0.995):
+    th = np.ascontiguousarray(theta, np.float64).copy()
+    Pm = np.ascontiguousarray(P, np.float64).copy()
+    rlib().oracle_rls_update(_p(th), _p(Pm), _p(np.ascontiguousarray(phi, np.float64)), float(y), lam)
+    return th, Pm

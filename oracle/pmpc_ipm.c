@@ -35,6 +35,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+
+/* IPOPT Compare_le: lhs <= rhs up to 10 machine epsilons of |base| */
+#define LE(l, r, b) ((l) - (r) <= 10.0 * 2.220446049250313e-16 * fabs(b))
 #ifdef ORACLE_DEBUG
 #include <stdio.h>
 #endif
@@ -411,19 +414,25 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
         amin *= gam_al;
         double alpha = amax, th_t = 0, ph_t = 0;
         int accepted = 0, ftype = 0, used_soc = 0;
+        /* IPOPT tiny-step test: max |d|/(1+|x|) < 10 eps_mach -> accept the full step, unfiltered */
+        double tn = 0.0;
+        for (int i = 0; i < ng; ++i) tn = fmax(tn, fabs(W->dX[i]) / (1.0 + fabs(W->X[i])));
+        for (int j = 0; j < nU; ++j) tn = fmax(tn, fabs(W->dU[j]) / (1.0 + fabs(W->U[j])));
+        const int tiny = tn < 10.0 * 2.220446049250313e-16;
         for (int ls = 0; ls < 80 && !accepted; ++ls) {
             if (alpha < amin && ls > 0) break;
             for (int i = 0; i < ng; ++i) W->Xt[i] = W->X[i] + alpha * W->dX[i];
             for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + alpha * W->dU[j];
             th_t = constraints(&C, W->Xt, W->Ut, W->gt);
             ph_t = barrier_obj(&C, W->Xt, W->Ut);
+            if (tiny) { accepted = 1; ftype = 1; break; }
             for (int pass = 0; pass < 5; ++pass) {        /* pass 0: plain trial; 1..4: SOC */
                 int in_filter = !(th_t < th_max) || !isfinite(ph_t);
                 for (int q = 0; q < nfilt && !in_filter; ++q) if (th_t >= W->filt_th[q] && ph_t >= W->filt_ph[q]) in_filter = 1;
                 if (!in_filter) {
                     int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
-                    if (th <= th_min && sw) { if (ph_t <= phi + eta_ph * alpha * gTd) { accepted = 1; ftype = 1; } }
-                    else if (th_t <= (1 - gam_th) * th || ph_t <= phi - gam_ph * th) accepted = 1;
+                    if (th <= th_min && sw) { if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { accepted = 1; ftype = 1; } }
+                    else if (LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi)) accepted = 1;
                 }
                 if (accepted || ls > 0 || th_t < th) break;
                 /* second-order correction: c_soc <- a c_soc + g(trial); solve; re-try */
@@ -445,8 +454,8 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
                 int acc = 0;
                 if (!inf) {
                     int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
-                    if (th <= th_min && sw) { if (ph_t <= phi + eta_ph * alpha * gTd) { acc = 1; ftype = 1; } }
-                    else if (th_t <= (1 - gam_th) * th || ph_t <= phi - gam_ph * th) acc = 1;
+                    if (th <= th_min && sw) { if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { acc = 1; ftype = 1; } }
+                    else if (LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi)) acc = 1;
                 }
                 if (acc) { accepted = 1; used_soc = 1; alpha = asoc; break; }
                 memcpy(W->dU, save_dU, sizeof(double) * nU); memcpy(W->dX, save_dX, sizeof(double) * ng); memcpy(W->lamp, save_lp, sizeof(double) * ng);

@@ -19,3 +19,10 @@ def goldens():
     import numpy as np
     d = np.load(os.path.join(ROOT, "tests", "golden", "pmpc_goldens.npz"))
     return {k: d[k] for k in d.files}
+
+
+@pytest.fixture(scope="session")
+def rmpc_goldens():
+    import numpy as np
+    d = np.load(os.path.join(ROOT, "tests", "golden", "rmpc_goldens.npz"))
+    return {k: d[k] for k in d.files}

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared_functions():
     src = open(os.path.join(ROOT, "include", "dart_mpc.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(dart_mpc_\w+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(dart_\w+)\s*\(", src)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -31,6 +31,7 @@ def test_defaults_follow_reference():
     assert (c.variant, c.N, c.Ts, c.tol, c.max_iter, c.gravity) == (0, 20, 0.002, 1e-8, 3000, -9.81)
     assert _lib.lib().dart_mpc_nw(20) == 166 and _lib.lib().dart_mpc_nw(15) == 126
     assert _lib.lib().dart_mpc_abi_version() == 1
+    assert _lib.lib().dart_rmpc_nw(20) == 124 and _lib.lib().dart_rmpc_nw(1) == 10      # 4(N+1) + 2N
 
 
 def test_create_rejects_bad_config_without_touching_a_gpu():
@@ -39,7 +40,28 @@ def test_create_rejects_bad_config_without_touching_a_gpu():
     for over in (dict(N=0), dict(N=64), dict(Ts=0.0), dict(tol=-1.0), dict(B_max=0), dict(variant=7)):
         c = _lib.default_config(**over)
         assert _lib.lib().dart_mpc_create(ctypes.byref(c), 0, ctypes.byref(h)) == -1
+    for over in (dict(variant=1, N=32), dict(variant=1, N=0)):       # RMPC horizon limit N <= 31
+        c = _lib.default_config(**over)
+        assert _lib.lib().dart_mpc_create(ctypes.byref(c), 0, ctypes.byref(h)) == -1
     assert _lib.lib().dart_mpc_solve_batch(None, 1, *([None] * 10)) == -1
+    assert _lib.lib().dart_rmpc_solve_batch(None, 1, *([None] * 6), 0.995, *([None] * 9)) == -1
+    assert _lib.lib().dart_rls_update_batch(-1, None, None, None, None, 0.995) == -1
+
+
+def test_rmpc_shim_validates_like_reference():
+    import dart_mpc
+    with pytest.raises(ValueError):
+        dart_mpc.AdaptiveNPMPCSmooth(None, None, nx=6)
+    with pytest.raises(ValueError):
+        dart_mpc.AdaptiveNPMPCSmooth(None, None, N=32)
+    c = dart_mpc.AdaptiveNPMPCSmooth(None, None, Ts=0.002, N=20, Qp=80.0, Qv=2.0, Ru=0.02, Rdu=1.0,
+                                     u_bounds=(-0.6, 0.6), du_bounds=(-0.06, 0.06), vmax=0.2, v_eps=0.1)
+    assert c.w0.shape == (124,) and c.gz == -9.81
+    np.testing.assert_array_equal(c.params(), [80, 2, 0.02, 1.0, -0.6, 0.6, -0.06, 0.06, 0.2, 0.1])
+    with pytest.raises(RuntimeError):
+        c.get_state()
+    with pytest.raises(ValueError):
+        dart_mpc.RLS(5)
 
 
 def test_pmpc_shim_validates_like_reference():

@@ -1,0 +1,155 @@
+"""GPU parity tests of the batched RMPC kernel + RLS (through the C ABI).
+
+Tolerances (fp64 path, IPOPT-equivalent algorithm with bound_relax 1e-8):
+  * against the two-solver goldens (exact NLP): every control within 1e-6 at
+    tol 1e-11 (the relaxation moves active rows by O(1e-8 / multiplier));
+  * against the C oracle with the same options: every control within 1e-6 at
+    tol 1e-11, u0 within 1e-5 at the reference's tol 1e-8;
+  * RLS (theta, P): relative 1e-12 against oracle/rmpc_ipm.c's oracle_rls_update.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib
+import rmpc_nlp
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dm():
+    import dart_mpc
+    return dart_mpc
+
+
+def _nw(N):
+    return 4 * (N + 1) + 2 * N
+
+
+def test_goldens_tight_tol(dm, rmpc_goldens):
+    G = rmpc_goldens
+    for N in np.unique(G["N"]):
+        N = int(N)
+        idx = np.nonzero(G["N"] == N)[0]
+        s = dm.RmpcSolver(N=N, tol=1e-11, max_iter=500, B_max=64)
+        out = s.solve_batch(G["x0"][idx], G["u_prev"][idx], G["theta"][idx], G["Rref"][idx][:, : 4 * (N + 1)],
+                            G["prm"][idx], want_w=True)
+        s.close()
+        assert np.all(out["status"] == 0), (N, out["status"], out["iters"])
+        nX = 4 * (N + 1)
+        err = np.abs(out["w"][:, nX:] - G["w"][idx][:, nX:_nw(N)]).max(axis=1)
+        assert np.all(err <= 1e-6), (N, err)
+
+
+@pytest.mark.parametrize("tol,u0_bound,U_bound", [(1e-8, 1e-5, 1e-4), (1e-11, 1e-6, 1e-6)])
+def test_c3_batch_vs_oracle(dm, tol, u0_bound, U_bound):
+    from dart_mpc.workload import rmpc_batch
+    D = rmpc_batch(2)
+    s = dm.RmpcSolver(N=20, tol=tol, max_iter=500, B_max=64)
+    out = s.solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"], want_w=True)
+    s.close()
+    ref = oracle_lib.rmpc_solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"], N=20, tol=tol,
+                                      max_iter=500, nthreads=4)
+    assert np.all(out["status"] == 0) and np.all(ref["status"] == 0), (out["status"], out["iters"])
+    assert np.max(np.abs(out["u0"] - ref["u0"])) <= u0_bound
+    assert np.max(np.abs(out["w"][:, 84:] - ref["w"][:, 84:])) <= U_bound
+    assert np.allclose(out["f"], ref["f"], rtol=1e-6, atol=1e-10)
+    assert np.max(np.abs(out["iters"] - ref["iters"])) <= 10, (out["iters"], ref["iters"])
+
+
+@pytest.mark.parametrize("N", [1, 2, 15, 31])
+def test_horizons(dm, N):
+    from dart_mpc.workload import rmpc_batch
+    D = rmpc_batch(1, seed0=3, N=N)
+    s = dm.RmpcSolver(N=N, tol=1e-11, max_iter=500, B_max=32)
+    out = s.solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"], want_w=True)
+    s.close()
+    ref = oracle_lib.rmpc_solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"], N=N, tol=1e-11,
+                                      max_iter=500, nthreads=4)
+    assert np.all(out["status"] == 0), out["status"]
+    nX = 4 * (N + 1)
+    assert np.max(np.abs(out["w"][:, nX:] - ref["w"][:, nX:])) <= 1e-6
+
+
+def test_fused_rls_matches_oracle_and_unfused(dm):
+    from dart_mpc.workload import rmpc_batch
+    D = rmpc_batch(1, seed0=5)
+    B = D["x0"].shape[0]
+    s = dm.RmpcSolver(N=20, tol=1e-10, max_iter=500, B_max=32)
+    fused = s.solve_batch(D["x0"], D["u_prev"], D["rls_theta"], D["Rref"], D["prm"], want_w=True,
+                          rls_P=D["rls_P"], rls_phi=D["phi_prev"], rls_y=D["y"], rls_lambda=0.995)
+    th_ref = np.zeros((B, 14)); P_ref = np.zeros((B, 2, 7, 7))
+    for b in range(B):
+        for a in range(2):
+            th_ref[b, 7 * a:7 * a + 7], P_ref[b, a] = oracle_lib.rls_update(
+                D["rls_theta"][b, 7 * a:7 * a + 7], D["rls_P"][b, a], D["phi_prev"][b], D["y"][b, a], 0.995)
+    assert np.allclose(fused["theta"], th_ref, rtol=1e-12, atol=1e-12)
+    assert np.allclose(fused["rls_P"], P_ref, rtol=1e-11, atol=1e-11 * np.abs(P_ref).max())
+    plain = s.solve_batch(D["x0"], D["u_prev"], th_ref, D["Rref"], D["prm"], want_w=True)
+    s.close()
+    assert np.max(np.abs(fused["w"] - plain["w"])) <= 1e-9
+
+
+def test_standalone_rls_batch(dm):
+    rng = np.random.default_rng(17)
+    B = 300
+    th = rng.normal(size=(B, 7)); A = rng.normal(size=(B, 7, 7)); P = A @ A.transpose(0, 2, 1) + np.eye(7)
+    phi = rng.normal(size=(B, 7)); y = rng.normal(size=B)
+    gt, gP = dm.rls_update_batch(th, P, phi, y, 0.99)
+    for b in range(0, B, 37):
+        t2, P2 = oracle_lib.rls_update(th[b], P[b], phi[b], y[b], 0.99)
+        assert np.allclose(gt[b], t2, rtol=1e-12, atol=1e-12) and np.allclose(gP[b], P2, rtol=1e-11, atol=1e-11)
+    r = dm.RLS(7)
+    ro = rmpc_nlp.RLS(7)
+    for _ in range(20):
+        f = rng.normal(size=7); yy = float(rng.normal())
+        r.update(f, yy); ro.update(f, yy)
+    assert np.allclose(r.get(), ro.get(), rtol=1e-10, atol=1e-10)
+
+
+def test_warm_start_and_edge_batches(dm):
+    from dart_mpc.workload import rmpc_batch
+    D = rmpc_batch(1)
+    s = dm.RmpcSolver(N=20, tol=1e-8, B_max=32)
+    cold = s.solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"], want_w=True)
+    warm = s.solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"], w_warm=cold["w"], want_w=True)
+    assert np.all(warm["status"] == 0) and np.max(np.abs(warm["u0"] - cold["u0"])) <= 1e-5
+    e = s.solve_batch(np.zeros((0, 4)), np.zeros((0, 2)), np.zeros((0, 14)), np.zeros((0, 84)), np.zeros((0, 10)))
+    assert e["u0"].shape == (0, 2)
+    with pytest.raises(dm.DartMPCError):
+        s.solve_batch(np.zeros((40, 4)), np.zeros((40, 2)), np.zeros((40, 14)), np.zeros((40, 84)),
+                      np.tile(D["prm"][0], (40, 1)))
+    s.close()
+
+
+def test_closed_loop_driver_matches_oracle_loop(dm):
+    """RMPCStep (rob_ctrl.py:331-352, RLS fused on the GPU) driving a plant integrated with the
+    true model; at every step the oracle (numpy RLS + C IPOPT restatement, own warm start) is
+    fed the same measurements and must give the same estimate and control."""
+    from dart_mpc.rmpc import AdaptiveNPMPCSmooth, RMPCStep
+    kw = dict(Ts=0.002, N=20, Qp=80.0, Qv=2.0, Ru=0.02, Rdu=1.0, u_bounds=(-0.6, 0.6), du_bounds=(-0.06, 0.06),
+              vmax=0.2, v_eps=0.1)
+    ctrl = AdaptiveNPMPCSmooth(None, None, tol=1e-10, max_iter=500, **kw)
+    target = np.array([0.08, 0.0, -0.05, 0.0])
+    x = np.zeros(4); xprev = x.copy(); up = np.zeros(2)
+    step = RMPCStep(ctrl, target, r_v0=x.copy())
+    truth = np.concatenate([[0, -1.0, 0, 0, -0.2, 0, 0], [0, 0, 0, -1.0, 0, -0.2, 0]])
+    rls = [rmpc_nlp.RLS(7), rmpc_nlp.RLS(7)]
+    r_v = x.copy(); w0 = np.zeros(_nw(20))
+    for k in range(25):
+        u, _ = step(x, xprev, up)
+        y = rmpc_nlp.rls_targets(x, xprev, 0.002)
+        f = rmpc_nlp.rls_features(xprev, 0.1)
+        rls[0].update(f, y[0]); rls[1].update(f, y[1])
+        th = np.concatenate([rls[0].get(), rls[1].get()])
+        assert np.allclose(step.theta, th, rtol=1e-9, atol=1e-9 * max(1.0, np.abs(th).max())), k
+        r_v = rmpc_nlp.governor_step(r_v, target)
+        assert np.allclose(step.r_v, r_v, rtol=0, atol=1e-15)
+        R = rmpc_nlp.build_ref_traj(x, r_v, target, 20)
+        o = oracle_lib.rmpc_solve_batch(x[None], up[None], step.theta[None], R[None], ctrl.params()[None], N=20,
+                                        tol=1e-10, w_init=w0[None], max_iter=500)
+        w0 = o["w"][0]
+        assert o["status"][0] == 0 and ctrl.w0 is not None
+        assert np.max(np.abs(u - o["u0"][0])) <= 1e-6, (k, u, o["u0"][0])
+        xprev, x = x, rmpc_nlp.rk4(x, u, truth, 0.1, 0.002)
+        up = u
