@@ -3,7 +3,7 @@
 // Used by the coupled-model solvers (RMPC, later LMPC), whose stage blocks are too large for the
 // lane-per-node register recursion of the PMPC kernel.  One wave64 owns one instance; the stage
 // data of all nodes sit in LDS; the backward Riccati sweep runs over the nodes in sequence and
-// the 64 lanes share each node's dense linear algebra ("lanes as matrix entries"):
+// the lanes share each node's dense algebra ("lanes as matrix entries"):
 //
 //   z = [x~ (NXA) ; u (2) ; 1]                      homogeneous stage vector, ND = NXA + 3
 //   x~+ = M z,  M = [[A B c]; [0 0 1]]  (NP x ND)   linearised dynamics incl. the defect c
@@ -11,14 +11,23 @@
 //   G = M^T Pt M + Ht                               stage QP incl. gradient (last row/column)
 //   Pt' = Schur complement of G on the u block      ->  gains K (2 x NXA), feed-forward k (2)
 //
-// Three lane-parallel products per node (Y = Pt M, G = M^T Y + Ht, Schur), each one LDS round trip.
+// One LDS round trip per node: lane e owns packed entry (i, j) of G_k and forms it from the
+// columns a_i, a_j of M_k (lane-private reads) and all of G_{k+1} (broadcast reads), with the
+// Schur complement that defines Pt_{k+1} folded into the bilinear form.  The gains [K | k] and
+// the multipliers are recovered from the stored G_k afterwards, lane per node, in parallel.
+//
+// The forward sweep dx~_{k+1} = Phi_k dx~_k + f_k (Phi = A + B K, f = c + B k, formed for all
+// nodes in parallel, lane per node) runs redundantly in every lane: no exchange on the chain.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include "wave.h"
 
 namespace dartmpc {
 
 __host__ __device__ constexpr int tri(int n) { return n * (n + 1) / 2; }
-__device__ __forceinline__ int hp(int i, int j) { return i >= j ? tri(i) + j : tri(j) + i; }
+__host__ __device__ constexpr int hp(int i, int j) { return i >= j ? tri(i) + j : tri(j) + i; }
+__host__ __device__ constexpr int even(int n) { return (n + 1) & ~1; }
 
 template <int NXA_, int NMAXS_>
 struct OcpLds {
@@ -26,106 +35,184 @@ struct OcpLds {
     static constexpr int NP = NXA + 1;        // value-function dimension (with homogeneous 1)
     static constexpr int ND = NXA + 3;        // stage vector dimension [x~; u; 1]
     static constexpr int NMAXS = NMAXS_;      // max shooting nodes (N + 1)
-    double M[NMAXS][ND][NP];                  // M columns: M[k][j][m] = M_k(m, j)
-    double H[NMAXS][tri(ND)];                 // stage Hessian + gradient, packed symmetric
-    double P[NMAXS][tri(NP)];                 // value functions Pt_k, packed symmetric
-    double K[NMAXS][2][NP];                   // [K | k] per node (row a, column p; p = NXA is k)
-    double Y[NP][ND];                         // scratch: Pt_{k+1} M_k
-    double G[tri(ND)];                        // scratch: G_k
-    double dz[NMAXS][ND];                     // forward sweep: [dx~_k ; du_k ; 1]
+    static constexpr int NC = even(NP);       // padded column stride of M (16-byte aligned reads)
+    static constexpr int NT = tri(ND);        // packed entries of G / Ht
+    static constexpr int NTP = even(NT);
+    static constexpr int NF = even(NXA + 1);  // closed-loop row stride [Phi row | f]
+    static_assert(NT <= 64, "one lane per entry of G");
+    double M[NMAXS][ND][NC];                  // M[k][j][m] = M_k(m, j): column j of M_k
+    double H[NMAXS][NTP];                     // stage Hessian + gradient, packed symmetric
+    double G[NMAXS][NTP];                     // G_k; G[N] = terminal surrogate (Pt_N, Quu = I)
+    double KK[NMAXS][2][NC];                  // [K | k]_k rows
+    double F[NMAXS][NXA][NF];                 // closed loop: F[k][r] = [Phi_k(r, :) | f_k(r)]
+    double dx0[NC];                           // forward sweep start dx~_0
 };
 
 // z index of value-function index p (the homogeneous coordinate sits last in both)
 template <int NXA>
-__device__ __forceinline__ int zi_of_p(int p) { return p < NXA ? p : NXA + 2; }
+__host__ __device__ constexpr int zi_of_p(int p) { return p < NXA ? p : NXA + 2; }
 
-// Backward Riccati sweep over nodes N-1 .. 0.  L->P[N] must hold the terminal value function.
-// Returns false (wave-uniform) if some Quu is not positive definite (inertia correction needed).
+// packed G offsets of the value-space block (p, q), the (p, u_a) block and Quu
+template <int NXA>
+__host__ __device__ constexpr int gzz(int p, int q) { return hp(zi_of_p<NXA>(p), zi_of_p<NXA>(q)); }
+template <int NXA>
+__host__ __device__ constexpr int gzu(int p, int a) { return hp(zi_of_p<NXA>(p), NXA + a); }
+
+// Per-lane role of the backward sweep (packed entry (i, j) of G), decoded once.
+struct RiccatiRoles {
+    int ci, cj;          // column offsets (j * NC) of a_i, a_j in M_k
+    bool on;             // lane owns an entry
+};
+
 template <class L>
-__device__ bool riccati_sweep(L* S, int N) {
-    constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND;
+__device__ RiccatiRoles riccati_roles() {
+    constexpr int NT = L::NT, NC = L::NC;
+    const int lane = threadIdx.x;
+    RiccatiRoles r{};
+    int i = 0;
+    const int e = lane < NT ? lane : 0;
+    while (tri(i + 1) <= e) ++i;
+    const int j = e - tri(i);
+    r.ci = i * NC; r.cj = j * NC;
+    r.on = lane < NT;
+    return r;
+}
+
+// Quu of a packed G, its positive-definiteness and its inverse (wave-uniform values)
+template <int NXA>
+__device__ __forceinline__ bool quu_inverse(const double* Gk, double& i00, double& i01, double& i11) {
+    const double g00 = Gk[hp(NXA, NXA)], g01 = Gk[hp(NXA + 1, NXA)], g11 = Gk[hp(NXA + 1, NXA + 1)];
+    const double det = g00 * g11 - g01 * g01;
+    const double idet = frcp(det);
+    i00 = g11 * idet; i01 = -g01 * idet; i11 = g00 * idet;
+    return (g00 > 0.0) && (det > 0.0) && isfinite(det);
+}
+
+// Backward Riccati sweep over nodes N-1 .. 0, one LDS round trip per node.  With
+// Pt_{k+1} = Gzz - Gzu Quu^-1 Guz (the Schur complement of G_{k+1}) folded in,
+//   G_k(i, j) = Ht_ij + a_i^T Gzz a_j - (a_i^T Gzu) Quu^-1 (Guz a_j),
+// lane e owning packed entry (i, j).  G[N] must hold the terminal surrogate.  Returns false
+// (wave-uniform) if some Quu is not positive definite (inertia correction needed).
+template <class L>
+__device__ bool riccati_sweep(L* S, int N, const RiccatiRoles& R) {
+    constexpr int NXA = L::NXA, NP = L::NP;
     const int lane = threadIdx.x;
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
-        // (A) Y = Pt_{k+1} M_k : NP x ND entries
-        for (int e = lane; e < NP * ND; e += 64) {
-            const int m = e / ND, j = e % ND;
-            double s = 0.0;
+        const double* Gn = S->G[k + 1];
+        double i00, i01, i11;
+        ok = quu_inverse<NXA>(Gn, i00, i01, i11) && ok;
+        if (R.on) {
+            const double* ai = &S->M[k][0][0] + R.ci;
+            const double* aj = &S->M[k][0][0] + R.cj;
+            double vi[NP], vj[NP];
 #pragma unroll
-            for (int l = 0; l < NP; ++l) s = fma(S->P[k + 1][hp(m, l)], S->M[k][j][l], s);
-            S->Y[m][j] = s;
-        }
-        __syncthreads();
-        // (B) G = M^T Y + Ht (packed lower triangle)
-        for (int e = lane; e < tri(ND); e += 64) {
-            int i = 0;
-            while (tri(i + 1) <= e) ++i;
-            const int j = e - tri(i);
-            double s = S->H[k][e];
+            for (int m = 0; m < NP; ++m) { vi[m] = ai[m]; vj[m] = aj[m]; }
+            // NP + 4 independent accumulators updated round-robin: dependency distance NP + 4
+            double t[NP];
+            double b0 = 0.0, b1 = 0.0, c0 = 0.0, c1 = 0.0;
 #pragma unroll
-            for (int m = 0; m < NP; ++m) s = fma(S->M[k][i][m], S->Y[m][j], s);
-            S->G[e] = s;
-        }
-        __syncthreads();
-        // (C) Schur complement on the u block (z indices NXA, NXA+1)
-        const double g00 = S->G[hp(NXA, NXA)], g01 = S->G[hp(NXA, NXA + 1)], g11 = S->G[hp(NXA + 1, NXA + 1)];
-        const double det = g00 * g11 - g01 * g01;
-        ok = ok && (g00 > 0.0) && (det > 0.0) && isfinite(det);
-        const double idet = 1.0 / det;
-        const double i00 = g11 * idet, i01 = -g01 * idet, i11 = g00 * idet;
-        for (int e = lane; e < tri(NP) + 2 * NP; e += 64) {
-            if (e < tri(NP)) {
-                int p = 0;
-                while (tri(p + 1) <= e) ++p;
-                const int q = e - tri(p);
-                const int zi = zi_of_p<NXA>(p), zj = zi_of_p<NXA>(q);
-                const double a0 = S->G[hp(zi, NXA)], a1 = S->G[hp(zi, NXA + 1)];
-                const double b0 = S->G[hp(NXA, zj)], b1 = S->G[hp(NXA + 1, zj)];
-                const double w0 = fma(i00, b0, i01 * b1), w1 = fma(i01, b0, i11 * b1);
-                S->P[k][e] = S->G[hp(zi, zj)] - fma(a0, w0, a1 * w1);
-            } else {
-                const int r = e - tri(NP), a = r / NP, p = r % NP;
-                const int zj = zi_of_p<NXA>(p);
-                const double b0 = S->G[hp(NXA, zj)], b1 = S->G[hp(NXA + 1, zj)];
-                S->K[k][a][p] = a == 0 ? -fma(i00, b0, i01 * b1) : -fma(i01, b0, i11 * b1);
+            for (int m = 0; m < NP; ++m) t[m] = 0.0;
+#pragma unroll
+            for (int n = 0; n < NP; ++n) {
+#pragma unroll
+                for (int m = 0; m < NP; ++m) t[m] = fma(Gn[gzz<NXA>(m, n)], vj[n], t[m]);
+                b0 = fma(vi[n], Gn[gzu<NXA>(n, 0)], b0);
+                b1 = fma(vi[n], Gn[gzu<NXA>(n, 1)], b1);
+                c0 = fma(vj[n], Gn[gzu<NXA>(n, 0)], c0);
+                c1 = fma(vj[n], Gn[gzu<NXA>(n, 1)], c1);
             }
+            double ga = S->H[k][lane], gb = 0.0;
+#pragma unroll
+            for (int m = 0; m < NP; m += 2) {
+                ga = fma(vi[m], t[m], ga);
+                if (m + 1 < NP) gb = fma(vi[m + 1], t[m + 1], gb);
+            }
+            const double w0 = fma(i00, c0, i01 * c1), w1 = fma(i01, c0, i11 * c1);
+            S->G[k][lane] = (ga + gb) - fma(b0, w0, b1 * w1);
         }
         __syncthreads();
     }
-    return ok;
+    double i00, i01, i11;
+    return quu_inverse<NXA>(S->G[0], i00, i01, i11) && ok;
 }
 
-// Forward sweep dx~_{k+1} = M_k [dx~_k; du_k; 1], du_k = K_k dx~_k + k_k.  L->dz[0][0..NXA) must hold
-// dx~_0 on entry; fills dz[k] = [dx~_k; du_k; 1] for k = 0..N (du_N = 0).
+// Gains and closed-loop matrices for the forward sweep, lane per node (lanes 0..N-1):
+// [K | k] = -Quu^-1 Guz, Phi_k = A_k + B_k K_k, f_k = c_k + B_k k_k.  Ends with a barrier.
 template <class L>
-__device__ void forward_sweep(L* S, int N) {
+__device__ void closed_loop(L* S, int N) {
     constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND;
-    const int lane = threadIdx.x;
-    for (int k = 0; k < N; ++k) {
-        double du0 = S->K[k][0][NXA], du1 = S->K[k][1][NXA];
+    const int k = threadIdx.x;
+    if (k < N) {
+        const double* Gk = S->G[k];
+        double i00, i01, i11;
+        quu_inverse<NXA>(Gk, i00, i01, i11);
+        double K0[NP], K1[NP];
 #pragma unroll
-        for (int j = 0; j < NXA; ++j) {
-            const double d = S->dz[k][j];
-            du0 = fma(S->K[k][0][j], d, du0);
-            du1 = fma(S->K[k][1][j], d, du1);
+        for (int p = 0; p < NP; ++p) {
+            const double c0 = Gk[gzu<NXA>(p, 0)], c1 = Gk[gzu<NXA>(p, 1)];
+            K0[p] = -fma(i00, c0, i01 * c1);
+            K1[p] = -fma(i01, c0, i11 * c1);
+            S->KK[k][0][p] = K0[p];
+            S->KK[k][1][p] = K1[p];
         }
-        if (lane < NXA) {
-            double s = S->M[k][ND - 1][lane];                 // c_k
 #pragma unroll
-            for (int j = 0; j < NXA; ++j) s = fma(S->M[k][j][lane], S->dz[k][j], s);
-            s = fma(S->M[k][NXA][lane], du0, s);
-            s = fma(S->M[k][NXA + 1][lane], du1, s);
-            S->dz[k + 1][lane] = s;
-        } else if (lane == NXA) {
-            S->dz[k][NXA] = du0;
-            S->dz[k][NXA + 1] = du1;
-            S->dz[k][NXA + 2] = 1.0;
+        for (int r = 0; r < NXA; ++r) {
+            const double b0 = S->M[k][NXA][r], b1 = S->M[k][NXA + 1][r];
+#pragma unroll
+            for (int j = 0; j < NXA; ++j) S->F[k][r][j] = fma(b0, K0[j], fma(b1, K1[j], S->M[k][j][r]));
+            S->F[k][r][NXA] = fma(b0, K0[NXA], fma(b1, K1[NXA], S->M[k][ND - 1][r]));
         }
-        __syncthreads();
     }
-    if (lane == 0) { S->dz[N][NXA] = 0.0; S->dz[N][NXA + 1] = 0.0; S->dz[N][NXA + 2] = 1.0; }
     __syncthreads();
-    (void)NP;
+}
+
+// Multiplier of the dynamics row into node k: lam~_k = -Pt_k [dx~; 1] (first NXA rows), with
+// Pt_k [dx~; 1] = Gzz [dx~; 1] + Gzu du (du = [K | k][dx~; 1]), read from G_k (lane per node).
+template <class L>
+__device__ __forceinline__ void node_multiplier(const L* S, int k, const double* dx, const double* du, double* lam) {
+    constexpr int NXA = L::NXA, NP = L::NP;
+    const double* Gk = S->G[k];
+#pragma unroll
+    for (int p = 0; p < NXA; ++p) {
+        double t = Gk[gzz<NXA>(p, NP - 1)];
+#pragma unroll
+        for (int q = 0; q < NXA; ++q) t = fma(Gk[gzz<NXA>(p, q)], dx[q], t);
+        t = fma(Gk[gzu<NXA>(p, 0)], du[0], t);
+        t = fma(Gk[gzu<NXA>(p, 1)], du[1], t);
+        lam[p] = -t;
+    }
+}
+
+// Forward sweep: lane r < NXA owns row r of the chain dx~_{k+1} = Phi_k dx~_k + f_k; the new
+// state is broadcast to every lane by readlane (scalar registers), and row r's closed-loop data
+// for node k+1 is prefetched while node k is processed.  Every lane returns in dxo the state step
+// of node `node` (lane-per-node use; node > N keeps dx~_0).  S->dx0 must hold dx~_0.
+template <class L>
+__device__ void forward_sweep(L* S, int N, int node, double* dxo) {
+    constexpr int NXA = L::NXA;
+    const int lane = threadIdx.x;
+    const int r = lane < NXA ? lane : 0;
+    double d[NXA];
+#pragma unroll
+    for (int i = 0; i < NXA; ++i) { d[i] = S->dx0[i]; dxo[i] = d[i]; }
+    double Fc[NXA + 1];
+#pragma unroll
+    for (int j = 0; j <= NXA; ++j) Fc[j] = S->F[0][r][j];
+    for (int k = 0; k < N; ++k) {
+        double Fn[NXA + 1];
+        const int kn = k + 1 < N ? k + 1 : k;
+#pragma unroll
+        for (int j = 0; j <= NXA; ++j) Fn[j] = S->F[kn][r][j];
+        double s = Fc[NXA];
+#pragma unroll
+        for (int j = 0; j < NXA; ++j) s = fma(Fc[j], d[j], s);
+        const bool mine = node == k + 1;
+#pragma unroll
+        for (int i = 0; i < NXA; ++i) { d[i] = readlane(s, i); dxo[i] = mine ? d[i] : dxo[i]; }
+#pragma unroll
+        for (int j = 0; j <= NXA; ++j) Fc[j] = Fn[j];
+    }
 }
 
 }  // namespace dartmpc

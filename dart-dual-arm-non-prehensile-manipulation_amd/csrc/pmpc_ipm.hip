@@ -25,22 +25,15 @@
 #include <stdint.h>
 
 #include "pmpc_ipm.h"
+#include "stamps.h"
 #include "wave.h"
 
 namespace dartmpc {
 
 #ifdef DART_STAMPS
 __device__ unsigned long long g_stamp[16];
-#define STAMP_DECL unsigned long long t_prev_ = __builtin_amdgcn_s_memtime(), t_acc_[12] = {0};
-#define STAMP_ADD(i, n) do { t_acc_[i] += (unsigned long long)(n); } while (0)
-#define STAMP(i) do { unsigned long long t_ = __builtin_amdgcn_s_memtime(); t_acc_[i] += t_ - t_prev_; t_prev_ = t_; } while (0)
-#define STAMP_FLUSH(b) do { if ((b) == 0 && threadIdx.x == 0) for (int q_ = 0; q_ < 12; ++q_) g_stamp[q_] = t_acc_[q_]; } while (0)
-#else
-#define STAMP_DECL
-#define STAMP_ADD(i, n) do {} while (0)
-#define STAMP(i) do {} while (0)
-#define STAMP_FLUSH(b) do {} while (0)
 #endif
+#define STAMP_FLUSH(b) STAMP_FLUSH_TO(g_stamp, b)
 
 // ---------------------------------------------------------------------------
 // model pieces

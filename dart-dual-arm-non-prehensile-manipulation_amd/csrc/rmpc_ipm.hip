@@ -27,6 +27,7 @@
 
 #include "ocp_wave.h"
 #include "rmpc_ipm.h"
+#include "stamps.h"
 #include "wave.h"
 
 namespace dartmpc {
@@ -34,6 +35,10 @@ namespace dartmpc {
 constexpr int RM_NMAXS = 32;      // max shooting nodes (N <= 31)
 constexpr int RM_NIQ = 6;         // inequality rows per node: du_x, du_y, vx-vmax, -vx-vmax, vy-vmax, -vy-vmax
 using RmLds = OcpLds<6, RM_NMAXS>;
+
+#ifdef DART_STAMPS
+__device__ unsigned long long g_stamp_rm[16];
+#endif
 
 struct RmShared {
     RmLds ocp;
@@ -49,8 +54,8 @@ struct RmModel {
 // continuous model (np_mpc...:178-186); also returns d f / d vx|vy of rows 1, 3 and tanh values
 __device__ __forceinline__ void rm_f(const RmModel& m, const double* y, double sa, double sb, double* f,
                                      double& j1vx, double& j1vy, double& j3vx, double& j3vy, double& tx, double& ty) {
-    tx = tanh(y[1] * m.ie);
-    ty = tanh(y[3] * m.ie);
+    tx = tanh_fast(y[1] * m.ie);
+    ty = tanh_fast(y[3] * m.ie);
     const double* a = m.th;
     const double* c = m.th + 7;
     f[0] = y[1];
@@ -143,6 +148,8 @@ __device__ __forceinline__ void rm_iq(const double* z, double vmax, double* c) {
 __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     __shared__ RmShared SH;
     RmLds* S = &SH.ocp;
+    const RiccatiRoles RR = riccati_roles<RmLds>();
+    STAMP_DECL
     const int b = blockIdx.x;
     const int k = threadIdx.x;
     const int N = a.N;
@@ -315,6 +322,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     double mu = 0.1, delta_last = 0.0;
     int status = -1, it = 0;
 
+    STAMP(0);
     for (it = 0; it < a.max_iter; ++it) {
         // ---------------- derivatives, residuals, optimality error ---------------------------
         double sa, ca, sb, cb;
@@ -419,6 +427,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             }
         }
         const double tau = fmax(0.99, 1.0 - mu);
+        STAMP(1);
 
         // ---------------- stage QPs into LDS ---------------------------------------------------
         const double isl0 = uon ? frcp(u[0] - lo) : 0.0, isl1 = uon ? frcp(u[1] - lo) : 0.0;
@@ -459,20 +468,24 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
                 for (int r = 0; r < 6; ++r) S->M[k][8][r] = cdef[r];
                 S->M[k][8][6] = 1.0;
             }
-            if (k == N) {   // terminal value function [[Q_N, q_N], [q_N^T, 0]]
-                for (int e = 0; e < tri(7); ++e) S->P[N][e] = 0.0;
-                S->P[N][hp(0, 0)] = sc * 2 * Qp; S->P[N][hp(2, 2)] = sc * 2 * Qp;
-                S->P[N][hp(1, 1)] = sc * 2 * Qv; S->P[N][hp(3, 3)] = sc * 2 * Qv;
+            if (k == N) {   // terminal surrogate G_N: value function [[Q_N, q_N], [q_N^T, 0]], Quu = I
+                double* GN = S->G[N];
+                for (int e = 0; e < tri(9); ++e) GN[e] = 0.0;
+                GN[hp(0, 0)] = sc * 2 * Qp; GN[hp(2, 2)] = sc * 2 * Qp;
+                GN[hp(1, 1)] = sc * 2 * Qv; GN[hp(3, 3)] = sc * 2 * Qv;
+                GN[hp(6, 6)] = 1.0; GN[hp(7, 7)] = 1.0;
 #pragma unroll
-                for (int j = 0; j < 6; ++j) S->P[N][hp(6, j)] = gq[j];
+                for (int j = 0; j < 6; ++j) GN[hp(8, j)] = gq[j];
             }
         }
         __syncthreads();
+        STAMP(2);
 
         // ---------------- Newton step: Riccati with inertia correction -----------------------
         double delta = 0.0, dapplied = 0.0;
-        bool ok = riccati_sweep(S, N);
-        for (int attempt = 1; attempt < 60 && !ok; ++attempt) {
+        bool ok = riccati_sweep(S, N, RR);
+        int attempt = 1;
+        for (; attempt < 60 && !ok; ++attempt) {
             delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last / 3.0))
                                    : delta * (delta_last == 0.0 ? 100.0 : 8.0);
             const double dd = delta - dapplied;
@@ -481,34 +494,36 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
                 for (int j = 0; j < 8; ++j) S->H[k][hp(j, j)] += dd;
             }
             if (k == N) {
-                // restore the terminal P (the sweep does not overwrite P[N]) and add delta on x~
+                // the sweep never overwrites the terminal surrogate: add delta on its x~ block
 #pragma unroll
-                for (int j = 0; j < 6; ++j) S->P[N][hp(j, j)] += dd;
+                for (int j = 0; j < 6; ++j) S->G[N][hp(j, j)] += dd;
             }
             dapplied = delta;
             __syncthreads();
-            ok = riccati_sweep(S, N);
+            ok = riccati_sweep(S, N, RR);
         }
+        STAMP_ADD(9, attempt);
+        STAMP(3);
         if (!ok) { status = -3; break; }
         if (delta > 0.0) delta_last = delta;
         if (k == 0) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) S->dz[0][i] = -gin[i];
+            for (int i = 0; i < 6; ++i) S->dx0[i] = -gin[i];
         }
-        __syncthreads();
-        forward_sweep(S, N);
-
+        closed_loop(S, N);
         double dx[6], dU[2], lamp[6];
+        forward_sweep(S, N, k, dx);
+        {
+            const int kk = xon ? k : 0;
+            const double* K0 = S->KK[uon ? k : 0][0];
+            const double* K1 = S->KK[uon ? k : 0][1];
+            double d0 = K0[6], d1 = K1[6];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) dx[i] = S->dz[xon ? k : 0][i];
-        dU[0] = uon ? S->dz[k][6] : 0.0; dU[1] = uon ? S->dz[k][7] : 0.0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            double t = S->P[xon ? k : 0][hp(i, 6)];
-#pragma unroll
-            for (int j = 0; j < 6; ++j) t = fma(S->P[xon ? k : 0][hp(i, j)], dx[j], t);
-            lamp[i] = -t;
+            for (int j = 0; j < 6; ++j) { d0 = fma(K0[j], dx[j], d0); d1 = fma(K1[j], dx[j], d1); }
+            dU[0] = uon ? d0 : 0.0; dU[1] = uon ? d1 : 0.0;
+            node_multiplier(S, kk, dx, dU, lamp);
         }
+        STAMP(4);
         // slack and multiplier steps
         double dS[RM_NIQ], dY[RM_NIQ], dvl[RM_NIQ], dvu[RM_NIQ], dzl[2], dzu[2];
         {
@@ -548,6 +563,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         amax = (double)wminf((float)amax) * (1.0 - 1.0 / 1048576.0);
         az = (double)wminf((float)az) * (1.0 - 1.0 / 1048576.0);
 
+        STAMP(5);
         // ---------------- filter line search -------------------------------------------------
         auto barrier_args = [&](const double* uu, const double* ss) {
             double pa = 1.0;
@@ -595,7 +611,9 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             for (int i = 0; i < RM_NIQ; ++i) tnl = fmaxf(tnl, fabsf((float)dS[i]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)s[i])));
         }
         const bool tiny = wmaxf(tnl) < 2.2e-15f;
-        for (int ls = 0; ls < 80; ++ls) {
+        STAMP(6);
+        int ls = 0;
+        for (; ls < 80; ++ls) {
             double xt[4], pt[2], ut[2], st_[RM_NIQ], gt[6];
 #pragma unroll
             for (int i = 0; i < 4; ++i) xt[i] = fma(alpha, dx[i], x[i]);
@@ -629,6 +647,8 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             alpha *= 0.5;
             if (alpha < amin) break;
         }
+        STAMP_ADD(10, ls + 1);
+        STAMP(7);
         if (!accepted) { status = -2; break; }
         if (!ftype && nfilt < kWave) {
             if (k == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
@@ -659,6 +679,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             }
         }
         theta = th_t;
+        STAMP(8);
     }
 
     // ---------------- outputs -------------------------------------------------------------
@@ -675,6 +696,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         }
         if (uon) { wo[4 * (N + 1) + 2 * k] = u[0]; wo[4 * (N + 1) + 2 * k + 1] = u[1]; }
     }
+    STAMP_FLUSH_TO(g_stamp_rm, b);
 }
 
 // Standalone batched RLS.update (np_mpc...:17-27): one p = 7 filter per workgroup, lanes as entries.
@@ -720,3 +742,10 @@ extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStre
     hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel, dim3(args->B), dim3(dartmpc::kWave), 0, stream, *args);
     return hipGetLastError();
 }
+
+#ifdef DART_STAMPS
+extern "C" hipError_t dartmpc_read_stamps_rmpc(unsigned long long* host_out) {
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp_rm), sizeof(unsigned long long) * 12, 0,
+                               hipMemcpyDeviceToHost);
+}
+#endif

@@ -118,6 +118,32 @@ __device__ __forceinline__ void tilt_sincos(bool poly, double x, double& s, doub
     else sincos(x, &s, &c);
 }
 
+// tanh(x) = em / (em + 2), em = expm1(2x) by Cody-Waite reduction and a degree-13 Taylor
+// polynomial on |r| <= ln2/2: <= 5e-16 relative error (host-checked against libm over
+// [-6, 6] and [-1e-3, 1e-3]), about a third of the instructions of the library tanh.
+__device__ __forceinline__ double tanh_fast(double x) {
+    const double y = fmin(fmax(2.0 * x, -80.0), 80.0);
+    const double n = __builtin_rint(y * 1.4426950408889634);
+    double r = fma(-n, 6.93147180369123816490e-01, y);
+    r = fma(-n, 1.90821492927058770002e-10, r);
+    double p = 1.0 / 6227020800.0;
+    p = fma(p, r, 1.0 / 479001600.0);
+    p = fma(p, r, 1.0 / 39916800.0);
+    p = fma(p, r, 1.0 / 3628800.0);
+    p = fma(p, r, 1.0 / 362880.0);
+    p = fma(p, r, 1.0 / 40320.0);
+    p = fma(p, r, 1.0 / 5040.0);
+    p = fma(p, r, 1.0 / 720.0);
+    p = fma(p, r, 1.0 / 120.0);
+    p = fma(p, r, 1.0 / 24.0);
+    p = fma(p, r, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    const double q = fma(p * r, r, r);
+    const double sc = __builtin_ldexp(1.0, (int)n);
+    const double em = fma(sc, q, sc - 1.0);
+    return em / (em + 2.0);
+}
+
 // IPOPT's Compare_le: lhs <= rhs up to 10 machine epsilons of |base| (filter acceptance tests)
 __device__ __forceinline__ bool cmp_le(double lhs, double rhs, double base) {
     return lhs - rhs <= 10.0 * 2.220446049250313e-16 * fabs(base);
