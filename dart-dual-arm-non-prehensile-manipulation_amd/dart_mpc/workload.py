@@ -155,3 +155,29 @@ def rmpc_batch(n_seeds: int = 1, seed0: int = 0, N: int = 20, n_rls: int = 50):
             out["phi_prev"][i] = _features(xp)
             out["y"][i] = (x0[[1, 3]] - xp[[1, 3]]) / 0.002
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# C5: LMPC batch = 18, N = 30.  The 34-vector model parameters are an input
+# fixture (the policy checkpoints cannot be loaded): pvec ~ U(0.01, 1.9)^34, the
+# output range of the policy's soft clip (LMPC/src/controller/rlmpc2.py:759-769).
+LMPC_SEED_BASE = 20251024 + 15485863
+
+
+def lmpc_batch(n_seeds: int = 1, seed0: int = 0):
+    """Return dict of C5 inputs for B = 18*n_seeds instances: state[B,8], u_prev[B,2],
+    pvec[B,34], target[B,8] (x0 as the PMPC workload plus theta, omega ~ U(-0.05, 0.05))."""
+    B = N_CONFIGS * n_seeds
+    out = dict(state=np.zeros((B, 8)), u_prev=np.zeros((B, 2)), pvec=np.zeros((B, 34)), target=np.zeros((B, 8)))
+    for s in range(n_seeds):
+        rng = np.random.default_rng(LMPC_SEED_BASE + seed0 + s)
+        for b in range(N_CONFIGS):
+            i = N_CONFIGS * s + b
+            out["state"][i] = [rng.uniform(-0.18, 0.18), rng.uniform(-0.15, 0.15),
+                               rng.uniform(-0.13, 0.13), rng.uniform(-0.15, 0.15),
+                               rng.uniform(-0.05, 0.05), rng.uniform(-0.05, 0.05),
+                               rng.uniform(-0.05, 0.05), rng.uniform(-0.05, 0.05)]
+            out["u_prev"][i] = rng.uniform(-0.2, 0.2, 2)
+            out["pvec"][i] = rng.uniform(0.01, 1.9, 34)
+            out["target"][i] = [rng.uniform(-0.15, 0.15), 0.0, rng.uniform(-0.12, 0.12), 0.0, 0.0, 0.0, 0.0, 0.0]
+    return out

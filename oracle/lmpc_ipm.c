@@ -1,0 +1,661 @@
+/*
+ * lmpc_ipm.c -- CPU oracle for the LMPC solve (8-state Stribeck / rolling model, pvec input).
+ *
+ * TEST INFRASTRUCTURE ONLY: loaded by tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg as the checker / timed CPU baseline.  Never
+ * linked into the shipped solver.
+ *
+ * Restates (LMPC/src/controller/rlmpc2.py): safe_dynamics :260-429 (the code's
+ * index map :301-334), _rk4 :431-436, the NLP :239-491 (w = [X; U] node-major,
+ * g = [x_0 - state; x_{k+1} - F(x_k, u_k)], cost :444-464 with the Delta-u rows
+ * u_0 - u_prev, u_k - u_{k-1}), solve with warm start w0 <- w_opt :494-524, and
+ * IPOPT with print_level 0 and max_iter / tol / acceptable_tol / acceptable_iter
+ * as passed (the reference: 50 / 1e-4 / 1e-3 / 5, :480-489; max_cpu_time 0.05 s
+ * is a wall-clock cap and is not restated).
+ * IPOPT's algorithm as in pmpc_ipm.c / rmpc_ipm.c: monotone mu, filter line
+ * search with second-order correction, inertia correction, bound_relax 1e-8,
+ * gradient-based scaling of the objective AND of the constraint rows
+ * (nlp_scaling_max_gradient 100), exact Hessian (second-order jets), and IPOPT's
+ * termination tests: optimal (scaled error <= tol, unscaled dual infeasibility
+ * <= 1, constraint violation <= 1e-4, complementarity <= 1e-4) and "acceptable"
+ * (acceptable_iter consecutive iterates with error <= acceptable_tol, violation
+ * and complementarity <= 1e-2).  The Delta-u coupling is carried by the
+ * augmented state [x_k; u_{k-1}] in the Riccati recursion.
+ * |v| is differentiated as CasADi does: sign(v), sign(0) = 0.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* IPOPT Compare_le: lhs <= rhs up to 10 machine epsilons of |base| */
+#define LE(l, r, b) ((l) - (r) <= 10.0 * 2.220446049250313e-16 * fabs(b))
+
+#define NXS 8           /* physical states px vx py vy th_x om_x th_y om_y */
+#define NA 10           /* augmented state [x; u_prev] */
+#define NU 2
+#define NZ 12           /* jet variables [x(8) up(2) u(2)] (up unused by the dynamics) */
+#define NH 78
+#define NMAX 64
+#define NPV 34
+#define GACC 9.81
+
+typedef struct { double v, d[NZ], h[NH]; } jet;
+static inline int hx(int i, int j) { if (i < j) { int t = i; i = j; j = t; } return i * (i + 1) / 2 + j; }
+static inline jet jconst(double c) { jet r; memset(&r, 0, sizeof r); r.v = c; return r; }
+static inline jet jvar(double v, int i) { jet r = jconst(v); r.d[i] = 1.0; return r; }
+static inline jet jaxpy(jet a, double s, jet b) {
+    jet r; r.v = a.v + s * b.v;
+    for (int i = 0; i < NZ; ++i) r.d[i] = a.d[i] + s * b.d[i];
+    for (int i = 0; i < NH; ++i) r.h[i] = a.h[i] + s * b.h[i];
+    return r;
+}
+static inline jet jadd(jet a, jet b) { return jaxpy(a, 1.0, b); }
+static inline jet jsub(jet a, jet b) { return jaxpy(a, -1.0, b); }
+static inline jet jscale(jet a, double s) {
+    jet r; r.v = s * a.v;
+    for (int i = 0; i < NZ; ++i) r.d[i] = s * a.d[i];
+    for (int i = 0; i < NH; ++i) r.h[i] = s * a.h[i];
+    return r;
+}
+static inline jet jaddc(jet a, double c) { a.v += c; return a; }
+static inline jet jmul(jet a, jet b) {
+    jet r; r.v = a.v * b.v;
+    for (int i = 0; i < NZ; ++i) r.d[i] = a.v * b.d[i] + b.v * a.d[i];
+    for (int i = 0; i < NZ; ++i) for (int j = 0; j <= i; ++j)
+        r.h[hx(i, j)] = a.v * b.h[hx(i, j)] + b.v * a.h[hx(i, j)] + a.d[i] * b.d[j] + a.d[j] * b.d[i];
+    return r;
+}
+/* f(a) with f' = f1, f'' = f2 at a.v */
+static inline jet junary(jet a, double f, double f1, double f2) {
+    jet r; r.v = f;
+    for (int i = 0; i < NZ; ++i) r.d[i] = f1 * a.d[i];
+    for (int i = 0; i < NZ; ++i) for (int j = 0; j <= i; ++j) r.h[hx(i, j)] = f1 * a.h[hx(i, j)] + f2 * a.d[i] * a.d[j];
+    return r;
+}
+static inline jet jsin(jet a) { return junary(a, sin(a.v), cos(a.v), -sin(a.v)); }
+static inline jet jtanh(jet a) { double t = tanh(a.v), d1 = 1.0 - t * t; return junary(a, t, d1, -2.0 * t * d1); }
+static inline jet jexp(jet a) { double e = exp(a.v); return junary(a, e, e, e); }
+static inline double sgn(double v) { return (v > 0) - (v < 0); }
+static inline jet jfabs(jet a) { return junary(a, fabs(a.v), sgn(a.v), 0.0); }
+
+typedef struct {
+    double m_x, m_y, c_x, c_y, k_x, k_y;
+    double F_s_x, F_c_x, B_x, v_s_x, eps_x, F_s_y, F_c_y, B_y, v_s_y, eps_y;
+    double I_x, I_y, r_x, r_y, c_rot_x, c_rot_y;
+    double F_s_rx, F_c_rx, B_rx, v_s_rx, eps_rx, F_s_ry, F_c_ry, B_ry, v_s_ry, eps_ry;
+    double h_x, h_y;
+} mparams;
+
+/* squash_param (:296-298) and the index map (:301-344) */
+static void unpack_params(const double *p, mparams *M) {
+#define SQ(v) (fabs(v) + 1e-6)
+    M->m_x = SQ(p[0]); M->m_y = SQ(p[1]); M->c_x = SQ(p[2]); M->c_y = SQ(p[3]); M->k_x = SQ(p[4]); M->k_y = SQ(p[5]);
+    M->F_s_x = p[6]; M->F_c_x = p[7]; M->B_x = p[8]; M->v_s_x = SQ(p[9]); M->eps_x = SQ(p[10]);
+    M->F_s_y = p[11]; M->F_c_y = p[12]; M->B_y = p[13]; M->v_s_y = SQ(p[14]); M->eps_y = SQ(p[15]);
+    M->I_x = SQ(p[16]); M->I_y = SQ(p[17]); M->r_x = SQ(p[18]); M->r_y = SQ(p[19]);
+    M->c_rot_x = SQ(p[20]); M->c_rot_y = SQ(p[21]);
+    M->F_s_rx = p[22]; M->F_c_rx = p[23]; M->B_rx = p[24]; M->v_s_rx = SQ(p[25]); M->eps_rx = SQ(p[26]);
+    M->F_s_ry = p[27]; M->F_c_ry = p[28]; M->B_ry = p[29]; M->v_s_ry = SQ(p[30]); M->eps_ry = SQ(p[31]);
+    M->h_x = SQ(p[32]); M->h_y = SQ(p[33]);
+#undef SQ
+}
+
+/* stribeck_fric (:372-376) */
+static jet jstribeck(jet v, double Fs, double Fc, double B, double vs, double eps) {
+    jet e = jexp(jscale(jfabs(v), -1.0 / (vs + 1e-12)));
+    jet s = jtanh(jscale(v, 1.0 / eps));
+    jet c = jaddc(jscale(e, Fs - Fc), Fc);
+    return jaxpy(jmul(s, c), B, v);
+}
+static double stribeck(double v, double Fs, double Fc, double B, double vs, double eps) {
+    double e = exp(-fabs(v) / (vs + 1e-12));
+    return tanh(v / eps) * (Fc + (Fs - Fc) * e) + B * v;
+}
+
+/* safe_dynamics (:260-429) on jets */
+static void dyn_jet(const mparams *M, const jet *x, const jet *u, jet *xd) {
+    jet Gx = jscale(jsin(u[0]), M->m_x * GACC), Gy = jscale(jsin(u[1]), M->m_y * GACC);
+    jet Ffx = jstribeck(x[1], M->F_s_x, M->F_c_x, M->B_x, M->v_s_x, M->eps_x);
+    jet Ffy = jstribeck(x[3], M->F_s_y, M->F_c_y, M->B_y, M->v_s_y, M->eps_y);
+    jet vsx = jaxpy(x[1], -M->r_x, x[7]);             /* vx - r_x om_y */
+    jet vsy = jaxpy(x[3], M->r_y, x[5]);              /* vy - (-r_y om_x) */
+    jet Frx = jstribeck(vsx, M->F_s_x, M->F_c_x, M->B_x, M->v_s_x, M->eps_x);
+    jet Fry = jstribeck(vsy, M->F_s_y, M->F_c_y, M->B_y, M->v_s_y, M->eps_y);
+    jet Tnx = jstribeck(x[5], M->F_s_rx, M->F_c_rx, M->B_rx, M->v_s_rx, M->eps_rx);
+    jet Tny = jstribeck(x[7], M->F_s_ry, M->F_c_ry, M->B_ry, M->v_s_ry, M->eps_ry);
+    jet tx = jscale(Fry, -M->r_y);
+    tx = jsub(tx, Tnx);
+    tx = jaxpy(tx, -M->c_rot_x, x[5]);
+    tx = jaxpy(tx, -M->m_y * GACC * M->h_x, jsin(x[4]));
+    jet ty = jscale(Frx, -M->r_x);
+    ty = jsub(ty, Tny);
+    ty = jaxpy(ty, -M->c_rot_y, x[7]);
+    ty = jaxpy(ty, -M->m_x * GACC * M->h_y, jsin(x[6]));
+    jet rx = jsub(jsub(jaxpy(jaxpy(Gx, -M->c_x, x[1]), -M->k_x, x[0]), Ffx), Frx);
+    jet ry = jsub(jsub(jaxpy(jaxpy(Gy, -M->c_y, x[3]), -M->k_y, x[2]), Ffy), Fry);
+    xd[0] = x[1]; xd[1] = jscale(rx, 1.0 / M->m_x);
+    xd[2] = x[3]; xd[3] = jscale(ry, 1.0 / M->m_y);
+    xd[4] = x[5]; xd[5] = jscale(tx, 1.0 / (M->I_x + 1e-12));
+    xd[6] = x[7]; xd[7] = jscale(ty, 1.0 / (M->I_y + 1e-12));
+}
+static void dyn_val(const mparams *M, const double *x, const double *u, double *xd) {
+    const double Gx = M->m_x * (GACC * sin(u[0])), Gy = M->m_y * (GACC * sin(u[1]));
+    const double Ffx = stribeck(x[1], M->F_s_x, M->F_c_x, M->B_x, M->v_s_x, M->eps_x);
+    const double Ffy = stribeck(x[3], M->F_s_y, M->F_c_y, M->B_y, M->v_s_y, M->eps_y);
+    const double Frx = stribeck(x[1] - M->r_x * x[7], M->F_s_x, M->F_c_x, M->B_x, M->v_s_x, M->eps_x);
+    const double Fry = stribeck(x[3] - (-M->r_y * x[5]), M->F_s_y, M->F_c_y, M->B_y, M->v_s_y, M->eps_y);
+    const double Tnx = stribeck(x[5], M->F_s_rx, M->F_c_rx, M->B_rx, M->v_s_rx, M->eps_rx);
+    const double Tny = stribeck(x[7], M->F_s_ry, M->F_c_ry, M->B_ry, M->v_s_ry, M->eps_ry);
+    const double tx = -M->r_y * Fry - Tnx - M->c_rot_x * x[5] + (-M->m_y * GACC * M->h_x * sin(x[4]));
+    const double ty = -M->r_x * Frx - Tny - M->c_rot_y * x[7] + (-M->m_x * GACC * M->h_y * sin(x[6]));
+    const double rx = Gx - M->c_x * x[1] - M->k_x * x[0] - Ffx - Frx;
+    const double ry = Gy - M->c_y * x[3] - M->k_y * x[2] - Ffy - Fry;
+    xd[0] = x[1]; xd[1] = rx / M->m_x; xd[2] = x[3]; xd[3] = ry / M->m_y;
+    xd[4] = x[5]; xd[5] = tx / (M->I_x + 1e-12); xd[6] = x[7]; xd[7] = ty / (M->I_y + 1e-12);
+}
+
+typedef struct {
+    int N; double Ts, Q[8], Qt[8], R[4], ulo, uhi;
+    mparams M;
+} prob_t;
+
+/* _rk4 (:431-436) */
+static void rk4_val(const prob_t *P, const double *x, const double *u, double *xn) {
+    double k1[8], k2[8], k3[8], k4[8], y[8], h = P->Ts;
+    dyn_val(&P->M, x, u, k1);
+    for (int i = 0; i < 8; ++i) y[i] = x[i] + 0.5 * h * k1[i];
+    dyn_val(&P->M, y, u, k2);
+    for (int i = 0; i < 8; ++i) y[i] = x[i] + 0.5 * h * k2[i];
+    dyn_val(&P->M, y, u, k3);
+    for (int i = 0; i < 8; ++i) y[i] = x[i] + h * k3[i];
+    dyn_val(&P->M, y, u, k4);
+    for (int i = 0; i < 8; ++i) xn[i] = x[i] + h * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]) / 6;
+}
+/* RK4 on jets over z = [x(8), up(2), u(2)]: value, Jacobian rows and nlam-contracted Hessian */
+static void rk4_derivs(const prob_t *P, const double *x, const double *u, const double *nlam,
+                       double *xn, double J[8][NZ], double H[NZ][NZ]) {
+    jet xj[8], uj[2], k1[8], k2[8], k3[8], k4[8], y[8];
+    const double h = P->Ts;
+    for (int i = 0; i < 8; ++i) xj[i] = jvar(x[i], i);
+    for (int i = 0; i < 2; ++i) uj[i] = jvar(u[i], NA + i);
+    dyn_jet(&P->M, xj, uj, k1);
+    for (int i = 0; i < 8; ++i) y[i] = jaxpy(xj[i], 0.5 * h, k1[i]);
+    dyn_jet(&P->M, y, uj, k2);
+    for (int i = 0; i < 8; ++i) y[i] = jaxpy(xj[i], 0.5 * h, k2[i]);
+    dyn_jet(&P->M, y, uj, k3);
+    for (int i = 0; i < 8; ++i) y[i] = jaxpy(xj[i], h, k3[i]);
+    dyn_jet(&P->M, y, uj, k4);
+    for (int a = 0; a < NZ; ++a) for (int b = 0; b < NZ; ++b) H[a][b] = 0.0;
+    for (int i = 0; i < 8; ++i) {
+        jet s = jaxpy(jaxpy(jaxpy(k1[i], 2.0, k2[i]), 2.0, k3[i]), 1.0, k4[i]);
+        jet r = jaxpy(xj[i], h / 6, s);
+        xn[i] = r.v;
+        for (int j = 0; j < NZ; ++j) J[i][j] = r.d[j];
+        for (int a = 0; a < NZ; ++a) for (int b = 0; b < NZ; ++b) H[a][b] += nlam[i] * r.h[hx(a, b)];
+    }
+}
+
+typedef struct {
+    double X[NA * (NMAX + 1)], U[NU * NMAX];
+    double lam[NA * (NMAX + 1)];                /* multipliers of the (unscaled) defect rows */
+    double zL[NU * NMAX], zU[NU * NMAX];
+    double A[NMAX][NA][NA], Bm[NMAX][NA][NU], Hs[NMAX][NZ][NZ];
+    double Lq[NMAX][3], Qux[NMAX][NU][NA], K[NMAX][NU][NA], Pm[NMAX + 1][NA][NA];
+    double kff[NMAX][NU], pv[NMAX + 1][NA];
+    double dX[NA * (NMAX + 1)], dU[NU * NMAX], lamp[NA * (NMAX + 1)], dzL[NU * NMAX], dzU[NU * NMAX];
+    double Xt[NA * (NMAX + 1)], Ut[NU * NMAX];
+    double dsc[NA * (NMAX + 1)];                /* constraint-row scaling factors */
+    double filt_th[256], filt_ph[256];
+} work_t;
+
+typedef struct {
+    const prob_t *P; const double *x0, *up0, *tgt; double sc, mu, lo, hi;
+} ctx_t;
+
+enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_MAXITER = -1, ST_LS_FAIL = -2, ST_INERTIA_FAIL = -3, ST_BAD_INPUT = -10 };
+
+static double g_relax = 1e-8;
+void oracle_lmpc_set_relax(double r) { g_relax = r; }
+
+static void stage_z(const double *X, const double *U, int k, double *z) {
+    for (int i = 0; i < NA; ++i) z[i] = X[NA * k + i];
+    z[NA] = U[NU * k]; z[NA + 1] = U[NU * k + 1];
+}
+
+/* cost :444-464: stage (x_k - t)^T Q (x_k - t) + [u; du]^T R [u; du], terminal Qt */
+static double objective(const prob_t *P, const double *X, const double *U, const double *t) {
+    double f = 0.0;
+    for (int k = 0; k <= P->N; ++k) {
+        const double *x = X + NA * k, *Q = k < P->N ? P->Q : P->Qt;
+        for (int i = 0; i < 8; ++i) f += Q[i] * (x[i] - t[i]) * (x[i] - t[i]);
+        if (k < P->N) {
+            const double *u = U + NU * k;
+            const double d0 = u[0] - x[8], d1 = u[1] - x[9];
+            f += P->R[0] * u[0] * u[0] + P->R[1] * u[1] * u[1] + P->R[2] * d0 * d0 + P->R[3] * d1 * d1;
+        }
+    }
+    return f;
+}
+static void cost_grad(const prob_t *P, const double *z, const double *t, int terminal, double *g) {
+    const double *Q = terminal ? P->Qt : P->Q;
+    for (int j = 0; j < NZ; ++j) g[j] = 0.0;
+    for (int i = 0; i < 8; ++i) g[i] = 2 * Q[i] * (z[i] - t[i]);
+    if (!terminal) {
+        const double d0 = z[10] - z[8], d1 = z[11] - z[9];
+        g[10] = 2 * P->R[0] * z[10] + 2 * P->R[2] * d0; g[11] = 2 * P->R[1] * z[11] + 2 * P->R[3] * d1;
+        g[8] = -2 * P->R[2] * d0; g[9] = -2 * P->R[3] * d1;
+    }
+}
+
+/* augmented defects (N+1 blocks of NA), unscaled; returns the scaled l1 norm (IPOPT's theta) */
+static double residuals(const ctx_t *C, const work_t *W, const double *X, const double *U, double g[][NA]) {
+    const prob_t *P = C->P; double th = 0.0;
+    for (int i = 0; i < 8; ++i) g[0][i] = X[i] - C->x0[i];
+    g[0][8] = X[8] - C->up0[0]; g[0][9] = X[9] - C->up0[1];
+    for (int k = 0; k < P->N; ++k) {
+        double xn[8];
+        rk4_val(P, X + NA * k, U + NU * k, xn);
+        for (int i = 0; i < 8; ++i) g[k + 1][i] = X[NA * (k + 1) + i] - xn[i];
+        g[k + 1][8] = X[NA * (k + 1) + 8] - U[NU * k]; g[k + 1][9] = X[NA * (k + 1) + 9] - U[NU * k + 1];
+    }
+    for (int k = 0; k <= P->N; ++k) for (int i = 0; i < NA; ++i) th += W->dsc[NA * k + i] * fabs(g[k][i]);
+    return th;
+}
+
+static double barrier_obj(const ctx_t *C, const double *X, const double *U) {
+    const prob_t *P = C->P;
+    double phi = C->sc * objective(P, X, U, C->tgt);
+    for (int j = 0; j < NU * P->N; ++j) {
+        double sl = U[j] - C->lo, su = C->hi - U[j];
+        if (!(sl > 0) || !(su > 0)) return INFINITY;
+        phi -= C->mu * (log(sl) + log(su));
+    }
+    return phi;
+}
+
+static int chol2(double a00, double a01, double a11, double L[3]) {
+    if (!(a00 > 0)) return 0;
+    double l00 = sqrt(a00), l10 = a01 / l00, d = a11 - l10 * l10;
+    if (!(d > 0)) return 0;
+    L[0] = l00; L[1] = l10; L[2] = sqrt(d);
+    return 1;
+}
+static void chol2_solve(const double L[3], const double *b, double *x) {
+    double y0 = b[0] / L[0], y1 = (b[1] - L[1] * y0) / L[2];
+    x[1] = y1 / L[2]; x[0] = (y0 - L[1] * x[1]) / L[0];
+}
+
+static void stage_qp(const ctx_t *C, const work_t *W, int k, double delta, double Hq[NZ][NZ], double *gq) {
+    const prob_t *P = C->P; const double sc = C->sc;
+    double z[NZ];
+    stage_z(W->X, W->U, k, z);
+    for (int a = 0; a < NZ; ++a) for (int b = 0; b < NZ; ++b) Hq[a][b] = W->Hs[k][a][b];
+    for (int i = 0; i < 8; ++i) Hq[i][i] += sc * 2 * P->Q[i];
+    for (int a = 0; a < 2; ++a) {
+        Hq[10 + a][10 + a] += sc * 2 * (P->R[a] + P->R[2 + a]); Hq[8 + a][8 + a] += sc * 2 * P->R[2 + a];
+        Hq[10 + a][8 + a] -= sc * 2 * P->R[2 + a]; Hq[8 + a][10 + a] -= sc * 2 * P->R[2 + a];
+    }
+    cost_grad(P, z, C->tgt, 0, gq);
+    for (int j = 0; j < NZ; ++j) gq[j] *= sc;
+    for (int a = 0; a < NU; ++a) {
+        const int j = NU * k + a;
+        double sl = W->U[j] - C->lo, su = C->hi - W->U[j];
+        Hq[10 + a][10 + a] += W->zL[j] / sl + W->zU[j] / su;
+        gq[10 + a] += -C->mu / sl + C->mu / su;
+    }
+    for (int a = 0; a < NZ; ++a) Hq[a][a] += delta;
+}
+
+static int riccati_factor(const ctx_t *C, work_t *W, double delta) {
+    const prob_t *P = C->P; const int N = P->N; const double sc = C->sc;
+    double (*Pn)[NA] = W->Pm[N];
+    for (int i = 0; i < NA; ++i) for (int j = 0; j < NA; ++j) Pn[i][j] = 0.0;
+    for (int i = 0; i < 8; ++i) Pn[i][i] = sc * 2 * P->Qt[i];
+    for (int i = 0; i < NA; ++i) Pn[i][i] += delta;
+    for (int k = N - 1; k >= 0; --k) {
+        double Hq[NZ][NZ], gq[NZ];
+        stage_qp(C, W, k, delta, Hq, gq);
+        double (*A)[NA] = W->A[k], (*Bm)[NU] = W->Bm[k], (*Pp)[NA] = W->Pm[k + 1];
+        double PA[NA][NA], PB[NA][NU], Quu[NU][NU];
+        for (int i = 0; i < NA; ++i) {
+            for (int j = 0; j < NA; ++j) { double s = 0; for (int m = 0; m < NA; ++m) s += Pp[i][m] * A[m][j]; PA[i][j] = s; }
+            for (int j = 0; j < NU; ++j) { double s = 0; for (int m = 0; m < NA; ++m) s += Pp[i][m] * Bm[m][j]; PB[i][j] = s; }
+        }
+        double Qxx[NA][NA];
+        for (int i = 0; i < NA; ++i) for (int j = 0; j < NA; ++j) {
+            double s = Hq[i][j]; for (int m = 0; m < NA; ++m) s += A[m][i] * PA[m][j]; Qxx[i][j] = s;
+        }
+        for (int a = 0; a < NU; ++a) {
+            for (int i = 0; i < NA; ++i) { double s = Hq[NA + a][i]; for (int m = 0; m < NA; ++m) s += Bm[m][a] * PA[m][i]; W->Qux[k][a][i] = s; }
+            for (int b = 0; b < NU; ++b) { double s = Hq[NA + a][NA + b]; for (int m = 0; m < NA; ++m) s += Bm[m][a] * PB[m][b]; Quu[a][b] = s; }
+        }
+        if (!chol2(Quu[0][0], 0.5 * (Quu[0][1] + Quu[1][0]), Quu[1][1], W->Lq[k])) return 0;
+        for (int i = 0; i < NA; ++i) {
+            double b2[2] = {W->Qux[k][0][i], W->Qux[k][1][i]}, x2[2];
+            chol2_solve(W->Lq[k], b2, x2); W->K[k][0][i] = -x2[0]; W->K[k][1][i] = -x2[1];
+        }
+        for (int i = 0; i < NA; ++i) for (int j = 0; j < NA; ++j)
+            W->Pm[k][i][j] = Qxx[i][j] + W->Qux[k][0][i] * W->K[k][0][j] + W->Qux[k][1][i] * W->K[k][1][j];
+        for (int i = 0; i < NA; ++i) for (int j = 0; j < i; ++j) { double s = 0.5 * (W->Pm[k][i][j] + W->Pm[k][j][i]); W->Pm[k][i][j] = W->Pm[k][j][i] = s; }
+    }
+    return 1;
+}
+
+/* vector pass + forward sweep for defect RHS rg (J d = -rg) */
+static void riccati_solve(const ctx_t *C, work_t *W, double rg[][NA]) {
+    const prob_t *P = C->P; const int N = P->N;
+    double zN[NZ], gN[NZ];
+    for (int i = 0; i < NA; ++i) zN[i] = W->X[NA * N + i];
+    zN[10] = zN[11] = 0.0;
+    cost_grad(P, zN, C->tgt, 1, gN);
+    for (int i = 0; i < NA; ++i) W->pv[N][i] = C->sc * gN[i];
+    for (int k = N - 1; k >= 0; --k) {
+        double Hq[NZ][NZ], gq[NZ];
+        stage_qp(C, W, k, 0.0, Hq, gq);   /* only the gradient is used */
+        double (*A)[NA] = W->A[k], (*Bm)[NU] = W->Bm[k], (*Pp)[NA] = W->Pm[k + 1], *pp = W->pv[k + 1];
+        double hh[NA], qx[NA], qu[NU], kf[2];
+        for (int i = 0; i < NA; ++i) { double s = pp[i]; for (int m = 0; m < NA; ++m) s -= Pp[i][m] * rg[k + 1][m]; hh[i] = s; }
+        for (int i = 0; i < NA; ++i) { double s = gq[i]; for (int m = 0; m < NA; ++m) s += A[m][i] * hh[m]; qx[i] = s; }
+        for (int a = 0; a < NU; ++a) { double s = gq[NA + a]; for (int m = 0; m < NA; ++m) s += Bm[m][a] * hh[m]; qu[a] = s; }
+        chol2_solve(W->Lq[k], qu, kf);
+        W->kff[k][0] = -kf[0]; W->kff[k][1] = -kf[1];
+        for (int i = 0; i < NA; ++i) W->pv[k][i] = qx[i] + W->Qux[k][0][i] * W->kff[k][0] + W->Qux[k][1][i] * W->kff[k][1];
+    }
+    for (int i = 0; i < NA; ++i) W->dX[i] = -rg[0][i];
+    for (int k = 0; k < N; ++k) {
+        double *dx = W->dX + NA * k, *du = W->dU + NU * k;
+        for (int a = 0; a < NU; ++a) { double s = W->kff[k][a]; for (int i = 0; i < NA; ++i) s += W->K[k][a][i] * dx[i]; du[a] = s; }
+        for (int i = 0; i < NA; ++i) {
+            double s = -rg[k + 1][i];
+            for (int m = 0; m < NA; ++m) s += W->A[k][i][m] * dx[m];
+            for (int a = 0; a < NU; ++a) s += W->Bm[k][i][a] * du[a];
+            W->dX[NA * (k + 1) + i] = s;
+        }
+    }
+    for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) {
+        double s = W->pv[k][i]; for (int m = 0; m < NA; ++m) s += W->Pm[k][i][m] * W->dX[NA * k + m];
+        W->lamp[NA * k + i] = -s;
+    }
+}
+
+static double frac_to_boundary(const ctx_t *C, const work_t *W, const double *dU, double tau) {
+    double a = 1.0;
+    for (int j = 0; j < NU * C->P->N; ++j) {
+        double sl = W->U[j] - C->lo, su = C->hi - W->U[j];
+        if (dU[j] < 0) a = fmin(a, -tau * sl / dU[j]);
+        if (dU[j] > 0) a = fmin(a, tau * su / dU[j]);
+    }
+    return a;
+}
+
+static void linearise(const prob_t *P, work_t *W) {
+    for (int k = 0; k < P->N; ++k) {
+        double xn[8], nl[8], J[8][NZ];
+        for (int i = 0; i < 8; ++i) nl[i] = -W->lam[NA * (k + 1) + i];
+        rk4_derivs(P, W->X + NA * k, W->U + NU * k, nl, xn, J, W->Hs[k]);
+        for (int i = 0; i < NA; ++i) { for (int j = 0; j < NA; ++j) W->A[k][i][j] = 0.0; W->Bm[k][i][0] = W->Bm[k][i][1] = 0.0; }
+        for (int i = 0; i < 8; ++i) {
+            for (int j = 0; j < 8; ++j) W->A[k][i][j] = J[i][j];
+            W->Bm[k][i][0] = J[i][NA]; W->Bm[k][i][1] = J[i][NA + 1];
+        }
+        W->Bm[k][8][0] = 1.0; W->Bm[k][9][1] = 1.0;
+    }
+}
+
+/* prm = [Q(8), Qt(8), R(4), u_lo, u_hi];  acc_tol / acc_iter: IPOPT acceptable_tol / acceptable_iter (0 = off) */
+int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_prev, const double *pvec,
+                      const double *target, const double *prm, const double *w_init, int max_iter, double tol,
+                      double acc_tol, int acc_iter, double *u0, double *fval, double *w_out, int32_t *iters_out) {
+    if (N < 1 || N > NMAX || !(Ts > 0) || !(prm[21] > prm[20])) return ST_BAD_INPUT;
+    work_t *W = (work_t *)calloc(1, sizeof(work_t));
+    if (!W) return ST_BAD_INPUT;
+    prob_t P;
+    memset(&P, 0, sizeof P);
+    P.N = N; P.Ts = Ts;
+    memcpy(P.Q, prm, sizeof(double) * 8); memcpy(P.Qt, prm + 8, sizeof(double) * 8); memcpy(P.R, prm + 16, sizeof(double) * 4);
+    P.ulo = prm[20]; P.uhi = prm[21];
+    unpack_params(pvec, &P.M);
+    const double lo = P.ulo - g_relax * fmax(1.0, fabs(P.ulo)), hi = P.uhi + g_relax * fmax(1.0, fabs(P.uhi));
+    const double mu_min = tol / 10, kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, s_max = 100.0;
+    const double gam_th = 1e-5, gam_ph = 1e-8, sw_delta = 1.0, s_th = 1.1, s_ph = 2.3, eta_ph = 1e-8, gam_al = 0.05, kap_soc = 0.99;
+    const int nU = NU * N, nA = NA * (N + 1);
+    ctx_t C;
+    memset(&C, 0, sizeof C);
+    C.P = &P; C.x0 = state; C.up0 = u_prev; C.tgt = target; C.mu = 0.1; C.lo = lo; C.hi = hi;
+    /* initial point: w_init (the worker's warm start, zeros on the first solve :492) */
+    for (int k = 0; k <= N; ++k)
+        for (int i = 0; i < 8; ++i) W->X[NA * k + i] = w_init ? w_init[8 * k + i] : 0.0;
+    for (int j = 0; j < nU; ++j) {
+        double u = w_init ? w_init[8 * (N + 1) + j] : 0.0;
+        double pl = fmin(1e-2 * fmax(1.0, fabs(lo)), 1e-2 * (hi - lo)), pu = fmin(1e-2 * fmax(1.0, fabs(hi)), 1e-2 * (hi - lo));
+        if (u < lo + pl) u = lo + pl;
+        if (u > hi - pu) u = hi - pu;
+        W->U[j] = u; W->zL[j] = 1.0; W->zU[j] = 1.0;
+    }
+    W->X[8] = u_prev[0]; W->X[9] = u_prev[1];
+    for (int k = 1; k <= N; ++k) { W->X[NA * k + 8] = W->U[NU * (k - 1)]; W->X[NA * k + 9] = W->U[NU * (k - 1) + 1]; }
+    /* gradient-based scaling of the objective and of every constraint row at the start point */
+    double gmax = 0.0;
+    for (int k = 0; k <= N; ++k) {
+        double z[NZ], g[NZ];
+        for (int i = 0; i < NA; ++i) z[i] = W->X[NA * k + i];
+        z[10] = k < N ? W->U[NU * k] : 0.0; z[11] = k < N ? W->U[NU * k + 1] : 0.0;
+        cost_grad(&P, z, target, k == N, g);
+        for (int j = 0; j < NZ; ++j) gmax = fmax(gmax, fabs(g[j]));
+    }
+    C.sc = gmax > 100.0 ? 100.0 / gmax : 1.0;
+    linearise(&P, W);
+    for (int i = 0; i < NA; ++i) W->dsc[i] = 1.0;
+    for (int k = 0; k < N; ++k) for (int i = 0; i < NA; ++i) {
+        double m = 1.0;   /* d/dx_{k+1} */
+        for (int j = 0; j < NA; ++j) m = fmax(m, fabs(W->A[k][i][j]));
+        m = fmax(m, fmax(fabs(W->Bm[k][i][0]), fabs(W->Bm[k][i][1])));
+        W->dsc[NA * (k + 1) + i] = m > 100.0 ? 100.0 / m : 1.0;
+    }
+
+    double (*g)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
+    double (*gt)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
+    double (*csg)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
+    double th = residuals(&C, W, W->X, W->U, g);
+    const double th_max = 1e4 * fmax(1.0, th), th_min = 1e-4 * fmax(1.0, th);
+    int nfilt = 0, status = ST_MAXITER, it, acc_count = 0;
+    double delta_last = 0.0;
+    for (it = 0;; ++it) {
+        if (it > 0) linearise(&P, W);
+        /* optimality error (IPOPT eq. 5) with scaled rows: y~ = lam / d */
+        double sum_l = 0, sum_z = 0, dinf = 0, pinf = 0, pinf_u = 0, c0 = 0;
+        for (int i = 0; i < nA; ++i) sum_l += fabs(W->lam[i]) / W->dsc[i];
+        for (int k = 0; k <= N; ++k) {
+            double z[NZ], gc[NZ], gl[NZ];
+            for (int i = 0; i < NA; ++i) z[i] = W->X[NA * k + i];
+            z[10] = k < N ? W->U[NU * k] : 0.0; z[11] = k < N ? W->U[NU * k + 1] : 0.0;
+            cost_grad(&P, z, target, k == N, gc);
+            for (int j = 0; j < NZ; ++j) gl[j] = C.sc * gc[j];
+            for (int i = 0; i < NA; ++i) gl[i] += W->lam[NA * k + i];
+            if (k < N) {
+                for (int m = 0; m < NA; ++m) {
+                    double l = W->lam[NA * (k + 1) + m];
+                    for (int i = 0; i < NA; ++i) gl[i] -= W->A[k][m][i] * l;
+                    gl[10] -= W->Bm[k][m][0] * l; gl[11] -= W->Bm[k][m][1] * l;
+                }
+                gl[10] += -W->zL[NU * k] + W->zU[NU * k]; gl[11] += -W->zL[NU * k + 1] + W->zU[NU * k + 1];
+                for (int j = 0; j < NZ; ++j) dinf = fmax(dinf, fabs(gl[j]));
+                for (int a = 0; a < NU; ++a) {
+                    const int j = NU * k + a;
+                    c0 = fmax(c0, fmax(fabs(W->zL[j] * (W->U[j] - lo)), fabs(W->zU[j] * (hi - W->U[j]))));
+                    sum_z += W->zL[j] + W->zU[j];
+                }
+            } else {
+                for (int i = 0; i < NA; ++i) dinf = fmax(dinf, fabs(gl[i]));
+            }
+            for (int i = 0; i < NA; ++i) {
+                pinf = fmax(pinf, W->dsc[NA * k + i] * fabs(g[k][i]));
+                pinf_u = fmax(pinf_u, fabs(g[k][i]));
+            }
+        }
+        const int nb = 2 * nU;
+        const double s_d = fmax(s_max, (sum_l + sum_z) / (nA + nb)) / s_max;
+        const double s_c = fmax(s_max, sum_z / nb) / s_max;
+        const double err = fmax(dinf / s_d, fmax(pinf, c0 / s_c));
+        /* IPOPT OptimalityErrorConvergenceCheck: optimal, then acceptable, then the iteration cap */
+        if (err <= tol && dinf / C.sc <= 1.0 && pinf_u <= 1e-4 && c0 / C.sc <= 1e-4) { status = ST_SOLVED; break; }
+        if (acc_iter > 0 && err <= acc_tol && pinf_u <= 1e-2 && c0 / C.sc <= 1e-2) {
+            if (++acc_count >= acc_iter) { status = ST_ACCEPTABLE; break; }
+        } else {
+            acc_count = 0;
+        }
+        if (it >= max_iter) { status = ST_MAXITER; break; }
+        for (;;) {
+            double cmu = 0;
+            for (int j = 0; j < nU; ++j)
+                cmu = fmax(cmu, fmax(fabs(W->zL[j] * (W->U[j] - lo) - C.mu), fabs(W->zU[j] * (hi - W->U[j]) - C.mu)));
+            if (fmax(dinf / s_d, fmax(pinf, cmu / s_c)) > kappa_eps * C.mu || C.mu <= mu_min) break;
+            C.mu = fmax(mu_min, fmin(kappa_mu * C.mu, pow(C.mu, theta_mu)));
+            nfilt = 0;
+        }
+        const double tau = fmax(0.99, 1.0 - C.mu);
+        double delta = 0.0;
+        int ok = riccati_factor(&C, W, 0.0);
+        for (int attempt = 0; !ok && attempt < 60; ++attempt) {
+            delta = (attempt == 0) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last / 3.0))
+                                   : delta * (delta_last == 0.0 ? 100.0 : 8.0);
+            ok = riccati_factor(&C, W, delta);
+        }
+        if (!ok) { status = ST_INERTIA_FAIL; break; }
+        if (delta > 0) delta_last = delta;
+        riccati_solve(&C, W, g);
+        double az = 1.0;
+        for (int j = 0; j < nU; ++j) {
+            double sl = W->U[j] - lo, su = hi - W->U[j], du = W->dU[j];
+            W->dzL[j] = C.mu / sl - W->zL[j] - W->zL[j] / sl * du;
+            W->dzU[j] = C.mu / su - W->zU[j] + W->zU[j] / su * du;
+            if (W->dzL[j] < 0) az = fmin(az, -tau * W->zL[j] / W->dzL[j]);
+            if (W->dzU[j] < 0) az = fmin(az, -tau * W->zU[j] / W->dzU[j]);
+        }
+        double amax = frac_to_boundary(&C, W, W->dU, tau);
+        const double phi = barrier_obj(&C, W->X, W->U);
+        double gTd = 0.0;
+        for (int k = 0; k <= N; ++k) {
+            double z[NZ], gc[NZ];
+            for (int i = 0; i < NA; ++i) z[i] = W->X[NA * k + i];
+            z[10] = k < N ? W->U[NU * k] : 0.0; z[11] = k < N ? W->U[NU * k + 1] : 0.0;
+            cost_grad(&P, z, target, k == N, gc);
+            for (int i = 0; i < NA; ++i) gTd += C.sc * gc[i] * W->dX[NA * k + i];
+            if (k < N)
+                for (int a = 0; a < NU; ++a) {
+                    const int j = NU * k + a;
+                    gTd += (C.sc * gc[10 + a] - C.mu / (W->U[j] - lo) + C.mu / (hi - W->U[j])) * W->dU[j];
+                }
+        }
+        double amin = gam_th;
+        if (gTd < 0) amin = fmin(gam_th, fmin(gam_ph * th / (-gTd), sw_delta * pow(th, s_th) / pow(-gTd, s_ph)));
+        if (th == 0.0 && gTd < 0) amin = 0.0;
+        amin *= gam_al;
+        double alpha = amax, th_t = 0, ph_t = 0;
+        int accepted = 0, ftype = 0;
+        double tn = 0.0;
+        for (int i = 0; i < nA; ++i) tn = fmax(tn, fabs(W->dX[i]) / (1.0 + fabs(W->X[i])));
+        for (int j = 0; j < nU; ++j) tn = fmax(tn, fabs(W->dU[j]) / (1.0 + fabs(W->U[j])));
+        const int tiny = tn < 10.0 * 2.220446049250313e-16;
+        for (int ls = 0; ls < 80 && !accepted; ++ls) {
+            if (alpha < amin && ls > 0) break;
+            for (int i = 0; i < nA; ++i) W->Xt[i] = W->X[i] + alpha * W->dX[i];
+            for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + alpha * W->dU[j];
+            th_t = residuals(&C, W, W->Xt, W->Ut, gt);
+            ph_t = barrier_obj(&C, W->Xt, W->Ut);
+            if (tiny) { accepted = 1; ftype = 1; break; }
+            for (int pass = 0; pass < 5; ++pass) {
+                int in_f = !(th_t < th_max) || !isfinite(ph_t);
+                for (int q = 0; q < nfilt && !in_f; ++q) if (th_t >= W->filt_th[q] && ph_t >= W->filt_ph[q]) in_f = 1;
+                if (!in_f) {
+                    int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
+                    if (th <= th_min && sw) { if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { accepted = 1; ftype = 1; } }
+                    else if (LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi)) accepted = 1;
+                }
+                if (accepted || ls > 0 || th_t < th) break;
+                if (pass == 0) { for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] = alpha * g[k][i] + gt[k][i]; }
+                else { for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] += gt[k][i]; }
+                /* SOC direction with the current factorisation */
+                double *sv = (double *)malloc(sizeof(double) * (2 * nA + nU));
+                memcpy(sv, W->dX, sizeof(double) * nA); memcpy(sv + nA, W->lamp, sizeof(double) * nA);
+                memcpy(sv + 2 * nA, W->dU, sizeof(double) * nU);
+                riccati_solve(&C, W, csg);
+                double asoc = frac_to_boundary(&C, W, W->dU, tau);
+                for (int i = 0; i < nA; ++i) W->Xt[i] = W->X[i] + asoc * W->dX[i];
+                for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + asoc * W->dU[j];
+                double th_prev = th_t;
+                th_t = residuals(&C, W, W->Xt, W->Ut, gt);
+                ph_t = barrier_obj(&C, W->Xt, W->Ut);
+                int inf = !(th_t < th_max) || !isfinite(ph_t), acc = 0;
+                for (int q = 0; q < nfilt && !inf; ++q) if (th_t >= W->filt_th[q] && ph_t >= W->filt_ph[q]) inf = 1;
+                if (!inf) {
+                    int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
+                    if (th <= th_min && sw) { if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { acc = 1; ftype = 1; } }
+                    else if (LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi)) acc = 1;
+                }
+                if (acc) { accepted = 1; alpha = asoc; free(sv); break; }
+                memcpy(W->dX, sv, sizeof(double) * nA); memcpy(W->lamp, sv + nA, sizeof(double) * nA);
+                memcpy(W->dU, sv + 2 * nA, sizeof(double) * nU);
+                free(sv);
+                if (th_t > kap_soc * th_prev) break;
+            }
+            if (!accepted) alpha *= 0.5;
+        }
+        if (!accepted) { status = ST_LS_FAIL; break; }
+        if (!ftype && nfilt < 256) { W->filt_th[nfilt] = (1 - gam_th) * th; W->filt_ph[nfilt] = phi - gam_ph * th; ++nfilt; }
+        memcpy(W->X, W->Xt, sizeof(double) * nA);
+        memcpy(W->U, W->Ut, sizeof(double) * nU);
+        memcpy(g, gt, sizeof(double) * NA * (N + 1));
+        th = th_t;
+        for (int i = 0; i < nA; ++i) W->lam[i] += alpha * (W->lamp[i] - W->lam[i]);
+        for (int j = 0; j < nU; ++j) {
+            double sl = W->U[j] - lo, su = hi - W->U[j];
+            double zl = W->zL[j] + az * W->dzL[j], zu = W->zU[j] + az * W->dzU[j];
+            W->zL[j] = fmax(fmin(zl, 1e10 * C.mu / sl), C.mu / (1e10 * sl));
+            W->zU[j] = fmax(fmin(zu, 1e10 * C.mu / su), C.mu / (1e10 * su));
+        }
+    }
+    if (iters_out) *iters_out = it;
+    if (u0) { u0[0] = W->U[0]; u0[1] = W->U[1]; }
+    if (fval) *fval = objective(&P, W->X, W->U, target);
+    if (w_out) {
+        for (int k = 0; k <= N; ++k) for (int i = 0; i < 8; ++i) w_out[8 * k + i] = W->X[NA * k + i];
+        memcpy(w_out + 8 * (N + 1), W->U, sizeof(double) * nU);
+    }
+    free(g); free(gt); free(csg);
+    free(W);
+    return status;
+}
+
+/* batched driver: state rows of 8, u_prev rows of 2, pvec rows of 34, target rows of 8, prm rows of 22,
+ * w rows of 8(N+1)+2N */
+int oracle_lmpc_solve_batch(int B, int N, double Ts, const double *state, const double *u_prev, const double *pvec,
+                            const double *target, const double *prm, const double *w_init, int max_iter, double tol,
+                            double acc_tol, int acc_iter, int nthreads, double *u0, double *f, double *w_out,
+                            int32_t *status, int32_t *iters) {
+    const int nw = 8 * (N + 1) + 2 * N;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    for (int b = 0; b < B; ++b) {
+        int32_t itb = 0;
+        status[b] = oracle_lmpc_solve(N, Ts, state + 8 * b, u_prev + 2 * b, pvec + NPV * b, target + 8 * b, prm + 22 * b,
+                                      w_init ? w_init + (size_t)nw * b : NULL, max_iter, tol, acc_tol, acc_iter,
+                                      u0 + 2 * b, f + b, w_out ? w_out + (size_t)nw * b : NULL, &itb);
+        iters[b] = itb;
+    }
+    (void)nthreads;
+    return 0;
+}
+
+/* one RK4 step (:431-436) for B states: the dynamics KAT hook */
+void oracle_lmpc_rk4(int B, double Ts, const double *x, const double *u, const double *pvec, double *xn) {
+    for (int b = 0; b < B; ++b) {
+        prob_t P;
+        memset(&P, 0, sizeof P);
+        P.Ts = Ts;
+        unpack_params(pvec + NPV * b, &P.M);
+        rk4_val(&P, x + 8 * b, u + 2 * b, xn + 8 * b);
+    }
+}

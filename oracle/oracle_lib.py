@@ -111,3 +111,53 @@ def rls_update(theta, P, phi, y, lam=0.995):
     Pm = np.ascontiguousarray(P, np.float64).copy()
     rlib().oracle_rls_update(_p(th), _p(Pm), _p(np.ascontiguousarray(phi, np.float64)), float(y), lam)
     return th, Pm
+
+
+_llib = None
+
+
+def llib():
+    global _llib
+    if _llib is None:
+        L = ctypes.CDLL(os.path.join(_HERE, "liboracle_lmpc.so"))
+        L.oracle_lmpc_solve_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, _dp, _dp, _dp, _dp, _dp,
+                                              _dp, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                              ctypes.c_int, _dp, _dp, _dp, _ip, _ip]
+        L.oracle_lmpc_solve_batch.restype = ctypes.c_int
+        L.oracle_lmpc_set_relax.argtypes = [ctypes.c_double]
+        L.oracle_lmpc_set_relax.restype = None
+        L.oracle_lmpc_rk4.argtypes = [ctypes.c_int, ctypes.c_double, _dp, _dp, _dp, _dp]
+        L.oracle_lmpc_rk4.restype = None
+        _llib = L
+    return _llib
+
+
+LMPC_PRM_DEFAULT = np.array([200.0, 2.0, 200.0, 2.0, 0.0, 0.0, 0.0, 0.0,      # Q   (LMPC/src/run.py:118)
+                             200.0, 2.0, 200.0, 2.0, 0.0, 0.0, 0.0, 0.0,      # Qt  (:119)
+                             0.1, 0.1, 1.0, 1.0,                              # R   (:120)
+                             -0.4, 0.4])                                      # u_bounds (:121)
+
+
+def lmpc_solve_batch(state, u_prev, pvec, target, prm=None, N=20, Ts=0.002, w_init=None, max_iter=50, tol=1e-4,
+                     acc_tol=1e-3, acc_iter=5, nthreads=1, want_w=True, relax=1e-8):
+    """LMPC oracle; defaults are the reference's IPOPT options (rlmpc2.py:480-489)."""
+    c = lambda a: np.ascontiguousarray(a, np.float64)
+    state, u_prev, pvec, target = c(state), c(u_prev), c(pvec), c(target)
+    B = state.shape[0]
+    prm = c(np.tile(LMPC_PRM_DEFAULT, (B, 1)) if prm is None else prm)
+    nw = 8 * (N + 1) + 2 * N
+    wi = None if w_init is None else c(w_init)
+    u0 = np.zeros((B, 2)); f = np.zeros(B); w = np.zeros((B, nw)) if want_w else None
+    st = np.zeros(B, np.int32); it = np.zeros(B, np.int32)
+    llib().oracle_lmpc_set_relax(float(relax))
+    llib().oracle_lmpc_solve_batch(B, N, Ts, _p(state), _p(u_prev), _p(pvec), _p(target), _p(prm),
+                                   _p(wi) if wi is not None else None, max_iter, tol, acc_tol, acc_iter, nthreads,
+                                   _p(u0), _p(f), _p(w) if want_w else None, _p(st, _ip), _p(it, _ip))
+    return dict(u0=u0, f=f, w=w, status=st, iters=it)
+
+
+def lmpc_rk4(x, u, pvec, Ts=0.002):
+    x, u, pvec = (np.ascontiguousarray(a, np.float64) for a in (x, u, pvec))
+    xn = np.zeros_like(x)
+    llib().oracle_lmpc_rk4(x.shape[0], Ts, _p(x), _p(u), _p(pvec), _p(xn))
+    return xn

@@ -26,3 +26,10 @@ def rmpc_goldens():
     import numpy as np
     d = np.load(os.path.join(ROOT, "tests", "golden", "rmpc_goldens.npz"))
     return {k: d[k] for k in d.files}
+
+
+@pytest.fixture(scope="session")
+def lmpc_goldens():
+    import numpy as np
+    d = np.load(os.path.join(ROOT, "tests", "golden", "lmpc_goldens.npz"))
+    return {k: d[k] for k in d.files}
