@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-calls", type=int, default=200, help="calls of the host-pointer (PCIe-inclusive) path")
     ap.add_argument("--rmpc-steps", type=int, default=200, help="launches of the supplementary C3 RMPC line (0 = skip)")
+    ap.add_argument("--lmpc-steps", type=int, default=100, help="launches of the supplementary C5 LMPC line (0 = skip)")
     ap.add_argument("--saturation-batch", type=int, default=18 * 1024,
                     help="supplementary single-launch batch for the saturated rate (0 = skip)")
     return ap.parse_args()
@@ -118,6 +119,75 @@ def bench_rmpc(args, torch, dev, stream, dart_mpc):
         cdt = time.perf_counter() - c0
         out["cpu_baseline"] = {"value": solved / cdt, "unit": "solves/s", "cores": nt, "kind": "port",
                                "sample": f"C oracle (oracle/rmpc_ipm.c), {solved} cold-start C3 solves in {cdt:.1f} s"}
+    s.close()
+    return out
+
+
+def bench_lmpc(args, torch, dev, stream, dart_mpc):
+    """C5: LMPC batch=18, N=30 (the reference runs N=20), the reference's IPOPT options
+    (tol 1e-4, max_iter 50, acceptable 1e-3 x 5), cold start, inputs resident in HBM."""
+    from dart_mpc.workload import lmpc_batch
+    from dart_mpc._lib import LMPC_PRM_DEFAULT
+    B, K, N = 18, args.lmpc_steps, 30
+    D = [lmpc_batch(1, seed0=7000 + i) for i in range(K + 3)]
+    T = lambda k: torch.tensor(np.stack([d[k] for d in D]), dtype=torch.float64, device=dev).contiguous()
+    ST0, UP, PV, TG = T("state"), T("u_prev"), T("pvec"), T("target")
+    PR = torch.tensor(np.tile(LMPC_PRM_DEFAULT, (B, 1)), dtype=torch.float64, device=dev)
+    U0 = torch.empty((K + 3, B, 2), dtype=torch.float64, device=dev)
+    FV = torch.empty((K + 3, B), dtype=torch.float64, device=dev)
+    ST = torch.empty((K + 3, B), dtype=torch.int32, device=dev)
+    IT = torch.empty((K + 3, B), dtype=torch.int32, device=dev)
+    s = dart_mpc.LmpcSolver(N=N, B_max=B, device=dev.index)
+    sp = stream.cuda_stream
+
+    def launch(i):
+        s.solve_batch_dev(B, ST0[i].data_ptr(), UP[i].data_ptr(), PV[i].data_ptr(), TG[i].data_ptr(), PR.data_ptr(),
+                          U0[i].data_ptr(), FV[i].data_ptr(), ST[i].data_ptr(), IT[i].data_ptr(), stream=sp)
+
+    for i in range(3):
+        launch(i)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for j in range(K):
+            ev[j][0].record(stream)
+            launch(3 + j)
+            ev[j][1].record(stream)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    st, its = ST[3:].cpu().numpy(), IT[3:].cpu().numpy()
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_lib   # checker + CPU baseline only
+    d = D[3]
+    ref = oracle_lib.lmpc_solve_batch(d["state"], d["u_prev"], d["pvec"], d["target"], N=N, nthreads=4, want_w=False)
+    exact = oracle_lib.lmpc_solve_batch(d["state"], d["u_prev"], d["pvec"], d["target"], N=N, tol=1e-11, acc_iter=0,
+                                        max_iter=500, nthreads=4, want_w=False)
+    u0 = U0[3].cpu().numpy()
+    ok = (exact["status"] == 0) & (st[0] >= 0)
+    out = {"workload": "C5: LMPC batch=18, N=30, Ts=0.002, pvec~U(0.01,1.9)^34 input, reference IPOPT options "
+                       "(tol 1e-4, max_iter 50, acceptable 1e-3 x 5), cold start",
+           "solves_per_s": B * K / dt, "ms_per_step": dt / K * 1e3, "kernel_ms": kern_ms,
+           "status_ok_frac": float(np.mean(st >= 0)), "iters_mean": float(its.mean()),
+           "max_abs_u0_err_vs_oracle_same_options": float(np.max(np.abs(u0 - ref["u0"]))),
+           "max_abs_u0_err_vs_exact_optimum": float(np.max(np.abs(u0[ok] - exact["u0"][ok]))) if ok.any() else None}
+    if not args.no_cpu_baseline:
+        try:
+            ncores = len(os.sched_getaffinity(0))
+        except AttributeError:
+            ncores = os.cpu_count() or 1
+        nt = max(1, min(16, ncores))
+        Db = lmpc_batch(max(1, nt // 2), seed0=4242)
+        solved, c0 = 0, time.perf_counter()
+        while time.perf_counter() - c0 < min(6.0, args.cpu_seconds):
+            oracle_lib.lmpc_solve_batch(Db["state"], Db["u_prev"], Db["pvec"], Db["target"], N=N, nthreads=nt,
+                                        want_w=False)
+            solved += Db["state"].shape[0]
+        cdt = time.perf_counter() - c0
+        out["cpu_baseline"] = {"value": solved / cdt, "unit": "solves/s", "cores": nt, "kind": "port",
+                               "sample": f"C oracle (oracle/lmpc_ipm.c, exact jet Hessian), {solved} cold-start C5 "
+                                         f"solves in {cdt:.1f} s"}
     s.close()
     return out
 
@@ -257,6 +327,11 @@ def main():
     if rank == 0 and args.rmpc_steps > 0:
         rmpc = bench_rmpc(args, torch, dev, stream, dart_mpc)
 
+    # supplementary C5 (BASELINE.json configs[4]): LMPC batch=18, N=30, pvec as input
+    lmpc = None
+    if rank == 0 and args.lmpc_steps > 0:
+        lmpc = bench_lmpc(args, torch, dev, stream, dart_mpc)
+
     # HBM traffic per launch from the committed rocprofv3 PMC passes of this build (tools/profile_round.sh)
     traffic = None
     pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")))
@@ -295,6 +370,7 @@ def main():
             "saturation": saturation,
             "host_path_pcie_inclusive": host_path,
             "rmpc_c3": rmpc,
+            "lmpc_c5": lmpc,
         }
         print(json.dumps(line))
     if world > 1:

@@ -12,6 +12,7 @@
 #include "dart_mpc.h"
 #include "pmpc_ipm.h"
 #include "rmpc_ipm.h"
+#include "lmpc_ipm.h"
 
 struct dart_mpc_handle {
     dart_mpc_config cfg;
@@ -43,9 +44,10 @@ int fail(dart_mpc_handle* h, int code, const char* what, hipError_t e = hipSucce
 
 int check_cfg(const dart_mpc_config* c) {
     if (!c) return 0;
-    if (c->variant != DART_MPC_PMPC && c->variant != DART_MPC_RMPC) return 0;
-    if (c->N < 1 || c->N > (c->variant == DART_MPC_RMPC ? 31 : 63)) return 0;
+    if (c->variant != DART_MPC_PMPC && c->variant != DART_MPC_RMPC && c->variant != DART_MPC_LMPC) return 0;
+    if (c->N < 1 || c->N > (c->variant == DART_MPC_PMPC ? 63 : 31)) return 0;
     if (!(c->Ts > 0.0) || !(c->tol > 0.0) || !(c->gravity == c->gravity) || c->max_iter < 1 || c->B_max < 1) return 0;
+    if (c->acceptable_iter < 0 || (c->acceptable_iter > 0 && !(c->acceptable_tol > 0.0))) return 0;
     return 1;
 }
 
@@ -72,11 +74,16 @@ void dart_mpc_config_default(dart_mpc_config* c) {
     c->max_iter = 3000;
     c->B_max = 1024;
     c->gravity = -9.81;
+    c->acceptable_tol = 1e-6;      // IPOPT defaults
+    c->acceptable_iter = 15;
+    c->reserved = 0;
 }
 
 int dart_mpc_nw(int N) { return 6 * (N + 1) + 2 * N; }
 
 int dart_rmpc_nw(int N) { return 4 * (N + 1) + 2 * N; }
+
+int dart_lmpc_nw(int N) { return 8 * (N + 1) + 2 * N; }
 
 int dart_mpc_abi_version(void) { return DART_MPC_ABI_VERSION; }
 
@@ -91,7 +98,10 @@ int dart_mpc_create(const dart_mpc_config* cfg, int device, dart_mpc_handle** ou
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     const size_t B = (size_t)cfg->B_max;
-    if (cfg->variant == DART_MPC_RMPC) {
+    if (cfg->variant == DART_MPC_LMPC) {
+        const size_t nw = (size_t)dart_lmpc_nw(cfg->N);
+        h->nd = B * (8 + 2 + dartmpc::LM_NPV + 8 + dartmpc::LM_NPRM + nw + 2 + 1 + nw);
+    } else if (cfg->variant == DART_MPC_RMPC) {
         const size_t nw = (size_t)dart_rmpc_nw(cfg->N);
         h->nd = B * (4 + 2 + 14 + 98 + 7 + 2 + 4 * (cfg->N + 1) + 10 + nw + 2 + 1 + nw);
     } else {
@@ -230,6 +240,68 @@ int dart_rmpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const dou
         HIPCHK(h, dn(theta, d_th, sizeof(double) * 14 * B), "copy theta");
         HIPCHK(h, dn(rls_P, d_P, sizeof(double) * 98 * B), "copy rls_P");
     }
+    HIPCHK(h, dn(status, d_st, sizeof(int32_t) * B), "copy status");
+    HIPCHK(h, dn(iters, d_it, sizeof(int32_t) * B), "copy iters");
+    HIPCHK(h, hipStreamSynchronize(s), "hipStreamSynchronize");
+    return DART_MPC_OK;
+}
+
+int dart_lmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* state, const double* u_prev,
+                              const double* pvec, const double* target, const double* prm, const double* w_warm,
+                              double* u0, double* f, double* w_out, int32_t* status, int32_t* iters, void* stream) {
+    if (!h) return DART_MPC_EINVAL;
+    if (h->cfg.variant != DART_MPC_LMPC) return fail(h, DART_MPC_EINVAL, "handle is not an LMPC handle");
+    if (B < 0 || (B > 0 && (!state || !u_prev || !pvec || !target || !prm || !u0 || !f || !status || !iters)))
+        return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
+    if (B == 0) return DART_MPC_OK;
+    HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    dartmpc::LmpcArgs a;
+    a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter;
+    a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter;
+    a.state = state; a.u_prev = u_prev; a.pvec = pvec; a.target = target; a.prm = prm; a.w_warm = w_warm;
+    a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
+    HIPCHK(h, dartmpc_launch_lmpc(&a, stream ? (hipStream_t)stream : h->stream), "kernel launch");
+    return DART_MPC_OK;
+}
+
+int dart_lmpc_solve_batch(dart_mpc_handle* h, int B, const double* state, const double* u_prev, const double* pvec,
+                          const double* target, const double* prm, const double* w_warm, double* u0, double* f,
+                          double* w_out, int32_t* status, int32_t* iters, void* stream) {
+    if (!h) return DART_MPC_EINVAL;
+    if (h->cfg.variant != DART_MPC_LMPC) return fail(h, DART_MPC_EINVAL, "handle is not an LMPC handle");
+    if (B < 0 || (B > 0 && (!state || !u_prev || !pvec || !target || !prm || !u0 || !f || !status || !iters)))
+        return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
+    if (B > h->cfg.B_max) return fail(h, DART_MPC_EINVAL, "batch larger than B_max");
+    if (B == 0) return DART_MPC_OK;
+    HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    const size_t nw = (size_t)dart_lmpc_nw(h->cfg.N), Bm = (size_t)h->cfg.B_max;
+    double* p = h->dbuf;
+    double* d_st0 = p; p += Bm * 8;
+    double* d_up = p; p += Bm * 2;
+    double* d_pv = p; p += Bm * dartmpc::LM_NPV;
+    double* d_tg = p; p += Bm * 8;
+    double* d_prm = p; p += Bm * dartmpc::LM_NPRM;
+    double* d_ww = p; p += Bm * nw;
+    double* d_u0 = p; p += Bm * 2;
+    double* d_f = p; p += Bm;
+    double* d_wo = p;
+    int32_t* d_st = h->ibuf;
+    int32_t* d_it = d_st + Bm;
+    auto up = [&](double* d, const double* hsrc, size_t n) { return hipMemcpyAsync(d, hsrc, sizeof(double) * n, hipMemcpyHostToDevice, s); };
+    HIPCHK(h, up(d_st0, state, 8 * B), "copy state");
+    HIPCHK(h, up(d_up, u_prev, 2 * B), "copy u_prev");
+    HIPCHK(h, up(d_pv, pvec, dartmpc::LM_NPV * B), "copy pvec");
+    HIPCHK(h, up(d_tg, target, 8 * B), "copy target");
+    HIPCHK(h, up(d_prm, prm, dartmpc::LM_NPRM * B), "copy prm");
+    if (w_warm) HIPCHK(h, up(d_ww, w_warm, nw * B), "copy w_warm");
+    int rc = dart_lmpc_solve_batch_dev(h, B, d_st0, d_up, d_pv, d_tg, d_prm, w_warm ? d_ww : nullptr, d_u0, d_f,
+                                       w_out ? d_wo : nullptr, d_st, d_it, s);
+    if (rc) return rc;
+    auto dn = [&](void* hdst, const void* d, size_t bytes) { return hipMemcpyAsync(hdst, d, bytes, hipMemcpyDeviceToHost, s); };
+    HIPCHK(h, dn(u0, d_u0, sizeof(double) * 2 * B), "copy u0");
+    HIPCHK(h, dn(f, d_f, sizeof(double) * B), "copy f");
+    if (w_out) HIPCHK(h, dn(w_out, d_wo, sizeof(double) * nw * B), "copy w_out");
     HIPCHK(h, dn(status, d_st, sizeof(int32_t) * B), "copy status");
     HIPCHK(h, dn(iters, d_it, sizeof(int32_t) * B), "copy iters");
     HIPCHK(h, hipStreamSynchronize(s), "hipStreamSynchronize");

@@ -1,0 +1,31 @@
+// lmpc_ipm.h -- launch arguments of the batched LMPC interior-point kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dartmpc {
+
+constexpr int LM_NPRM = 22;   // [Q(8), Qt(8), R(4), u_lo, u_hi]
+constexpr int LM_NPV = 34;    // model parameter vector (LMPC/src/controller/rlmpc2.py:301-344)
+
+struct LmpcArgs {
+    int B, N;
+    double Ts, tol, acc_tol;
+    int max_iter, acc_iter;
+    const double* state;     // [B][8]  [px, vx, py, vy, theta_x, omega_x, theta_y, omega_y]
+    const double* u_prev;    // [B][2]
+    const double* pvec;      // [B][34]
+    const double* target;    // [B][8]
+    const double* prm;       // [B][22]
+    const double* w_warm;    // [B][8(N+1)+2N] nullable
+    double* u0;              // [B][2]
+    double* f;               // [B]
+    double* w_out;           // [B][8(N+1)+2N] nullable
+    int32_t* status;         // [B]
+    int32_t* iters;          // [B]
+};
+
+}  // namespace dartmpc
+
+extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStream_t stream);
+extern "C" size_t dartmpc_lmpc_lds_bytes(void);

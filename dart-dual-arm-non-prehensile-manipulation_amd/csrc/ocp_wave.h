@@ -39,7 +39,7 @@ struct OcpLds {
     static constexpr int NT = tri(ND);        // packed entries of G / Ht
     static constexpr int NTP = even(NT);
     static constexpr int NF = even(NXA + 1);  // closed-loop row stride [Phi row | f]
-    static_assert(NT <= 64, "one lane per entry of G");
+    static constexpr int EPL = (NT + 63) / 64;     // packed entries of G per lane
     double M[NMAXS][ND][NC];                  // M[k][j][m] = M_k(m, j): column j of M_k
     double H[NMAXS][NTP];                     // stage Hessian + gradient, packed symmetric
     double G[NMAXS][NTP];                     // G_k; G[N] = terminal surrogate (Pt_N, Quu = I)
@@ -58,23 +58,28 @@ __host__ __device__ constexpr int gzz(int p, int q) { return hp(zi_of_p<NXA>(p),
 template <int NXA>
 __host__ __device__ constexpr int gzu(int p, int a) { return hp(zi_of_p<NXA>(p), NXA + a); }
 
-// Per-lane role of the backward sweep (packed entry (i, j) of G), decoded once.
+// Per-lane roles of the backward sweep (packed entries e = lane + 64 r of G), decoded once.
+template <int EPL>
 struct RiccatiRoles {
-    int ci, cj;          // column offsets (j * NC) of a_i, a_j in M_k
-    bool on;             // lane owns an entry
+    int ci[EPL], cj[EPL];   // column offsets (j * NC) of a_i, a_j in M_k
+    bool on[EPL];           // lane owns entry r
 };
 
 template <class L>
-__device__ RiccatiRoles riccati_roles() {
+__device__ RiccatiRoles<L::EPL> riccati_roles() {
     constexpr int NT = L::NT, NC = L::NC;
     const int lane = threadIdx.x;
-    RiccatiRoles r{};
-    int i = 0;
-    const int e = lane < NT ? lane : 0;
-    while (tri(i + 1) <= e) ++i;
-    const int j = e - tri(i);
-    r.ci = i * NC; r.cj = j * NC;
-    r.on = lane < NT;
+    RiccatiRoles<L::EPL> r{};
+#pragma unroll
+    for (int q = 0; q < L::EPL; ++q) {
+        const int e0 = lane + 64 * q;
+        const int e = e0 < NT ? e0 : 0;
+        int i = 0;
+        while (tri(i + 1) <= e) ++i;
+        const int j = e - tri(i);
+        r.ci[q] = i * NC; r.cj[q] = j * NC;
+        r.on[q] = e0 < NT;
+    }
     return r;
 }
 
@@ -94,7 +99,7 @@ __device__ __forceinline__ bool quu_inverse(const double* Gk, double& i00, doubl
 // lane e owning packed entry (i, j).  G[N] must hold the terminal surrogate.  Returns false
 // (wave-uniform) if some Quu is not positive definite (inertia correction needed).
 template <class L>
-__device__ bool riccati_sweep(L* S, int N, const RiccatiRoles& R) {
+__device__ bool riccati_sweep(L* S, int N, const RiccatiRoles<L::EPL>& R) {
     constexpr int NXA = L::NXA, NP = L::NP;
     const int lane = threadIdx.x;
     bool ok = true;
@@ -102,9 +107,12 @@ __device__ bool riccati_sweep(L* S, int N, const RiccatiRoles& R) {
         const double* Gn = S->G[k + 1];
         double i00, i01, i11;
         ok = quu_inverse<NXA>(Gn, i00, i01, i11) && ok;
-        if (R.on) {
-            const double* ai = &S->M[k][0][0] + R.ci;
-            const double* aj = &S->M[k][0][0] + R.cj;
+        double gout[L::EPL];
+#pragma unroll
+        for (int q = 0; q < L::EPL; ++q) {
+            if (!R.on[q]) continue;
+            const double* ai = &S->M[k][0][0] + R.ci[q];
+            const double* aj = &S->M[k][0][0] + R.cj[q];
             double vi[NP], vj[NP];
 #pragma unroll
             for (int m = 0; m < NP; ++m) { vi[m] = ai[m]; vj[m] = aj[m]; }
@@ -122,15 +130,19 @@ __device__ bool riccati_sweep(L* S, int N, const RiccatiRoles& R) {
                 c0 = fma(vj[n], Gn[gzu<NXA>(n, 0)], c0);
                 c1 = fma(vj[n], Gn[gzu<NXA>(n, 1)], c1);
             }
-            double ga = S->H[k][lane], gb = 0.0;
+            double ga = S->H[k][lane + 64 * q], gb = 0.0;
 #pragma unroll
             for (int m = 0; m < NP; m += 2) {
                 ga = fma(vi[m], t[m], ga);
                 if (m + 1 < NP) gb = fma(vi[m + 1], t[m + 1], gb);
             }
             const double w0 = fma(i00, c0, i01 * c1), w1 = fma(i01, c0, i11 * c1);
-            S->G[k][lane] = (ga + gb) - fma(b0, w0, b1 * w1);
+            gout[q] = (ga + gb) - fma(b0, w0, b1 * w1);
         }
+        // all reads of G_{k+1} and M_k precede the writes of G_k (distinct rows: no hazard)
+#pragma unroll
+        for (int q = 0; q < L::EPL; ++q)
+            if (R.on[q]) S->G[k][lane + 64 * q] = gout[q];
         __syncthreads();
     }
     double i00, i01, i11;
@@ -212,6 +224,181 @@ __device__ void forward_sweep(L* S, int N, int node, double* dxo) {
         for (int i = 0; i < NXA; ++i) { d[i] = readlane(s, i); dxo[i] = mine ? d[i] : dxo[i]; }
 #pragma unroll
         for (int j = 0; j <= NXA; ++j) Fc[j] = Fn[j];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Three-phase variant with an explicit value function, for wide augmented states (LMPC,
+// NXA = 10): per node (A) T = Pt_{k+1} M_k (NP x ND entries, 11 FMA each), (B) G = Ht + M^T T
+// (packed, 11 FMA each), (C) the 2 x 2 Schur complement -> Pt_k (packed) and [K | k].  Each
+// lane holds only the operands of its own few entries (no uniform block in registers).
+template <int NXA_, int NMAXS_>
+struct OcpLds3 {
+    static constexpr int NXA = NXA_, NP = NXA + 1, ND = NXA + 3, NMAXS = NMAXS_;
+    static constexpr int NC = even(NP);
+    static constexpr int NT = tri(ND), NTP = even(NT);
+    static constexpr int NPT = tri(NP);
+    static constexpr int NPK = even(NPT + 2 * NP);   // [Pt packed | K row 0 | K row 1] per node
+    static constexpr int NF = even(NXA + 1);
+    static constexpr int NTT = NP * ND;               // entries of T
+    static constexpr int EA = (NTT + 63) / 64, EB = (NT + 63) / 64, EC = (NPT + 2 * NP + 63) / 64;
+    double M[NMAXS][ND][NC];
+    double H[NMAXS][NTP];
+    double PK[NMAXS][NPK];
+    double T[NP][ND + 1];                             // scratch Pt_{k+1} M_k (row m, column j)
+    double G[NTP];                                    // scratch G_k
+    double F[NMAXS][NXA][NF];
+    double dx0[NC];
+};
+
+template <class L>
+struct Riccati3Roles {
+    int am[L::EA], aj[L::EA];            // (A) row m of Pt, column offset of a_j
+    bool aon[L::EA];
+    int bi[L::EB], bj[L::EB];            // (B) column offsets of a_i, T column j
+    bool bon[L::EB];
+    int ga0[L::EC], ga1[L::EC], gb0[L::EC], gb1[L::EC], gzz[L::EC];   // (C) packed G offsets
+    bool isK[L::EC], con[L::EC];
+    int ka[L::EC];
+};
+
+template <class L>
+__device__ Riccati3Roles<L> riccati3_roles() {
+    constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, NC = L::NC, NT = L::NT, NPT = L::NPT, NTT = L::NTT;
+    const int lane = threadIdx.x;
+    Riccati3Roles<L> r{};
+#pragma unroll
+    for (int q = 0; q < L::EA; ++q) {
+        const int e0 = lane + 64 * q, e = e0 < NTT ? e0 : 0;
+        r.am[q] = e / ND; r.aj[q] = (e % ND) * NC; r.aon[q] = e0 < NTT;
+    }
+#pragma unroll
+    for (int q = 0; q < L::EB; ++q) {
+        const int e0 = lane + 64 * q, e = e0 < NT ? e0 : 0;
+        int i = 0;
+        while (tri(i + 1) <= e) ++i;
+        const int j = e - tri(i);
+        r.bi[q] = i * NC; r.bj[q] = j; r.bon[q] = e0 < NT;
+    }
+#pragma unroll
+    for (int q = 0; q < L::EC; ++q) {
+        const int e = lane + 64 * q;
+        int zi = 0, zj = 0;
+        r.isK[q] = e >= NPT;
+        r.ka[q] = 0;
+        if (e < NPT) {
+            int p = 0;
+            while (tri(p + 1) <= e) ++p;
+            const int qq = e - tri(p);
+            zi = zi_of_p<NXA>(p); zj = zi_of_p<NXA>(qq);
+        } else {
+            const int rr = (e - NPT) < 2 * NP ? e - NPT : 0;
+            r.ka[q] = rr / NP;
+            zi = zi_of_p<NXA>(rr % NP); zj = zi;
+        }
+        r.ga0[q] = hp(zi, NXA); r.ga1[q] = hp(zi, NXA + 1);
+        r.gb0[q] = hp(NXA, zj); r.gb1[q] = hp(NXA + 1, zj);
+        r.gzz[q] = hp(zi, zj);
+        r.con[q] = e < NPT + 2 * NP;
+    }
+    return r;
+}
+
+// Backward sweep; PK[N] (value part) must hold the terminal value function.
+template <class L>
+__device__ bool riccati3_sweep(L* S, int N, const Riccati3Roles<L>& R) {
+    constexpr int NXA = L::NXA, NP = L::NP, NPT = L::NPT;
+    const int lane = threadIdx.x;
+    bool ok = true;
+    for (int k = N - 1; k >= 0; --k) {
+        // (A) T(m, j) = sum_n Pt_{k+1}(m, n) M_k(n, j)
+        {
+            const double* Pn = S->PK[k + 1];
+            double tv[L::EA];
+#pragma unroll
+            for (int q = 0; q < L::EA; ++q) {
+                const double* aj = &S->M[k][0][0] + R.aj[q];
+                const int m = R.am[q];
+                double t = 0.0;
+#pragma unroll
+                for (int n = 0; n < NP; ++n) t = fma(Pn[m >= n ? tri(m) + n : tri(n) + m], aj[n], t);
+                tv[q] = t;
+            }
+#pragma unroll
+            for (int q = 0; q < L::EA; ++q)
+                if (R.aon[q]) (&S->T[0][0])[(lane + 64 * q) / L::ND * (L::ND + 1) + (lane + 64 * q) % L::ND] = tv[q];
+        }
+        __syncthreads();
+        // (B) G(i, j) = Ht(i, j) + sum_m M_k(m, i) T(m, j)
+        {
+            double gv[L::EB];
+#pragma unroll
+            for (int q = 0; q < L::EB; ++q) {
+                const double* ai = &S->M[k][0][0] + R.bi[q];
+                double g = S->H[k][(lane + 64 * q) < L::NT ? lane + 64 * q : 0];
+#pragma unroll
+                for (int mm = 0; mm < NP; ++mm) g = fma(ai[mm], S->T[mm][R.bj[q]], g);
+                gv[q] = g;
+            }
+#pragma unroll
+            for (int q = 0; q < L::EB; ++q)
+                if (R.bon[q]) S->G[lane + 64 * q] = gv[q];
+        }
+        __syncthreads();
+        // (C) Schur complement on the u block
+        double i00, i01, i11;
+        ok = quu_inverse<NXA>(S->G, i00, i01, i11) && ok;
+        {
+            double cv[L::EC];
+#pragma unroll
+            for (int q = 0; q < L::EC; ++q) {
+                const double b0 = S->G[R.gb0[q]], b1 = S->G[R.gb1[q]];
+                const double w0 = fma(i00, b0, i01 * b1), w1 = fma(i01, b0, i11 * b1);
+                const double a0 = S->G[R.ga0[q]], a1 = S->G[R.ga1[q]], gz = S->G[R.gzz[q]];
+                const double pv = gz - fma(a0, w0, a1 * w1);
+                const double kv = R.ka[q] == 0 ? -w0 : -w1;
+                cv[q] = R.isK[q] ? kv : pv;
+            }
+#pragma unroll
+            for (int q = 0; q < L::EC; ++q)
+                if (R.con[q]) S->PK[k][lane + 64 * q] = cv[q];
+        }
+        __syncthreads();
+    }
+    (void)NPT;
+    return ok;
+}
+
+// [Phi | f] of every node from the stored gains, lane per node.  Ends with a barrier.
+template <class L>
+__device__ void closed_loop3(L* S, int N) {
+    constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, NPT = L::NPT;
+    const int k = threadIdx.x;
+    if (k < N) {
+        const double* K0 = S->PK[k] + NPT;
+        const double* K1 = K0 + NP;
+#pragma unroll
+        for (int r = 0; r < NXA; ++r) {
+            const double b0 = S->M[k][NXA][r], b1 = S->M[k][NXA + 1][r];
+#pragma unroll
+            for (int j = 0; j < NXA; ++j) S->F[k][r][j] = fma(b0, K0[j], fma(b1, K1[j], S->M[k][j][r]));
+            S->F[k][r][NXA] = fma(b0, K0[NXA], fma(b1, K1[NXA], S->M[k][ND - 1][r]));
+        }
+    }
+    __syncthreads();
+}
+
+// lam~_k = -Pt_k [dx~; 1] (first NXA rows), lane per node
+template <class L>
+__device__ __forceinline__ void node_multiplier3(const L* S, int k, const double* dx, double* lam) {
+    constexpr int NXA = L::NXA;
+    const double* Pk = S->PK[k];
+#pragma unroll
+    for (int p = 0; p < NXA; ++p) {
+        double t = Pk[hp(NXA, p)];
+#pragma unroll
+        for (int q = 0; q < NXA; ++q) t = fma(Pk[hp(p, q)], dx[q], t);
+        lam[p] = -t;
     }
 }
 

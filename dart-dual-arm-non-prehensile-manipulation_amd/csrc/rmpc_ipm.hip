@@ -148,7 +148,7 @@ __device__ __forceinline__ void rm_iq(const double* z, double vmax, double* c) {
 __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     __shared__ RmShared SH;
     RmLds* S = &SH.ocp;
-    const RiccatiRoles RR = riccati_roles<RmLds>();
+    const RiccatiRoles<RmLds::EPL> RR = riccati_roles<RmLds>();
     STAMP_DECL
     const int b = blockIdx.x;
     const int k = threadIdx.x;

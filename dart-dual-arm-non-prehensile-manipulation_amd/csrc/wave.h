@@ -144,6 +144,32 @@ __device__ __forceinline__ double tanh_fast(double x) {
     return em / (em + 2.0);
 }
 
+// exp(x) by Cody-Waite reduction and a degree-13 Taylor polynomial on |r| <= ln2/2:
+// <= 2.3e-16 relative error over [-200, 5] (host-checked against libm); underflows to the
+// subnormals and 0 like libm.
+__device__ __forceinline__ double exp_fast(double x) {
+    const double y = fmin(fmax(x, -745.0), 709.0);
+    const double n = __builtin_rint(y * 1.4426950408889634);
+    double r = fma(-n, 6.93147180369123816490e-01, y);
+    r = fma(-n, 1.90821492927058770002e-10, r);
+    double p = 1.0 / 6227020800.0;
+    p = fma(p, r, 1.0 / 479001600.0);
+    p = fma(p, r, 1.0 / 39916800.0);
+    p = fma(p, r, 1.0 / 3628800.0);
+    p = fma(p, r, 1.0 / 362880.0);
+    p = fma(p, r, 1.0 / 40320.0);
+    p = fma(p, r, 1.0 / 5040.0);
+    p = fma(p, r, 1.0 / 720.0);
+    p = fma(p, r, 1.0 / 120.0);
+    p = fma(p, r, 1.0 / 24.0);
+    p = fma(p, r, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    const int ni = (int)n, n1 = ni / 2, n2 = ni - n1;       // two halves: exact down to the subnormals
+    return __builtin_ldexp(__builtin_ldexp(p, n1), n2);
+}
+
 // IPOPT's Compare_le: lhs <= rhs up to 10 machine epsilons of |base| (filter acceptance tests)
 __device__ __forceinline__ bool cmp_le(double lhs, double rhs, double base) {
     return lhs - rhs <= 10.0 * 2.220446049250313e-16 * fabs(base);

@@ -7,11 +7,11 @@ Drop-in for the reference's MPC hot path:
   - ``RMPCStep``        <- RMPC/dev_dual/rob_ctrl.py:331-352 (RLS fused into the solve launch)
   - ``Solver``, ``RmpcSolver``  the C ABI of include/dart_mpc.h (libdartmpc.so)
 """
-from ._lib import DartMPCError, RmpcSolver, Solver, build, lib, rls_update_batch, STATUS_NAMES  # noqa: F401
+from ._lib import DartMPCError, LmpcSolver, RmpcSolver, Solver, build, lib, rls_update_batch, STATUS_NAMES  # noqa: F401
 from .pmpc import PMPC, tilt_to_quat  # noqa: F401
 from .worker import mpc_worker  # noqa: F401
 from .rmpc import AdaptiveNPMPCSmooth, RLS, RMPCStep  # noqa: F401
 from . import workload  # noqa: F401
 
-__all__ = ["PMPC", "mpc_worker", "Solver", "RmpcSolver", "AdaptiveNPMPCSmooth", "RLS", "RMPCStep", "DartMPCError",
+__all__ = ["PMPC", "mpc_worker", "Solver", "RmpcSolver", "LmpcSolver", "AdaptiveNPMPCSmooth", "RLS", "RMPCStep", "DartMPCError",
            "build", "lib", "rls_update_batch", "tilt_to_quat", "workload"]

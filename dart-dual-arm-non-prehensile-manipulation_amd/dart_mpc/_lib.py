@@ -16,17 +16,19 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libdartmpc.so")
 
-SOLVED, MAXITER, LS_FAIL, INERTIA_FAIL = 0, -1, -2, -3
-STATUS_NAMES = {SOLVED: "Solve_Succeeded", MAXITER: "Maximum_Iterations_Exceeded",
-                LS_FAIL: "Restoration_Failed", INERTIA_FAIL: "Error_In_Step_Computation"}
+SOLVED, ACCEPTABLE, MAXITER, LS_FAIL, INERTIA_FAIL = 0, 1, -1, -2, -3
+STATUS_NAMES = {SOLVED: "Solve_Succeeded", ACCEPTABLE: "Solved_To_Acceptable_Level",
+                MAXITER: "Maximum_Iterations_Exceeded", LS_FAIL: "Restoration_Failed",
+                INERTIA_FAIL: "Error_In_Step_Computation"}
 
 # exported symbols of include/dart_mpc.h (tests check every one is present)
 EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch", "dart_mpc_solve_batch_dev",
            "dart_mpc_sync", "dart_mpc_last_error", "dart_mpc_destroy", "dart_mpc_nw", "dart_mpc_abi_version",
            "dart_rmpc_solve_batch", "dart_rmpc_solve_batch_dev", "dart_rmpc_nw",
-           "dart_rls_update_batch", "dart_rls_update_batch_dev")
-VARIANT_PMPC, VARIANT_RMPC = 0, 1
-ABI_VERSION = 1
+           "dart_rls_update_batch", "dart_rls_update_batch_dev",
+           "dart_lmpc_solve_batch", "dart_lmpc_solve_batch_dev", "dart_lmpc_nw")
+VARIANT_PMPC, VARIANT_RMPC, VARIANT_LMPC = 0, 1, 2
+ABI_VERSION = 2
 
 
 class DartMPCError(RuntimeError):
@@ -37,7 +39,8 @@ class Config(ctypes.Structure):
     """Mirror of ``struct dart_mpc_config``."""
     _fields_ = [("variant", ctypes.c_int32), ("N", ctypes.c_int32), ("Ts", ctypes.c_double),
                 ("tol", ctypes.c_double), ("max_iter", ctypes.c_int32), ("B_max", ctypes.c_int32),
-                ("gravity", ctypes.c_double)]
+                ("gravity", ctypes.c_double), ("acceptable_tol", ctypes.c_double),
+                ("acceptable_iter", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -88,6 +91,13 @@ def lib():
     L.dart_rmpc_solve_batch_dev.restype = ctypes.c_int
     L.dart_rmpc_nw.argtypes = [ctypes.c_int]
     L.dart_rmpc_nw.restype = ctypes.c_int
+    lsig = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 12
+    L.dart_lmpc_solve_batch.argtypes = lsig
+    L.dart_lmpc_solve_batch.restype = ctypes.c_int
+    L.dart_lmpc_solve_batch_dev.argtypes = lsig
+    L.dart_lmpc_solve_batch_dev.restype = ctypes.c_int
+    L.dart_lmpc_nw.argtypes = [ctypes.c_int]
+    L.dart_lmpc_nw.restype = ctypes.c_int
     L.dart_rls_update_batch.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_double]
     L.dart_rls_update_batch.restype = ctypes.c_int
     L.dart_rls_update_batch_dev.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_double, ctypes.c_void_p]
@@ -222,6 +232,52 @@ class RmpcSolver(Solver):
                                              w_out or None, status, iters, stream or None)
         if rc != 0:
             self._err(rc, "dart_rmpc_solve_batch_dev")
+
+
+LMPC_PRM_DEFAULT = np.array([200.0, 2.0, 200.0, 2.0, 0.0, 0.0, 0.0, 0.0,     # Q   LMPC/src/run.py:118
+                             200.0, 2.0, 200.0, 2.0, 0.0, 0.0, 0.0, 0.0,     # Qt  :119
+                             0.1, 0.1, 1.0, 1.0,                             # R   :120
+                             -0.4, 0.4])                                     # u_bounds :121
+
+
+class LmpcSolver(Solver):
+    """``dart_mpc_handle`` of variant LMPC, N <= 31.  Defaults are the reference's IPOPT options
+    (LMPC/src/controller/rlmpc2.py:480-489): max_iter 50, tol 1e-4, acceptable_tol 1e-3,
+    acceptable_iter 5."""
+
+    def __init__(self, N=20, Ts=0.002, tol=1e-4, max_iter=50, acceptable_tol=1e-3, acceptable_iter=5,
+                 B_max=1024, device=0):
+        self._h = ctypes.c_void_p()
+        self.cfg = default_config(variant=VARIANT_LMPC, N=int(N), Ts=float(Ts), tol=float(tol), max_iter=int(max_iter),
+                                  B_max=int(B_max), acceptable_tol=float(acceptable_tol),
+                                  acceptable_iter=int(acceptable_iter))
+        rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
+        if rc != 0:
+            raise DartMPCError(f"dart_mpc_create(LMPC) failed with code {rc} (no gfx950 device or bad config)")
+        self.N = int(N)
+        self.nw = lib().dart_lmpc_nw(self.N)
+
+    def solve_batch(self, state, u_prev, pvec, target, prm=None, w_warm=None, want_w=False):
+        c = lambda a, n: np.ascontiguousarray(a, np.float64).reshape(-1, n)
+        state = c(state, 8)
+        B = state.shape[0]
+        u_prev, pvec, target = c(u_prev, 2), c(pvec, 34), c(target, 8)
+        prm = c(np.tile(LMPC_PRM_DEFAULT, (B, 1)) if prm is None else prm, 22)
+        ww = None if w_warm is None else c(w_warm, self.nw)
+        u0 = np.empty((B, 2)); f = np.empty(B)
+        w = np.empty((B, self.nw)) if want_w else None
+        st = np.empty(B, np.int32); it = np.empty(B, np.int32)
+        rc = lib().dart_lmpc_solve_batch(self._h, B, _ptr(state), _ptr(u_prev), _ptr(pvec), _ptr(target), _ptr(prm),
+                                         _ptr(ww), _ptr(u0), _ptr(f), _ptr(w), _ptr(st), _ptr(it), None)
+        if rc != 0:
+            self._err(rc, "dart_lmpc_solve_batch")
+        return dict(u0=u0, f=f, w=w, status=st, iters=it)
+
+    def solve_batch_dev(self, B, state, u_prev, pvec, target, prm, u0, f, status, iters, w_warm=0, w_out=0, stream=0):
+        rc = lib().dart_lmpc_solve_batch_dev(self._h, int(B), state, u_prev, pvec, target, prm, w_warm or None, u0, f,
+                                             w_out or None, status, iters, stream or None)
+        if rc != 0:
+            self._err(rc, "dart_lmpc_solve_batch_dev")
 
 
 def rls_update_batch(theta, P, phi, y, lam=0.995):

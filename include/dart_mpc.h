@@ -14,6 +14,9 @@
  *   dart_rmpc_solve_batch(_dev) <- AdaptiveNPMPCSmooth.solve + the driver's RLS updates
  *                             RMPC/dev_dual/controller/np_mpc_adaptive_with_linear_regressor.py
  *                             :212-222 (RLS :10-30), RMPC/dev_dual/rob_ctrl.py:335-352
+ *   dart_lmpc_solve_batch(_dev) <- the solve of RLMPC._solver_worker
+ *                             LMPC/src/controller/rlmpc2.py:229-533 (NLP :239-491, solver call
+ *                             and warm start :510-520), fed by RLMPC.solve :986-1021
  *   dart_mpc_sync / dart_mpc_last_error / dart_mpc_destroy
  *                           <- process-lifetime handling of the solver object in
  *                             mpc_worker (main_parallel_enhanced.py:22-55)
@@ -46,15 +49,17 @@
 extern "C" {
 #endif
 
-#define DART_MPC_ABI_VERSION 1
+#define DART_MPC_ABI_VERSION 2
 
 enum dart_mpc_variant {
     DART_MPC_PMPC = 0,      /* PMPC/src/controller/mpc_3d.py, N <= 63 */
-    DART_MPC_RMPC = 1       /* RMPC/dev_dual/controller/np_mpc_adaptive_with_linear_regressor.py, N <= 31 */
+    DART_MPC_RMPC = 1,      /* RMPC/dev_dual/controller/np_mpc_adaptive_with_linear_regressor.py, N <= 31 */
+    DART_MPC_LMPC = 2       /* LMPC/src/controller/rlmpc2.py, N <= 31 */
 };
 
 enum dart_mpc_status {
     DART_MPC_SOLVED = 0,
+    DART_MPC_ACCEPTABLE = 1,       /* IPOPT "Solved To Acceptable Level" (LMPC: acceptable_tol / _iter) */
     DART_MPC_MAXITER = -1,
     DART_MPC_LS_FAIL = -2,
     DART_MPC_INERTIA_FAIL = -3
@@ -79,6 +84,9 @@ typedef struct dart_mpc_config {
     int32_t max_iter;   /* interior-point iteration cap */
     int32_t B_max;      /* largest batch the handle's device workspace serves */
     double gravity;     /* model.opt.gravity[2] (mpc_3d.py:23), default -9.81 */
+    double acceptable_tol;   /* IPOPT acceptable_tol; used by LMPC (rlmpc2.py:487: 1e-3) */
+    int32_t acceptable_iter; /* IPOPT acceptable_iter, 0 = off; used by LMPC (rlmpc2.py:488: 5) */
+    int32_t reserved;
 } dart_mpc_config;
 
 typedef struct dart_mpc_handle dart_mpc_handle;
@@ -136,6 +144,32 @@ int dart_rmpc_solve_batch_dev(dart_mpc_handle *h, int B,
 
 /* Number of fp64 entries of the RMPC w for horizon N: 4(N+1) + 2N. */
 int dart_rmpc_nw(int N);
+
+/* LMPC (handle created with variant DART_MPC_LMPC).  Replaces the solver call of
+ * RLMPC._solver_worker (LMPC/src/controller/rlmpc2.py:510-520): one NLP per instance with
+ *   state [B][8] = [px, vx, py, vy, theta_x, omega_x, theta_y, omega_y] (views["state"], :503)
+ *   u_prev [B][2] (views["control"], the last applied control, :505)
+ *   pvec [B][34] (views["model_params"], :506; squashed inside as |p| + 1e-6 where the
+ *                 reference does, :296-344)
+ *   target [B][8] (views["target"], :504)
+ *   prm [B][22] = [Q(8), Qt(8), R(4), u_lo, u_hi]   (LMPC/src/run.py:118-121)
+ *   w_warm [B][8(N+1)+2N] nullable (the worker's w0 <- w_opt, :492, :519), w_out same layout.
+ * Termination follows IPOPT with the handle's tol, max_iter, acceptable_tol and acceptable_iter
+ * (the reference: 1e-4, 50, 1e-3, 5); status DART_MPC_ACCEPTABLE when the acceptable test ends it. */
+int dart_lmpc_solve_batch(dart_mpc_handle *h, int B,
+                          const double *state, const double *u_prev, const double *pvec, const double *target,
+                          const double *prm, const double *w_warm,
+                          double *u0, double *f, double *w_out,
+                          int32_t *status, int32_t *iters, void *hip_stream);
+
+int dart_lmpc_solve_batch_dev(dart_mpc_handle *h, int B,
+                              const double *state, const double *u_prev, const double *pvec, const double *target,
+                              const double *prm, const double *w_warm,
+                              double *u0, double *f, double *w_out,
+                              int32_t *status, int32_t *iters, void *hip_stream);
+
+/* Number of fp64 entries of the LMPC w for horizon N: 8(N+1) + 2N. */
+int dart_lmpc_nw(int N);
 
 /* Batched standalone RLS.update (np_mpc...:17-27) for B independent p = 7 filters:
  * theta [B][7] and P [B][7][7] updated in place with regressors phi [B][7], targets y [B],

@@ -27,6 +27,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef ORACLE_DEBUG
+#include <stdio.h>
+#endif
 
 /* IPOPT Compare_le: lhs <= rhs up to 10 machine epsilons of |base| */
 #define LE(l, r, b) ((l) - (r) <= 10.0 * 2.220446049250313e-16 * fabs(b))
@@ -602,6 +605,10 @@ int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_pre
             }
             if (!accepted) alpha *= 0.5;
         }
+#ifdef ORACLE_DEBUG
+        fprintf(stderr, "it %3d mu %.2e err %.2e dinf %.2e pinf %.2e c0 %.2e delta %.1e amax %.3e alpha %.3e th %.3e th_t %.3e phi %.6e ph_t %.6e gTd %.3e acc %d\n",
+                it, C.mu, err, dinf / s_d, pinf, c0 / s_c, delta, amax, alpha, th, th_t, phi, ph_t, gTd, accepted);
+#endif
         if (!accepted) { status = ST_LS_FAIL; break; }
         if (!ftype && nfilt < 256) { W->filt_th[nfilt] = (1 - gam_th) * th; W->filt_ph[nfilt] = phi - gam_ph * th; ++nfilt; }
         memcpy(W->X, W->Xt, sizeof(double) * nA);

@@ -30,8 +30,10 @@ def test_defaults_follow_reference():
     c = _lib.default_config()
     assert (c.variant, c.N, c.Ts, c.tol, c.max_iter, c.gravity) == (0, 20, 0.002, 1e-8, 3000, -9.81)
     assert _lib.lib().dart_mpc_nw(20) == 166 and _lib.lib().dart_mpc_nw(15) == 126
-    assert _lib.lib().dart_mpc_abi_version() == 1
+    assert _lib.lib().dart_mpc_abi_version() == 2
+    assert (c.acceptable_tol, c.acceptable_iter) == (1e-6, 15)                              # IPOPT defaults
     assert _lib.lib().dart_rmpc_nw(20) == 124 and _lib.lib().dart_rmpc_nw(1) == 10      # 4(N+1) + 2N
+    assert _lib.lib().dart_lmpc_nw(20) == 208 and _lib.lib().dart_lmpc_nw(30) == 308
 
 
 def test_create_rejects_bad_config_without_touching_a_gpu():
@@ -40,12 +42,14 @@ def test_create_rejects_bad_config_without_touching_a_gpu():
     for over in (dict(N=0), dict(N=64), dict(Ts=0.0), dict(tol=-1.0), dict(B_max=0), dict(variant=7)):
         c = _lib.default_config(**over)
         assert _lib.lib().dart_mpc_create(ctypes.byref(c), 0, ctypes.byref(h)) == -1
-    for over in (dict(variant=1, N=32), dict(variant=1, N=0)):       # RMPC horizon limit N <= 31
+    for over in (dict(variant=1, N=32), dict(variant=1, N=0), dict(variant=2, N=32),   # RMPC/LMPC: N <= 31
+                 dict(variant=2, acceptable_iter=-1), dict(variant=2, acceptable_iter=5, acceptable_tol=0.0)):
         c = _lib.default_config(**over)
         assert _lib.lib().dart_mpc_create(ctypes.byref(c), 0, ctypes.byref(h)) == -1
     assert _lib.lib().dart_mpc_solve_batch(None, 1, *([None] * 10)) == -1
     assert _lib.lib().dart_rmpc_solve_batch(None, 1, *([None] * 6), 0.995, *([None] * 9)) == -1
     assert _lib.lib().dart_rls_update_batch(-1, None, None, None, None, 0.995) == -1
+    assert _lib.lib().dart_lmpc_solve_batch(None, 1, *([None] * 12)) == -1
 
 
 def test_rmpc_shim_validates_like_reference():

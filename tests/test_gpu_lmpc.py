@@ -1,0 +1,94 @@
+"""GPU parity tests of the batched LMPC kernel (through the C ABI).
+
+Tolerances (fp64, IPOPT-equivalent algorithm with bound_relax 1e-8):
+  * against the two-solver goldens (exact NLP): every control within 1e-6 at tol 1e-11;
+  * against the C oracle at the same tol 1e-8: u0 within 1e-5, all controls within 1e-4;
+  * with the reference's IPOPT options (rlmpc2.py:480-489: tol 1e-4, max_iter 50,
+    acceptable_tol 1e-3, acceptable_iter 5) the iterate that ends the solve is only
+    1e-4-optimal: u0 within 5e-3 of the exact optimum, as the oracle (observed <= 1.1e-3).
+"""
+import numpy as np
+import pytest
+
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dm():
+    import dart_mpc
+    return dart_mpc
+
+
+def _nw(N):
+    return 8 * (N + 1) + 2 * N
+
+
+def test_goldens_tight_tol(dm, lmpc_goldens):
+    G = lmpc_goldens
+    for N in np.unique(G["N"]):
+        N = int(N)
+        idx = np.nonzero(G["N"] == N)[0]
+        s = dm.LmpcSolver(N=N, tol=1e-11, max_iter=500, acceptable_iter=0, B_max=64)
+        out = s.solve_batch(G["state"][idx], G["u_prev"][idx], G["pvec"][idx], G["target"][idx], G["prm"][idx],
+                            want_w=True)
+        s.close()
+        assert np.all(out["status"] == 0), (N, out["status"], out["iters"])
+        nX = 8 * (N + 1)
+        err = np.abs(out["w"][:, nX:] - G["w"][idx][:, nX:_nw(N)]).max(axis=1)
+        assert np.all(err <= 1e-6), (N, err)
+
+
+def test_c5_batch_vs_oracle(dm):
+    from dart_mpc.workload import lmpc_batch
+    D = lmpc_batch(2)
+    s = dm.LmpcSolver(N=30, tol=1e-8, max_iter=500, acceptable_iter=0, B_max=64)
+    out = s.solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], want_w=True)
+    s.close()
+    ref = oracle_lib.lmpc_solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], N=30, tol=1e-8, acc_iter=0,
+                                      max_iter=500, nthreads=4)
+    assert np.all(out["status"] == 0) and np.all(ref["status"] == 0), (out["status"], out["iters"])
+    assert np.max(np.abs(out["u0"] - ref["u0"])) <= 1e-5
+    assert np.max(np.abs(out["w"][:, 8 * 31:] - ref["w"][:, 8 * 31:])) <= 1e-4
+    assert np.allclose(out["f"], ref["f"], rtol=1e-6, atol=1e-9)
+
+
+def test_reference_options(dm, lmpc_goldens):
+    G = lmpc_goldens
+    idx = np.nonzero(G["group"] == "c5")[0]
+    s = dm.LmpcSolver(N=30, B_max=64)               # tol 1e-4, max_iter 50, acceptable 1e-3 x 5
+    out = s.solve_batch(G["state"][idx], G["u_prev"][idx], G["pvec"][idx], G["target"][idx], want_w=True)
+    assert np.all(out["status"] >= 0) and np.all(out["iters"] <= 50), (out["status"], out["iters"])
+    assert np.max(np.abs(out["u0"] - G["w"][idx][:, 8 * 31:8 * 31 + 2])) <= 5e-3
+    warm = s.solve_batch(G["state"][idx], G["u_prev"][idx], G["pvec"][idx], G["target"][idx], w_warm=out["w"])
+    s.close()
+    assert np.all(warm["status"] >= 0) and warm["iters"].mean() <= out["iters"].mean()
+
+
+@pytest.mark.parametrize("N", [1, 2, 15, 31])
+def test_horizons(dm, N):
+    from dart_mpc.workload import lmpc_batch
+    D = lmpc_batch(1, seed0=3)
+    s = dm.LmpcSolver(N=N, tol=1e-10, max_iter=500, acceptable_iter=0, B_max=32)
+    out = s.solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], want_w=True)
+    s.close()
+    ref = oracle_lib.lmpc_solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], N=N, tol=1e-10, acc_iter=0,
+                                      max_iter=500, nthreads=4)
+    # seed 3 holds an instance (#15) on which IPOPT's line search fails from the cold start (it would
+    # enter its restoration phase, which neither the oracle nor the kernel restates): the kernel must
+    # fail exactly where the oracle fails, at the same iteration, and agree everywhere else
+    assert np.array_equal(out["status"], ref["status"]), (out["status"], ref["status"])
+    ok = ref["status"] == 0
+    assert np.array_equal(out["iters"][~ok], ref["iters"][~ok])
+    nX = 8 * (N + 1)
+    assert np.max(np.abs(out["w"][ok][:, nX:] - ref["w"][ok][:, nX:])) <= 1e-6
+
+
+def test_edge_batches(dm):
+    s = dm.LmpcSolver(N=20, B_max=16)
+    e = s.solve_batch(np.zeros((0, 8)), np.zeros((0, 2)), np.zeros((0, 34)), np.zeros((0, 8)))
+    assert e["u0"].shape == (0, 2)
+    with pytest.raises(dm.DartMPCError):
+        s.solve_batch(np.zeros((20, 8)), np.zeros((20, 2)), np.ones((20, 34)), np.zeros((20, 8)))
+    s.close()
