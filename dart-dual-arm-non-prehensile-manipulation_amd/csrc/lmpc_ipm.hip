@@ -11,10 +11,9 @@
 // objective and of the constraint rows) with IPOPT's optimal / acceptable termination tests.
 // The Delta-u cost couples consecutive controls: the Riccati recursion runs on the augmented
 // state x~_k = [x_k; u_{k-1}] (nx~ = 10), three LDS phases per node (ocp_wave.h, OcpLds3).
-// Exact RK4 Jacobians (forward mode, 10 directions, two at a time over LDS-staged stage
-// derivatives); the dynamics part of the Lagrangian Hessian is the RK-weighted
-// Ts * sum_s w_s lambda^T f''(y_s) (error O(Ts^2) relative; it changes the Newton path only,
-// never the KKT point).
+// Exact derivatives as IPOPT gets them from CasADi: per direction of z = [x; u], the RK4 tangent
+// (a column of the step Jacobian) and a second-order adjoint sweep back through the four stages
+// (a column of the exact Hessian of lambda^T x+), from per-stage derivative data staged in LDS.
 //
 // Mapping: one wave64 per instance, lane k = shooting node k (N <= 31) for node-local work;
 // the node-coupled Riccati / forward sweeps run through LDS (ocp_wave.h).  The LDS image
@@ -51,8 +50,11 @@ struct LmModel {
 
 struct LmShared {
     LmLds ocp;
-    double SC[kWave][4][LM_NSC];      // per lane, per RK stage: d f / d y coefficients (tangent pass)
-    double JL[kWave][12];             // per lane: J^T lambda_{k+1} staging, primal residual maxima
+    // per node (row 32: scratch of the idle lanes), per RK stage: d f / d y coefficients, and the
+    // second-derivative data turned into adjoint-weighted curvature coefficients
+    double SC[LM_NMAXS + 1][4][LM_NSC];
+    double SD[LM_NMAXS + 1][4][8];
+    double JL[LM_NMAXS + 1][12];      // J^T lambda_{k+1} staging, primal residual maxima
     LmModel model;                    // uniform problem data, read at the use sites (keeps VGPRs free)
     double Q[8], Qt[8], tgt[8];
 };
@@ -126,17 +128,14 @@ __device__ __forceinline__ void lm_rk4(const LmModel& m, const double* x, double
     for (int i = 0; i < 8; ++i) xn[i] = fma(m.h / 6.0, acc[i], x[i]);
 }
 
-// Value pass of RK4 that also stores the tangent coefficients of every stage in sc[4][10] and
-// accumulates the RK-weighted curvature -Ts sum_s w_s/6 lamn^T f''(y_s) (lamn = lambda_{k+1}).
-// hd = [vxvx, vxwy, wywy, vyvy, vywx, wxwx, txtx, tyty, aa, bb] (state indices 1,7 / 3,5 / 4 / 6, u).
-__device__ __forceinline__ void lm_rk4_lin(const LmModel& m, const double* x, double sa, double sb,
-                                           const double* lamn, double* xn, double (*sc)[LM_NSC], double* hd) {
-    const double nl[8] = {0.0, -lamn[1], 0.0, -lamn[3], 0.0, -lamn[5], 0.0, -lamn[7]};
+// Value pass of RK4 that also stores, per stage s, the tangent coefficients sc[s][10] (the
+// nonzero entries of d f / d y at y_s) and the second-derivative data sd[s][8] = [S''(vx),
+// S''(slip x), S''(vy), S''(slip y), S''(om_x), S''(om_y), sin th_x, sin th_y].
+__device__ __forceinline__ void lm_rk4_lin(const LmModel& m, const double* x, double sa, double sb, double* xn,
+                                           double (*sc)[LM_NSC], double (*sd)[8]) {
     double y[8], acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { y[i] = x[i]; acc[i] = 0.0; }
-#pragma unroll
-    for (int i = 0; i < 10; ++i) hd[i] = 0.0;
 #pragma unroll 1
     for (int s = 0; s < 4; ++s) {
         const double wts = (s == 0 || s == 3) ? 1.0 : 2.0, cst = s < 2 ? 0.5 : (s == 2 ? 1.0 : 0.0);
@@ -168,22 +167,8 @@ __device__ __forceinline__ void lm_rk4_lin(const LmModel& m, const double* x, do
         sc[s][7] = -m.r_x * Srx1 * m.iIy;
         sc[s][8] = (m.r_x * m.r_x * Srx1 - Sny1 - m.c_ry) * m.iIy;
         sc[s][9] = -m.tqy * cty * m.iIy;
-        // curvature of nl^T f at y_s
-        const double W = m.h * wts / 6.0;
-        const double c_vx = nl[1] * (-Sfx2 * m.im_x);
-        const double c_sx = nl[1] * (-Srx2 * m.im_x) + nl[7] * (-m.r_x * Srx2 * m.iIy);
-        const double c_vy = nl[3] * (-Sfy2 * m.im_y);
-        const double c_sy = nl[3] * (-Sry2 * m.im_y) + nl[5] * (-m.r_y * Sry2 * m.iIx);
-        const double c_ox = nl[5] * (-Snx2 * m.iIx);
-        const double c_oy = nl[7] * (-Sny2 * m.iIy);
-        hd[0] = fma(W, c_vx + c_sx, hd[0]);
-        hd[1] = fma(W, -m.r_x * c_sx, hd[1]);
-        hd[2] = fma(W, fma(m.r_x * m.r_x, c_sx, c_oy), hd[2]);
-        hd[3] = fma(W, c_vy + c_sy, hd[3]);
-        hd[4] = fma(W, m.r_y * c_sy, hd[4]);
-        hd[5] = fma(W, fma(m.r_y * m.r_y, c_sy, c_ox), hd[5]);
-        hd[6] = fma(W, nl[5] * m.tqx * stx * m.iIx, hd[6]);
-        hd[7] = fma(W, nl[7] * m.tqy * sty * m.iIy, hd[7]);
+        sd[s][0] = Sfx2; sd[s][1] = Srx2; sd[s][2] = Sfy2; sd[s][3] = Sry2;
+        sd[s][4] = Snx2; sd[s][5] = Sny2; sd[s][6] = stx; sd[s][7] = sty;
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[i] = fma(wts, k[i], acc[i]);
 #pragma unroll
@@ -191,34 +176,86 @@ __device__ __forceinline__ void lm_rk4_lin(const LmModel& m, const double* x, do
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) xn[i] = fma(m.h / 6.0, acc[i], x[i]);
-    hd[8] = m.h * nl[1] * (-LM_G * sa);
-    hd[9] = m.h * nl[3] * (-LM_G * sb);
 }
 
-// Tangent of RK4 along direction d (0..7 state, 8..9 tilt) from the stored stage coefficients:
-// column d of the step Jacobian J = d x+ / d [x; u], written to column jc(d) of the node's M~;
-// returns col . lamn (the J^T lambda term of the dual residual).
-__device__ __forceinline__ double lm_column(const LmModel& m, const double (*sc)[LM_NSC], double gca, double gcb,
-                                            int d, const double* lamn, double* Mk) {
-    double yd[8], acc[8], e[8];
+// q = (d f / d y at stage s)^T v from the stage's tangent coefficients
+__device__ __forceinline__ void lm_jtv(const LmModel& m, const double* c, const double* v, double* q) {
+    const double kx1 = -m.k_x * m.im_x, ky3 = -m.k_y * m.im_y;
+    q[0] = kx1 * v[1];
+    q[1] = fma(c[0], v[1], fma(c[7], v[7], v[0]));
+    q[2] = ky3 * v[3];
+    q[3] = fma(c[2], v[3], fma(c[4], v[5], v[2]));
+    q[4] = c[6] * v[5];
+    q[5] = fma(c[3], v[3], fma(c[5], v[5], v[4]));
+    q[6] = c[9] * v[7];
+    q[7] = fma(c[1], v[1], fma(c[8], v[7], v[6]));
+}
+
+// First-order adjoint of L = nl^T x+ (nl = -lambda_{k+1}) through the four RK4 stages; converts the
+// stage second-derivative data sd[s] in place into the curvature coefficients of kb_s^T f'' at y_s:
+// [A1, A2, A3, B1, B2, B3, C1, C2] with (vx, om_y) block [[A1, A2], [A2, A3]], (vy, om_x) block
+// [[B1, B2], [B2, B3]], th_x: C1, th_y: C2; returns the tilt curvature huu[2] = sum_s kb_s^T f_uu.
+__device__ __forceinline__ void lm_adjoint_curv(const LmModel& m, const double (*sc)[LM_NSC], double (*sd)[8],
+                                                const double* lamn, double sa, double sb, double* huu) {
+    double kb[8], yb[8];
+    const double h = m.h;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { e[i] = (i == d) ? 1.0 : 0.0; yd[i] = e[i]; acc[i] = 0.0; }
+    for (int i = 0; i < 8; ++i) kb[i] = -(h / 6.0) * lamn[i];        // kb_4
+    huu[0] = 0.0; huu[1] = 0.0;
+#pragma unroll 1
+    for (int s = 3; s >= 0; --s) {
+        double* d = sd[s];
+        const double c_vx = kb[1] * (-d[0] * m.im_x);
+        const double c_sx = kb[1] * (-d[1] * m.im_x) + kb[7] * (-m.r_x * d[1] * m.iIy);
+        const double c_vy = kb[3] * (-d[2] * m.im_y);
+        const double c_sy = kb[3] * (-d[3] * m.im_y) + kb[5] * (-m.r_y * d[3] * m.iIx);
+        const double c_ox = kb[5] * (-d[4] * m.iIx);
+        const double c_oy = kb[7] * (-d[5] * m.iIy);
+        const double c_tx = kb[5] * (m.tqx * d[6] * m.iIx);
+        const double c_ty = kb[7] * (m.tqy * d[7] * m.iIy);
+        d[0] = c_vx + c_sx; d[1] = -m.r_x * c_sx; d[2] = fma(m.r_x * m.r_x, c_sx, c_oy);
+        d[3] = c_vy + c_sy; d[4] = m.r_y * c_sy; d[5] = fma(m.r_y * m.r_y, c_sy, c_ox);
+        d[6] = c_tx; d[7] = c_ty;
+        huu[0] = fma(kb[1], -LM_G * sa, huu[0]);
+        huu[1] = fma(kb[3], -LM_G * sb, huu[1]);
+        if (s > 0) {      // kb_{s-1} = w_{s-1} h/6 nl + c_s h J_s^T kb_s  (c = 1, 1/2, 1/2 for s = 3, 2, 1)
+            lm_jtv(m, sc[s], kb, yb);
+            const double cs = s == 3 ? h : 0.5 * h, ws = (s == 1 ? 1.0 : 2.0) * h / 6.0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) kb[i] = fma(cs, yb[i], -ws * lamn[i]);
+        }
+    }
+}
+
+// Direction d (0..7 state, 8..9 tilt): tangent of RK4 -> column d of the step Jacobian (written to
+// column jc(d) of M~, returns col . lamn), then the second-order adjoint sweep back through the
+// stages -> column d of the exact Hessian of -lambda^T x+ over z = [x; u], written to the packed
+// stage Hessian (rows i >= d).
+__device__ __forceinline__ double lm_direction(const LmModel& m, const double (*sc)[LM_NSC], const double (*cv)[8],
+                                               const double* huu, double gca, double gcb, int d, const double* lamn,
+                                               double* Mk, double* Hk) {
+    double yd[4][8], acc[8], e[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { e[i] = (i == d) ? 1.0 : 0.0; yd[0][i] = e[i]; acc[i] = 0.0; }
     const double fa = d == 8 ? gca : 0.0, fb = d == 9 ? gcb : 0.0;
     const double kx1 = -m.k_x * m.im_x, ky3 = -m.k_y * m.im_y;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const double wts = (s == 0 || s == 3) ? 1.0 : 2.0, cst = s < 2 ? 0.5 : (s == 2 ? 1.0 : 0.0);
         const double* c = sc[s];
+        const double* y = yd[s];
         double k[8];
-        k[0] = yd[1]; k[2] = yd[3]; k[4] = yd[5]; k[6] = yd[7];
-        k[1] = fma(kx1, yd[0], fma(c[0], yd[1], fma(c[1], yd[7], fa)));
-        k[3] = fma(ky3, yd[2], fma(c[2], yd[3], fma(c[3], yd[5], fb)));
-        k[5] = fma(c[4], yd[3], fma(c[5], yd[5], c[6] * yd[4]));
-        k[7] = fma(c[7], yd[1], fma(c[8], yd[7], c[9] * yd[6]));
+        k[0] = y[1]; k[2] = y[3]; k[4] = y[5]; k[6] = y[7];
+        k[1] = fma(kx1, y[0], fma(c[0], y[1], fma(c[1], y[7], fa)));
+        k[3] = fma(ky3, y[2], fma(c[2], y[3], fma(c[3], y[5], fb)));
+        k[5] = fma(c[4], y[3], fma(c[5], y[5], c[6] * y[4]));
+        k[7] = fma(c[7], y[1], fma(c[8], y[7], c[9] * y[6]));
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[i] = fma(wts, k[i], acc[i]);
+        if (s < 3) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) yd[i] = fma(cst * m.h, k[i], e[i]);
+            for (int i = 0; i < 8; ++i) yd[s + 1][i] = fma(cst * m.h, k[i], e[i]);
+        }
     }
     const int jc = d < 8 ? d : d + 2;
     double dot = 0.0;
@@ -228,14 +265,46 @@ __device__ __forceinline__ double lm_column(const LmModel& m, const double (*sc)
         Mk[jc * LmLds::NC + i] = col;
         dot = fma(col, lamn[i], dot);
     }
+    // second-order adjoint: kbd_s = d/dd kb_s, ybd_s = J_s^T kbd_s + (kb_s^T f'')_s yd_s
+    double kbd[8], hx[8], hu0 = d == 8 ? huu[0] : 0.0, hu1 = d == 9 ? huu[1] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { kbd[i] = 0.0; hx[i] = 0.0; }
+#pragma unroll
+    for (int s = 3; s >= 0; --s) {
+        const double* cc = cv[s];
+        const double* y = yd[s];
+        double q[8];
+        lm_jtv(m, sc[s], kbd, q);
+        q[1] = fma(cc[0], y[1], fma(cc[1], y[7], q[1]));
+        q[7] = fma(cc[1], y[1], fma(cc[2], y[7], q[7]));
+        q[3] = fma(cc[3], y[3], fma(cc[4], y[5], q[3]));
+        q[5] = fma(cc[4], y[3], fma(cc[5], y[5], q[5]));
+        q[4] = fma(cc[6], y[4], q[4]);
+        q[6] = fma(cc[7], y[6], q[6]);
+        hu0 = fma(gca, kbd[1], hu0);
+        hu1 = fma(gcb, kbd[3], hu1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) hx[i] += q[i];
+        const double cs = s == 3 ? m.h : 0.5 * m.h;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kbd[i] = cs * q[i];
+    }
+    // rows i >= d of column d (z indices: x 0..7, tilt 10, 11)
+    const int zd = jc;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (i >= d) Hk[hp(i, zd)] = hx[i];
+    Hk[hp(10, zd)] = hu0;
+    Hk[hp(11, zd)] = hu1;
     return dot;
 }
 
-// all ten columns, one direction at a time; J^T lambda_{k+1} into jl[10]
-__device__ __forceinline__ void lm_columns(const LmModel& m, const double (*sc)[LM_NSC], double gca, double gcb,
-                                           const double* lamn, double* Mk, double* jl, double* jl_lds) {
+// all ten directions, one at a time; J^T lambda_{k+1} into jl[10]
+__device__ __forceinline__ void lm_directions(const LmModel& m, const double (*sc)[LM_NSC], const double (*cv)[8],
+                                              const double* huu, double gca, double gcb, const double* lamn, double* Mk,
+                                              double* Hk, double* jl, double* jl_lds) {
 #pragma unroll 1
-    for (int d = 0; d < 10; ++d) jl_lds[d] = lm_column(m, sc, gca, gcb, d, lamn, Mk);
+    for (int d = 0; d < 10; ++d) jl_lds[d] = lm_direction(m, sc, cv, huu, gca, gcb, d, lamn, Mk, Hk);
 #pragma unroll
     for (int d = 0; d < 10; ++d) jl[d] = jl_lds[d];
 }
@@ -250,6 +319,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     const int k = threadIdx.x;
     const int N = a.N;
     const bool xon = k <= N, uon = k < N;
+    const int sr = xon ? k : LM_NMAXS;        // per-node LDS scratch row (idle lanes share row 32)
     constexpr int NC = LmLds::NC;
 
     // ---------------- model parameters (uniform, staged in LDS) -------------------------------
@@ -362,19 +432,16 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
 
     double dsc[8];          // scaling of the incoming physical defect rows of node k (up rows: 1)
     {
-        double sa, ca, sb, cb, xn[8], hd[10], nl0[10];
-#pragma unroll
-        for (int i = 0; i < 10; ++i) nl0[i] = 0.0;
+        double sa, ca, sb, cb, xn[8], huu[2];
+        const double lz[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         tilt_sincos(poly, u[0], sa, ca);
         tilt_sincos(poly, u[1], sb, cb);
-        lm_rk4_lin(m, x, sa, sb, nl0, xn, SH.SC[k], hd);
+        lm_rk4_lin(m, x, sa, sb, xn, SH.SC[sr], SH.SD[sr]);
+        lm_adjoint_curv(m, SH.SC[sr], SH.SD[sr], lz, sa, sb, huu);
         double* Mt = &S->M[xon ? k : 0][0][0];
-        const double lz[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        const double (*scs)[LM_NSC] = SH.SC[k];
-        const double gca = LM_G * ca, gcb = LM_G * cb;
         if (uon) {
             double jl0[10];
-            lm_columns(m, scs, gca, gcb, lz, Mt, jl0, SH.JL[k]);
+            lm_directions(m, SH.SC[sr], SH.SD[sr], huu, LM_G * ca, LM_G * cb, lz, Mt, Hk, jl0, SH.JL[sr]);
         }
         double rs[8];
 #pragma unroll
@@ -427,26 +494,24 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             tilt_sincos(poly, u[0], sa, ca);
             tilt_sincos(poly, u[1], sb, cb);
             double xn[8];
+            lm_rk4_lin(m, x, sa, sb, xn, SH.SC[sr], SH.SD[sr]);
             {
-                double hd[10];
-                lm_rk4_lin(m, x, sa, sb, lamn, xn, SH.SC[k], hd);
-                if (uon) {   // z = [x(8), up(2), u(2), 1]: packed Hessian (gradient row later)
+                double huu[2];
+                lm_adjoint_curv(m, SH.SC[sr], SH.SD[sr], lamn, sa, sb, huu);
+                if (uon) {
+                    // exact dynamics Hessian (x, u blocks) and the Jacobian columns, then the cost /
+                    // barrier terms: z = [x(8), up(2), u(2), 1], gradient row later
+                    lm_directions(m, SH.SC[sr], SH.SD[sr], huu, LM_G * ca, LM_G * cb, lamn, Mk, Hk, jl, SH.JL[sr]);
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) Hk[hp(i, i)] = sc * 2.0 * Q[i];
-                    Hk[hp(1, 1)] += hd[0]; Hk[hp(7, 1)] = hd[1]; Hk[hp(7, 7)] += hd[2];
-                    Hk[hp(3, 3)] += hd[3]; Hk[hp(5, 3)] = hd[4]; Hk[hp(5, 5)] += hd[5];
-                    Hk[hp(4, 4)] += hd[6]; Hk[hp(6, 6)] += hd[7];
+                    for (int i = 0; i < 8; ++i) Hk[hp(i, i)] += sc * 2.0 * Q[i];
                     Hk[hp(8, 8)] = sc * 2.0 * R2; Hk[hp(9, 9)] = sc * 2.0 * R3;
-                    Hk[hp(10, 10)] = sc * 2.0 * (R0 + R2) + hd[8] + zl[0] * isl0 + zu[0] * isu0;
-                    Hk[hp(11, 11)] = sc * 2.0 * (R1 + R3) + hd[9] + zl[1] * isl1 + zu[1] * isu1;
+                    Hk[hp(10, 10)] += sc * 2.0 * (R0 + R2) + zl[0] * isl0 + zu[0] * isu0;
+                    Hk[hp(11, 11)] += sc * 2.0 * (R1 + R3) + zl[1] * isl1 + zu[1] * isu1;
                     Hk[hp(10, 8)] = -sc * 2.0 * R2; Hk[hp(11, 9)] = -sc * 2.0 * R3;
-                }
-            }
-            if (uon) {
-                lm_columns(m, SH.SC[k], LM_G * ca, LM_G * cb, lamn, Mk, jl, SH.JL[k]);
-            } else {
+                } else {
 #pragma unroll
-                for (int i = 0; i < 10; ++i) jl[i] = 0.0;
+                    for (int i = 0; i < 10; ++i) jl[i] = 0.0;
+                }
             }
             // outgoing augmented defect c_k = [F(z_k); u_k] - x~_{k+1} -> defect column of M~
             double cdef[10];
@@ -469,10 +534,10 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 plu = fmax(plu, xon ? fabs(gi) : 0.0);
                 if (k == 0) S->dx0[i] = -gi;
             }
-            SH.JL[k][10] = pl; SH.JL[k][11] = plu;      // primal residual maxima (LDS: frees registers)
+            SH.JL[sr][10] = pl; SH.JL[sr][11] = plu;    // primal residual maxima (LDS: frees registers)
         }
         double dinf = 0.0, c0 = 0.0, cmin = 1e300, suml = 0.0, sumz = 0.0;
-        double pinf = SH.JL[k][10], pinf_u = SH.JL[k][11];
+        double pinf = SH.JL[sr][10], pinf_u = SH.JL[sr][11];
         {
             double gl[12];
             cost_grad(x, u, up, gl);

@@ -92,3 +92,20 @@ def test_edge_batches(dm):
     with pytest.raises(dm.DartMPCError):
         s.solve_batch(np.zeros((20, 8)), np.zeros((20, 2)), np.ones((20, 34)), np.zeros((20, 8)))
     s.close()
+
+
+def test_reference_options_same_path_as_oracle(dm):
+    """With the reference's options (tol 1e-4, acceptable 1e-3 x 5, max_iter 50) the solve ends at a
+    loose iterate, so the comparison is path-level: against the oracle with the second-order
+    correction switched off (the kernel's line search has none) the kernel takes the same number of
+    iterations, ends with the same status and returns the same control (|du0| <= 1e-6; observed
+    2.5e-8 over 360 instances)."""
+    from dart_mpc.workload import lmpc_batch
+    D = lmpc_batch(4, seed0=7003)
+    s = dm.LmpcSolver(N=30, B_max=128)
+    g = s.solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"])
+    s.close()
+    o = oracle_lib.lmpc_solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], N=30, nthreads=8, soc=False)
+    assert np.array_equal(g["status"], o["status"])
+    assert np.array_equal(g["iters"], o["iters"])
+    assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6

@@ -92,3 +92,14 @@ def test_lmpc_workload_shapes_and_determinism():
     assert np.all((a["pvec"] >= 0.01) & (a["pvec"] <= 1.9))
     for k in a:
         assert np.array_equal(a[k], b[k])
+
+
+def test_soc_switch_changes_path_not_solution(lmpc_goldens):
+    """The oracle's second-order correction (IPOPT default) can be switched off to mirror the GPU
+    kernel's line search; both end at the same optimum on the goldens."""
+    G = lmpc_goldens
+    idx = np.nonzero(G["group"] == "c5")[0][:6]
+    a = _solve(G, idx, 30, tol=1e-11, acc_iter=0, max_iter=500, soc=True)
+    b = _solve(G, idx, 30, tol=1e-11, acc_iter=0, max_iter=500, soc=False)
+    assert np.all(a["status"] == 0) and np.all(b["status"] == 0)
+    assert np.max(np.abs(a["u0"] - b["u0"])) <= 1e-7

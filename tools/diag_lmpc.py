@@ -1,17 +1,39 @@
-import sys, numpy as np
-sys.path.insert(0, 'dart-dual-arm-non-prehensile-manipulation_amd'); sys.path.insert(0, 'oracle')
-import dart_mpc, oracle_lib
-from dart_mpc.workload import lmpc_batch
-D = lmpc_batch(1, seed0=3)
-for N in (25, 28, 29, 30, 31):
-    for tol in (1e-4, 1e-8, 1e-10):
-        s = dart_mpc.LmpcSolver(N=N, tol=tol, max_iter=500, acceptable_iter=0, B_max=32)
-        out = s.solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], want_w=True)
-        s.close()
-        bad = np.nonzero(out["status"] != 0)[0]
-        print(N, tol, "bad", bad.tolist(), "st", out["status"][bad].tolist(), "it", out["iters"][bad].tolist(), "maxit", out["iters"].max())
-i = 15
-print("pvec", np.round(D["pvec"][i], 3).tolist())
-print("state", D["state"][i], "target", D["target"][i], "u_prev", D["u_prev"][i])
-r = oracle_lib.lmpc_solve_batch(D["state"][i:i+1], D["u_prev"][i:i+1], D["pvec"][i:i+1], D["target"][i:i+1], N=31, tol=1e-10, acc_iter=0, max_iter=500)
-print("oracle", r["status"], r["iters"], r["u0"])
+"""Diagnostic: LMPC kernel vs oracle status agreement at the reference's IPOPT options over many
+seeds (cold start).  Prints status histograms and the disagreeing instances."""
+import sys
+from collections import Counter
+
+import numpy as np
+
+sys.path.insert(0, "dart-dual-arm-non-prehensile-manipulation_amd")
+sys.path.insert(0, "oracle")
+import dart_mpc  # noqa: E402
+import oracle_lib  # noqa: E402
+from dart_mpc.workload import lmpc_batch  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+D = lmpc_batch(20, seed0=7003)
+s = dart_mpc.LmpcSolver(N=N, B_max=512)
+g = s.solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], want_w=True)
+o = oracle_lib.lmpc_solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], N=N, nthreads=16)
+print("kernel", dict(Counter(g["status"].tolist())), "iters mean", g["iters"].mean())
+print("oracle", dict(Counter(o["status"].tolist())), "iters mean", o["iters"].mean())
+bad = np.nonzero(g["status"] != o["status"])[0]
+for i in bad[:20]:
+    print(i, "gpu", g["status"][i], g["iters"][i], "oracle", o["status"][i], o["iters"][i])
+ok = (g["status"] >= 0) & (o["status"] >= 0)
+print("max |u0 gpu - u0 oracle| where both ok:", np.abs(g["u0"][ok] - o["u0"][ok]).max())
+for tol in (1e-8,):
+    s2 = dart_mpc.LmpcSolver(N=N, B_max=512, tol=tol, max_iter=500, acceptable_iter=0)
+    g2 = s2.solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"])
+    o2 = oracle_lib.lmpc_solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], N=N, tol=tol, acc_iter=0,
+                                     max_iter=500, nthreads=16)
+    print(tol, "kernel", dict(Counter(g2["status"].tolist())), g2["iters"].mean(), "oracle",
+          dict(Counter(o2["status"].tolist())), o2["iters"].mean())
+
+# path parity: the kernel against the oracle with the second-order correction off (the kernel has none)
+o3 = oracle_lib.lmpc_solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], N=N, nthreads=16, soc=False)
+same_st = g["status"] == o3["status"]
+same_it = g["iters"] == o3["iters"]
+print("no-SOC oracle: status agree", same_st.mean(), "iters agree", same_it.mean(),
+      "max |du0|", np.abs(g["u0"] - o3["u0"]).max(), "max |du0| where iters agree", np.abs(g["u0"] - o3["u0"])[same_it].max())
