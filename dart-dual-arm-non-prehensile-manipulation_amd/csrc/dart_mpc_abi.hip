@@ -13,6 +13,9 @@
 #include "pmpc_ipm.h"
 #include "rmpc_ipm.h"
 #include "lmpc_ipm.h"
+#include "lmpc_policy.h"
+
+#include <cmath>
 
 struct dart_mpc_handle {
     dart_mpc_config cfg;
@@ -306,6 +309,97 @@ int dart_lmpc_solve_batch(dart_mpc_handle* h, int B, const double* state, const 
     HIPCHK(h, dn(iters, d_it, sizeof(int32_t) * B), "copy iters");
     HIPCHK(h, hipStreamSynchronize(s), "hipStreamSynchronize");
     return DART_MPC_OK;
+}
+
+void dart_lmpc_policy_config_default(dart_lmpc_policy_config* c) {
+    if (!c) return;
+    c->update_every = 8;
+    c->reserved = 0;
+    c->max_delta = 0.02;
+    c->k_max = 2.0;
+    c->min_k = 1e-2;
+    c->k_ceiling_margin = std::fmax(1e-3, 0.05 * c->k_max);
+    c->action_scale = 1.0;
+    c->smooth_alpha = 0.5;
+    c->log_std_min = std::log(1e-2);
+    c->log_std_max = std::log(2.0);
+}
+
+static int policy_args(const dart_lmpc_policy_config* c, int B, const float* w, dartmpc::PolicyArgs& a) {
+    if (!c || B < 0 || !w || c->update_every < 1 || !(c->k_max > c->min_k) || !(c->min_k > 0.0)) return DART_MPC_EINVAL;
+    a.B = B;
+    a.w.W1 = w; a.w.b1 = w + 520 * 64; a.w.W2 = a.w.b1 + 64; a.w.b2 = a.w.W2 + 64 * 64;
+    a.w.W3 = a.w.b2 + 64; a.w.b3 = a.w.W3 + 64 * 34; a.w.log_std = a.w.b3 + 34;
+    a.update_every = c->update_every;
+    a.max_delta = c->max_delta; a.k_max = c->k_max; a.min_k = c->min_k; a.k_ceiling_margin = c->k_ceiling_margin;
+    a.action_scale = c->action_scale; a.smooth_alpha = c->smooth_alpha;
+    a.log_std_min = c->log_std_min; a.log_std_max = c->log_std_max;
+    return DART_MPC_OK;
+}
+
+int dart_lmpc_policy_step_dev(const dart_lmpc_policy_config* cfg, int B, const float* weights, const double* state,
+                              const double* target, const double* control, const double* current_k, double* obs_mean,
+                              double* obs_M2, int32_t* obs_count, float* history, int32_t* timestep, const float* noise,
+                              double* model_params, float* action_out, void* stream) {
+    dartmpc::PolicyArgs a;
+    if (policy_args(cfg, B, weights, a) != DART_MPC_OK) return DART_MPC_EINVAL;
+    if (B > 0 && (!state || !target || !control || !current_k || !obs_mean || !obs_M2 || !obs_count || !history ||
+                  !timestep || !noise || !model_params)) return DART_MPC_EINVAL;
+    if (B == 0) return DART_MPC_OK;
+    a.state = state; a.target = target; a.control = control; a.current_k = current_k; a.obs_mean = obs_mean;
+    a.obs_M2 = obs_M2; a.obs_count = obs_count; a.history = history; a.timestep = timestep; a.noise = noise;
+    a.model_params = model_params; a.action_out = action_out;
+    return dartmpc_launch_policy(&a, (hipStream_t)stream) == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
+}
+
+int dart_lmpc_policy_step(const dart_lmpc_policy_config* cfg, int B, const float* weights, const double* state,
+                          const double* target, const double* control, const double* current_k, double* obs_mean,
+                          double* obs_M2, int32_t* obs_count, float* history, int32_t* timestep, const float* noise,
+                          double* model_params, float* action_out) {
+    dartmpc::PolicyArgs a;
+    if (policy_args(cfg, B, weights, a) != DART_MPC_OK) return DART_MPC_EINVAL;
+    if (B > 0 && (!state || !target || !control || !current_k || !obs_mean || !obs_M2 || !obs_count || !history ||
+                  !timestep || !noise || !model_params)) return DART_MPC_EINVAL;
+    if (B == 0) return DART_MPC_OK;
+    const size_t nd = (size_t)B * (8 + 8 + 2 + 34 + 52 + 52 + 34);
+    const size_t nf = (size_t)DART_LMPC_POLICY_NWEIGHTS + (size_t)B * (10 * 52 + 34 + 34);
+    double* d = nullptr; float* fl = nullptr; int32_t* iv = nullptr;
+    hipError_t e = hipMalloc(&d, nd * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&fl, nf * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&iv, (size_t)2 * B * sizeof(int32_t));
+    double *d_st = d, *d_tg = d_st + 8 * B, *d_ct = d_tg + 8 * B, *d_ck = d_ct + 2 * B, *d_mn = d_ck + 34 * B,
+           *d_m2 = d_mn + 52 * B, *d_mp = d_m2 + 52 * B;
+    float *d_w = fl, *d_h = d_w + DART_LMPC_POLICY_NWEIGHTS, *d_nz = d_h + 520 * B, *d_ao = d_nz + 34 * B;
+    int32_t *d_cnt = iv, *d_ts = iv + B;
+    auto up = [&](void* dst, const void* src, size_t bytes) {
+        if (e == hipSuccess) e = hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+    };
+    auto dn = [&](void* dst, const void* src, size_t bytes) {
+        if (e == hipSuccess) e = hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+    };
+    up(d_w, weights, sizeof(float) * DART_LMPC_POLICY_NWEIGHTS);
+    up(d_st, state, sizeof(double) * 8 * B); up(d_tg, target, sizeof(double) * 8 * B);
+    up(d_ct, control, sizeof(double) * 2 * B); up(d_ck, current_k, sizeof(double) * 34 * B);
+    up(d_mn, obs_mean, sizeof(double) * 52 * B); up(d_m2, obs_M2, sizeof(double) * 52 * B);
+    up(d_mp, model_params, sizeof(double) * 34 * B); up(d_h, history, sizeof(float) * 520 * B);
+    up(d_nz, noise, sizeof(float) * 34 * B); up(d_cnt, obs_count, sizeof(int32_t) * B);
+    up(d_ts, timestep, sizeof(int32_t) * B);
+    if (e == hipSuccess) {
+        a.w.W1 = d_w; a.w.b1 = d_w + 520 * 64; a.w.W2 = a.w.b1 + 64; a.w.b2 = a.w.W2 + 64 * 64;
+        a.w.W3 = a.w.b2 + 64; a.w.b3 = a.w.W3 + 64 * 34; a.w.log_std = a.w.b3 + 34;
+        a.state = d_st; a.target = d_tg; a.control = d_ct; a.current_k = d_ck; a.obs_mean = d_mn; a.obs_M2 = d_m2;
+        a.obs_count = d_cnt; a.history = d_h; a.timestep = d_ts; a.noise = d_nz; a.model_params = d_mp;
+        a.action_out = d_ao;
+        e = dartmpc_launch_policy(&a, nullptr);
+    }
+    dn(obs_mean, d_mn, sizeof(double) * 52 * B); dn(obs_M2, d_m2, sizeof(double) * 52 * B);
+    dn(model_params, d_mp, sizeof(double) * 34 * B); dn(history, d_h, sizeof(float) * 520 * B);
+    dn(obs_count, d_cnt, sizeof(int32_t) * B); dn(timestep, d_ts, sizeof(int32_t) * B);
+    if (action_out) dn(action_out, d_ao, sizeof(float) * 34 * B);
+    if (d) (void)hipFree(d);
+    if (fl) (void)hipFree(fl);
+    if (iv) (void)hipFree(iv);
+    return e == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
 }
 
 int dart_rls_update_batch_dev(int B, double* theta, double* P, const double* phi, const double* y, double lambda,

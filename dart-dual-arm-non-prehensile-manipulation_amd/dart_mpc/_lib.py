@@ -26,7 +26,8 @@ EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch",
            "dart_mpc_sync", "dart_mpc_last_error", "dart_mpc_destroy", "dart_mpc_nw", "dart_mpc_abi_version",
            "dart_rmpc_solve_batch", "dart_rmpc_solve_batch_dev", "dart_rmpc_nw",
            "dart_rls_update_batch", "dart_rls_update_batch_dev",
-           "dart_lmpc_solve_batch", "dart_lmpc_solve_batch_dev", "dart_lmpc_nw")
+           "dart_lmpc_solve_batch", "dart_lmpc_solve_batch_dev", "dart_lmpc_nw",
+           "dart_lmpc_policy_config_default", "dart_lmpc_policy_step", "dart_lmpc_policy_step_dev")
 VARIANT_PMPC, VARIANT_RMPC, VARIANT_LMPC = 0, 1, 2
 ABI_VERSION = 2
 
@@ -98,6 +99,12 @@ def lib():
     L.dart_lmpc_solve_batch_dev.restype = ctypes.c_int
     L.dart_lmpc_nw.argtypes = [ctypes.c_int]
     L.dart_lmpc_nw.restype = ctypes.c_int
+    L.dart_lmpc_policy_config_default.argtypes = [ctypes.c_void_p]
+    L.dart_lmpc_policy_config_default.restype = None
+    L.dart_lmpc_policy_step.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 13
+    L.dart_lmpc_policy_step.restype = ctypes.c_int
+    L.dart_lmpc_policy_step_dev.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 14
+    L.dart_lmpc_policy_step_dev.restype = ctypes.c_int
     L.dart_rls_update_batch.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_double]
     L.dart_rls_update_batch.restype = ctypes.c_int
     L.dart_rls_update_batch_dev.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_double, ctypes.c_void_p]

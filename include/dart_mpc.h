@@ -17,6 +17,8 @@
  *   dart_lmpc_solve_batch(_dev) <- the solve of RLMPC._solver_worker
  *                             LMPC/src/controller/rlmpc2.py:229-533 (NLP :239-491, solver call
  *                             and warm start :510-520), fed by RLMPC.solve :986-1021
+ *   dart_lmpc_policy_step(_dev) <- the inference / parameter-write half of RLMPC._rl_worker
+ *                             rlmpc2.py:537-769 (Policy :33-80, write_params_to_shm :606-616)
  *   dart_mpc_sync / dart_mpc_last_error / dart_mpc_destroy
  *                           <- process-lifetime handling of the solver object in
  *                             mpc_worker (main_parallel_enhanced.py:22-55)
@@ -170,6 +172,49 @@ int dart_lmpc_solve_batch_dev(dart_mpc_handle *h, int B,
 
 /* Number of fp64 entries of the LMPC w for horizon N: 8(N+1) + 2N. */
 int dart_lmpc_nw(int N);
+
+/* LMPC parameter policy: the inference half of RLMPC._rl_worker
+ * (LMPC/src/controller/rlmpc2.py:537-769) for B independent controllers, producing the
+ * 34-vector model parameters the next solve reads (views["model_params"]).  Per call:
+ * Welford-normalised observation [state, target, control, current_k] (:648-666), 10-step
+ * history (:668-670), mean_net MLP 520 -> 64 -> 64 -> 34 with tanh (Policy :33-80, fp32),
+ * raw action = mean + exp(clamp(log_std)) * noise (Normal.rsample, :674-680; noise [B][34] are
+ * the standard-normal draws), and every update_every-th step the logit-space update
+ * (:742-756, fp32) followed by the EMA + tanh soft clip of write_params_to_shm (:606-616).
+ * Weights (fp32) are given input-major: W1[520][64], b1[64], W2[64][64], b2[64], W3[64][34],
+ * b3[34], log_std[34] packed in this order (39748 floats); nn.Linear stores W transposed. */
+typedef struct dart_lmpc_policy_config {
+    int32_t update_every;      /* 8 (:742) */
+    int32_t reserved;
+    double max_delta;          /* max_delta_abs, 0.02 (LMPC/src/run.py:140) */
+    double k_max;              /* max_param_abs, 2.0 (run.py:139) */
+    double min_k;              /* 1e-2 (:560) */
+    double k_ceiling_margin;   /* max(1e-3, 0.05 k_max) (:563) */
+    double action_scale;       /* 1.0 (:564) */
+    double smooth_alpha;       /* shm_smooth_alpha, 0.5 (:609) */
+    double log_std_min;        /* log(policy_std_min = 1e-2) (:60) */
+    double log_std_max;        /* log(policy_std_max = 2.0) (:61) */
+} dart_lmpc_policy_config;
+
+#define DART_LMPC_POLICY_NWEIGHTS 39748
+
+void dart_lmpc_policy_config_default(dart_lmpc_policy_config *cfg);
+
+/* Device pointers, asynchronous on hip_stream.  In/out: obs_mean[B][52], obs_M2[B][52],
+ * obs_count[B], history[B][10][52] (fp32), timestep[B], model_params[B][34]; action_out
+ * [B][34] (fp32) nullable. */
+int dart_lmpc_policy_step_dev(const dart_lmpc_policy_config *cfg, int B, const float *weights,
+                              const double *state, const double *target, const double *control,
+                              const double *current_k, double *obs_mean, double *obs_M2, int32_t *obs_count,
+                              float *history, int32_t *timestep, const float *noise, double *model_params,
+                              float *action_out, void *hip_stream);
+
+/* Host pointers (stages through device memory and blocks). */
+int dart_lmpc_policy_step(const dart_lmpc_policy_config *cfg, int B, const float *weights,
+                          const double *state, const double *target, const double *control,
+                          const double *current_k, double *obs_mean, double *obs_M2, int32_t *obs_count,
+                          float *history, int32_t *timestep, const float *noise, double *model_params,
+                          float *action_out);
 
 /* Batched standalone RLS.update (np_mpc...:17-27) for B independent p = 7 filters:
  * theta [B][7] and P [B][7][7] updated in place with regressors phi [B][7], targets y [B],

@@ -1,0 +1,55 @@
+"""GPU parity of the LMPC parameter-policy kernel (row L5) against oracle/lmpc_policy.py.
+
+Tolerances: the MLP is fp32 (as the reference's torch Policy), so raw actions agree to 1e-5
+relative; Welford statistics are fp64 (1e-12); the parameter vectors after the fp32 logit update
+and the fp64 EMA / soft clip agree to 1e-6."""
+import numpy as np
+import pytest
+
+import lmpc_policy as lp
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+
+def test_policy_kernel_matches_oracle_over_steps():
+    import dart_mpc
+    B, T = 6, 20
+    rng = np.random.default_rng(5)
+    pol = dart_mpc.LmpcPolicy(B, seed=11)
+    orc = [lp.PolicyState(pol.current_k[b]) for b in range(B)]
+    for t in range(T):
+        s, g, c = rng.normal(size=(B, 8)) * 0.1, rng.normal(size=(B, 8)) * 0.1, rng.uniform(-0.4, 0.4, (B, 2))
+        eps = rng.standard_normal((B, 34)).astype(np.float32)
+        act = pol.step(s, g, c, noise=eps)
+        ref = np.stack([lp.policy_step(orc[b], pol.weights, s[b], g[b], c[b], eps[b]) for b in range(B)])
+        assert np.allclose(act, ref, rtol=1e-5, atol=1e-5), t
+        assert np.allclose(pol.obs_mean, np.stack([o.obs_mean for o in orc]), rtol=1e-12, atol=1e-12)
+        assert np.allclose(pol.model_params, np.stack([o.model_params for o in orc]), rtol=0, atol=1e-6), t
+        assert np.array_equal(pol.timestep, np.full(B, t + 1))
+    hist = np.stack([np.stack(list(o.history)) for o in orc])
+    assert np.allclose(pol.history, hist, rtol=1e-5, atol=1e-6)
+
+
+def test_rlmpc_front_end_step():
+    """RLMPC.solve (rlmpc2.py:986-1021) on an explicit state: policy step -> pvec -> warm-started solve,
+    against the oracle chain (restated policy + C solver without SOC, the kernel's line search)."""
+    import dart_mpc
+    ctl = dart_mpc.RLMPC(None, None, dict(N=20), seed=4)
+    st = lp.PolicyState(ctl.policy.current_k[0])
+    rng = np.random.default_rng(9)
+    state = np.array([0.02, 0.0, -0.01, 0.0, 0.0, 0.0, 0.0, 0.0]); target = np.array([0.1, 0, -0.05, 0, 0, 0, 0, 0])
+    w0 = np.zeros(8 * 21 + 40); uprev = np.zeros(2)
+    for k in range(4):
+        eps = rng.standard_normal(34).astype(np.float32)
+        ctl._rng = np.random.default_rng(0)
+        ctl.policy.step(state, target, ctl.last_control, noise=eps[None])
+        out = ctl.solver.solve_batch(state[None], ctl.last_control[None], ctl.policy.model_params, target[None],
+                                     ctl.prm, w_warm=ctl.w0[None], want_w=True)
+        ctl.w0 = out["w"][0]; ctl.last_control = out["u0"][0]
+        lp.policy_step(st, ctl.policy.weights, state, target, uprev, eps)
+        o = oracle_lib.lmpc_solve_batch(state[None], uprev[None], st.model_params[None], target[None], N=20,
+                                        w_init=w0[None], soc=False)
+        w0 = o["w"][0]; uprev = o["u0"][0]
+        assert np.allclose(ctl.policy.model_params[0], st.model_params, atol=1e-6)
+        assert np.max(np.abs(out["u0"][0] - o["u0"][0])) <= 1e-6, k
