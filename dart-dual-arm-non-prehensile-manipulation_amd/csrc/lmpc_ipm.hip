@@ -52,9 +52,9 @@ struct LmShared {
     LmLds ocp;
     // per node (row 32: scratch of the idle lanes), per RK stage: d f / d y coefficients, and the
     // second-derivative data turned into adjoint-weighted curvature coefficients
-    double SC[LM_NMAXS + 1][4][LM_NSC];
-    double SD[LM_NMAXS + 1][4][8];
-    double JL[LM_NMAXS + 1][12];      // J^T lambda_{k+1} staging, primal residual maxima
+    NodeArr<double[4][LM_NSC], LM_NMAXS + 1> SC;
+    NodeArr<double[4][8], LM_NMAXS + 1> SD;
+    NodeArr<double[12], LM_NMAXS + 1> JL;      // J^T lambda_{k+1} staging, primal residual maxima
     LmModel model;                    // uniform problem data, read at the use sites (keeps VGPRs free)
     double Q[8], Qt[8], tgt[8];
 };
@@ -785,7 +785,7 @@ extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStre
 
 #ifdef DART_STAMPS
 extern "C" hipError_t dartmpc_read_stamps_lmpc(unsigned long long* host_out) {
-    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp_lm), sizeof(unsigned long long) * 12, 0,
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp_lm), sizeof(unsigned long long) * 16, 0,
                                hipMemcpyDeviceToHost);
 }
 #endif

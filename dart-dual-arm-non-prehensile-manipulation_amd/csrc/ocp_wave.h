@@ -29,6 +29,20 @@ __host__ __device__ constexpr int tri(int n) { return n * (n + 1) / 2; }
 __host__ __device__ constexpr int hp(int i, int j) { return i >= j ? tri(i) + j : tri(j) + i; }
 __host__ __device__ constexpr int even(int n) { return (n + 1) & ~1; }
 
+// Per-node LDS array whose per-node stride is an odd number of 16-byte units: lane-per-node
+// accesses (lane k reads or writes its own node's block) then spread over 16 bank groups (2-way at
+// most for ds_*_b64) instead of the 2-4 that a power-of-two-ish stride gives, and every node block
+// stays 16-byte aligned for ds_read_b128 (MI355X_MICROARCH.md §LDS: bank = (a/4) mod 64 / mod 32).
+template <class T, int N>
+struct NodeArr {
+    static constexpr int W = (int)(sizeof(T) / sizeof(double));
+    static constexpr int W2 = (W + 1) & ~1;
+    static constexpr int SW = (W2 / 2) % 2 ? W2 : W2 + 2;
+    alignas(16) double buf[N * SW];
+    __device__ __forceinline__ T& operator[](int k) { return *reinterpret_cast<T*>(buf + k * SW); }
+    __device__ __forceinline__ const T& operator[](int k) const { return *reinterpret_cast<const T*>(buf + k * SW); }
+};
+
 template <int NXA_, int NMAXS_>
 struct OcpLds {
     static constexpr int NXA = NXA_;          // augmented state dimension
@@ -40,11 +54,11 @@ struct OcpLds {
     static constexpr int NTP = even(NT);
     static constexpr int NF = even(NXA + 1);  // closed-loop row stride [Phi row | f]
     static constexpr int EPL = (NT + 63) / 64;     // packed entries of G per lane
-    double M[NMAXS][ND][NC];                  // M[k][j][m] = M_k(m, j): column j of M_k
-    double H[NMAXS][NTP];                     // stage Hessian + gradient, packed symmetric
-    double G[NMAXS][NTP];                     // G_k; G[N] = terminal surrogate (Pt_N, Quu = I)
-    double KK[NMAXS][2][NC];                  // [K | k]_k rows
-    double F[NMAXS][NXA][NF];                 // closed loop: F[k][r] = [Phi_k(r, :) | f_k(r)]
+    NodeArr<double[ND][NC], NMAXS> M;         // M[k][j][m] = M_k(m, j): column j of M_k
+    NodeArr<double[NTP], NMAXS> H;            // stage Hessian + gradient, packed symmetric
+    NodeArr<double[NTP], NMAXS> G;            // G_k; G[N] = terminal surrogate (Pt_N, Quu = I)
+    NodeArr<double[2][NC], NMAXS> KK;         // [K | k]_k rows
+    NodeArr<double[NXA][NF], NMAXS> F;        // closed loop: F[k][r] = [Phi_k(r, :) | f_k(r)]
     double dx0[NC];                           // forward sweep start dx~_0
 };
 

@@ -478,7 +478,7 @@ extern "C" hipError_t dartmpc_wave_selftest(double* d_out, hipStream_t stream) {
 #ifdef DART_STAMPS
 // diagnostic build only: per-phase s_memtime cycles of block 0 from the last launch
 extern "C" hipError_t dartmpc_read_stamps(unsigned long long* host_out) {
-    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp), sizeof(unsigned long long) * 12, 0,
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp), sizeof(unsigned long long) * 16, 0,
                                hipMemcpyDeviceToHost);
 }
 #endif

@@ -14,10 +14,9 @@
 // Method: IPOPT's primal-dual barrier method as in pmpc_ipm.hip (monotone mu, filter line search,
 // inertia correction, bound_relax 1e-8, gradient scaling), with IPOPT's slack formulation of the
 // inequality rows (g(w) - s = 0, bounds on s) eliminated per stage.  The Delta-u coupling is
-// carried by the augmented state x~_k = [x_k; u_{k-1}] (nx~ = 6).  Exact RK4 Jacobians (forward
-// mode, 6 directions); the dynamics part of the Lagrangian Hessian is the RK4-weighted average of
-// Ts * sum_i lambda_i f_i'' over the RK stages (error O(Ts^2) relative; it changes the Newton path
-// only, never the KKT point).
+// carried by the augmented state x~_k = [x_k; u_{k-1}] (nx~ = 6).  Exact derivatives as IPOPT
+// gets them from CasADi: per direction the RK4 tangent (a Jacobian column) and a second-order
+// adjoint sweep through the four stages (a column of the exact Hessian of lambda^T x+).
 //
 // Mapping: one wave64 per instance; lane k owns shooting node k (N <= 31) for everything that is
 // node-local (model evaluation, slacks, multipliers, line search); the node-coupled Riccati and
@@ -40,15 +39,20 @@ using RmLds = OcpLds<6, RM_NMAXS>;
 __device__ unsigned long long g_stamp_rm[16];
 #endif
 
+struct RmModel {
+    double th[14];
+    double gz, h, ie;             // gravity, Ts, 1/v_eps
+};
+
 struct RmShared {
     RmLds ocp;
     double theta[14];
     double rls_Pphi[2][7], rls_phiP[2][7];
-};
-
-struct RmModel {
-    double th[14];
-    double gz, h, ie;             // gravity, Ts, 1/v_eps
+    RmModel model;                            // uniform, read at the use sites (keeps VGPRs free)
+    NodeArr<double[4][4], RM_NMAXS + 1> SC;   // per node (row 32: idle lanes), per RK stage: d f1,3 / d vx,vy
+    NodeArr<double[4][2], RM_NMAXS + 1> SD;   // tanh curvature per stage -> adjoint-weighted coefficients
+    NodeArr<double[8], RM_NMAXS + 1> JL;      // J^T lambda staging, primal residual maxima
+    NodeArr<double[10], RM_NMAXS + 1> DL;     // per node: lambda_{k+1}, tilt curvature, g cos(u) for the mirror lanes
 };
 
 // continuous model (np_mpc...:178-186); also returns d f / d vx|vy of rows 1, 3 and tanh values
@@ -84,55 +88,140 @@ __device__ __forceinline__ void rm_rk4(const RmModel& m, const double* x, double
     for (int i = 0; i < 4; ++i) xn[i] = x[i] + m.h / 6 * (acc[i] + k[i]);
 }
 
-// RK4 value + exact Jacobian J = d x+ / d [px vx py vy alpha beta] (forward mode, 6 directions)
-// + the RK-weighted dynamics curvature diag (vx, vy, alpha, beta) contracted with -lambda_{k+1}.
-__device__ __forceinline__ void rm_rk4_jac(const RmModel& m, const double* x, double sa, double ca, double sb,
-                                           double cb, const double* lam, double* xn, double J[4][6],
-                                           double& hvx, double& hvy, double& haa, double& hbb) {
-    double yd[6][4], acc[6][4], k[4], y[4], kacc[4];
+// Value pass of RK4 storing per stage s the tangent coefficients sc[s] = [d f1/d vx, d f1/d vy,
+// d f3/d vx, d f3/d vy] and the tanh curvature sd[s] = [T''(vx), T''(vy)] (T = tanh(v / v_eps)).
+__device__ __forceinline__ void rm_rk4_lin(const RmModel& m, const double* x, double sa, double sb, double* xn,
+                                           double (*sc)[4], double (*sd)[2]) {
+    double y[4], acc[4];
 #pragma unroll
-    for (int d = 0; d < 6; ++d)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { yd[d][i] = (i == d) ? 1.0 : 0.0; acc[d][i] = 0.0; }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { y[i] = x[i]; kacc[i] = 0.0; }
-    const double wts[4] = {1.0, 2.0, 2.0, 1.0}, cst[4] = {0.5, 0.5, 1.0, 0.0};
-    hvx = 0.0; hvy = 0.0;
-    const double lx = lam[1], ly = lam[3];
-#pragma unroll
+    for (int i = 0; i < 4; ++i) { y[i] = x[i]; acc[i] = 0.0; }
+#pragma unroll 1
     for (int s = 0; s < 4; ++s) {
-        double j1vx, j1vy, j3vx, j3vy, tx, ty;
+        const double wts = (s == 0 || s == 3) ? 1.0 : 2.0, cst = s < 2 ? 0.5 : (s == 2 ? 1.0 : 0.0);
+        double k[4], j1vx, j1vy, j3vx, j3vy, tx, ty;
         rm_f(m, y, sa, sb, k, j1vx, j1vy, j3vx, j3vy, tx, ty);
-        // curvature of f in vx, vy at this RK stage: T'' = -2 T (1 - T^2) / eps^2
-        const double t2x = -2.0 * tx * (1.0 - tx * tx) * m.ie * m.ie, t2y = -2.0 * ty * (1.0 - ty * ty) * m.ie * m.ie;
-        const double w = m.h * wts[s] / 6.0;
-        hvx -= w * (lx * m.th[4] + ly * m.th[11]) * t2x;
-        hvy -= w * (lx * m.th[5] + ly * m.th[12]) * t2y;
+        sc[s][0] = j1vx; sc[s][1] = j1vy; sc[s][2] = j3vx; sc[s][3] = j3vy;
+        sd[s][0] = -2.0 * tx * (1.0 - tx * tx) * m.ie * m.ie;
+        sd[s][1] = -2.0 * ty * (1.0 - ty * ty) * m.ie * m.ie;
 #pragma unroll
-        for (int d = 0; d < 6; ++d) {
-            const double k0 = yd[d][1], k2 = yd[d][3];
-            const double k1 = m.th[0] * yd[d][0] + j1vx * yd[d][1] + m.th[2] * yd[d][2] + j1vy * yd[d][3] + (d == 4 ? m.gz * ca : 0.0);
-            const double k3 = m.th[7] * yd[d][0] + j3vx * yd[d][1] + m.th[9] * yd[d][2] + j3vy * yd[d][3] + (d == 5 ? m.gz * cb : 0.0);
-            acc[d][0] += wts[s] * k0; acc[d][1] += wts[s] * k1; acc[d][2] += wts[s] * k2; acc[d][3] += wts[s] * k3;
-            yd[d][0] = (d == 0 ? 1.0 : 0.0) + cst[s] * m.h * k0;
-            yd[d][1] = (d == 1 ? 1.0 : 0.0) + cst[s] * m.h * k1;
-            yd[d][2] = (d == 2 ? 1.0 : 0.0) + cst[s] * m.h * k2;
-            yd[d][3] = (d == 3 ? 1.0 : 0.0) + cst[s] * m.h * k3;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) kacc[i] += wts[s] * k[i];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) y[i] = x[i] + cst[s] * m.h * k[i];
+        for (int i = 0; i < 4; ++i) { acc[i] = fma(wts, k[i], acc[i]); y[i] = fma(cst * m.h, k[i], x[i]); }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xn[i] = x[i] + m.h / 6 * kacc[i];
+    for (int i = 0; i < 4; ++i) xn[i] = fma(m.h / 6.0, acc[i], x[i]);
+}
+
+// q = (d f / d y at stage s)^T v
+__device__ __forceinline__ void rm_jtv(const RmModel& m, const double* c, const double* v, double* q) {
+    q[0] = fma(m.th[0], v[1], m.th[7] * v[3]);
+    q[1] = fma(c[0], v[1], fma(c[2], v[3], v[0]));
+    q[2] = fma(m.th[2], v[1], m.th[9] * v[3]);
+    q[3] = fma(c[1], v[1], fma(c[3], v[3], v[2]));
+}
+
+// First-order adjoint of nl^T x+ (nl = -lambda_{k+1}) through the RK4 stages; turns sd[s] into the
+// curvature coefficients of kb_s^T f'' at y_s ((vx, vx) and (vy, vy)); returns the tilt curvature.
+__device__ __forceinline__ void rm_adjoint_curv(const RmModel& m, const double (*sc)[4], double (*sd)[2],
+                                                const double* lamn, double sa, double sb, double* huu) {
+    double kb[4], yb[4];
+    const double h = m.h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) kb[i] = -(h / 6.0) * lamn[i];
+    huu[0] = 0.0; huu[1] = 0.0;
+#pragma unroll 1
+    for (int s = 3; s >= 0; --s) {
+        sd[s][0] = fma(kb[1], m.th[4], kb[3] * m.th[11]) * sd[s][0];
+        sd[s][1] = fma(kb[1], m.th[5], kb[3] * m.th[12]) * sd[s][1];
+        huu[0] = fma(kb[1], -m.gz * sa, huu[0]);
+        huu[1] = fma(kb[3], -m.gz * sb, huu[1]);
+        if (s > 0) {
+            rm_jtv(m, sc[s], kb, yb);
+            const double cs = s == 3 ? h : 0.5 * h, ws = (s == 1 ? 1.0 : 2.0) * h / 6.0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) kb[i] = fma(cs, yb[i], -ws * lamn[i]);
+        }
+    }
+}
+
+// Direction d (0..3 state, 4..5 tilt): RK4 tangent -> Jacobian column (into M~, returns col . lamn),
+// then the second-order adjoint sweep -> column d of the exact Hessian of -lambda^T x+ (rows >= d,
+// z indices x 0..3, tilt 6..7).
+__device__ __forceinline__ double rm_direction(const RmModel& m, const double (*sc)[4], const double (*cv)[2],
+                                               const double* huu, double gca, double gcb, int d, const double* lamn,
+                                               double* Mk, double* Hk) {
+    double yd[4][4], acc[4], e[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { e[i] = (i == d) ? 1.0 : 0.0; yd[0][i] = e[i]; acc[i] = 0.0; }
+    const double fa = d == 4 ? gca : 0.0, fb = d == 5 ? gcb : 0.0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const double wts = (s == 0 || s == 3) ? 1.0 : 2.0, cst = s < 2 ? 0.5 : (s == 2 ? 1.0 : 0.0);
+        const double* c = sc[s];
+        const double* y = yd[s];
+        double k[4];
+        k[0] = y[1]; k[2] = y[3];
+        k[1] = fma(m.th[0], y[0], fma(c[0], y[1], fma(m.th[2], y[2], fma(c[1], y[3], fa))));
+        k[3] = fma(m.th[7], y[0], fma(c[2], y[1], fma(m.th[9], y[2], fma(c[3], y[3], fb))));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = fma(wts, k[i], acc[i]);
+        if (s < 3) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) yd[s + 1][i] = fma(cst * m.h, k[i], e[i]);
+        }
+    }
+    const int jc = d < 4 ? d : d + 2;
+    double dot = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const double col = fma(m.h / 6.0, acc[i], e[i]);
+        Mk[jc * RmLds::NC + i] = col;
+        dot = fma(col, lamn[i], dot);
+    }
+    double kbd[4], hx[4], hu0 = d == 4 ? huu[0] : 0.0, hu1 = d == 5 ? huu[1] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { kbd[i] = 0.0; hx[i] = 0.0; }
+#pragma unroll
+    for (int s = 3; s >= 0; --s) {
+        double q[4];
+        rm_jtv(m, sc[s], kbd, q);
+        q[1] = fma(cv[s][0], yd[s][1], q[1]);
+        q[3] = fma(cv[s][1], yd[s][3], q[3]);
+        hu0 = fma(gca, kbd[1], hu0);
+        hu1 = fma(gcb, kbd[3], hu1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hx[i] += q[i];
+        const double cs = s == 3 ? m.h : 0.5 * m.h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) kbd[i] = cs * q[i];
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
+        if (i >= d) Hk[hp(i, jc)] = hx[i];
+    Hk[hp(6, jc)] = hu0;
+    Hk[hp(7, jc)] = hu1;
+    return dot;
+}
+
+// directions d0 .. d0+2 of one node (the two half-waves of the wave split the six directions);
+// per-node inputs from LDS: dl = [lambda_{k+1}(6), huu(2), g cos a, g cos b]
+__device__ __forceinline__ void rm_directions(const RmModel& m, const double (*sc)[4], const double (*cv)[2],
+                                              const double* dl, int d0, double* Mk, double* Hk, double* jl_lds) {
+    double lamn[6], huu[2], scr[4][4], cvr[4][2];
 #pragma unroll
-        for (int d = 0; d < 6; ++d) J[i][d] = ((i == d) ? 1.0 : 0.0) + m.h / 6 * acc[d][i];
-    // alpha, beta: f'' = -gz sin, contracted with -lambda and Ts
-    haa = m.h * lx * m.gz * sa;
-    hbb = m.h * ly * m.gz * sb;
+    for (int i = 0; i < 6; ++i) lamn[i] = dl[i];
+    huu[0] = dl[6]; huu[1] = dl[7];
+    const double gca = dl[8], gcb = dl[9];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {       // stage data to registers once for the three directions
+#pragma unroll
+        for (int i = 0; i < 4; ++i) scr[st][i] = sc[st][i];
+        cvr[st][0] = cv[st][0]; cvr[st][1] = cv[st][1];
+    }
+    RmModel mr;
+#pragma unroll
+    for (int i = 0; i < 14; ++i) mr.th[i] = m.th[i];
+    mr.gz = m.gz; mr.h = m.h; mr.ie = m.ie;
+#pragma unroll 1
+    for (int d = d0; d < d0 + 3; ++d) jl_lds[d] = rm_direction(mr, scr, cvr, huu, gca, gcb, d, lamn, Mk, Hk);
 }
 
 // z = [px vx py vy upx upy ux uy]: inequality row values C z (np_mpc...:114-127)
@@ -203,10 +292,19 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     }
     __syncthreads();
 
-    RmModel m;
-#pragma unroll
-    for (int i = 0; i < 14; ++i) m.th[i] = SH.theta[i];
-    m.gz = a.g; m.h = a.Ts; m.ie = 1.0 / veps;
+    if (k < 14) SH.model.th[k] = SH.theta[k];
+    if (k == 0) { SH.model.gz = a.g; SH.model.h = a.Ts; SH.model.ie = 1.0 / veps; }
+    __syncthreads();
+    const RmModel& m = SH.model;
+    const int sr = xon ? k : RM_NMAXS;        // per-node LDS scratch row (idle lanes share row 32)
+    double* Mk = &S->M[xon ? k : 0][0][0];
+    double* Hk = S->H[xon ? k : 0];
+    if (uon) {       // constant structure: zero once, then only the variable entries are written
+        for (int e = 0; e < RmLds::ND * RmLds::NC; ++e) Mk[e] = 0.0;
+        for (int e = 0; e < tri(9); ++e) Hk[e] = 0.0;
+        Mk[6 * RmLds::NC + 4] = 1.0; Mk[7 * RmLds::NC + 5] = 1.0;     // up+ = u
+        Mk[8 * RmLds::NC + 6] = 1.0;                                  // homogeneous coordinate
+    }
 
     const double lo = ulo - 1e-8 * fmax(1.0, fabs(ulo)), hi = uhi + 1e-8 * fmax(1.0, fabs(uhi));
     double sL[RM_NIQ], sU[RM_NIQ];            // relaxed slack bounds (lower only on the du rows)
@@ -325,36 +423,54 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     STAMP(0);
     for (it = 0; it < a.max_iter; ++it) {
         // ---------------- derivatives, residuals, optimality error ---------------------------
-        double sa, ca, sb, cb;
-        tilt_sincos(poly, u[0], sa, ca);
-        tilt_sincos(poly, u[1], sb, cb);
+        // stage data go to LDS as soon as they exist (Jacobian columns, dynamics Hessian, defect
+        // column, dx~_0) to keep the register working set small
         double lamn[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) { const double t = from_next(lam[i]); lamn[i] = uon ? t : 0.0; }
-        double xn[4], J[4][6], hvx, hvy, haa, hbb;
-        rm_rk4_jac(m, x, sa, ca, sb, cb, lamn, xn, J, hvx, hvy, haa, hbb);
-        double cdef[6];           // outgoing defect c_k = F(z_k) - x~_{k+1}
+        double jl[6];            // J^T lambda_{k+1} (x columns 0..3, tilt 4..5)
         {
-            double nx_[6];
+            double sa, ca, sb, cb;
+            tilt_sincos(poly, u[0], sa, ca);
+            tilt_sincos(poly, u[1], sb, cb);
+            double xn[4], huu[2];
+            rm_rk4_lin(m, x, sa, sb, xn, SH.SC[sr], SH.SD[sr]);
+            rm_adjoint_curv(m, SH.SC[sr], SH.SD[sr], lamn, sa, sb, huu);
+            if (k < 32) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) nx_[i] = from_next(x[i]);
-            nx_[4] = from_next(up[0]); nx_[5] = from_next(up[1]);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) cdef[i] = xn[i] - nx_[i];
-            cdef[4] = u[0] - nx_[4]; cdef[5] = u[1] - nx_[5];
-        }
-        double gin[6];            // incoming defect g_k
-        {
-            double f[6];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) f[i] = from_prev(cdef[i]);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) gin[i] = -f[i];
-            if (k == 0) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) gin[i] = x[i] - x0[i];
-                gin[4] = up[0] - upv[0]; gin[5] = up[1] - upv[1];
+                for (int i = 0; i < 6; ++i) SH.DL[k][i] = lamn[i];
+                SH.DL[k][6] = huu[0]; SH.DL[k][7] = huu[1]; SH.DL[k][8] = m.gz * ca; SH.DL[k][9] = m.gz * cb;
             }
+            __syncthreads();
+            STAMP(11);
+            {   // lanes k and k + 32 own directions 0..2 and 3..5 of node k
+                const int kn = k & 31;
+                if (kn < N)
+                    rm_directions(m, SH.SC[kn], SH.SD[kn], SH.DL[kn], k < 32 ? 0 : 3, &S->M[kn][0][0], S->H[kn],
+                                  SH.JL[kn]);
+            }
+            __syncthreads();
+            STAMP(12);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) jl[i] = uon ? SH.JL[sr][i] : 0.0;
+            double cdef[6];      // outgoing defect c_k = F(z_k) - x~_{k+1} -> defect column of M~
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { const double t = from_next(x[i]); cdef[i] = xn[i] - t; }
+            { const double t0 = from_next(up[0]), t1 = from_next(up[1]); cdef[4] = u[0] - t0; cdef[5] = u[1] - t1; }
+            if (uon) {
+#pragma unroll
+                for (int r = 0; r < 6; ++r) Mk[8 * RmLds::NC + r] = cdef[r];
+            }
+            double pl = 0.0;     // incoming defect g_k: primal residual, -g_0 = dx~_0
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double t = from_prev(cdef[i]);
+                double gi = -t;
+                if (k == 0) gi = i < 4 ? x[i] - x0[i] : up[i - 4] - upv[i - 4];
+                pl = fmax(pl, xon ? fabs(gi) : 0.0);
+                if (k == 0) S->dx0[i] = -gi;
+            }
+            SH.JL[sr][6] = pl;
         }
         const double zz[8] = {x[0], x[1], x[2], x[3], up[0], up[1], u[0], u[1]};
         double cz[RM_NIQ], rq[RM_NIQ], sig[RM_NIQ], psi[RM_NIQ];
@@ -366,23 +482,18 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             sig[i] = uon ? (i < 2 ? vl[i] / dl : 0.0) + vu[i] / du_ : 0.0;
             psi[i] = uon ? (i < 2 ? -mu / dl : 0.0) + mu / du_ : 0.0;
         }
-        double gz_[8];
-        cost_grad(x, u, up, gz_);
-        double dinf = 0.0, pinf = 0.0, c0 = 0.0, cmin = 1e300, suml = 0.0, sumz = 0.0;
+        double dinf = 0.0, pinf = SH.JL[sr][6], c0 = 0.0, cmin = 1e300, suml = 0.0, sumz = 0.0;
         {
             double gl[8];
+            cost_grad(x, u, up, gl);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) gl[j] = sc * gz_[j];
+            for (int j = 0; j < 8; ++j) gl[j] *= sc;
 #pragma unroll
             for (int i = 0; i < 6; ++i) gl[i] += lam[i];
             // - A~^T lam_{k+1} - B~^T lam_{k+1}
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) gl[j] -= J[r][j] * lamn[r];
-                gl[6] -= J[r][4] * lamn[r]; gl[7] -= J[r][5] * lamn[r];
-            }
-            gl[6] -= lamn[4]; gl[7] -= lamn[5];
+            for (int j = 0; j < 4; ++j) gl[j] -= jl[j];
+            gl[6] -= jl[4] + lamn[4]; gl[7] -= jl[5] + lamn[5];
             // + C^T y
             gl[6] += yq[0]; gl[4] -= yq[0]; gl[7] += yq[1]; gl[5] -= yq[1];
             gl[1] += yq[2] - yq[3]; gl[3] += yq[4] - yq[5];
@@ -392,7 +503,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 #pragma unroll
             for (int i = 0; i < RM_NIQ; ++i) dinf = fmax(dinf, uon ? fabs(-yq[i] - vl[i] + vu[i]) : 0.0);
 #pragma unroll
-            for (int i = 0; i < 6; ++i) { pinf = fmax(pinf, xon ? fabs(gin[i]) : 0.0); suml += xon ? fabs(lam[i]) : 0.0; }
+            for (int i = 0; i < 6; ++i) suml += xon ? fabs(lam[i]) : 0.0;
 #pragma unroll
             for (int i = 0; i < RM_NIQ; ++i) {
                 pinf = fmax(pinf, fabs(rq[i]));
@@ -433,40 +544,27 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         const double isl0 = uon ? frcp(u[0] - lo) : 0.0, isl1 = uon ? frcp(u[1] - lo) : 0.0;
         const double isu0 = uon ? frcp(hi - u[0]) : 0.0, isu1 = uon ? frcp(hi - u[1]) : 0.0;
         {
-            // gradient column (index 8): scaled cost + box barrier + C^T (Sigma r + psi)
+            // gradient column (index 8): scaled cost + box barrier + C^T (Sigma r + psi); the
+            // cost / slack / barrier parts of the Hessian on top of the dynamics part
             double gq[8];
+            cost_grad(x, u, up, gq);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) gq[j] = sc * gz_[j];
+            for (int j = 0; j < 8; ++j) gq[j] *= sc;
             if (uon) {
                 gq[6] += -mu * isl0 + mu * isu0; gq[7] += -mu * isl1 + mu * isu1;
                 const double t0 = sig[0] * rq[0] + psi[0], t1 = sig[1] * rq[1] + psi[1];
                 gq[6] += t0; gq[4] -= t0; gq[7] += t1; gq[5] -= t1;
                 gq[1] += (sig[2] * rq[2] + psi[2]) - (sig[3] * rq[3] + psi[3]);
                 gq[3] += (sig[4] * rq[4] + psi[4]) - (sig[5] * rq[5] + psi[5]);
-                double* Hk = S->H[k];
-                for (int e = 0; e < tri(9); ++e) Hk[e] = 0.0;
-                Hk[hp(0, 0)] = sc * 2 * Qp; Hk[hp(2, 2)] = sc * 2 * Qp;
-                Hk[hp(1, 1)] = sc * 2 * Qv + hvx + sig[2] + sig[3];
-                Hk[hp(3, 3)] = sc * 2 * Qv + hvy + sig[4] + sig[5];
-                Hk[hp(6, 6)] = sc * 2 * (Ru + Rdu) + haa + zl[0] * isl0 + zu[0] * isu0 + sig[0];
-                Hk[hp(7, 7)] = sc * 2 * (Ru + Rdu) + hbb + zl[1] * isl1 + zu[1] * isu1 + sig[1];
+                Hk[hp(0, 0)] += sc * 2 * Qp; Hk[hp(2, 2)] += sc * 2 * Qp;
+                Hk[hp(1, 1)] += sc * 2 * Qv + sig[2] + sig[3];
+                Hk[hp(3, 3)] += sc * 2 * Qv + sig[4] + sig[5];
+                Hk[hp(6, 6)] += sc * 2 * (Ru + Rdu) + zl[0] * isl0 + zu[0] * isu0 + sig[0];
+                Hk[hp(7, 7)] += sc * 2 * (Ru + Rdu) + zl[1] * isl1 + zu[1] * isu1 + sig[1];
                 Hk[hp(4, 4)] = sc * 2 * Rdu + sig[0]; Hk[hp(5, 5)] = sc * 2 * Rdu + sig[1];
                 Hk[hp(6, 4)] = -sc * 2 * Rdu - sig[0]; Hk[hp(7, 5)] = -sc * 2 * Rdu - sig[1];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) Hk[hp(8, j)] = gq[j];
-                // M~ columns: x (0..3), up (4,5), u (6,7), 1 (8); rows x~ (0..5), 1 (6)
-                for (int j = 0; j < 9; ++j)
-                    for (int r = 0; r < 7; ++r) S->M[k][j][r] = 0.0;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) S->M[k][j][r] = J[r][j];
-                    S->M[k][6][r] = J[r][4]; S->M[k][7][r] = J[r][5];
-                }
-                S->M[k][6][4] = 1.0; S->M[k][7][5] = 1.0;
-#pragma unroll
-                for (int r = 0; r < 6; ++r) S->M[k][8][r] = cdef[r];
-                S->M[k][8][6] = 1.0;
             }
             if (k == N) {   // terminal surrogate G_N: value function [[Q_N, q_N], [q_N^T, 0]], Quu = I
                 double* GN = S->G[N];
@@ -491,7 +589,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             const double dd = delta - dapplied;
             if (uon) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) S->H[k][hp(j, j)] += dd;
+                for (int j = 0; j < 8; ++j) Hk[hp(j, j)] += dd;
             }
             if (k == N) {
                 // the sweep never overwrites the terminal surrogate: add delta on its x~ block
@@ -506,13 +604,11 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         STAMP(3);
         if (!ok) { status = -3; break; }
         if (delta > 0.0) delta_last = delta;
-        if (k == 0) {
-#pragma unroll
-            for (int i = 0; i < 6; ++i) S->dx0[i] = -gin[i];
-        }
         closed_loop(S, N);
+        STAMP(13);
         double dx[6], dU[2], lamp[6];
         forward_sweep(S, N, k, dx);
+        STAMP(14);
         {
             const int kk = xon ? k : 0;
             const double* K0 = S->KK[uon ? k : 0][0];
@@ -580,8 +676,9 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             const double pa = barrier_args(u, s);
             phil -= uon ? mu * log(pa) : 0.0;
             double gq[8];
+            cost_grad(x, u, up, gq);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) gq[j] = sc * gz_[j];
+            for (int j = 0; j < 8; ++j) gq[j] *= sc;
 #pragma unroll
             for (int i = 0; i < 6; ++i) gtdl += xon ? gq[i] * dx[i] : 0.0;
             if (uon) {
@@ -745,7 +842,7 @@ extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStre
 
 #ifdef DART_STAMPS
 extern "C" hipError_t dartmpc_read_stamps_rmpc(unsigned long long* host_out) {
-    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp_rm), sizeof(unsigned long long) * 12, 0,
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp_rm), sizeof(unsigned long long) * 16, 0,
                                hipMemcpyDeviceToHost);
 }
 #endif

@@ -163,6 +163,9 @@ enum { ST_SOLVED = 0, ST_MAXITER = -1, ST_LS_FAIL = -2, ST_INERTIA_FAIL = -3, ST
 /* IPOPT bound_relax_factor (1e-8 default); the golden generator sets 0 to solve the exact NLP */
 static double g_relax = 1e-8;
 void oracle_rmpc_set_relax(double r) { g_relax = r; }
+/* second-order correction on/off (IPOPT default on; off mirrors the GPU kernel's line search) */
+static int g_soc = 1;
+void oracle_rmpc_set_soc(int on) { g_soc = on; }
 
 static void stage_z(const double *X, const double *U, int k, double *z) {
     for (int i = 0; i < NA; ++i) z[i] = X[NA * k + i];
@@ -593,7 +596,7 @@ int oracle_rmpc_solve(int N, double Ts, const double *x0, const double *u_prev, 
                     if (th <= th_min && sw) { if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { accepted = 1; ftype = 1; } }
                     else if (LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi)) accepted = 1;
                 }
-                if (accepted || ls > 0 || th_t < th) break;
+                if (accepted || ls > 0 || th_t < th || !g_soc) break;
                 if (pass == 0) {
                     for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] = alpha * g[k][i] + gt[k][i];
                     for (int k = 0; k < N; ++k) for (int i = 0; i < NIQ; ++i) csr[k][i] = alpha * r[k][i] + rt[k][i];

@@ -153,3 +153,19 @@ def test_closed_loop_driver_matches_oracle_loop(dm):
         assert np.max(np.abs(u - o["u0"][0])) <= 1e-6, (k, u, o["u0"][0])
         xprev, x = x, rmpc_nlp.rk4(x, u, truth, 0.1, 0.002)
         up = u
+
+
+def test_same_path_as_oracle_without_soc(dm):
+    """Exact derivatives in the kernel: against the C oracle with its second-order correction off
+    (the kernel's line search has none) every instance takes the same iterations, ends with the same
+    status and returns the same control at the reference's tol 1e-8."""
+    from dart_mpc.workload import rmpc_batch
+    D = rmpc_batch(8, seed0=40)
+    s = dm.RmpcSolver(N=20, tol=1e-8, B_max=256)
+    g = s.solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
+    s.close()
+    o = oracle_lib.rmpc_solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"], N=20, tol=1e-8,
+                                    nthreads=8, soc=False)
+    assert np.array_equal(g["status"], o["status"])
+    assert np.mean(g["iters"] == o["iters"]) >= 0.99, (g["iters"], o["iters"])
+    assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(ROOT, "dart-dual-arm-non-prehensile-manipulation
 from dart_mpc import _lib  # noqa: E402
 from dart_mpc.workload import pmpc_batch  # noqa: E402
 
-_lib.LIB_PATH = os.path.join(_lib.PKG_DIR, "libdartmpc_stamps.so")
+_lib.LIB_PATH = os.path.join(_lib.PKG_DIR, os.environ.get("DART_STAMPS_LIB", "libdartmpc_stamps.so"))
 L = _lib.lib()
 L.dartmpc_read_stamps.argtypes = [ctypes.c_void_p]
 PHASES = ["setup", "eval+errors", "mu update", "riccati", "forward+dz", "ls prep", "ls trials", "update", "outputs"]
@@ -23,7 +23,7 @@ S, T, P = pmpc_batch(1)
 s = _lib.Solver(N=20, B_max=64)
 for rep in range(3):
     out = s.solve_batch(S, T, P)
-st = np.zeros(12, dtype=np.uint64)
+st = np.zeros(16, dtype=np.uint64)
 L.dartmpc_read_stamps(ctypes.c_void_p(st.ctypes.data))
 tot = float(st[:9].sum())
 print(f"block0 iters={out['iters'][0]} total cycles={tot:.0f}")

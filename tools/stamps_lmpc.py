@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(ROOT, "dart-dual-arm-non-prehensile-manipulation
 from dart_mpc import _lib  # noqa: E402
 from dart_mpc.workload import lmpc_batch  # noqa: E402
 
-_lib.LIB_PATH = os.path.join(_lib.PKG_DIR, "libdartmpc_stamps.so")
+_lib.LIB_PATH = os.path.join(_lib.PKG_DIR, os.environ.get("DART_STAMPS_LIB", "libdartmpc_stamps.so"))
 L = _lib.lib()
 L.dartmpc_read_stamps_lmpc.argtypes = [ctypes.c_void_p]
 PHASES = ["setup", "eval+errors+mu", "gradient rows", "riccati", "forward+dz", "bound steps", "ls prep",
@@ -23,7 +23,7 @@ D = lmpc_batch(1)
 s = _lib.LmpcSolver(N=30, tol=1e-8, max_iter=500, acceptable_iter=0, B_max=64)
 for rep in range(3):
     out = s.solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"])
-st = np.zeros(12, dtype=np.uint64)
+st = np.zeros(16, dtype=np.uint64)
 L.dartmpc_read_stamps_lmpc(ctypes.c_void_p(st.ctypes.data))
 tot = float(st[:9].sum())
 it = max(1, out["iters"][0])

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(ROOT, "dart-dual-arm-non-prehensile-manipulation
 from dart_mpc import _lib  # noqa: E402
 from dart_mpc.workload import rmpc_batch  # noqa: E402
 
-_lib.LIB_PATH = os.path.join(_lib.PKG_DIR, "libdartmpc_stamps.so")
+_lib.LIB_PATH = os.path.join(_lib.PKG_DIR, os.environ.get("DART_STAMPS_LIB", "libdartmpc_stamps.so"))
 L = _lib.lib()
 L.dartmpc_read_stamps_rmpc.argtypes = [ctypes.c_void_p]
 PHASES = ["setup+rls", "eval+errors+mu", "qp build", "riccati", "forward+dz", "slack steps", "ls prep", "ls trials",
@@ -23,12 +23,14 @@ D = rmpc_batch(1)
 s = _lib.RmpcSolver(N=20, B_max=64)
 for rep in range(3):
     out = s.solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
-st = np.zeros(12, dtype=np.uint64)
+st = np.zeros(16, dtype=np.uint64)
 L.dartmpc_read_stamps_rmpc(ctypes.c_void_p(st.ctypes.data))
-tot = float(st[:9].sum())
+tot = float(st[:9].sum() + st[11:15].sum())
 it = max(1, out["iters"][0])
 print(f"block0 iters={out['iters'][0]} total cycles={tot:.0f}")
 for i, n in enumerate(PHASES):
+    print(f"  {n:15s} {int(st[i]):10d}  {100 * st[i] / tot:5.1f}%  per-iter {st[i] / it:9.0f}")
+for i, n in zip(range(11, 15), ["eval: rk4+adjoint", "eval: directions", "closed loop", "forward sweep"]):
     print(f"  {n:15s} {int(st[i]):10d}  {100 * st[i] / tot:5.1f}%  per-iter {st[i] / it:9.0f}")
 print(f"  riccati passes {int(st[9])}, line-search trials {int(st[10])}")
 print("batch iters:", out["iters"].tolist())
