@@ -14,6 +14,7 @@
 #include "rmpc_ipm.h"
 #include "lmpc_ipm.h"
 #include "lmpc_policy.h"
+#include "arm_qp.h"
 
 #include <cmath>
 
@@ -453,3 +454,67 @@ void dart_mpc_destroy(dart_mpc_handle* h) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// per-arm impedance QP (ARMCONTROL.solver_worker, PMPC/src/controller/arm.py:266-457)
+void dart_arm_config_default(dart_arm_config* c) {
+    if (!c) return;
+    c->tol = 1e-10;
+    c->acceptable_tol = 1e-7;
+    c->max_iter = 60;
+    c->reserved = 0;
+}
+
+int dart_arm_snapshot_len(int n) { return (n >= 1 && n <= DART_ARM_NMAX) ? dartmpc::arm_snap_len(n) : DART_MPC_EINVAL; }
+int dart_arm_param_len(int n) { return (n >= 1 && n <= DART_ARM_NMAX) ? dartmpc::arm_prm_len(n) : DART_MPC_EINVAL; }
+
+static int arm_args(const dart_arm_config* c, int B, int n, int prm_stride, dartmpc::ArmArgs& a) {
+    if (!c || B < 0 || n < 1 || n > DART_ARM_NMAX) return DART_MPC_EINVAL;
+    if (prm_stride != 0 && prm_stride != dartmpc::arm_prm_len(n)) return DART_MPC_EINVAL;
+    if (!(c->tol > 0.0) || !(c->acceptable_tol >= c->tol) || c->max_iter < 1 || c->max_iter > 100000) return DART_MPC_EINVAL;
+    a = dartmpc::ArmArgs{};
+    a.B = B; a.n = n; a.prm_stride = prm_stride; a.max_iter = c->max_iter;
+    a.tol = c->tol; a.acc_tol = c->acceptable_tol;
+    return DART_MPC_OK;
+}
+
+int dart_arm_solve_batch_dev(const dart_arm_config* cfg, int B, int n, const double* snap, const double* prm,
+                             int prm_stride, double* qdd, double* tau, double* loss, int32_t* status, int32_t* iters,
+                             void* stream) {
+    dartmpc::ArmArgs a;
+    if (arm_args(cfg, B, n, prm_stride, a) != DART_MPC_OK) return DART_MPC_EINVAL;
+    if (B == 0) return DART_MPC_OK;
+    if (!snap || !prm || !qdd || !tau || !loss || !status || !iters) return DART_MPC_EINVAL;
+    a.snap = snap; a.prm = prm; a.qdd = qdd; a.tau = tau; a.loss = loss; a.status = status; a.iters = iters;
+    return dartmpc_launch_arm(&a, (hipStream_t)stream) == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
+}
+
+int dart_arm_solve_batch(const dart_arm_config* cfg, int B, int n, const double* snap, const double* prm,
+                         int prm_stride, double* qdd, double* tau, double* loss, int32_t* status, int32_t* iters) {
+    dartmpc::ArmArgs a;
+    if (arm_args(cfg, B, n, prm_stride, a) != DART_MPC_OK) return DART_MPC_EINVAL;
+    if (B == 0) return DART_MPC_OK;
+    if (!snap || !prm || !qdd || !tau || !loss || !status || !iters) return DART_MPC_EINVAL;
+    const size_t SL = (size_t)dartmpc::arm_snap_len(n), PL = (size_t)dartmpc::arm_prm_len(n);
+    const size_t np = prm_stride ? PL * B : PL;
+    const size_t nd = SL * B + np + (size_t)B * (2 * n + 1);
+    double* d = nullptr;
+    int32_t* iv = nullptr;
+    hipError_t e = hipMalloc(&d, nd * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&iv, (size_t)2 * B * sizeof(int32_t));
+    double *d_s = d, *d_p = d_s + SL * B, *d_q = d_p + np, *d_t = d_q + (size_t)n * B, *d_l = d_t + (size_t)n * B;
+    if (e == hipSuccess) e = hipMemcpy(d_s, snap, sizeof(double) * SL * B, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_p, prm, sizeof(double) * np, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        a.snap = d_s; a.prm = d_p; a.qdd = d_q; a.tau = d_t; a.loss = d_l; a.status = iv; a.iters = iv + B;
+        e = dartmpc_launch_arm(&a, nullptr);
+    }
+    if (e == hipSuccess) e = hipMemcpy(qdd, d_q, sizeof(double) * n * B, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(tau, d_t, sizeof(double) * n * B, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(loss, d_l, sizeof(double) * B, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(status, iv, sizeof(int32_t) * B, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(iters, iv + B, sizeof(int32_t) * B, hipMemcpyDeviceToHost);
+    if (d) (void)hipFree(d);
+    if (iv) (void)hipFree(iv);
+    return e == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
+}

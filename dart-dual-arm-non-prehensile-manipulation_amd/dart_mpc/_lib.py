@@ -27,7 +27,9 @@ EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch",
            "dart_rmpc_solve_batch", "dart_rmpc_solve_batch_dev", "dart_rmpc_nw",
            "dart_rls_update_batch", "dart_rls_update_batch_dev",
            "dart_lmpc_solve_batch", "dart_lmpc_solve_batch_dev", "dart_lmpc_nw",
-           "dart_lmpc_policy_config_default", "dart_lmpc_policy_step", "dart_lmpc_policy_step_dev")
+           "dart_lmpc_policy_config_default", "dart_lmpc_policy_step", "dart_lmpc_policy_step_dev",
+           "dart_arm_config_default", "dart_arm_snapshot_len", "dart_arm_param_len", "dart_arm_solve_batch",
+           "dart_arm_solve_batch_dev")
 VARIANT_PMPC, VARIANT_RMPC, VARIANT_LMPC = 0, 1, 2
 ABI_VERSION = 2
 
@@ -64,6 +66,14 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise DartMPCError(f"{LIB_PATH} not built: run __graft_entry__.build() or `make -C {CSRC_DIR}`")
+    # One HIP runtime per process: libamdhip64.so.7 is the SONAME of both the system ROCm runtime and
+    # the one torch bundles, and the first one loaded serves both.  torch only works on its own, so
+    # load torch first when it is installed (it is the device-memory / stream plumbing of the
+    # package); our library then binds to the same runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:     # pragma: no cover - the C ABI works without torch
+        pass
     L = ctypes.CDLL(LIB_PATH)
     L.dart_mpc_config_default.argtypes = [ctypes.POINTER(Config)]
     L.dart_mpc_config_default.restype = None
@@ -109,6 +119,18 @@ def lib():
     L.dart_rls_update_batch.restype = ctypes.c_int
     L.dart_rls_update_batch_dev.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_double, ctypes.c_void_p]
     L.dart_rls_update_batch_dev.restype = ctypes.c_int
+    L.dart_arm_config_default.argtypes = [ctypes.c_void_p]
+    L.dart_arm_config_default.restype = None
+    L.dart_arm_snapshot_len.argtypes = [ctypes.c_int]
+    L.dart_arm_snapshot_len.restype = ctypes.c_int
+    L.dart_arm_param_len.argtypes = [ctypes.c_int]
+    L.dart_arm_param_len.restype = ctypes.c_int
+    L.dart_arm_solve_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_int] + [ctypes.c_void_p] * 5
+    L.dart_arm_solve_batch.restype = ctypes.c_int
+    L.dart_arm_solve_batch_dev.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6
+    L.dart_arm_solve_batch_dev.restype = ctypes.c_int
     if L.dart_mpc_abi_version() != ABI_VERSION:
         raise DartMPCError("libdartmpc.so ABI version mismatch")
     _lib = L

@@ -181,3 +181,88 @@ def lmpc_batch(n_seeds: int = 1, seed0: int = 0):
             out["pvec"][i] = rng.uniform(0.01, 1.9, 34)
             out["target"][i] = [rng.uniform(-0.15, 0.15), 0.0, rng.uniform(-0.12, 0.12), 0.0, 0.0, 0.0, 0.0, 0.0]
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Per-arm impedance QP (PMPC/src/controller/arm.py:266-457).  MuJoCo is not in
+# this image, so the shared-memory snapshot that compute_dynamics (arm.py:111-199) publishes is
+# synthesised with the same structure: a revolute 7-DOF chain (joint axes z_i, origins p_i) gives
+# J = [z_i x (p_ee - p_i); z_i], a link-inertia sum gives an SPD M, Mx_inv = J M^-1 J^T as
+# arm.py:133-138 forms it for a fixed-base arm.  Scenario mix per instance: 60 % nominal tracking,
+# 20 % large task error (torque bounds active), 10 % joint at its limit drifting outward
+# (position-row bound active), 10 % near-singular task Jacobian (|det Mx_inv| <= 1e-8 -> the
+# pinv(rcond=1e-3) branch of arm.py:346-350).
+ARM_SEED_BASE = 20251024 + 32452843
+ARM_N = 7
+
+
+def _arm_instance(rng, kind: str, n: int = ARM_N):
+    from_lim = 0.3
+    qmin = np.array([-6.28319, -2.059, -6.28319, -0.19198, -6.28319, -1.69297, -6.28319])[:n]
+    qmax = np.array([6.28319, 2.0944, 6.28319, 3.927, 6.28319, 3.14159, 6.28319])[:n]
+    lo_q = np.maximum(qmin + from_lim, -2.5)
+    hi_q = np.minimum(qmax - from_lim, 2.5)
+    q = rng.uniform(lo_q, hi_q)
+    qd = rng.normal(0.0, 0.05, n)
+    # kinematic chain
+    z = np.zeros((n, 3))
+    p = np.zeros((n, 3))
+    axis = np.array([0.0, 0.0, 1.0])
+    pos = np.array([0.0, 0.0, 0.27])
+    for i in range(n):
+        a = axis + rng.normal(0.0, 0.6, 3)
+        z[i] = a / np.linalg.norm(a)
+        p[i] = pos
+        pos = pos + rng.normal(0.0, 0.12, 3) + np.array([0.0, 0.0, 0.05])
+    p_ee = pos + np.array([0.0, 0.0, 0.125])
+    J = np.zeros((6, n))
+    for i in range(n):
+        J[:3, i] = np.cross(z[i], p_ee - p[i])
+        J[3:, i] = z[i]
+    if kind == "singular":
+        J[5] *= 1e-4                                   # task direction nearly unreachable
+    # mass matrix: sum of link contributions + armature
+    Jb = rng.normal(0.0, 0.35, (12, n)) * np.linspace(1.0, 0.3, n)
+    M = Jb.T @ np.diag(rng.uniform(0.5, 3.0, 12)) @ Jb + np.diag(rng.uniform(0.01, 0.05, n))
+    M = 0.5 * (M + M.T)
+    Mx_inv = J @ np.linalg.inv(M) @ J.T
+    Mx_inv = 0.5 * (Mx_inv + Mx_inv.T)
+    Jd = rng.normal(0.0, 0.4, (6, n)) * (0.2 + np.mean(np.abs(qd)))
+    h = np.clip(rng.normal(0.0, 8.0, n), -25.0, 25.0)
+    ee_pos = p_ee.copy()
+    if kind == "large":
+        d = rng.normal(0.0, 1.0, 3)
+        mocap = ee_pos + d / np.linalg.norm(d) * rng.uniform(0.08, 0.2)
+        rotvec = rng.normal(0.0, 0.3, 3)
+    else:
+        mocap = ee_pos + rng.normal(0.0, 0.003, 3)
+        rotvec = rng.normal(0.0, 0.02, 3)
+    if kind == "limit":
+        j = int(rng.integers(0, n))
+        if rng.uniform() < 0.5:
+            q[j] = qmax[j] - rng.uniform(0.0, 2e-5)
+            qd[j] = rng.uniform(0.002, 0.02)
+        else:
+            q[j] = qmin[j] + rng.uniform(0.0, 2e-5)
+            qd[j] = -rng.uniform(0.002, 0.02)
+    return {"q": q, "qd": qd, "qdd_prev": rng.normal(0.0, 1.0, n), "mocap_pos": mocap, "ee_pos": ee_pos,
+            "rotvec": rotvec, "jac": J, "jacDot": Jd, "M": M, "h": h, "Mx_inv": Mx_inv}
+
+
+def arm_batch(n_seeds: int = 1, seed0: int = 0, n: int = ARM_N):
+    """Return (snaps, kinds) for B = 36*n_seeds arm instances (18 configs x 2 arms per seed):
+    snaps[key] = [B, ...] arrays with the fields of arm.py:185-199."""
+    kinds_cycle = ["nominal"] * 6 + ["large"] * 2 + ["limit", "singular"]
+    out, kinds = None, []
+    B = 2 * N_CONFIGS * n_seeds
+    for s in range(n_seeds):
+        rng = np.random.default_rng(ARM_SEED_BASE + seed0 + s)
+        for b in range(2 * N_CONFIGS):
+            kind = kinds_cycle[int(rng.integers(0, len(kinds_cycle)))]
+            inst = _arm_instance(rng, kind, n)
+            if out is None:
+                out = {k: np.zeros((B,) + np.shape(v)) for k, v in inst.items()}
+            for k, v in inst.items():
+                out[k][2 * N_CONFIGS * s + b] = v
+            kinds.append(kind)
+    return out, kinds

@@ -19,6 +19,10 @@
  *                             and warm start :510-520), fed by RLMPC.solve :986-1021
  *   dart_lmpc_policy_step(_dev) <- the inference / parameter-write half of RLMPC._rl_worker
  *                             rlmpc2.py:537-769 (Policy :33-80, write_params_to_shm :606-616)
+ *   dart_arm_solve_batch(_dev) <- ARMCONTROL.solver_worker, the per-arm impedance QP
+ *                             PMPC/src/controller/arm.py:266-457 (same code in
+ *                             RMPC/dev_dual/controller/parallel.py, LMPC/src/controller/parallel.py),
+ *                             fed by ARMCONTROL.compute_torque / compute_dynamics :111-231
  *   dart_mpc_sync / dart_mpc_last_error / dart_mpc_destroy
  *                           <- process-lifetime handling of the solver object in
  *                             mpc_worker (main_parallel_enhanced.py:22-55)
@@ -222,6 +226,51 @@ int dart_lmpc_policy_step(const dart_lmpc_policy_config *cfg, int B, const float
 int dart_rls_update_batch(int B, double *theta, double *P, const double *phi, const double *y, double lambda);
 int dart_rls_update_batch_dev(int B, double *theta, double *P, const double *phi, const double *y, double lambda,
                               void *hip_stream);
+
+/* Per-arm impedance QP: the body of ARMCONTROL.solver_worker (PMPC/src/controller/arm.py:266-457)
+ * for B independent arm snapshots (two per dual-arm simulation step).  Stateless (no handle).
+ *   snap [B][dart_arm_snapshot_len(n)] = the shared-memory fields the worker reads (:314-324):
+ *        q[n] qd[n] qdd_prev[n] mocap_pos[3] ee_pos[3] rotvec[3] jac[6][n] jacDot[6][n] M[n][n]
+ *        h[n] Mx_inv[6][6]
+ *   prm  [B or 1][dart_arm_param_len(n)] = the worker's params (:290-302):
+ *        Wimp[6][6] Wpos[n][n] Wsmooth[n][n] Qmin[n] Qmax[n] Qdotmin[n] Qdotmax[n] taumin[n]
+ *        taumax[n] K[6][6] K_null[n][n] dt;   prm_stride = 0 shares one row across the batch,
+ *        else dart_arm_param_len(n)
+ *   qdd [B][n] the optimal joint accelerations (the next qdd_prev, :431), tau [B][n] = M qdd + h
+ *   (torque_out, :424/:432), loss [B] = the objective value (loss_out, :425/:433),
+ *   status [B] (DART_ARM_*), iters [B] interior-point iterations.
+ * The QP is strictly convex (Wpos > 0); IPOPT's answer is its unique KKT point with the bounds
+ * relaxed by bound_relax_factor = 1e-8, which is what the solver returns (scaled KKT error <= tol).
+ * n <= DART_ARM_NMAX; bounds with |value| >= 1e19 are treated as absent (IPOPT's convention). */
+#define DART_ARM_NMAX 8
+
+enum dart_arm_status {
+    DART_ARM_SOLVED = 0,
+    DART_ARM_ACCEPTABLE = 1,     /* normal matrix lost definiteness with the KKT error <= acceptable_tol */
+    DART_ARM_MAXITER = -1,
+    DART_ARM_BREAKDOWN = -2,
+    DART_ARM_INFEASIBLE = -3     /* multipliers diverging: the bounds admit no qdd */
+};
+
+typedef struct dart_arm_config {
+    double tol;                  /* scaled KKT tolerance, default 1e-10 */
+    double acceptable_tol;       /* default 1e-7 */
+    int32_t max_iter;            /* default 60 */
+    int32_t reserved;
+} dart_arm_config;
+
+void dart_arm_config_default(dart_arm_config *cfg);
+int dart_arm_snapshot_len(int n);
+int dart_arm_param_len(int n);
+
+/* Device pointers, asynchronous on hip_stream. */
+int dart_arm_solve_batch_dev(const dart_arm_config *cfg, int B, int n, const double *snap, const double *prm,
+                             int prm_stride, double *qdd, double *tau, double *loss, int32_t *status,
+                             int32_t *iters, void *hip_stream);
+
+/* Host pointers (stages through device memory and blocks). */
+int dart_arm_solve_batch(const dart_arm_config *cfg, int B, int n, const double *snap, const double *prm,
+                         int prm_stride, double *qdd, double *tau, double *loss, int32_t *status, int32_t *iters);
 
 int dart_mpc_sync(dart_mpc_handle *h);
 

@@ -87,3 +87,27 @@ def test_tilt_to_quat_matches_reference_formula():
     for u in ([0.1, -0.2], [0.6, 0.6], [0.0, 0.0]):
         q = Rot.from_euler("xyz", [u[1], -u[0], 0.0]).as_quat()          # main.py:107-116
         np.testing.assert_allclose(tilt_to_quat(u), [q[3], q[0], q[1], q[2]], atol=1e-15)
+
+
+def test_arm_qp_abi_lengths_and_validation():
+    """dart_arm_* (ARMCONTROL.solver_worker boundary): row lengths, defaults, argument checks that
+    return before any device work."""
+    import ctypes
+    import dart_mpc
+    from dart_mpc.arm import ArmConfig, arm_config
+    L = dart_mpc.lib()
+    assert L.dart_arm_snapshot_len(7) == 206 and L.dart_arm_param_len(7) == 262
+    assert L.dart_arm_snapshot_len(0) < 0 and L.dart_arm_snapshot_len(9) < 0 and L.dart_arm_param_len(9) < 0
+    c = arm_config()
+    assert c.tol == 1e-10 and c.acceptable_tol == 1e-7 and c.max_iter == 60
+    z = ctypes.c_void_p(0)
+    args = lambda cfg, B, n, stride: (ctypes.byref(cfg), B, n, z, z, stride, z, z, z, z, z)  # noqa: E731
+    assert L.dart_arm_solve_batch(*args(c, 0, 7, 0)) == 0                      # empty batch
+    assert L.dart_arm_solve_batch(*args(c, 0, 9, 0)) == -1                     # n > DART_ARM_NMAX
+    assert L.dart_arm_solve_batch(*args(c, 0, 7, 17)) == -1                    # bad parameter stride
+    assert L.dart_arm_solve_batch(*args(c, 4, 7, 0)) == -1                     # null buffers
+    bad = ArmConfig(tol=0.0, acceptable_tol=1e-7, max_iter=60)
+    assert L.dart_arm_solve_batch(*args(bad, 0, 7, 0)) == -1
+    bad = ArmConfig(tol=1e-6, acceptable_tol=1e-8, max_iter=60)              # acceptable < tol
+    assert L.dart_arm_solve_batch(*args(bad, 0, 7, 0)) == -1
+    assert L.dart_arm_solve_batch_dev(*(args(c, 0, 7, 262) + (z,))) == 0
