@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--host-calls", type=int, default=200, help="calls of the host-pointer (PCIe-inclusive) path")
     ap.add_argument("--rmpc-steps", type=int, default=200, help="launches of the supplementary C3 RMPC line (0 = skip)")
     ap.add_argument("--lmpc-steps", type=int, default=100, help="launches of the supplementary C5 LMPC line (0 = skip)")
+    ap.add_argument("--arm-steps", type=int, default=200, help="launches of the supplementary arm-QP line (0 = skip)")
     ap.add_argument("--saturation-batch", type=int, default=18 * 1024,
                     help="supplementary single-launch batch for the saturated rate (0 = skip)")
     return ap.parse_args()
@@ -192,6 +193,85 @@ def bench_lmpc(args, torch, dev, stream, dart_mpc):
     return out
 
 
+def bench_arm(args, torch, dev, stream, dart_mpc):
+    """Per-arm impedance QP (ARMCONTROL.solver_worker): 36 arm snapshots per launch
+    (18 object configs x 2 arms = one dual-arm simulation step of the C2 batch), fresh synthetic
+    snapshots every launch, resident in HBM; plus one saturated launch."""
+    from dart_mpc.arm import pack_params, pack_snapshot
+    from dart_mpc.workload import arm_batch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import arm_qp   # checker + CPU baseline only
+    K, n = args.arm_steps, 7
+    snaps = [arm_batch(1, seed0=5000 + i)[0] for i in range(K + 3)]
+    B = snaps[0]["q"].shape[0]
+    prm = arm_qp.default_params()
+    SR = torch.tensor(np.stack([pack_snapshot(x) for x in snaps]), dtype=torch.float64, device=dev).contiguous()
+    PR = torch.tensor(pack_params(prm), dtype=torch.float64, device=dev)
+    QD = torch.empty((K + 3, B, n), dtype=torch.float64, device=dev)
+    TQ = torch.empty((K + 3, B, n), dtype=torch.float64, device=dev)
+    LS = torch.empty((K + 3, B), dtype=torch.float64, device=dev)
+    ST = torch.empty((K + 3, B), dtype=torch.int32, device=dev)
+    IT = torch.empty((K + 3, B), dtype=torch.int32, device=dev)
+    s = dart_mpc.ArmSolver(n)
+    sp = stream.cuda_stream
+
+    def launch(i):
+        s.solve_batch_dev(B, SR[i].data_ptr(), PR.data_ptr(), True, QD[i].data_ptr(), TQ[i].data_ptr(),
+                          LS[i].data_ptr(), ST[i].data_ptr(), IT[i].data_ptr(), stream=sp)
+
+    for i in range(3):
+        launch(i)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for j in range(K):
+            ev[j][0].record(stream)
+            launch(3 + j)
+            ev[j][1].record(stream)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    st, its = ST[3:].cpu().numpy(), IT[3:].cpu().numpy()
+    ref = arm_qp.solve_batch(snaps[3], prm)
+    ok = ref["status"] >= 0
+    dq = np.abs(QD[3].cpu().numpy() - ref["qdd"])[ok] / (1 + np.abs(ref["qdd"][ok]))
+    out = {"workload": "arm QP: 36 arm snapshots per launch (18 configs x 2 arms), n=7, reference parameters "
+                       "(rob_ctrl.py:232-275), synthetic dynamics, qdd_prev warm start, scaled KKT tol 1e-10",
+           "solves_per_s": B * K / dt, "ms_per_step": dt / K * 1e3, "kernel_ms": kern_ms,
+           "status_ok_frac": float(np.mean(st >= 0)), "iters_mean": float(its.mean()),
+           "status_equal_to_oracle": bool(np.array_equal(st[0], ref["status"])),
+           "max_rel_qdd_err_vs_oracle": float(dq.max()) if ok.any() else None}
+    if args.saturation_batch > 0:
+        nb = max(1, args.saturation_batch // B)
+        big = arm_batch(nb, seed0=90000)[0]
+        Bs = big["q"].shape[0]
+        bs = torch.tensor(pack_snapshot(big), device=dev)
+        bo = [torch.empty((Bs, n), dtype=torch.float64, device=dev) for _ in range(2)] + \
+             [torch.empty(Bs, dtype=torch.float64, device=dev)] + [torch.empty(Bs, dtype=torch.int32, device=dev) for _ in range(2)]
+        for rep in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            s.solve_batch_dev(Bs, bs.data_ptr(), PR.data_ptr(), True, *[t.data_ptr() for t in bo], stream=sp)
+            e1.record(stream)
+            torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        out["saturation"] = {"batch": Bs, "ms_per_launch": ms, "solves_per_s": Bs / (ms * 1e-3),
+                             "ok_frac": float((bo[3] >= 0).float().mean())}
+    if not args.no_cpu_baseline:
+        Sb = arm_batch(4, seed0=4242)[0]
+        solved, c0 = 0, time.perf_counter()
+        while time.perf_counter() - c0 < min(5.0, args.cpu_seconds):
+            arm_qp.solve_batch(Sb, prm)
+            solved += Sb["q"].shape[0]
+        cdt = time.perf_counter() - c0
+        out["cpu_baseline"] = {"value": solved / cdt, "unit": "solves/s", "cores": 1, "kind": "port",
+                               "sample": f"numpy oracle (oracle/arm_qp.py: numpy pinv/inv/eigh QP build + Mehrotra "
+                                         f"IPM), {solved} solves in {cdt:.1f} s; the reference additionally rebuilds "
+                                         f"the CasADi nlpsol every step (arm.py:407-408)"}
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -332,6 +412,11 @@ def main():
     if rank == 0 and args.lmpc_steps > 0:
         lmpc = bench_lmpc(args, torch, dev, stream, dart_mpc)
 
+    # supplementary: per-arm impedance QP
+    arm = None
+    if rank == 0 and args.arm_steps > 0:
+        arm = bench_arm(args, torch, dev, stream, dart_mpc)
+
     # HBM traffic per launch from the committed rocprofv3 PMC passes of this build (tools/profile_round.sh)
     traffic = None
     pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")))
@@ -371,6 +456,7 @@ def main():
             "host_path_pcie_inclusive": host_path,
             "rmpc_c3": rmpc,
             "lmpc_c5": lmpc,
+            "arm_qp": arm,
         }
         print(json.dumps(line))
     if world > 1:

@@ -125,7 +125,7 @@ def qp_ipm(H, c, A, b, lo, hi, x0=None, tol=1e-10, acc_tol=1e-7, max_iter=60):
     """Mehrotra predictor-corrector IPM for min 1/2 x'Hx + c'x s.t. lo <= Ax + b <= hi.
 
     Inequalities G x <= g with G = [A; -A], g = [hi - b; b - lo] (infinite rows dropped),
-    slacks s = g - G x > 0, multipliers z > 0, start s = max(g - G x0, 1), z = 1.  Per iteration
+    slacks s = g - G x > 0, multipliers z > 0, start s = max(g - G x0, 1), z = (1 + |c|max) / #rows.  Per iteration
     the normal matrix K = H + G' S^-1 Z G is factored once (Cholesky) and solved for the affine
     direction (rc = s z) and the corrector (rc = s z + ds_a dz_a - sigma mu, sigma = (mu_a/mu)^3);
     one common step 0.99 x the fraction to the boundary for (x, s, z).
@@ -143,9 +143,9 @@ def qp_ipm(H, c, A, b, lo, hi, x0=None, tol=1e-10, acc_tol=1e-7, max_iter=60):
     x = np.zeros(n) if x0 is None else np.array(x0, dtype=float)
     r = g - G @ x
     s = np.where(on, np.maximum(r, 1.0), 1.0)
-    z = np.where(on, 1.0, 0.0)
     nact = max(1, int(on.sum()))
     sd = 1.0 + np.max(np.abs(c))
+    z = np.where(on, sd / nact, 0.0)              # multipliers on the scale of the cost gradient
     sp = 1.0 + np.max(np.abs(np.where(on, g, 0.0)))
     status, it = -1, 0
     for it in range(max_iter):
