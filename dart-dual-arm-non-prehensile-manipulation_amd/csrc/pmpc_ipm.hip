@@ -64,6 +64,32 @@ __device__ __forceinline__ void z_rk4(double h, double w, double pz, double vz, 
     vzn = vz + h / 6 * (k1v + 2 * k2v + 2 * k3v + k4v);
 }
 
+// DPP move with an explicit fill value for lanes whose source is outside the row / masked out
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_fill(double fill, double x) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+    const unsigned long long o = __builtin_bit_cast(unsigned long long, fill);
+    const int rlo = __builtin_amdgcn_update_dpp((int)(unsigned)(o & 0xffffffffu), (int)(unsigned)(b & 0xffffffffu),
+                                                CTRL, ROWMASK, 0xf, false);
+    const int rhi = __builtin_amdgcn_update_dpp((int)(unsigned)(o >> 32), (int)(unsigned)(b >> 32), CTRL, ROWMASK, 0xf,
+                                                false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)rhi << 32) | (unsigned)rlo);
+}
+// one Hillis-Steele level of an inclusive scan of 2-D affine maps x -> F x + c (later o earlier):
+// (F, c) <- (F, c) o (P, q) = (F P, F q + c), (P, q) fetched by DPP, identity where out of range
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void affine_scan_level(double& f11, double& f12, double& f21, double& f22, double& c1,
+                                                  double& c2) {
+    const double p11 = dpp_fill<CTRL, ROWMASK>(1.0, f11), p12 = dpp_fill<CTRL, ROWMASK>(0.0, f12);
+    const double p21 = dpp_fill<CTRL, ROWMASK>(0.0, f21), p22 = dpp_fill<CTRL, ROWMASK>(1.0, f22);
+    const double q1 = dpp_fill<CTRL, ROWMASK>(0.0, c1), q2 = dpp_fill<CTRL, ROWMASK>(0.0, c2);
+    const double n11 = fma(f11, p11, f12 * p21), n12 = fma(f11, p12, f12 * p22);
+    const double n21 = fma(f21, p11, f22 * p21), n22 = fma(f21, p12, f22 * p22);
+    c1 = fma(f11, q1, fma(f12, q2, c1));
+    c2 = fma(f21, q1, fma(f22, q2, c2));
+    f11 = n11; f12 = n12; f21 = n21; f22 = n22;
+}
+
 // ---------------------------------------------------------------------------
 // the kernel: one wave64 = one instance.
 //   NAX = 1 (N <= 31): lane = axis*32 + k, one axis per lane (x in lanes 0-31, y in 32-63)
@@ -127,6 +153,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
 
     const double tol = a.tol, mu_min = tol / 10;
     const double n_eq = 6.0 * (N + 1), n_b = 4.0 * N;       // IPOPT counts on the full NLP
+    const double inv_neb = 1.0 / (n_eq + n_b), inv_nb = 1.0 / n_b;
     const double gam_th = 1e-5, gam_ph = 1e-8, s_th = 1.1, s_ph = 2.3, eta_ph = 1e-8, gam_al = 0.05;
 
     // defect g_k = x_k - f(x_{k-1}, u_{k-1}) (mpc_3d.py:48), g_0 = x_0 - state (:37)
@@ -183,16 +210,18 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
         }
         const double dinf_w = wmaxf((float)dinf), pinf_w = wmaxf((float)pinf), c0_w = wmaxf((float)c0);
         const double cmin_w = wminf((float)cmin);
-        const double s_d = fmax(100.0, (double)(wsumf((float)suml) + wsumf((float)sumz)) / (n_eq + n_b)) / 100.0;
-        const double s_c = fmax(100.0, (double)wsumf((float)sumz) / n_b) / 100.0;
+        // IPOPT's scalings s_d, s_c (>= 1) as reciprocals: one division each instead of one per test
+        const float sz_w = wsumf((float)sumz);
+        const double is_d = 100.0 / fmax(100.0, (double)(wsumf((float)suml) + sz_w) * inv_neb);
+        const double is_c = 100.0 / fmax(100.0, (double)sz_w * inv_nb);
         dinf = dinf_w; pinf = pinf_w; c0 = c0_w;
         STAMP(1);
-        if (fmax(dinf / s_d, fmax(pinf, c0 / s_c)) <= tol) { status = 0; break; }
+        if (fmax(dinf * is_d, fmax(pinf, c0 * is_c)) <= tol) { status = 0; break; }
         // -------- monotone barrier update (Fiacco-McCormick, may fire repeatedly) --
         // max_i |z_i s_i - mu| = max(max z s - mu, mu - min z s): one reduction pair, scalar loop
         for (;;) {
             const double cmu = fmax(c0 - mu, mu - cmin_w);
-            if (fmax(dinf / s_d, fmax(pinf, cmu / s_c)) > 10.0 * mu || mu <= mu_min) break;
+            if (fmax(dinf * is_d, fmax(pinf, cmu * is_c)) > 10.0 * mu || mu <= mu_min) break;
             mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
             nfilt = 0;
         }
@@ -272,6 +301,22 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
         double dp[NAX], dv[NAX];
 #pragma unroll
         for (int j = 0; j < NAX; ++j) { dp[j] = -g1[j]; dv[j] = -g2[j]; }
+        if constexpr (NAX == 1) {
+            // dx_k = F_{k-1} dx_{k-1} + f_{k-1} - g_k as an inclusive scan of affine maps within each
+            // 32-lane axis half (DPP row_shr 1/2/4/8 inside the 16-lane rows, then row_bcast:15 into
+            // the second row of each half): 5 composition levels instead of N dependent steps
+            const double pw1 = from_prev(W1[0]), pw2 = from_prev(W2[0]), pkf = from_prev(kff[0]);
+            const double pb1 = from_prev(be1[0]), pb2 = from_prev(be2[0]);
+            double f11 = 1.0 - pb1 * pw1, f12 = fma(-pb1, pw2, a12), f21 = -pb2 * pw1, f22 = fma(-pb2, pw2, a22);
+            double c1 = fma(pb1, pkf, -g1[0]), c2 = fma(pb2, pkf, -g2[0]);
+            if (k == 0) { f11 = 0.0; f12 = 0.0; f21 = 0.0; f22 = 0.0; c1 = -g1[0]; c2 = -g2[0]; }
+            affine_scan_level<0x111, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:1
+            affine_scan_level<0x112, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:2
+            affine_scan_level<0x114, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:4
+            affine_scan_level<0x118, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:8
+            affine_scan_level<0x142, 0xa>(f11, f12, f21, f22, c1, c2);   // row_bcast:15 -> rows 1, 3
+            dp[0] = c1; dv[0] = c2;
+        } else
         for (int step = 0; step < N; ++step) {
             double op[NAX], ov[NAX];
 #pragma unroll
