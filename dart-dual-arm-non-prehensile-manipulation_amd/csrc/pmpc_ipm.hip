@@ -240,7 +240,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
             q1[j] = qp2 * (p[j] - rp[j]); q2[j] = qv2 * (v[j] - rv[j]);
             gn1[j] = from_next(g1[j]); gn2[j] = from_next(g2[j]);
         }
-        double W1[NAX], W2[NAX], kff[NAX], P11[NAX], P12[NAX], P22[NAX], p1[NAX], p2[NAX];
+        double W1[NAX], W2[NAX], kff[NAX], P11[NAX], P12[NAX], P22[NAX], p1[NAX], p2[NAX], iQs[NAX];
         double delta = 0.0;
         bool ok = false;
         int attempt = 0;
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
 #pragma unroll
                 for (int j = 0; j < NAX; ++j) {
                     n11[j] = from_next(P11[j]); n12[j] = from_next(P12[j]); n22[j] = from_next(P22[j]);
-                    n1[j] = from_next(p1[j]); n2[j] = from_next(p2[j]);
+                    if constexpr (NAX == 2) { n1[j] = from_next(p1[j]); n2[j] = from_next(p2[j]); }
                 }
 #pragma unroll
                 for (int j = 0; j < NAX; ++j) {
@@ -273,24 +273,61 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                     const double U1 = PB1, U2 = fma(PB1, a12k, PB2 * a22k);
                     const double X12 = fma(n11[j], a12k, n12[j] * a22k);
                     const double X22 = fma(A11k, n11[j], fma(A12k, n12[j], fma(A22k, n22[j], X22d)));
-                    const double h1 = n1[j] - fma(n11[j], gn1[j], n12[j] * gn2[j]);
-                    const double h2 = n2[j] - fma(n12[j], gn1[j], n22[j] * gn2[j]);
-                    const double qu = fma(e1, h1, fma(e2, h2, rt[j]));
                     const double iQ = frcp(Q);
-                    const double kf = -iQ * qu, w1 = iQ * U1, w2 = iQ * U2;
+                    const double w1 = iQ * U1, w2 = iQ * U2;
                     P11[j] = fma(-w1, U1, fma(f11, n11[j], X11d));
                     P12[j] = fma(-w1, U2, X12);
                     P22[j] = fma(-w2, U2, X22);
-                    p1[j] = fma(U1, kf, fma(f11, h1, q1[j]));
-                    p2[j] = fma(U2, kf, q2[j] + fma(a12k, h1, a22k * h2));
-                    W1[j] = w1; W2[j] = w2; kff[j] = kf;
-                    Quu[j] = Q;
+                    if constexpr (NAX == 2) {   // NAX == 1 runs the linear part as a scan afterwards
+                        const double h1 = n1[j] - fma(n11[j], gn1[j], n12[j] * gn2[j]);
+                        const double h2 = n2[j] - fma(n12[j], gn1[j], n22[j] * gn2[j]);
+                        const double qu = fma(e1, h1, fma(e2, h2, rt[j]));
+                        const double kf = -iQ * qu;
+                        p1[j] = fma(U1, kf, fma(f11, h1, q1[j]));
+                        p2[j] = fma(U2, kf, q2[j] + fma(a12k, h1, a22k * h2));
+                        kff[j] = kf;
+                    }
+                    W1[j] = w1; W2[j] = w2;
+                    Quu[j] = Q; iQs[j] = iQ;
                 }
             }
             bool bad = false;
 #pragma unroll
             for (int j = 0; j < NAX; ++j) bad = bad || !(Quu[j] > 0.0) || !isfinite(Quu[j]);
             ok = !wany(bad);
+        }
+        if constexpr (NAX == 1) {
+            if (ok) {
+                // linear part of the value function, p_k = M_k p_{k+1} + m_k with M_k = A_k^T - w_k e_k^T
+                // and m_k = q_k - w_k rt_k - M_k P_{k+1} g_{k+1}: a suffix scan of affine maps (row_shl
+                // 1/2/4/8 inside the rows, then row 1 -> row 0 of each half by a lane shuffle); the
+                // terminal/idle lanes carry M = 0, so each suffix stops at node N
+                const double e1 = be1[0], e2 = be2[0], w1 = W1[0], w2 = W2[0];
+                const double nP11 = from_next(P11[0]), nP12 = from_next(P12[0]), nP22 = from_next(P22[0]);
+                const double t1 = fma(nP11, gn1[0], nP12 * gn2[0]), t2 = fma(nP12, gn1[0], nP22 * gn2[0]);
+                double m11 = fma(-w1, e1, f11), m12 = -w1 * e2, m21 = fma(-w2, e1, a12k), m22 = fma(-w2, e2, a22k);
+                const double rtk = rt[0];
+                double c1 = fma(-w1, rtk, q1[0]) - fma(m11, t1, m12 * t2);
+                double c2 = fma(-w2, rtk, q2[0]) - fma(m21, t1, m22 * t2);
+                affine_scan_level<0x101, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:1
+                affine_scan_level<0x102, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:2
+                affine_scan_level<0x104, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:4
+                affine_scan_level<0x108, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:8
+                {   // rows 0 and 2 compose with the suffix held by the first lane of rows 1 and 3
+                    const int src = (lane & 32) | 16;
+                    const bool lo_row = (lane & 16) == 0;
+                    const double r1 = __shfl(c1, src), r2 = __shfl(c2, src);   // only the constant is needed now
+                    if (lo_row) {
+                        c1 = fma(m11, r1, fma(m12, r2, c1));
+                        c2 = fma(m21, r1, fma(m22, r2, c2));
+                    }
+                }
+                p1[0] = c1; p2[0] = c2;
+                // feed-forward k_k = -(e^T h + rt) / Q with h = p_{k+1} - P_{k+1} g_{k+1}
+                const double np1 = from_next(c1), np2 = from_next(c2);
+                const double h1 = np1 - t1, h2 = np2 - t2;
+                kff[0] = -iQs[0] * fma(e1, h1, fma(e2, h2, rtk));
+            }
         }
         STAMP_ADD(9, attempt);
         STAMP(3);
