@@ -20,9 +20,10 @@ DST = os.path.join(ROOT, "profiles", TAG)
 os.makedirs(DST, exist_ok=True)
 
 KERNELS = {"pmpc_ipm_kernel": "PMPC (C2, B=18, N=20)", "rmpc_ipm_kernel": "RMPC (C3, B=18, N=20)",
-           "lmpc_ipm_kernel": "LMPC (C5, B=18, N=30)"}
+           "lmpc_ipm_kernel": "LMPC (C5, B=18, N=30)", "arm_qp_kernel": "Arm QP (36 arms per launch, n=7)"}
 ALGO_BYTES = {"pmpc_ipm_kernel": 18 * 176, "rmpc_ipm_kernel": 18 * (4 + 2 + 14 + 98 + 7 + 2 + 84 + 10 + 14 + 98 + 4) * 8,
-              "lmpc_ipm_kernel": 18 * (8 + 2 + 34 + 8 + 22 + 4) * 8}
+              "lmpc_ipm_kernel": 18 * (8 + 2 + 34 + 8 + 22 + 4) * 8,
+              "arm_qp_kernel": 36 * (206 + 262 + 7 + 7 + 1 + 1) * 8}   # snapshot + (shared) params read per wave + outputs
 
 
 def short(name):
