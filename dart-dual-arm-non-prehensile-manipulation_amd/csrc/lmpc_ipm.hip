@@ -55,6 +55,7 @@ struct LmShared {
     NodeArr<double[4][LM_NSC], LM_NMAXS + 1> SC;
     NodeArr<double[4][8], LM_NMAXS + 1> SD;
     NodeArr<double[12], LM_NMAXS + 1> JL;      // J^T lambda_{k+1} staging, primal residual maxima
+    NodeArr<double[14], LM_NMAXS + 1> DL;      // per node: lambda_{k+1}, tilt curvature, g cos(u) for the mirror lanes
     LmModel model;                    // uniform problem data, read at the use sites (keeps VGPRs free)
     double Q[8], Qt[8], tgt[8];
 };
@@ -309,6 +310,19 @@ __device__ __forceinline__ void lm_directions(const LmModel& m, const double (*s
     for (int d = 0; d < 10; ++d) jl[d] = jl_lds[d];
 }
 
+// directions d0 .. d0+4 of one node (the two half-waves of the wave split the ten directions);
+// per-node inputs from LDS: dl = [lambda_{k+1}(10), huu(2), g cos a, g cos b]
+__device__ __forceinline__ void lm_directions_half(const LmModel& m, const double (*sc)[LM_NSC], const double (*cv)[8],
+                                                   const double* dl, int d0, double* Mk, double* Hk, double* jl_lds) {
+    double lamn[10], huu[2];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) lamn[i] = dl[i];
+    huu[0] = dl[10]; huu[1] = dl[11];
+    const double gca = dl[12], gcb = dl[13];
+#pragma unroll 1
+    for (int d = d0; d < d0 + 5; ++d) jl_lds[d] = lm_direction(m, sc, cv, huu, gca, gcb, d, lamn, Mk, Hk);
+}
+
 __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     LmShared& SH = *reinterpret_cast<LmShared*>(smem);
@@ -498,10 +512,24 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             {
                 double huu[2];
                 lm_adjoint_curv(m, SH.SC[sr], SH.SD[sr], lamn, sa, sb, huu);
+                if (k < 32) {
+#pragma unroll
+                    for (int i = 0; i < 10; ++i) SH.DL[k][i] = lamn[i];
+                    SH.DL[k][10] = huu[0]; SH.DL[k][11] = huu[1]; SH.DL[k][12] = LM_G * ca; SH.DL[k][13] = LM_G * cb;
+                }
+                __syncthreads();
+                {   // exact dynamics Hessian (x, u blocks) and the Jacobian columns: lanes k and k + 32 take
+                    // directions 0..4 and 5..9 of node k
+                    const int kn = k & 31;
+                    if (kn < N)
+                        lm_directions_half(m, SH.SC[kn], SH.SD[kn], SH.DL[kn], k < 32 ? 0 : 5, &S->M[kn][0][0], S->H[kn],
+                                           SH.JL[kn]);
+                }
+                __syncthreads();
                 if (uon) {
-                    // exact dynamics Hessian (x, u blocks) and the Jacobian columns, then the cost /
-                    // barrier terms: z = [x(8), up(2), u(2), 1], gradient row later
-                    lm_directions(m, SH.SC[sr], SH.SD[sr], huu, LM_G * ca, LM_G * cb, lamn, Mk, Hk, jl, SH.JL[sr]);
+                    // the cost / barrier terms: z = [x(8), up(2), u(2), 1], gradient row later
+#pragma unroll
+                    for (int i = 0; i < 10; ++i) jl[i] = SH.JL[sr][i];
 #pragma unroll
                     for (int i = 0; i < 8; ++i) Hk[hp(i, i)] += sc * 2.0 * Q[i];
                     Hk[hp(8, 8)] = sc * 2.0 * R2; Hk[hp(9, 9)] = sc * 2.0 * R3;
