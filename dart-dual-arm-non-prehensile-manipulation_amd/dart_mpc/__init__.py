@@ -7,6 +7,8 @@ Drop-in for the reference's MPC hot path:
   - ``RMPCStep``        <- RMPC/dev_dual/rob_ctrl.py:331-352 (RLS fused into the solve launch)
   - ``RLMPC``, ``LmpcPolicy``, ``LmpcSolver`` <- LMPC/src/controller/rlmpc2.py (solver worker, policy worker, front-end)
   - ``ArmControl``, ``ArmSolver`` <- ARMCONTROL (PMPC/src/controller/arm.py), the per-arm impedance QP
+  - ``harness``         <- the closed loops of main_parallel_enhanced.py / rob_ctrl.py without MuJoCo, and the
+                           reference's result formats (logger.py npz + metrics, rob_ctrl.py episode JSON)
   - ``Solver``, ``RmpcSolver``  the C ABI of include/dart_mpc.h (libdartmpc.so)
 """
 from ._lib import DartMPCError, LmpcSolver, RmpcSolver, Solver, build, lib, rls_update_batch, STATUS_NAMES  # noqa: F401
@@ -15,7 +17,7 @@ from .worker import mpc_worker  # noqa: F401
 from .rmpc import AdaptiveNPMPCSmooth, RLS, RMPCStep  # noqa: F401
 from .lmpc import RLMPC, LmpcPolicy, init_policy_weights  # noqa: F401
 from .arm import ArmControl, ArmSolver  # noqa: F401
-from . import workload  # noqa: F401
+from . import harness, workload  # noqa: F401
 
 __all__ = ["PMPC", "mpc_worker", "Solver", "RmpcSolver", "LmpcSolver", "RLMPC", "LmpcPolicy", "init_policy_weights", "ArmControl", "ArmSolver", "AdaptiveNPMPCSmooth", "RLS", "RMPCStep", "DartMPCError",
-           "build", "lib", "rls_update_batch", "tilt_to_quat", "workload"]
+           "build", "lib", "rls_update_batch", "tilt_to_quat", "workload", "harness"]
