@@ -259,7 +259,9 @@ struct OcpLds3 {
     double M[NMAXS][ND][NC];
     double H[NMAXS][NTP];
     double PK[NMAXS][NPK];
-    double T[NP][ND + 1];                             // scratch Pt_{k+1} M_k (row m, column j)
+    static constexpr int NPF = even(NP);              // row stride of the full copy of Pt_{k+1}
+    double T[ND][NP + 1];                             // scratch Pt_{k+1} M_k, transposed: T[j][m]
+    double PF[NP][NPF];                               // scratch Pt_{k+1}, full rows (16-byte aligned)
     double G[NTP];                                    // scratch G_k
     double F[NMAXS][NXA][NF];
     double dx0[NC];
@@ -274,6 +276,7 @@ struct Riccati3Roles {
     int ga0[L::EC], ga1[L::EC], gb0[L::EC], gb1[L::EC], gzz[L::EC];   // (C) packed G offsets
     bool isK[L::EC], con[L::EC];
     int ka[L::EC];
+    int fpq[L::EC], fqp[L::EC];          // (C) offsets (p, q) and (q, p) of a value entry in the full copy
 };
 
 template <class L>
@@ -300,11 +303,13 @@ __device__ Riccati3Roles<L> riccati3_roles() {
         int zi = 0, zj = 0;
         r.isK[q] = e >= NPT;
         r.ka[q] = 0;
+        r.fpq[q] = 0; r.fqp[q] = 0;
         if (e < NPT) {
             int p = 0;
             while (tri(p + 1) <= e) ++p;
             const int qq = e - tri(p);
             zi = zi_of_p<NXA>(p); zj = zi_of_p<NXA>(qq);
+            r.fpq[q] = p * L::NPF + qq; r.fqp[q] = qq * L::NPF + p;
         } else {
             const int rr = (e - NPT) < 2 * NP ? e - NPT : 0;
             r.ka[q] = rr / NP;
@@ -324,23 +329,32 @@ __device__ bool riccati3_sweep(L* S, int N, const Riccati3Roles<L>& R) {
     constexpr int NXA = L::NXA, NP = L::NP, NPT = L::NPT;
     const int lane = threadIdx.x;
     bool ok = true;
+    {   // full copy of the terminal value function
+        const int i = lane / NP, j = lane % NP;
+        for (int e = lane; e < NP * NP; e += 64) {
+            const int ii = e / NP, jj = e % NP;
+            S->PF[ii][jj] = S->PK[N][ii >= jj ? tri(ii) + jj : tri(jj) + ii];
+        }
+        (void)i; (void)j;
+    }
+    __syncthreads();
     for (int k = N - 1; k >= 0; --k) {
-        // (A) T(m, j) = sum_n Pt_{k+1}(m, n) M_k(n, j)
+        // (A) T(m, j) = sum_n Pt_{k+1}(m, n) M_k(n, j): row m of the full copy and column j of M_k are
+        // both contiguous (16-byte aligned), stored transposed for (B)
         {
-            const double* Pn = S->PK[k + 1];
             double tv[L::EA];
 #pragma unroll
             for (int q = 0; q < L::EA; ++q) {
                 const double* aj = &S->M[k][0][0] + R.aj[q];
-                const int m = R.am[q];
+                const double* pm = S->PF[R.am[q]];
                 double t = 0.0;
 #pragma unroll
-                for (int n = 0; n < NP; ++n) t = fma(Pn[m >= n ? tri(m) + n : tri(n) + m], aj[n], t);
+                for (int n = 0; n < NP; ++n) t = fma(pm[n], aj[n], t);
                 tv[q] = t;
             }
 #pragma unroll
             for (int q = 0; q < L::EA; ++q)
-                if (R.aon[q]) (&S->T[0][0])[(lane + 64 * q) / L::ND * (L::ND + 1) + (lane + 64 * q) % L::ND] = tv[q];
+                if (R.aon[q]) S->T[(lane + 64 * q) % L::ND][(lane + 64 * q) / L::ND] = tv[q];
         }
         __syncthreads();
         // (B) G(i, j) = Ht(i, j) + sum_m M_k(m, i) T(m, j)
@@ -349,9 +363,10 @@ __device__ bool riccati3_sweep(L* S, int N, const Riccati3Roles<L>& R) {
 #pragma unroll
             for (int q = 0; q < L::EB; ++q) {
                 const double* ai = &S->M[k][0][0] + R.bi[q];
+                const double* tj = S->T[R.bj[q]];
                 double g = S->H[k][(lane + 64 * q) < L::NT ? lane + 64 * q : 0];
 #pragma unroll
-                for (int mm = 0; mm < NP; ++mm) g = fma(ai[mm], S->T[mm][R.bj[q]], g);
+                for (int mm = 0; mm < NP; ++mm) g = fma(ai[mm], tj[mm], g);
                 gv[q] = g;
             }
 #pragma unroll
@@ -359,7 +374,7 @@ __device__ bool riccati3_sweep(L* S, int N, const Riccati3Roles<L>& R) {
                 if (R.bon[q]) S->G[lane + 64 * q] = gv[q];
         }
         __syncthreads();
-        // (C) Schur complement on the u block
+        // (C) Schur complement on the u block -> packed Pt_k, gains, and the full copy for node k-1
         double i00, i01, i11;
         ok = quu_inverse<NXA>(S->G, i00, i01, i11) && ok;
         {
@@ -374,8 +389,13 @@ __device__ bool riccati3_sweep(L* S, int N, const Riccati3Roles<L>& R) {
                 cv[q] = R.isK[q] ? kv : pv;
             }
 #pragma unroll
-            for (int q = 0; q < L::EC; ++q)
+            for (int q = 0; q < L::EC; ++q) {
                 if (R.con[q]) S->PK[k][lane + 64 * q] = cv[q];
+                if (R.con[q] && !R.isK[q]) {
+                    (&S->PF[0][0])[R.fpq[q]] = cv[q];
+                    (&S->PF[0][0])[R.fqp[q]] = cv[q];
+                }
+            }
         }
         __syncthreads();
     }
