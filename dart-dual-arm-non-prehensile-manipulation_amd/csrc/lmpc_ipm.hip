@@ -658,8 +658,10 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         if (!ok) { status = -3; break; }
         if (delta > 0.0) delta_last = delta;
         closed_loop3(S, N);
+        STAMP(11);
         double dx[10], dU[2], lamp[10];
         forward_sweep(S, N, k, dx);
+        STAMP(12);
         asm volatile("" ::: "memory");     // keep the K / Pt reads below after the sweep (register pressure)
         {
             const int kk = xon ? k : 0;
