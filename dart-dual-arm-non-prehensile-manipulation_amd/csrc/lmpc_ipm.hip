@@ -140,36 +140,46 @@ __device__ __forceinline__ void lm_rk4_lin(const LmModel& m, const double* x, do
 #pragma unroll 1
     for (int s = 0; s < 4; ++s) {
         const double wts = (s == 0 || s == 3) ? 1.0 : 2.0, cst = s < 2 ? 0.5 : (s == 2 ? 1.0 : 0.0);
-        double Sfx, Sfx1, Sfx2, Srx, Srx1, Srx2, Sfy, Sfy1, Sfy2, Sry, Sry1, Sry2, Snx, Snx1, Snx2, Sny, Sny1, Sny2;
-        strb_d(m.sx, y[1], Sfx, Sfx1, Sfx2);
-        strb_d(m.sx, fma(-m.r_x, y[7], y[1]), Srx, Srx1, Srx2);
-        strb_d(m.sy, y[3], Sfy, Sfy1, Sfy2);
-        strb_d(m.sy, fma(m.r_y, y[5], y[3]), Sry, Sry1, Sry2);
-        strb_d(m.srx, y[5], Snx, Snx1, Snx2);
-        strb_d(m.sry, y[7], Sny, Sny1, Sny2);
-        double stx, ctx, sty, cty;
-        sincos_any(y[4], stx, ctx);
-        sincos_any(y[6], sty, cty);
+        // each friction term's value / slope / curvature goes into k, sc, sd as soon as it exists
+        // (short live ranges: this pass runs under heavy register pressure)
         double k[8];
         k[0] = y[1]; k[2] = y[3]; k[4] = y[5]; k[6] = y[7];
-        k[1] = (m.m_x * (LM_G * sa) - m.c_x * y[1] - m.k_x * y[0] - Sfx - Srx) * m.im_x;
-        k[3] = (m.m_y * (LM_G * sb) - m.c_y * y[3] - m.k_y * y[2] - Sfy - Sry) * m.im_y;
-        k[5] = (-m.r_y * Sry - Snx - m.c_rx * y[5] - m.tqx * stx) * m.iIx;
-        k[7] = (-m.r_x * Srx - Sny - m.c_ry * y[7] - m.tqy * sty) * m.iIy;
-        // tangent coefficients: d f1/d vx, d f1/d om_y, d f3/d vy, d f3/d om_x, d f5/d vy, d f5/d om_x,
-        // d f5/d th_x, d f7/d vx, d f7/d om_y, d f7/d th_y
-        sc[s][0] = (-m.c_x - Sfx1 - Srx1) * m.im_x;
-        sc[s][1] = m.r_x * Srx1 * m.im_x;
-        sc[s][2] = (-m.c_y - Sfy1 - Sry1) * m.im_y;
-        sc[s][3] = -m.r_y * Sry1 * m.im_y;
-        sc[s][4] = -m.r_y * Sry1 * m.iIx;
-        sc[s][5] = (-m.r_y * m.r_y * Sry1 - Snx1 - m.c_rx) * m.iIx;
-        sc[s][6] = -m.tqx * ctx * m.iIx;
-        sc[s][7] = -m.r_x * Srx1 * m.iIy;
-        sc[s][8] = (m.r_x * m.r_x * Srx1 - Sny1 - m.c_ry) * m.iIy;
-        sc[s][9] = -m.tqy * cty * m.iIy;
-        sd[s][0] = Sfx2; sd[s][1] = Srx2; sd[s][2] = Sfy2; sd[s][3] = Sry2;
-        sd[s][4] = Snx2; sd[s][5] = Sny2; sd[s][6] = stx; sd[s][7] = sty;
+        {
+            double Sfx, Sfx1, Sfx2, Srx, Srx1, Srx2;
+            strb_d(m.sx, y[1], Sfx, Sfx1, Sfx2);
+            strb_d(m.sx, fma(-m.r_x, y[7], y[1]), Srx, Srx1, Srx2);
+            sd[s][0] = Sfx2; sd[s][1] = Srx2;
+            sc[s][0] = (-m.c_x - Sfx1 - Srx1) * m.im_x;
+            sc[s][1] = m.r_x * Srx1 * m.im_x;
+            sc[s][7] = -m.r_x * Srx1 * m.iIy;
+            k[1] = (m.m_x * (LM_G * sa) - m.c_x * y[1] - m.k_x * y[0] - Sfx - Srx) * m.im_x;
+            k[7] = -m.r_x * Srx;                                   // completed below
+            double Sny, Sny1, Sny2, sty, cty;
+            strb_d(m.sry, y[7], Sny, Sny1, Sny2);
+            sincos_any(y[6], sty, cty);
+            sd[s][5] = Sny2; sd[s][7] = sty;
+            sc[s][8] = (m.r_x * m.r_x * Srx1 - Sny1 - m.c_ry) * m.iIy;
+            sc[s][9] = -m.tqy * cty * m.iIy;
+            k[7] = (k[7] - Sny - m.c_ry * y[7] - m.tqy * sty) * m.iIy;
+        }
+        {
+            double Sfy, Sfy1, Sfy2, Sry, Sry1, Sry2;
+            strb_d(m.sy, y[3], Sfy, Sfy1, Sfy2);
+            strb_d(m.sy, fma(m.r_y, y[5], y[3]), Sry, Sry1, Sry2);
+            sd[s][2] = Sfy2; sd[s][3] = Sry2;
+            sc[s][2] = (-m.c_y - Sfy1 - Sry1) * m.im_y;
+            sc[s][3] = -m.r_y * Sry1 * m.im_y;
+            sc[s][4] = -m.r_y * Sry1 * m.iIx;
+            k[3] = (m.m_y * (LM_G * sb) - m.c_y * y[3] - m.k_y * y[2] - Sfy - Sry) * m.im_y;
+            k[5] = -m.r_y * Sry;                                   // completed below
+            double Snx, Snx1, Snx2, stx, ctx;
+            strb_d(m.srx, y[5], Snx, Snx1, Snx2);
+            sincos_any(y[4], stx, ctx);
+            sd[s][4] = Snx2; sd[s][6] = stx;
+            sc[s][5] = (-m.r_y * m.r_y * Sry1 - Snx1 - m.c_rx) * m.iIx;
+            sc[s][6] = -m.tqx * ctx * m.iIx;
+            k[5] = (k[5] - Snx - m.c_rx * y[5] - m.tqx * stx) * m.iIx;
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[i] = fma(wts, k[i], acc[i]);
 #pragma unroll
@@ -518,6 +528,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     SH.DL[k][10] = huu[0]; SH.DL[k][11] = huu[1]; SH.DL[k][12] = LM_G * ca; SH.DL[k][13] = LM_G * cb;
                 }
                 __syncthreads();
+                STAMP(13);
                 {   // exact dynamics Hessian (x, u blocks) and the Jacobian columns: lanes k and k + 32 take
                     // directions 0..4 and 5..9 of node k
                     const int kn = k & 31;
@@ -526,6 +537,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                                            SH.JL[kn]);
                 }
                 __syncthreads();
+                STAMP(14);
                 if (uon) {
                     // the cost / barrier terms: z = [x(8), up(2), u(2), 1], gradient row later
 #pragma unroll

@@ -141,7 +141,7 @@ __device__ __forceinline__ double tanh_fast(double x) {
     const double q = fma(p * r, r, r);
     const double sc = __builtin_ldexp(1.0, (int)n);
     const double em = fma(sc, q, sc - 1.0);
-    return em / (em + 2.0);
+    return em * frcp(em + 2.0);                 // em + 2 in [1, 6e34]: frcp (rcp + Newton) to ~4e-16
 }
 
 // exp(x) by Cody-Waite reduction and a degree-13 Taylor polynomial on |r| <= ln2/2:

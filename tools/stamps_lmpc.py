@@ -25,12 +25,12 @@ for rep in range(3):
     out = s.solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"])
 st = np.zeros(16, dtype=np.uint64)
 L.dartmpc_read_stamps_lmpc(ctypes.c_void_p(st.ctypes.data))
-tot = float(st[:9].sum() + st[11:13].sum())
+tot = float(st[:9].sum() + st[11:15].sum())
 it = max(1, out["iters"][0])
 print(f"block0 iters={out['iters'][0]} total cycles={tot:.0f}")
 for i, n in enumerate(PHASES):
     print(f"  {n:15s} {int(st[i]):10d}  {100 * st[i] / tot:5.1f}%  per-iter {st[i] / it:9.0f}")
-for i, n in zip((11, 12), ("closed loop", "forward sweep")):
+for i, n in zip((11, 12, 13, 14), ("closed loop", "forward sweep", "eval: rk4+adjoint", "eval: directions")):
     print(f"  {n:15s} {int(st[i]):10d}  {100 * st[i] / tot:5.1f}%  per-iter {st[i] / it:9.0f}")
 print(f"  riccati passes {int(st[9])}, line-search trials {int(st[10])}")
 print("batch iters:", out["iters"].tolist())
