@@ -114,7 +114,8 @@ __device__ __forceinline__ void lm_f(const LmModel& m, const double* y, double s
     f[4] = y[5]; f[5] = tx * m.iIx; f[6] = y[7]; f[7] = ty * m.iIy;
 }
 
-__device__ __forceinline__ void lm_rk4(const LmModel& m, const double* x, double sa, double sb, double* xn) {
+__device__ __forceinline__ void lm_rk4(const LmModel& mlds, const double* x, double sa, double sb, double* xn) {
+    const LmModel m = mlds;     // model to registers once (LDS round trips off the stage chains)
     double k[8], y[8], acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { y[i] = x[i]; acc[i] = 0.0; }
@@ -132,8 +133,9 @@ __device__ __forceinline__ void lm_rk4(const LmModel& m, const double* x, double
 // Value pass of RK4 that also stores, per stage s, the tangent coefficients sc[s][10] (the
 // nonzero entries of d f / d y at y_s) and the second-derivative data sd[s][8] = [S''(vx),
 // S''(slip x), S''(vy), S''(slip y), S''(om_x), S''(om_y), sin th_x, sin th_y].
-__device__ __forceinline__ void lm_rk4_lin(const LmModel& m, const double* x, double sa, double sb, double* xn,
+__device__ __forceinline__ void lm_rk4_lin(const LmModel& mlds, const double* x, double sa, double sb, double* xn,
                                            double (*sc)[LM_NSC], double (*sd)[8]) {
+    const LmModel m = mlds;     // model to registers once: the stage loop reads every field ~4 times
     double y[8], acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { y[i] = x[i]; acc[i] = 0.0; }
@@ -329,8 +331,9 @@ __device__ __forceinline__ void lm_directions_half(const LmModel& m, const doubl
     for (int i = 0; i < 10; ++i) lamn[i] = dl[i];
     huu[0] = dl[10]; huu[1] = dl[11];
     const double gca = dl[12], gcb = dl[13];
+    const LmModel mr = m;       // model to registers once for the five directions
 #pragma unroll 1
-    for (int d = d0; d < d0 + 5; ++d) jl_lds[d] = lm_direction(m, sc, cv, huu, gca, gcb, d, lamn, Mk, Hk);
+    for (int d = d0; d < d0 + 5; ++d) jl_lds[d] = lm_direction(mr, sc, cv, huu, gca, gcb, d, lamn, Mk, Hk);
 }
 
 __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
