@@ -72,7 +72,8 @@ __device__ __forceinline__ void rm_f(const RmModel& m, const double* y, double s
 }
 
 // RK4 value (np_mpc...:188-193)
-__device__ __forceinline__ void rm_rk4(const RmModel& m, const double* x, double sa, double sb, double* xn) {
+__device__ __forceinline__ void rm_rk4(const RmModel& mlds, const double* x, double sa, double sb, double* xn) {
+    const RmModel m = mlds;     // model to registers once (LDS round trips off the stage chains)
     double k[4], y[4], acc[4], d0, d1, d2, d3, tx, ty;
     rm_f(m, x, sa, sb, k, d0, d1, d2, d3, tx, ty);
 #pragma unroll
@@ -90,8 +91,9 @@ __device__ __forceinline__ void rm_rk4(const RmModel& m, const double* x, double
 
 // Value pass of RK4 storing per stage s the tangent coefficients sc[s] = [d f1/d vx, d f1/d vy,
 // d f3/d vx, d f3/d vy] and the tanh curvature sd[s] = [T''(vx), T''(vy)] (T = tanh(v / v_eps)).
-__device__ __forceinline__ void rm_rk4_lin(const RmModel& m, const double* x, double sa, double sb, double* xn,
+__device__ __forceinline__ void rm_rk4_lin(const RmModel& mlds, const double* x, double sa, double sb, double* xn,
                                            double (*sc)[4], double (*sd)[2]) {
+    const RmModel m = mlds;     // model to registers once
     double y[4], acc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) { y[i] = x[i]; acc[i] = 0.0; }
@@ -120,8 +122,9 @@ __device__ __forceinline__ void rm_jtv(const RmModel& m, const double* c, const 
 
 // First-order adjoint of nl^T x+ (nl = -lambda_{k+1}) through the RK4 stages; turns sd[s] into the
 // curvature coefficients of kb_s^T f'' at y_s ((vx, vx) and (vy, vy)); returns the tilt curvature.
-__device__ __forceinline__ void rm_adjoint_curv(const RmModel& m, const double (*sc)[4], double (*sd)[2],
+__device__ __forceinline__ void rm_adjoint_curv(const RmModel& mlds, const double (*sc)[4], double (*sd)[2],
                                                 const double* lamn, double sa, double sb, double* huu) {
+    const RmModel m = mlds;
     double kb[4], yb[4];
     const double h = m.h;
 #pragma unroll
