@@ -90,6 +90,23 @@ __device__ __forceinline__ void affine_scan_level(double& f11, double& f12, doub
     f11 = n11; f12 = n12; f21 = n21; f22 = n22;
 }
 
+// One level of a suffix scan of 4x4 matrices (T <- T * F, F fetched from lane k + d by DPP
+// row_shl:d, identity where out of range)
+template <int CTRL>
+__device__ __forceinline__ void mat4_scan_level(double* T) {
+    double F[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) F[e] = dpp_fill<CTRL, 0xf>((e % 5 == 0) ? 1.0 : 0.0, T[e]);
+    double N[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            N[4 * i + j] = fma(T[4 * i], F[j], fma(T[4 * i + 1], F[4 + j], fma(T[4 * i + 2], F[8 + j], T[4 * i + 3] * F[12 + j])));
+#pragma unroll
+    for (int e = 0; e < 16; ++e) T[e] = N[e];
+}
+
 // ---------------------------------------------------------------------------
 // the kernel: one wave64 = one instance.
 //   NAX = 1 (N <= 31): lane = axis*32 + k, one axis per lane (x in lanes 0-31, y in 32-63)
@@ -121,6 +138,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
     // per-lane stage map: the real Phi on stages k < N, zero on the terminal/idle lanes, so that the
     // backward sweep reproduces the terminal value function there without a branch
     const double f11 = uon ? 1.0 : 0.0, a12k = uon ? a12 : 0.0, a22k = uon ? a22 : 0.0;
+    const double ai22 = 1.0 / a22, ai12 = -a12 * ai22;        // A^-1 = [[1, ai12], [0, ai22]]
     const double A11k = a12k * a12k, A12k = 2.0 * a12k * a22k, A22k = a22k * a22k;
 
     // per-lane axis slots
@@ -256,6 +274,70 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 p1[j] = q1[j]; p2[j] = q2[j];
                 Rt[j] = Rt0[j] + delta;
             }
+            // Quadratic part as a scan: with P = Y U^-1 the stage map P_k = X + A^T (P_{k+1}^-1 + G_k)^-1 A
+            // (G_k = B_k B_k^T / R_k) is linear on [U; Y]: [U; Y]_k = S_k [U; Y]_{k+1},
+            // S_k = [[A^-1, A^-1 G], [X A^-1, X A^-1 G + A^T]], so [U; Y]_k = S_k ... S_{N-1} [I; X]
+            // is a suffix product (5 DPP levels).  Exact in the reals; in fp64 it matches the
+            // sequential sweep to ~1e-15 while every stage is mildly stiff (B_k B_k^T X / R_k <= 2
+            // per axis, checked here); otherwise, and for NAX == 2, the sequential sweep runs.
+            bool use_scan = false;
+            if constexpr (NAX == 1) {
+                const double ratio = fmax(E11[0] * X11d, E22[0] * X22d);
+                use_scan = !wany(uon && !(Rt[0] > 0.0 && ratio <= 2.0 * Rt[0]));
+            }
+            STAMP_ADD(11, use_scan ? 1 : 0);
+            if (use_scan) {
+                const double iR = uon ? frcp(Rt[0]) : 0.0;
+                const double G11 = be1[0] * be1[0] * iR, G12 = be1[0] * be2[0] * iR, G22 = be2[0] * be2[0] * iR;
+                const double g11 = G11 + ai12 * G12, g12 = G12 + ai12 * G22, g21 = ai22 * G12, g22 = ai22 * G22;
+                double T[16] = {1.0, ai12, g11, g12,
+                                0.0, ai22, g21, g22,
+                                X11d, X11d * ai12, fma(X11d, g11, 1.0), X11d * g12,
+                                0.0, X22d * ai22, fma(X22d, g21, a12), fma(X22d, g22, a22)};
+                if (!uon) {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) T[e] = (e % 5 == 0) ? 1.0 : 0.0;
+                }
+                mat4_scan_level<0x101>(T);
+                mat4_scan_level<0x102>(T);
+                mat4_scan_level<0x104>(T);
+                mat4_scan_level<0x108>(T);
+                {   // rows 0 and 2 of each half: compose with the suffix held by lane 16 (48)
+                    const int src = (lane & 32) | 16;
+                    double F[16];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) F[e] = __shfl(T[e], src);
+                    if ((lane & 16) == 0) {
+                        double Nn[16];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+#pragma unroll
+                            for (int jj = 0; jj < 4; ++jj)
+                                Nn[4 * i + jj] = fma(T[4 * i], F[jj], fma(T[4 * i + 1], F[4 + jj],
+                                                     fma(T[4 * i + 2], F[8 + jj], T[4 * i + 3] * F[12 + jj])));
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) T[e] = Nn[e];
+                    }
+                }
+                // [U; Y] = T [I; X], P = Y U^-1 (symmetrised)
+                const double U11 = fma(T[2], X11d, T[0]), U12 = fma(T[3], X22d, T[1]);
+                const double U21 = fma(T[6], X11d, T[4]), U22 = fma(T[7], X22d, T[5]);
+                const double Y11 = fma(T[10], X11d, T[8]), Y12 = fma(T[11], X22d, T[9]);
+                const double Y21 = fma(T[14], X11d, T[12]), Y22 = fma(T[15], X22d, T[13]);
+                const double idet = frcp(fma(U11, U22, -U12 * U21));
+                const double q11 = fma(Y11, U22, -Y12 * U21) * idet, q12 = fma(Y12, U11, -Y11 * U12) * idet;
+                const double q21 = fma(Y21, U22, -Y22 * U21) * idet, q22 = fma(Y22, U11, -Y21 * U12) * idet;
+                P11[0] = q11; P12[0] = 0.5 * (q12 + q21); P22[0] = q22;
+                // the stage quantities of node k from P_{k+1}
+                const double n11 = from_next(P11[0]), n12 = from_next(P12[0]), n22 = from_next(P22[0]);
+                const double e1 = be1[0], e2 = be2[0];
+                const double Q = fma(E11[0], n11, fma(E12[0], n12, fma(E22[0], n22, Rt[0])));
+                const double PB1 = fma(n11, e1, n12 * e2), PB2 = fma(n12, e1, n22 * e2);
+                const double U1 = PB1, U2 = fma(PB1, a12k, PB2 * a22k);
+                const double iQ = frcp(Q);
+                W1[0] = iQ * U1; W2[0] = iQ * U2;
+                Quu[0] = Q; iQs[0] = iQ;
+            } else
             // backward sweep: every lane maps its neighbour's value function through its own
             // stage; after step j lane N-1-j is final.  Terminal/idle lanes have Phi = 0, B = 0.
             for (int step = 0; step < N; ++step) {

@@ -29,5 +29,6 @@ tot = float(st[:9].sum())
 print(f"block0 iters={out['iters'][0]} total cycles={tot:.0f}")
 for i, n in enumerate(PHASES):
     print(f"  {n:12s} {int(st[i]):10d}  {100 * st[i] / tot:5.1f}%  per-iter {st[i] / max(1, out['iters'][0]):9.0f}")
+print(f"  scan-path Riccati passes {int(st[11])}")
 print(f"  riccati passes {int(st[9])}, line-search trials {int(st[10])}")
 print("batch iters:", out["iters"].tolist())
