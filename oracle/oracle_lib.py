@@ -43,7 +43,7 @@ def _p(a, t=_dp):
     return a.ctypes.data_as(t)
 
 
-def solve_batch(states, targets, params, N=20, Ts=0.002, max_iter=200, tol=1e-9, nthreads=1, want_w=True):
+def solve_batch(states, targets, params, N=20, Ts=0.002, max_iter=200, tol=1e-9, nthreads=1, want_w=True, soc=True):
     states = np.ascontiguousarray(states, np.float64)
     targets = np.ascontiguousarray(targets, np.float64)
     params = np.ascontiguousarray(params, np.float64)
@@ -54,6 +54,7 @@ def solve_batch(states, targets, params, N=20, Ts=0.002, max_iter=200, tol=1e-9,
     w = np.zeros((B, nw)) if want_w else None
     st = np.zeros(B, np.int32)
     it = np.zeros(B, np.int32)
+    lib().oracle_pmpc_set_soc(int(bool(soc)))
     lib().oracle_pmpc_solve_batch(B, N, Ts, _p(states), _p(targets), _p(params), max_iter, tol, nthreads,
                                   _p(u0), _p(f), _p(w) if want_w else None, _p(st, _ip), _p(it, _ip))
     return dict(u0=u0, f=f, w=w, status=st, iters=it)

@@ -38,6 +38,10 @@
 
 /* IPOPT Compare_le: lhs <= rhs up to 10 machine epsilons of |base| */
 #define LE(l, r, b) ((l) - (r) <= 10.0 * 2.220446049250313e-16 * fabs(b))
+
+/* second-order correction on/off (IPOPT default on; the GPU kernel mirrors the off path) */
+static int g_soc = 1;
+void oracle_pmpc_set_soc(int on) { g_soc = on; }
 #ifdef ORACLE_DEBUG
 #include <stdio.h>
 #endif
@@ -434,7 +438,7 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
                     if (th <= th_min && sw) { if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { accepted = 1; ftype = 1; } }
                     else if (LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi)) accepted = 1;
                 }
-                if (accepted || ls > 0 || th_t < th) break;
+                if (accepted || ls > 0 || th_t < th || !g_soc) break;
                 /* second-order correction: c_soc <- a c_soc + g(trial); solve; re-try */
                 if (pass == 0) { for (int k = 0; k <= N; ++k) for (int i = 0; i < NX; ++i) W->csoc[k][i] = alpha * g[k][i] + W->gt[k][i]; }
                 else {
