@@ -342,7 +342,8 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     LmLds* S = &SH.ocp;
     const Riccati3Roles<LmLds> RR = riccati3_roles<LmLds>();
     STAMP_DECL
-    const int b = blockIdx.x;
+    if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
+    const int b = blockIdx.x / a.pack;
     const int k = threadIdx.x;
     const int N = a.N;
     const bool xon = k <= N, uon = k < N;
@@ -824,7 +825,9 @@ extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStre
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL(dartmpc::lmpc_ipm_kernel, dim3(args->B), dim3(dartmpc::kWave), lds, stream, *args);
+    dartmpc::LmpcArgs a = *args;
+    a.pack = (a.B <= 32) ? 8 : 1;            // one XCD (and its L2) for the code of a small batch
+    hipLaunchKernelGGL(dartmpc::lmpc_ipm_kernel, dim3(a.B * a.pack), dim3(dartmpc::kWave), lds, stream, a);
     return hipGetLastError();
 }
 

@@ -9,6 +9,7 @@ struct PmpcArgs {
     int B, N;
     double Ts, tol, g;      // g = model.opt.gravity[2]
     int max_iter;
+    int pack;               // blocks per instance slot: 8 packs a small batch onto one XCD (launcher)
     const double* x0;       // [B][6]   device
     const double* ref;      // [B][6]
     const double* prm;      // [B][6]  mu, Qp, Qv, R, u_lo, u_hi

@@ -115,7 +115,10 @@ __device__ __forceinline__ void mat4_scan_level(double* T) {
 template <int NAX>
 __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
     STAMP_DECL
-    const int b = blockIdx.x;
+    // small batches: the launcher deals 8 blocks per instance and only every 8th works, so all
+    // instances land on one XCD (blocks go round-robin over the 8 XCDs) and share its L2 for the code
+    if (blockIdx.x % a.pack) return;
+    const int b = blockIdx.x / a.pack;
     const int lane = threadIdx.x;
     const int k = NAX == 1 ? (lane & 31) : lane;            // shooting node of this lane
     const int ax0 = NAX == 1 ? (lane >> 5) : 0;               // axis of slot 0 (NAX == 1)
@@ -626,10 +629,13 @@ __global__ __launch_bounds__(kWave) void wave_selftest_kernel(double* out) {
 
 extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStream_t stream) {
     if (args->B <= 0) return hipSuccess;
-    if (args->N <= 31)
-        hipLaunchKernelGGL(dartmpc::pmpc_ipm_kernel<1>, dim3(args->B), dim3(dartmpc::kWave), 0, stream, *args);
+    dartmpc::PmpcArgs a = *args;
+    a.pack = (a.B <= 32) ? 8 : 1;          // <= 32 waves fit one XCD's CUs
+    const dim3 grid(a.B * a.pack);
+    if (a.N <= 31)
+        hipLaunchKernelGGL(dartmpc::pmpc_ipm_kernel<1>, grid, dim3(dartmpc::kWave), 0, stream, a);
     else
-        hipLaunchKernelGGL(dartmpc::pmpc_ipm_kernel<2>, dim3(args->B), dim3(dartmpc::kWave), 0, stream, *args);
+        hipLaunchKernelGGL(dartmpc::pmpc_ipm_kernel<2>, grid, dim3(dartmpc::kWave), 0, stream, a);
     return hipGetLastError();
 }
 

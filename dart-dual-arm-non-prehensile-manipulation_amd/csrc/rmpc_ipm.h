@@ -9,6 +9,7 @@ struct RmpcArgs {
     int B, N;
     double Ts, tol, g;
     int max_iter;
+    int pack;                // blocks per instance slot (set by the launcher; 8 = one XCD for small B)
     const double* x0;        // [B][4]
     const double* u_prev;    // [B][2]
     double* theta;           // [B][14] theta_hat (in), or RLS theta (in/out) when rls_P != nullptr

@@ -242,7 +242,8 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     RmLds* S = &SH.ocp;
     const RiccatiRoles<RmLds::EPL> RR = riccati_roles<RmLds>();
     STAMP_DECL
-    const int b = blockIdx.x;
+    if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
+    const int b = blockIdx.x / a.pack;
     const int k = threadIdx.x;
     const int N = a.N;
     const bool xon = k <= N, uon = k < N;
@@ -839,7 +840,9 @@ extern "C" hipError_t dartmpc_launch_rls(int B, double* theta, double* P, const 
 extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStream_t stream) {
     if (args->B <= 0) return hipSuccess;
     if (args->N < 1 || args->N >= dartmpc::RM_NMAXS) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel, dim3(args->B), dim3(dartmpc::kWave), 0, stream, *args);
+    dartmpc::RmpcArgs a = *args;
+    a.pack = (a.B <= 32) ? 8 : 1;            // blocks go round-robin over the 8 XCDs: one XCD, one L2 for the code
+    hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel, dim3(a.B * a.pack), dim3(dartmpc::kWave), 0, stream, a);
     return hipGetLastError();
 }
 
