@@ -52,6 +52,7 @@ int check_cfg(const dart_mpc_config* c) {
     if (c->N < 1 || c->N > (c->variant == DART_MPC_PMPC ? 63 : 31)) return 0;
     if (!(c->Ts > 0.0) || !(c->tol > 0.0) || !(c->gravity == c->gravity) || c->max_iter < 1 || c->B_max < 1) return 0;
     if (c->acceptable_iter < 0 || (c->acceptable_iter > 0 && !(c->acceptable_tol > 0.0))) return 0;
+    if (c->max_soc < 0 || c->max_soc > 8) return 0;
     return 1;
 }
 
@@ -80,7 +81,7 @@ void dart_mpc_config_default(dart_mpc_config* c) {
     c->gravity = -9.81;
     c->acceptable_tol = 1e-6;      // IPOPT defaults
     c->acceptable_iter = 15;
-    c->reserved = 0;
+    c->max_soc = 4;
 }
 
 int dart_mpc_nw(int N) { return 6 * (N + 1) + 2 * N; }
@@ -261,7 +262,7 @@ int dart_lmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* state, co
     HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
     dartmpc::LmpcArgs a;
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter;
-    a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter;
+    a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc;
     a.state = state; a.u_prev = u_prev; a.pvec = pvec; a.target = target; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     HIPCHK(h, dartmpc_launch_lmpc(&a, stream ? (hipStream_t)stream : h->stream), "kernel launch");

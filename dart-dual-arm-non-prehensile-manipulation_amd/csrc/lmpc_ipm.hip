@@ -56,6 +56,8 @@ struct LmShared {
     NodeArr<double[4][8], LM_NMAXS + 1> SD;
     NodeArr<double[12], LM_NMAXS + 1> JL;      // J^T lambda_{k+1} staging, primal residual maxima
     NodeArr<double[14], LM_NMAXS + 1> DL;      // per node: lambda_{k+1}, tilt curvature, g cos(u) for the mirror lanes
+    NodeArr<double[10], LM_NMAXS + 1> CS;      // second-order correction: c_soc rows of node k (incoming defect)
+    NodeArr<double[22], LM_NMAXS + 1> SV;      // second-order correction: the plain step (dx~, lambda+, du) of node k
     LmModel model;                    // uniform problem data, read at the use sites (keeps VGPRs free)
     double Q[8], Qt[8], tgt[8];
 };
@@ -577,6 +579,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 pl = fmax(pl, xon ? d * fabs(gi) : 0.0);
                 plu = fmax(plu, xon ? fabs(gi) : 0.0);
                 if (k == 0) S->dx0[i] = -gi;
+                SH.CS[sr][i] = gi;       // c(x) for a second-order correction
             }
             SH.JL[sr][10] = pl; SH.JL[sr][11] = plu;    // primal residual maxima (LDS: frees registers)
         }
@@ -649,37 +652,23 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         __syncthreads();
         STAMP(2);
 
-        // ---------------- Newton step: Riccati with inertia correction -----------------------
-        double delta = 0.0, dapplied = 0.0;
-        bool ok = riccati3_sweep(S, N, RR);
-        int attempt = 1;
-        for (; attempt < 60 && !ok; ++attempt) {
-            delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last / 3.0))
-                                   : delta * (delta_last == 0.0 ? 100.0 : 8.0);
-            const double dd = delta - dapplied;
-            if (uon) {
-#pragma unroll
-                for (int j = 0; j < 12; ++j) Hk[hp(j, j)] += dd;
-            }
-            if (k == N) {
-#pragma unroll
-                for (int j = 0; j < 10; ++j) S->PK[N][hp(j, j)] += dd;
-            }
-            dapplied = delta;
-            __syncthreads();
-            ok = riccati3_sweep(S, N, RR);
-        }
-        STAMP_ADD(9, attempt);
-        STAMP(3);
-        if (!ok) { status = -3; break; }
-        if (delta > 0.0) delta_last = delta;
-        closed_loop3(S, N);
-        STAMP(11);
-        double dx[10], dU[2], lamp[10];
-        forward_sweep(S, N, k, dx);
-        STAMP(12);
-        asm volatile("" ::: "memory");     // keep the K / Pt reads below after the sweep (register pressure)
-        {
+        // ---------------- Newton step and filter line search ----------------------------------
+        // One copy of the Riccati solve serves the plain Newton step (with inertia correction) and
+        // IPOPT's second-order correction passes (FilterLSAcceptor::TrySecondOrderCorrection; max_soc,
+        // kappa_soc 0.99): a rejected full step with theta(trial) >= theta re-solves the system with
+        // c_soc <- alpha_soc c_soc + c(x_trial) (from c(x), alpha_soc = alpha) in the defect column of
+        // M~ and dx~_0 (H~, incl. the inertia shift, is unchanged) and tries x + alpha_soc d_soc.
+        double dx[10], dU[2], lamp[10], gt[10], dzl[2], dzu[2];
+        double amax = 1.0, az = 1.0, phi = 0.0, gTd = 0.0, amin = 0.0, alpha = 1.0, th_t = 0.0, ph_t = 0.0;
+        double th_prev = 0.0;
+        float lg_sw = 0.0f;
+        bool accepted = false, ftype = false, tiny = false, ok = true;
+        int ls = 0, soc = -1;        // soc: -1 plain step, >= 0 second-order-correction pass
+        // the Newton step from the factorised value functions: forward sweep, du = K [dx~; 1], lambda+
+        auto recover_step = [&]() {
+            forward_sweep(S, N, k, dx);
+            STAMP(12);
+            asm volatile("" ::: "memory");     // keep the K / Pt reads below after the sweep (register pressure)
             const int kk = xon ? k : 0;
             const double* K0 = S->PK[uon ? k : 0] + LmLds::NPT;
             const double* K1 = K0 + LmLds::NP;
@@ -688,84 +677,191 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             for (int j = 0; j < 10; ++j) { d0 = fma(K0[j], dx[j], d0); d1 = fma(K1[j], dx[j], d1); }
             dU[0] = uon ? d0 : 0.0; dU[1] = uon ? d1 : 0.0;
             node_multiplier3(S, kk, dx, lamp);
-        }
-        STAMP(4);
-        double dzl[2], dzu[2];
-        dzl[0] = uon ? mu * isl0 - zl[0] - zl[0] * isl0 * dU[0] : 0.0;
-        dzl[1] = uon ? mu * isl1 - zl[1] - zl[1] * isl1 * dU[1] : 0.0;
-        dzu[0] = uon ? mu * isu0 - zu[0] + zu[0] * isu0 * dU[0] : 0.0;
-        dzu[1] = uon ? mu * isu1 - zu[1] + zu[1] * isu1 * dU[1] : 0.0;
-        double amax = 1.0, az = 1.0;
-        if (uon) {
+        };
+        // primal fraction to the boundary of dU (wave-uniform)
+        auto primal_ftb = [&]() {
+            double am = 1.0;
+            if (uon) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                if (dU[j] < 0) amax = fmin(amax, -tau * (u[j] - lo) / dU[j]);
-                if (dU[j] > 0) amax = fmin(amax, tau * (hi - u[j]) / dU[j]);
-                if (dzl[j] < 0) az = fmin(az, -tau * zl[j] / dzl[j]);
-                if (dzu[j] < 0) az = fmin(az, -tau * zu[j] / dzu[j]);
+                for (int j = 0; j < 2; ++j) {
+                    if (dU[j] < 0) am = fmin(am, -tau * (u[j] - lo) / dU[j]);
+                    if (dU[j] > 0) am = fmin(am, tau * (hi - u[j]) / dU[j]);
+                }
             }
-        }
-        amax = (double)wminf((float)amax) * (1.0 - 1.0 / 1048576.0);
-        az = (double)wminf((float)az) * (1.0 - 1.0 / 1048576.0);
-        STAMP(5);
-
-        // ---------------- filter line search -------------------------------------------------
-        double phil = sc * cost_val(x, u, up), gtdl = 0.0;
-        if (uon) phil -= mu * log((u[0] - lo) * (hi - u[0]) * (u[1] - lo) * (hi - u[1]));
-        {
-            double gz_[12];
-            cost_grad(x, u, up, gz_);
+            return (double)wminf((float)am) * (1.0 - 1.0 / 1048576.0);
+        };
+        // bound-multiplier directions of dU and their fraction to the boundary (wave-uniform)
+        auto dual_step = [&]() {
+            dzl[0] = uon ? mu * isl0 - zl[0] - zl[0] * isl0 * dU[0] : 0.0;
+            dzl[1] = uon ? mu * isl1 - zl[1] - zl[1] * isl1 * dU[1] : 0.0;
+            dzu[0] = uon ? mu * isu0 - zu[0] + zu[0] * isu0 * dU[0] : 0.0;
+            dzu[1] = uon ? mu * isu1 - zu[1] + zu[1] * isu1 * dU[1] : 0.0;
+            double az_ = 1.0;
+            if (uon) {
 #pragma unroll
-            for (int i = 0; i < 10; ++i) gtdl += xon ? sc * gz_[i] * dx[i] : 0.0;
-            if (uon) gtdl += (sc * gz_[10] - mu * isl0 + mu * isu0) * dU[0] + (sc * gz_[11] - mu * isl1 + mu * isu1) * dU[1];
-        }
-        const double phi = wsum(phil), gTd = wsum(gtdl);
-        const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
-        const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
-        const float lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;
-        double amin = gam_th;
-        if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta / (-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
-        amin *= gam_al;
-        double alpha = amax, th_t = 0.0, ph_t = 0.0;
-        bool accepted = false, ftype = false;
-        float tnl = 0.0f;
+                for (int j = 0; j < 2; ++j) {
+                    if (dzl[j] < 0) az_ = fmin(az_, -tau * zl[j] / dzl[j]);
+                    if (dzu[j] < 0) az_ = fmin(az_, -tau * zu[j] / dzu[j]);
+                }
+            }
+            return (double)wminf((float)az_) * (1.0 - 1.0 / 1048576.0);
+        };
+        // trial point x + al d: incoming defects gt of node k, wave-summed theta and barrier objective
+        auto trial = [&](double al) {
+            double xt[8], pt[2], ut[2];
 #pragma unroll
-        for (int i = 0; i < 10; ++i) {
-            const double xi = i < 8 ? x[i] : up[i - 8];
-            tnl = fmaxf(tnl, xon ? fabsf((float)dx[i]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)xi)) : 0.0f);
-        }
-        if (uon) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) tnl = fmaxf(tnl, fabsf((float)dU[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)u[j])));
-        }
-        const bool tiny = wmaxf(tnl) < 2.2e-15f;
-        STAMP(6);
-        int ls = 0;
-        for (; ls < 80; ++ls) {
-            double xt[8], pt[2], ut[2], gt[10];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) xt[i] = fma(alpha, dx[i], x[i]);
-            pt[0] = fma(alpha, dx[8], up[0]); pt[1] = fma(alpha, dx[9], up[1]);
-            ut[0] = fma(alpha, dU[0], u[0]); ut[1] = fma(alpha, dU[1], u[1]);
+            for (int i = 0; i < 8; ++i) xt[i] = fma(al, dx[i], x[i]);
+            pt[0] = fma(al, dx[8], up[0]); pt[1] = fma(al, dx[9], up[1]);
+            ut[0] = fma(al, dU[0], u[0]); ut[1] = fma(al, dU[1], u[1]);
             defects(xt, pt, ut, gt);
             double phl = sc * cost_val(xt, ut, pt);
             if (uon) phl -= mu * log((ut[0] - lo) * (hi - ut[0]) * (ut[1] - lo) * (hi - ut[1]));
             th_t = wsum(theta_of(gt)); ph_t = wsum(phl);
-            if (tiny) { accepted = true; ftype = true; break; }
+        };
+        // filter acceptance of (th_t, ph_t) for the step size al_test (IPOPT alpha_primal_test)
+        auto acceptable = [&](double al_test, bool& ft) {
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
             in_filter = in_filter || wany(k < nfilt && th_t >= fth && ph_t >= fph);
-            if (!in_filter) {
-                const bool sw = gTd < 0.0 && lg2(alpha) > lg_sw;
-                if (theta <= th_min && sw) {
-                    if (cmp_le(ph_t, phi + eta_ph * alpha * gTd, phi)) { accepted = true; ftype = true; }
-                } else if (cmp_le(th_t, (1 - gam_th) * theta, theta) || cmp_le(ph_t - phi, -gam_ph * theta, phi)) {
-                    accepted = true;
-                }
+            if (in_filter) return false;
+            const bool sw = gTd < 0.0 && lg2(al_test) > lg_sw;
+            if (theta <= th_min && sw) {
+                if (cmp_le(ph_t, phi + eta_ph * al_test * gTd, phi)) { ft = true; return true; }
+                return false;
             }
-            if (accepted) break;
-            alpha *= 0.5;
-            if (alpha < amin) break;
+            return cmp_le(th_t, (1 - gam_th) * theta, theta) || cmp_le(ph_t - phi, -gam_ph * theta, phi);
+        };
+        for (;;) {
+            // Riccati (one call site): plain step with inertia correction, or a second-order
+            // correction with the same factorisation and the defects c_soc
+            if (soc >= 0) {
+                double cs[10];
+#pragma unroll
+                for (int i = 0; i < 10; ++i) cs[i] = xon ? SH.CS[sr][i] : 0.0;
+#pragma unroll
+                for (int r = 0; r < 10; ++r) {
+                    const double t = from_next(cs[r]);
+                    if (uon) Mk[12 * NC + r] = -t;
+                    if (k == 0) S->dx0[r] = -cs[r];
+                }
+                __syncthreads();
+                STAMP_ADD(15, 1);
+            }
+            {
+                double delta = 0.0, dapplied = 0.0;
+                int attempt = 0;
+                for (;;) {
+                    ok = riccati3_sweep(S, N, RR);
+                    if (ok || soc >= 0 || ++attempt >= 60) break;
+                    delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last / 3.0))
+                                           : delta * (delta_last == 0.0 ? 100.0 : 8.0);
+                    const double dd = delta - dapplied;
+                    if (uon) {
+#pragma unroll
+                        for (int j = 0; j < 12; ++j) Hk[hp(j, j)] += dd;
+                    }
+                    if (k == N) {
+#pragma unroll
+                        for (int j = 0; j < 10; ++j) S->PK[N][hp(j, j)] += dd;
+                    }
+                    dapplied = delta;
+                    __syncthreads();
+                }
+                STAMP_ADD(9, attempt + 1);
+                if (soc >= 0) ok = true;
+                else if (ok && delta > 0.0) delta_last = delta;
+            }
+            STAMP(3);
+            if (!ok) break;
+            closed_loop3(S, N);
+            STAMP(11);
+            recover_step();
+            STAMP(4);
+            double al_try;
+            if (soc < 0) {
+                amax = primal_ftb();
+                az = dual_step();
+                STAMP(5);
+                double phil = sc * cost_val(x, u, up), gtdl = 0.0;
+                if (uon) phil -= mu * log((u[0] - lo) * (hi - u[0]) * (u[1] - lo) * (hi - u[1]));
+                {
+                    double gz_[12];
+                    cost_grad(x, u, up, gz_);
+#pragma unroll
+                    for (int i = 0; i < 10; ++i) gtdl += xon ? sc * gz_[i] * dx[i] : 0.0;
+                    if (uon) gtdl += (sc * gz_[10] - mu * isl0 + mu * isu0) * dU[0] + (sc * gz_[11] - mu * isl1 + mu * isu1) * dU[1];
+                }
+                phi = wsum(phil); gTd = wsum(gtdl);
+                const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
+                const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
+                lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;
+                amin = gam_th;
+                if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta / (-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
+                amin *= gam_al;
+                float tnl = 0.0f;
+#pragma unroll
+                for (int i = 0; i < 10; ++i) {
+                    const double xi = i < 8 ? x[i] : up[i - 8];
+                    tnl = fmaxf(tnl, xon ? fabsf((float)dx[i]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)xi)) : 0.0f);
+                }
+                if (uon) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) tnl = fmaxf(tnl, fabsf((float)dU[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)u[j])));
+                }
+                tiny = wmaxf(tnl) < 2.2e-15f;
+                alpha = amax;
+                al_try = alpha;
+                STAMP(6);
+            } else {
+                al_try = primal_ftb();
+            }
+            bool resolve = false;
+            for (;;) {
+                trial(al_try);
+                if (soc < 0) {
+                    if (tiny) { accepted = true; ftype = true; break; }
+                    if (acceptable(alpha, ftype)) { accepted = true; break; }
+                    if (ls == 0 && a.max_soc > 0 && !(th_t < theta)) {
+                        if (xon) {      // c_soc = alpha c(x) + c(x_trial); keep the plain step
+#pragma unroll
+                            for (int i = 0; i < 10; ++i) {
+                                SH.CS[sr][i] = fma(alpha, SH.CS[sr][i], gt[i]);
+                                SH.SV[sr][i] = dx[i]; SH.SV[sr][10 + i] = lamp[i];
+                            }
+                            SH.SV[sr][20] = dU[0]; SH.SV[sr][21] = dU[1];
+                        }
+                        th_prev = th_t; soc = 0; resolve = true;
+                        break;
+                    }
+                } else {
+                    bool ft = false;
+                    if (acceptable(alpha, ft)) {
+                        accepted = true; ftype = ft; alpha = al_try;
+                        az = dual_step();      // IPOPT takes the corrected solve as the whole step
+                        break;
+                    }
+                    if (soc + 1 < a.max_soc && th_t <= 0.99 * th_prev) {
+                        if (xon) {      // c_soc <- alpha_soc c_soc + c(x_soc trial)
+#pragma unroll
+                            for (int i = 0; i < 10; ++i) SH.CS[sr][i] = fma(al_try, SH.CS[sr][i], gt[i]);
+                        }
+                        th_prev = th_t; ++soc; resolve = true;
+                        break;
+                    }
+                    if (xon) {      // corrections failed: back to the plain step, backtrack
+#pragma unroll
+                        for (int i = 0; i < 10; ++i) { dx[i] = SH.SV[sr][i]; lamp[i] = SH.SV[sr][10 + i]; }
+                        dU[0] = SH.SV[sr][20]; dU[1] = SH.SV[sr][21];
+                    }
+                    soc = -1;
+                }
+                ++ls;
+                alpha *= 0.5;
+                if (alpha < amin || ls >= 80) break;
+                al_try = alpha;
+            }
+            if (!resolve) break;
         }
+        if (!ok) { status = -3; break; }
         STAMP_ADD(10, ls + 1);
         STAMP(7);
         if (!accepted) { status = -2; break; }

@@ -112,7 +112,9 @@ __device__ __forceinline__ void mat4_scan_level(double* T) {
 //   NAX = 1 (N <= 31): lane = axis*32 + k, one axis per lane (x in lanes 0-31, y in 32-63)
 //   NAX = 2 (N <= 63): lane = k, both axes in every lane
 // ---------------------------------------------------------------------------
-template <int NAX>
+//   QSCAN: compile the quadratic-Riccati scan (latency regime); without it the kernel fits 2 waves
+//   per SIMD (throughput regime)
+template <int NAX, bool QSCAN>
 __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
     STAMP_DECL
     // small batches: the launcher deals 8 blocks per instance and only every 8th works, so all
@@ -284,7 +286,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
             // sequential sweep to ~1e-15 while every stage is mildly stiff (B_k B_k^T X / R_k <= 2
             // per axis, checked here); otherwise, and for NAX == 2, the sequential sweep runs.
             bool use_scan = false;
-            if constexpr (NAX == 1) {
+            if constexpr (NAX == 1 && QSCAN) {
                 const double ratio = fmax(E11[0] * X11d, E22[0] * X22d);
                 use_scan = !wany(uon && !(Rt[0] > 0.0 && ratio <= 2.0 * Rt[0]));
             }
@@ -631,11 +633,15 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
     if (args->B <= 0) return hipSuccess;
     dartmpc::PmpcArgs a = *args;
     a.pack = (a.B <= 32) ? 8 : 1;          // <= 32 waves fit one XCD's CUs
+    // The quadratic scan shortens the dependent chain but needs more registers (one wave per SIMD
+    // instead of two): worth it while every wave has a SIMD of its own (B <= 4 x 256), not beyond.
     const dim3 grid(a.B * a.pack);
-    if (a.N <= 31)
-        hipLaunchKernelGGL(dartmpc::pmpc_ipm_kernel<1>, grid, dim3(dartmpc::kWave), 0, stream, a);
+    if (a.N <= 31 && a.B <= 1024)
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+    else if (a.N <= 31)
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, false>), grid, dim3(dartmpc::kWave), 0, stream, a);
     else
-        hipLaunchKernelGGL(dartmpc::pmpc_ipm_kernel<2>, grid, dim3(dartmpc::kWave), 0, stream, a);
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<2, false>), grid, dim3(dartmpc::kWave), 0, stream, a);
     return hipGetLastError();
 }
 

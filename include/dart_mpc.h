@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define DART_MPC_ABI_VERSION 2
+#define DART_MPC_ABI_VERSION 3
 
 enum dart_mpc_variant {
     DART_MPC_PMPC = 0,      /* PMPC/src/controller/mpc_3d.py, N <= 63 */
@@ -92,7 +92,8 @@ typedef struct dart_mpc_config {
     double gravity;     /* model.opt.gravity[2] (mpc_3d.py:23), default -9.81 */
     double acceptable_tol;   /* IPOPT acceptable_tol; used by LMPC (rlmpc2.py:487: 1e-3) */
     int32_t acceptable_iter; /* IPOPT acceptable_iter, 0 = off; used by LMPC (rlmpc2.py:488: 5) */
-    int32_t reserved;
+    int32_t max_soc;    /* IPOPT max_soc (second-order corrections per line search), default 4, 0 = off,
+                           <= 8; used by LMPC (the reference leaves IPOPT's default, rlmpc2.py:480-489) */
 } dart_mpc_config;
 
 typedef struct dart_mpc_handle dart_mpc_handle;

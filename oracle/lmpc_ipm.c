@@ -221,8 +221,8 @@ enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_MAXITER = -1, ST_LS_FAIL = -2, ST_IN
 static double g_relax = 1e-8;
 void oracle_lmpc_set_relax(double r) { g_relax = r; }
 /* second-order correction on/off (IPOPT default on; off mirrors the GPU kernel's line search) */
-static int g_soc = 1;
-void oracle_lmpc_set_soc(int on) { g_soc = on; }
+static int g_max_soc = 4;
+void oracle_lmpc_set_soc(int max_soc) { g_max_soc = max_soc < 0 ? 0 : max_soc; }
 
 static void stage_z(const double *X, const double *U, int k, double *z) {
     for (int i = 0; i < NA; ++i) z[i] = X[NA * k + i];
@@ -410,6 +410,36 @@ static void linearise(const prob_t *P, work_t *W) {
 }
 
 /* prm = [Q(8), Qt(8), R(4), u_lo, u_hi];  acc_tol / acc_iter: IPOPT acceptable_tol / acceptable_iter (0 = off) */
+/* filter line-search acceptance of a trial (th_t, ph_t) for the step size alpha (IPOPT
+   FilterLSAcceptor::CheckAcceptabilityOfTrialPoint with alpha_primal_test = alpha); *ftype is set
+   when the Armijo (f-type) condition accepted it */
+static int filter_accept(const work_t *W, int nfilt, double th_t, double ph_t, double th, double phi, double gTd,
+                         double alpha, double th_max, double th_min, int *ftype) {
+    const double gam_th = 1e-5, gam_ph = 1e-8, sw_delta = 1.0, s_th = 1.1, s_ph = 2.3, eta_ph = 1e-8;
+    if (!(th_t < th_max) || !isfinite(ph_t)) return 0;
+    for (int q = 0; q < nfilt; ++q) if (th_t >= W->filt_th[q] && ph_t >= W->filt_ph[q]) return 0;
+    const int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
+    if (th <= th_min && sw) {
+        if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { *ftype = 1; return 1; }
+        return 0;
+    }
+    return LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi);
+}
+
+/* bound-multiplier directions of the primal step dU (the complementarity rows of the KKT system)
+   and their fraction-to-the-boundary step */
+static double bound_dual_step(const ctx_t *C, work_t *W, int nU, double tau) {
+    double az = 1.0;
+    for (int j = 0; j < nU; ++j) {
+        double sl = W->U[j] - C->lo, su = C->hi - W->U[j], du = W->dU[j];
+        W->dzL[j] = C->mu / sl - W->zL[j] - W->zL[j] / sl * du;
+        W->dzU[j] = C->mu / su - W->zU[j] + W->zU[j] / su * du;
+        if (W->dzL[j] < 0) az = fmin(az, -tau * W->zL[j] / W->dzL[j]);
+        if (W->dzU[j] < 0) az = fmin(az, -tau * W->zU[j] / W->dzU[j]);
+    }
+    return az;
+}
+
 int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_prev, const double *pvec,
                       const double *target, const double *prm, const double *w_init, int max_iter, double tol,
                       double acc_tol, int acc_iter, double *u0, double *fval, double *w_out, int32_t *iters_out) {
@@ -424,7 +454,7 @@ int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_pre
     unpack_params(pvec, &P.M);
     const double lo = P.ulo - g_relax * fmax(1.0, fabs(P.ulo)), hi = P.uhi + g_relax * fmax(1.0, fabs(P.uhi));
     const double mu_min = tol / 10, kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, s_max = 100.0;
-    const double gam_th = 1e-5, gam_ph = 1e-8, sw_delta = 1.0, s_th = 1.1, s_ph = 2.3, eta_ph = 1e-8, gam_al = 0.05, kap_soc = 0.99;
+    const double gam_th = 1e-5, gam_ph = 1e-8, sw_delta = 1.0, s_th = 1.1, s_ph = 2.3, gam_al = 0.05, kap_soc = 0.99;
     const int nU = NU * N, nA = NA * (N + 1);
     ctx_t C;
     memset(&C, 0, sizeof C);
@@ -531,14 +561,7 @@ int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_pre
         if (!ok) { status = ST_INERTIA_FAIL; break; }
         if (delta > 0) delta_last = delta;
         riccati_solve(&C, W, g);
-        double az = 1.0;
-        for (int j = 0; j < nU; ++j) {
-            double sl = W->U[j] - lo, su = hi - W->U[j], du = W->dU[j];
-            W->dzL[j] = C.mu / sl - W->zL[j] - W->zL[j] / sl * du;
-            W->dzU[j] = C.mu / su - W->zU[j] + W->zU[j] / su * du;
-            if (W->dzL[j] < 0) az = fmin(az, -tau * W->zL[j] / W->dzL[j]);
-            if (W->dzU[j] < 0) az = fmin(az, -tau * W->zU[j] / W->dzU[j]);
-        }
+        double az = bound_dual_step(&C, W, nU, tau);
         double amax = frac_to_boundary(&C, W, W->dU, tau);
         const double phi = barrier_obj(&C, W->X, W->U);
         double gTd = 0.0;
@@ -571,40 +594,38 @@ int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_pre
             th_t = residuals(&C, W, W->Xt, W->Ut, gt);
             ph_t = barrier_obj(&C, W->Xt, W->Ut);
             if (tiny) { accepted = 1; ftype = 1; break; }
-            for (int pass = 0; pass < 5; ++pass) {
-                int in_f = !(th_t < th_max) || !isfinite(ph_t);
-                for (int q = 0; q < nfilt && !in_f; ++q) if (th_t >= W->filt_th[q] && ph_t >= W->filt_ph[q]) in_f = 1;
-                if (!in_f) {
-                    int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
-                    if (th <= th_min && sw) { if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { accepted = 1; ftype = 1; } }
-                    else if (LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi)) accepted = 1;
-                }
-                if (accepted || ls > 0 || th_t < th || !g_soc) break;
-                if (pass == 0) { for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] = alpha * g[k][i] + gt[k][i]; }
-                else { for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] += gt[k][i]; }
-                /* SOC direction with the current factorisation */
+            accepted = filter_accept(W, nfilt, th_t, ph_t, th, phi, gTd, alpha, th_max, th_min, &ftype);
+            if (!accepted && ls == 0 && !(th_t < th) && g_max_soc > 0) {
+                /* IPOPT FilterLSAcceptor::TrySecondOrderCorrection: c_soc <- a_soc c_soc + c(trial),
+                   starting from c(x) with a_soc = alpha; the corrected step re-uses the factorisation;
+                   at most max_soc passes, continued while theta(trial) <= kappa_soc theta(previous) */
                 double *sv = (double *)malloc(sizeof(double) * (2 * nA + nU));
                 memcpy(sv, W->dX, sizeof(double) * nA); memcpy(sv + nA, W->lamp, sizeof(double) * nA);
                 memcpy(sv + 2 * nA, W->dU, sizeof(double) * nU);
-                riccati_solve(&C, W, csg);
-                double asoc = frac_to_boundary(&C, W, W->dU, tau);
-                for (int i = 0; i < nA; ++i) W->Xt[i] = W->X[i] + asoc * W->dX[i];
-                for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + asoc * W->dU[j];
-                double th_prev = th_t;
-                th_t = residuals(&C, W, W->Xt, W->Ut, gt);
-                ph_t = barrier_obj(&C, W->Xt, W->Ut);
-                int inf = !(th_t < th_max) || !isfinite(ph_t), acc = 0;
-                for (int q = 0; q < nfilt && !inf; ++q) if (th_t >= W->filt_th[q] && ph_t >= W->filt_ph[q]) inf = 1;
-                if (!inf) {
-                    int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
-                    if (th <= th_min && sw) { if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { acc = 1; ftype = 1; } }
-                    else if (LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi)) acc = 1;
+                double asoc = alpha, th_old = 0.0;
+                for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] = g[k][i];
+                for (int c = 0; c < g_max_soc; ++c) {
+                    if (c > 0 && !(th_t <= kap_soc * th_old)) break;
+                    th_old = th_t;
+                    for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] = asoc * csg[k][i] + gt[k][i];
+                    riccati_solve(&C, W, csg);
+                    asoc = frac_to_boundary(&C, W, W->dU, tau);
+                    for (int i = 0; i < nA; ++i) W->Xt[i] = W->X[i] + asoc * W->dX[i];
+                    for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + asoc * W->dU[j];
+                    th_t = residuals(&C, W, W->Xt, W->Ut, gt);
+                    ph_t = barrier_obj(&C, W->Xt, W->Ut);
+                    if (filter_accept(W, nfilt, th_t, ph_t, th, phi, gTd, alpha, th_max, th_min, &ftype)) {
+                        /* IPOPT takes the SOC solve as the whole step: its bound-multiplier
+                           directions and their fraction to the boundary follow the corrected dU */
+                        accepted = 1; alpha = asoc; az = bound_dual_step(&C, W, nU, tau);
+                        break;
+                    }
                 }
-                if (acc) { accepted = 1; alpha = asoc; free(sv); break; }
-                memcpy(W->dX, sv, sizeof(double) * nA); memcpy(W->lamp, sv + nA, sizeof(double) * nA);
-                memcpy(W->dU, sv + 2 * nA, sizeof(double) * nU);
+                if (!accepted) {    /* back to the plain direction */
+                    memcpy(W->dX, sv, sizeof(double) * nA); memcpy(W->lamp, sv + nA, sizeof(double) * nA);
+                    memcpy(W->dU, sv + 2 * nA, sizeof(double) * nU);
+                }
                 free(sv);
-                if (th_t > kap_soc * th_prev) break;
             }
             if (!accepted) alpha *= 0.5;
         }

@@ -19,6 +19,15 @@ _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int32)
 
 
+def _max_soc(soc):
+    """IPOPT max_soc from the ``soc`` argument: True = IPOPT's default 4, False = off, or a count."""
+    if soc is True:
+        return 4
+    if soc is False or soc is None:
+        return 0
+    return max(0, int(soc))
+
+
 def build():
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
 
@@ -54,7 +63,7 @@ def solve_batch(states, targets, params, N=20, Ts=0.002, max_iter=200, tol=1e-9,
     w = np.zeros((B, nw)) if want_w else None
     st = np.zeros(B, np.int32)
     it = np.zeros(B, np.int32)
-    lib().oracle_pmpc_set_soc(int(bool(soc)))
+    lib().oracle_pmpc_set_soc(_max_soc(soc))
     lib().oracle_pmpc_solve_batch(B, N, Ts, _p(states), _p(targets), _p(params), max_iter, tol, nthreads,
                                   _p(u0), _p(f), _p(w) if want_w else None, _p(st, _ip), _p(it, _ip))
     return dict(u0=u0, f=f, w=w, status=st, iters=it)
@@ -103,7 +112,7 @@ def rmpc_solve_batch(x0, u_prev, theta, Rref, prm, N=20, Ts=0.002, w_init=None, 
     u0 = np.zeros((B, 2)); f = np.zeros(B); w = np.zeros((B, nw)) if want_w else None
     st = np.zeros(B, np.int32); it = np.zeros(B, np.int32)
     rlib().oracle_rmpc_set_relax(float(relax))
-    rlib().oracle_rmpc_set_soc(int(bool(soc)))
+    rlib().oracle_rmpc_set_soc(_max_soc(soc))
     rlib().oracle_rmpc_solve_batch(B, N, Ts, _p(x0), _p(u_prev), _p(theta), _p(Rref), _p(prm),
                                    _p(wi) if wi is not None else None, max_iter, tol, nthreads,
                                    _p(u0), _p(f), _p(w) if want_w else None, _p(st, _ip), _p(it, _ip))
@@ -156,7 +165,7 @@ def lmpc_solve_batch(state, u_prev, pvec, target, prm=None, N=20, Ts=0.002, w_in
     u0 = np.zeros((B, 2)); f = np.zeros(B); w = np.zeros((B, nw)) if want_w else None
     st = np.zeros(B, np.int32); it = np.zeros(B, np.int32)
     llib().oracle_lmpc_set_relax(float(relax))
-    llib().oracle_lmpc_set_soc(int(bool(soc)))
+    llib().oracle_lmpc_set_soc(_max_soc(soc))
     llib().oracle_lmpc_solve_batch(B, N, Ts, _p(state), _p(u_prev), _p(pvec), _p(target), _p(prm),
                                    _p(wi) if wi is not None else None, max_iter, tol, acc_tol, acc_iter, nthreads,
                                    _p(u0), _p(f), _p(w) if want_w else None, _p(st, _ip), _p(it, _ip))

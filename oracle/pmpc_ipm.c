@@ -40,8 +40,8 @@
 #define LE(l, r, b) ((l) - (r) <= 10.0 * 2.220446049250313e-16 * fabs(b))
 
 /* second-order correction on/off (IPOPT default on; the GPU kernel mirrors the off path) */
-static int g_soc = 1;
-void oracle_pmpc_set_soc(int on) { g_soc = on; }
+static int g_max_soc = 4;      /* IPOPT max_soc (second-order corrections per line search) */
+void oracle_pmpc_set_soc(int max_soc) { g_max_soc = max_soc < 0 ? 0 : max_soc; }
 #ifdef ORACLE_DEBUG
 #include <stdio.h>
 #endif
@@ -305,6 +305,36 @@ static double frac_to_boundary(const ctx_t *C, const work_t *W, const double *dU
     return a;
 }
 
+/* filter line-search acceptance of a trial (th_t, ph_t) for the step size alpha (IPOPT
+   FilterLSAcceptor::CheckAcceptabilityOfTrialPoint with alpha_primal_test = alpha); *ftype is set
+   when the Armijo (f-type) condition accepted it */
+static int filter_accept(const work_t *W, int nfilt, double th_t, double ph_t, double th, double phi, double gTd,
+                         double alpha, double th_max, double th_min, int *ftype) {
+    const double gam_th = 1e-5, gam_ph = 1e-8, sw_delta = 1.0, s_th = 1.1, s_ph = 2.3, eta_ph = 1e-8;
+    if (!(th_t < th_max) || !isfinite(ph_t)) return 0;
+    for (int q = 0; q < nfilt; ++q) if (th_t >= W->filt_th[q] && ph_t >= W->filt_ph[q]) return 0;
+    const int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
+    if (th <= th_min && sw) {
+        if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { *ftype = 1; return 1; }
+        return 0;
+    }
+    return LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi);
+}
+
+/* bound-multiplier directions of the primal step dU (the complementarity rows of the KKT system)
+   and their fraction-to-the-boundary step */
+static double bound_dual_step(const ctx_t *C, work_t *W, int nU, double tau) {
+    double az = 1.0;
+    for (int j = 0; j < nU; ++j) {
+        double sl = W->U[j] - C->lo, su = C->hi - W->U[j], du = W->dU[j];
+        W->dzL[j] = C->mu / sl - W->zL[j] - W->zL[j] / sl * du;
+        W->dzU[j] = C->mu / su - W->zU[j] + W->zU[j] / su * du;
+        if (W->dzL[j] < 0) az = fmin(az, -tau * W->zL[j] / W->dzL[j]);
+        if (W->dzU[j] < 0) az = fmin(az, -tau * W->zU[j] / W->dzU[j]);
+    }
+    return az;
+}
+
 int oracle_pmpc_solve(int N, double Ts, const double *state, const double *target, const double *prm,
                       const double *w_init, int max_iter, double tol,
                       double *u0, double *fval, double *w_out, int32_t *iters_out) {
@@ -316,7 +346,7 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
     const double lo = P.ulo - 1e-8 * fmax(1.0, fabs(P.ulo)), hi = P.uhi + 1e-8 * fmax(1.0, fabs(P.uhi));
     const double mu_min = tol / 10, kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, s_max = 100.0;
     /* filter line-search constants (IPOPT defaults) */
-    const double gam_th = 1e-5, gam_ph = 1e-8, sw_delta = 1.0, s_th = 1.1, s_ph = 2.3, eta_ph = 1e-8, gam_al = 0.05, kap_soc = 0.99;
+    const double gam_th = 1e-5, gam_ph = 1e-8, sw_delta = 1.0, s_th = 1.1, s_ph = 2.3, gam_al = 0.05, kap_soc = 0.99;
     const int nU = NU * N, ng = NX * (N + 1);
 
     /* initial point: cold start (mpc_3d.py:123) or caller warm start; bound push kappa_1 = kappa_2 = 1e-2 */
@@ -395,14 +425,7 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
         if (delta > 0) delta_last = delta;
         riccati_solve(&C, W, g);
 
-        double amax = frac_to_boundary(&C, W, W->dU, tau), az = 1.0;
-        for (int j = 0; j < nU; ++j) {
-            double sl = W->U[j] - lo, su = hi - W->U[j], du = W->dU[j];
-            W->dzL[j] = C.mu / sl - W->zL[j] - W->zL[j] / sl * du;
-            W->dzU[j] = C.mu / su - W->zU[j] + W->zU[j] / su * du;
-            if (W->dzL[j] < 0) az = fmin(az, -tau * W->zL[j] / W->dzL[j]);
-            if (W->dzU[j] < 0) az = fmin(az, -tau * W->zU[j] / W->dzU[j]);
-        }
+        double amax = frac_to_boundary(&C, W, W->dU, tau), az = bound_dual_step(&C, W, nU, tau);
         /* ---- filter line search with second-order correction (W&B 2006, Alg. A) */
         const double phi = barrier_obj(&C, W->X, W->U);
         double gTd = 0.0;
@@ -430,40 +453,35 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
             th_t = constraints(&C, W->Xt, W->Ut, W->gt);
             ph_t = barrier_obj(&C, W->Xt, W->Ut);
             if (tiny) { accepted = 1; ftype = 1; break; }
-            for (int pass = 0; pass < 5; ++pass) {        /* pass 0: plain trial; 1..4: SOC */
-                int in_filter = !(th_t < th_max) || !isfinite(ph_t);
-                for (int q = 0; q < nfilt && !in_filter; ++q) if (th_t >= W->filt_th[q] && ph_t >= W->filt_ph[q]) in_filter = 1;
-                if (!in_filter) {
-                    int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
-                    if (th <= th_min && sw) { if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { accepted = 1; ftype = 1; } }
-                    else if (LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi)) accepted = 1;
-                }
-                if (accepted || ls > 0 || th_t < th || !g_soc) break;
-                /* second-order correction: c_soc <- a c_soc + g(trial); solve; re-try */
-                if (pass == 0) { for (int k = 0; k <= N; ++k) for (int i = 0; i < NX; ++i) W->csoc[k][i] = alpha * g[k][i] + W->gt[k][i]; }
-                else {
-                    for (int k = 0; k <= N; ++k) for (int i = 0; i < NX; ++i) W->csoc[k][i] = W->csoc[k][i] + W->gt[k][i];
-                }
+            accepted = filter_accept(W, nfilt, th_t, ph_t, th, phi, gTd, alpha, th_max, th_min, &ftype);
+            if (!accepted && ls == 0 && !(th_t < th) && g_max_soc > 0) {
+                /* IPOPT FilterLSAcceptor::TrySecondOrderCorrection: c_soc <- a_soc c_soc + c(trial),
+                   starting from c(x) with a_soc = alpha; the corrected step re-uses the factorisation;
+                   at most max_soc passes, continued while theta(trial) <= kappa_soc theta(previous) */
                 double save_dU[NU * NMAX], save_dX[NX * (NMAX + 1)], save_lp[NX * (NMAX + 1)];
                 memcpy(save_dU, W->dU, sizeof(double) * nU); memcpy(save_dX, W->dX, sizeof(double) * ng); memcpy(save_lp, W->lamp, sizeof(double) * ng);
-                riccati_solve(&C, W, W->csoc);
-                double asoc = frac_to_boundary(&C, W, W->dU, tau);
-                for (int i = 0; i < ng; ++i) W->Xt[i] = W->X[i] + asoc * W->dX[i];
-                for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + asoc * W->dU[j];
-                double th_prev = th_t;
-                th_t = constraints(&C, W->Xt, W->Ut, W->gt);
-                ph_t = barrier_obj(&C, W->Xt, W->Ut);
-                int inf = !(th_t < th_max) || !isfinite(ph_t);
-                for (int q = 0; q < nfilt && !inf; ++q) if (th_t >= W->filt_th[q] && ph_t >= W->filt_ph[q]) inf = 1;
-                int acc = 0;
-                if (!inf) {
-                    int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
-                    if (th <= th_min && sw) { if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { acc = 1; ftype = 1; } }
-                    else if (LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi)) acc = 1;
+                double asoc = alpha, th_old = 0.0;
+                for (int k = 0; k <= N; ++k) for (int i = 0; i < NX; ++i) W->csoc[k][i] = g[k][i];
+                for (int c = 0; c < g_max_soc; ++c) {
+                    if (c > 0 && !(th_t <= kap_soc * th_old)) break;
+                    th_old = th_t;
+                    for (int k = 0; k <= N; ++k) for (int i = 0; i < NX; ++i) W->csoc[k][i] = asoc * W->csoc[k][i] + W->gt[k][i];
+                    riccati_solve(&C, W, W->csoc);
+                    asoc = frac_to_boundary(&C, W, W->dU, tau);
+                    for (int i = 0; i < ng; ++i) W->Xt[i] = W->X[i] + asoc * W->dX[i];
+                    for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + asoc * W->dU[j];
+                    th_t = constraints(&C, W->Xt, W->Ut, W->gt);
+                    ph_t = barrier_obj(&C, W->Xt, W->Ut);
+                    if (filter_accept(W, nfilt, th_t, ph_t, th, phi, gTd, alpha, th_max, th_min, &ftype)) {
+                        /* IPOPT takes the SOC solve as the whole step: its bound-multiplier
+                           directions and their fraction to the boundary follow the corrected dU */
+                        accepted = 1; used_soc = 1; alpha = asoc; az = bound_dual_step(&C, W, nU, tau);
+                        break;
+                    }
                 }
-                if (acc) { accepted = 1; used_soc = 1; alpha = asoc; break; }
-                memcpy(W->dU, save_dU, sizeof(double) * nU); memcpy(W->dX, save_dX, sizeof(double) * ng); memcpy(W->lamp, save_lp, sizeof(double) * ng);
-                if (th_t > kap_soc * th_prev) break;
+                if (!accepted) {    /* back to the plain direction */
+                    memcpy(W->dU, save_dU, sizeof(double) * nU); memcpy(W->dX, save_dX, sizeof(double) * ng); memcpy(W->lamp, save_lp, sizeof(double) * ng);
+                }
             }
             if (!accepted) {
                 alpha *= 0.5;

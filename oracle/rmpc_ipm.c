@@ -164,8 +164,8 @@ enum { ST_SOLVED = 0, ST_MAXITER = -1, ST_LS_FAIL = -2, ST_INERTIA_FAIL = -3, ST
 static double g_relax = 1e-8;
 void oracle_rmpc_set_relax(double r) { g_relax = r; }
 /* second-order correction on/off (IPOPT default on; off mirrors the GPU kernel's line search) */
-static int g_soc = 1;
-void oracle_rmpc_set_soc(int on) { g_soc = on; }
+static int g_max_soc = 4;      /* IPOPT max_soc (second-order corrections per line search) */
+void oracle_rmpc_set_soc(int max_soc) { g_max_soc = max_soc < 0 ? 0 : max_soc; }
 
 static void stage_z(const double *X, const double *U, int k, double *z) {
     for (int i = 0; i < NA; ++i) z[i] = X[NA * k + i];
@@ -383,6 +383,50 @@ static double frac_to_boundary(const ctx_t *C, const work_t *W, const double *dU
     return a;
 }
 
+/* filter line-search acceptance of a trial (th_t, ph_t) for the step size alpha (IPOPT
+   FilterLSAcceptor::CheckAcceptabilityOfTrialPoint with alpha_primal_test = alpha); *ftype is set
+   when the Armijo (f-type) condition accepted it */
+static int filter_accept(const work_t *W, int nfilt, double th_t, double ph_t, double th, double phi, double gTd,
+                         double alpha, double th_max, double th_min, int *ftype) {
+    const double gam_th = 1e-5, gam_ph = 1e-8, sw_delta = 1.0, s_th = 1.1, s_ph = 2.3, eta_ph = 1e-8;
+    if (!(th_t < th_max) || !isfinite(ph_t)) return 0;
+    for (int q = 0; q < nfilt; ++q) if (th_t >= W->filt_th[q] && ph_t >= W->filt_ph[q]) return 0;
+    const int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
+    if (th <= th_min && sw) {
+        if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { *ftype = 1; return 1; }
+        return 0;
+    }
+    return LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi);
+}
+
+/* dual directions of the primal step (dU, dS): box multipliers, slack-row multipliers y from
+   the eliminated system, slack-bound multipliers; returns their fraction-to-the-boundary step */
+static double dual_steps(const ctx_t *C, work_t *W, int nU, double tau) {
+    double az = 1.0;
+    for (int j = 0; j < nU; ++j) {
+        double sl = W->U[j] - C->lo, su = C->hi - W->U[j], du = W->dU[j];
+        W->dzL[j] = C->mu / sl - W->zL[j] - W->zL[j] / sl * du;
+        W->dzU[j] = C->mu / su - W->zU[j] + W->zU[j] / su * du;
+        if (W->dzL[j] < 0) az = fmin(az, -tau * W->zL[j] / W->dzL[j]);
+        if (W->dzU[j] < 0) az = fmin(az, -tau * W->zU[j] / W->dzU[j]);
+    }
+    for (int k = 0; k < C->P->N; ++k) for (int i = 0; i < NIQ; ++i) {
+        double s = W->S[k][i], ds = W->dS[k][i], sig, psi;
+        slack_terms(C, W, k, i, &sig, &psi);
+        /* dy from the eliminated system: y + dy = Sigma*ds + psi' with psi' = -mu/(s-sL)+mu/(sU-s) */
+        W->dy[k][i] = sig * ds + psi - W->y[k][i];
+        if (C->sL[i] > -1e299) {
+            double d = s - C->sL[i];
+            W->dvL[k][i] = C->mu / d - W->vL[k][i] - W->vL[k][i] / d * ds;
+            if (W->dvL[k][i] < 0) az = fmin(az, -tau * W->vL[k][i] / W->dvL[k][i]);
+        } else W->dvL[k][i] = 0.0;
+        double d = C->sU[i] - s;
+        W->dvU[k][i] = C->mu / d - W->vU[k][i] + W->vU[k][i] / d * ds;
+        if (W->dvU[k][i] < 0) az = fmin(az, -tau * W->vU[k][i] / W->dvU[k][i]);
+    }
+    return az;
+}
+
 int oracle_rmpc_solve(int N, double Ts, const double *x0, const double *u_prev, const double *theta,
                       const double *Rref, const double *prm, const double *w_init, int max_iter, double tol,
                       double *u0, double *fval, double *w_out, int32_t *iters_out) {
@@ -394,7 +438,7 @@ int oracle_rmpc_solve(int N, double Ts, const double *x0, const double *u_prev, 
     memcpy(P.th, theta, sizeof(double) * 14);
     const double lo = P.ulo - g_relax * fmax(1.0, fabs(P.ulo)), hi = P.uhi + g_relax * fmax(1.0, fabs(P.uhi));
     const double mu_min = tol / 10, kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, s_max = 100.0;
-    const double gam_th = 1e-5, gam_ph = 1e-8, sw_delta = 1.0, s_th = 1.1, s_ph = 2.3, eta_ph = 1e-8, gam_al = 0.05, kap_soc = 0.99;
+    const double gam_th = 1e-5, gam_ph = 1e-8, sw_delta = 1.0, s_th = 1.1, s_ph = 2.3, gam_al = 0.05, kap_soc = 0.99;
     const int nU = NU * N, nA = NA * (N + 1), nI = NIQ * N;
     ctx_t C;
     memset(&C, 0, sizeof C);
@@ -524,29 +568,7 @@ int oracle_rmpc_solve(int N, double Ts, const double *x0, const double *u_prev, 
         if (!ok) { status = ST_INERTIA_FAIL; break; }
         if (delta > 0) delta_last = delta;
         riccati_solve(&C, W, g, r);
-        /* dual steps: box, slack multipliers */
-        double az = 1.0;
-        for (int j = 0; j < nU; ++j) {
-            double sl = W->U[j] - lo, su = hi - W->U[j], du = W->dU[j];
-            W->dzL[j] = C.mu / sl - W->zL[j] - W->zL[j] / sl * du;
-            W->dzU[j] = C.mu / su - W->zU[j] + W->zU[j] / su * du;
-            if (W->dzL[j] < 0) az = fmin(az, -tau * W->zL[j] / W->dzL[j]);
-            if (W->dzU[j] < 0) az = fmin(az, -tau * W->zU[j] / W->dzU[j]);
-        }
-        for (int k = 0; k < N; ++k) for (int i = 0; i < NIQ; ++i) {
-            double s = W->S[k][i], ds = W->dS[k][i], sig, psi;
-            slack_terms(&C, W, k, i, &sig, &psi);
-            /* dy from the eliminated system: y + dy = Sigma*ds + psi' with psi' = -mu/(s-sL)+mu/(sU-s) */
-            W->dy[k][i] = sig * ds + psi - W->y[k][i];
-            if (C.sL[i] > -1e299) {
-                double d = s - C.sL[i];
-                W->dvL[k][i] = C.mu / d - W->vL[k][i] - W->vL[k][i] / d * ds;
-                if (W->dvL[k][i] < 0) az = fmin(az, -tau * W->vL[k][i] / W->dvL[k][i]);
-            } else W->dvL[k][i] = 0.0;
-            double d = C.sU[i] - s;
-            W->dvU[k][i] = C.mu / d - W->vU[k][i] + W->vU[k][i] / d * ds;
-            if (W->dvU[k][i] < 0) az = fmin(az, -tau * W->vU[k][i] / W->dvU[k][i]);
-        }
+        double az = dual_steps(&C, W, nU, tau);
         double amax = frac_to_boundary(&C, W, W->dU, W->dS, tau);
         /* filter line search with second-order correction */
         const double phi = barrier_obj(&C, W->X, W->U, W->S);
@@ -588,46 +610,41 @@ int oracle_rmpc_solve(int N, double Ts, const double *x0, const double *u_prev, 
             th_t = residuals(&C, W->Xt, W->Ut, W->St, gt, rt);
             ph_t = barrier_obj(&C, W->Xt, W->Ut, W->St);
             if (tiny) { accepted = 1; ftype = 1; break; }
-            for (int pass = 0; pass < 5; ++pass) {
-                int in_f = !(th_t < th_max) || !isfinite(ph_t);
-                for (int q = 0; q < nfilt && !in_f; ++q) if (th_t >= W->filt_th[q] && ph_t >= W->filt_ph[q]) in_f = 1;
-                if (!in_f) {
-                    int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
-                    if (th <= th_min && sw) { if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { accepted = 1; ftype = 1; } }
-                    else if (LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi)) accepted = 1;
-                }
-                if (accepted || ls > 0 || th_t < th || !g_soc) break;
-                if (pass == 0) {
-                    for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] = alpha * g[k][i] + gt[k][i];
-                    for (int k = 0; k < N; ++k) for (int i = 0; i < NIQ; ++i) csr[k][i] = alpha * r[k][i] + rt[k][i];
-                } else {
-                    for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] += gt[k][i];
-                    for (int k = 0; k < N; ++k) for (int i = 0; i < NIQ; ++i) csr[k][i] += rt[k][i];
-                }
-                /* SOC direction with the current factorisation (dual RHS unchanged) */
+            accepted = filter_accept(W, nfilt, th_t, ph_t, th, phi, gTd, alpha, th_max, th_min, &ftype);
+            if (!accepted && ls == 0 && !(th_t < th) && g_max_soc > 0) {
+                /* IPOPT FilterLSAcceptor::TrySecondOrderCorrection: c_soc <- a_soc c_soc + c(trial)
+                   (defects and slack rows d(x) - s), starting from c(x) with a_soc = alpha; the
+                   corrected step re-uses the factorisation (dual RHS unchanged); at most max_soc
+                   passes, continued while theta(trial) <= kappa_soc theta(previous) */
                 work_t *Sv = (work_t *)malloc(sizeof(work_t));
                 memcpy(Sv, W, sizeof(work_t));
-                riccati_solve(&C, W, csg, csr);
-                double asoc = frac_to_boundary(&C, W, W->dU, W->dS, tau);
-                for (int i = 0; i < nA; ++i) W->Xt[i] = W->X[i] + asoc * W->dX[i];
-                for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + asoc * W->dU[j];
-                for (int k = 0; k < N; ++k) for (int i = 0; i < NIQ; ++i) W->St[k][i] = W->S[k][i] + asoc * W->dS[k][i];
-                double th_prev = th_t;
-                th_t = residuals(&C, W->Xt, W->Ut, W->St, gt, rt);
-                ph_t = barrier_obj(&C, W->Xt, W->Ut, W->St);
-                int inf = !(th_t < th_max) || !isfinite(ph_t), acc = 0;
-                for (int q = 0; q < nfilt && !inf; ++q) if (th_t >= W->filt_th[q] && ph_t >= W->filt_ph[q]) inf = 1;
-                if (!inf) {
-                    int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > sw_delta * pow(th, s_th);
-                    if (th <= th_min && sw) { if (LE(ph_t, phi + eta_ph * alpha * gTd, phi)) { acc = 1; ftype = 1; } }
-                    else if (LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi)) acc = 1;
+                double asoc = alpha, th_old = 0.0;
+                for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] = g[k][i];
+                for (int k = 0; k < N; ++k) for (int i = 0; i < NIQ; ++i) csr[k][i] = r[k][i];
+                for (int c = 0; c < g_max_soc; ++c) {
+                    if (c > 0 && !(th_t <= kap_soc * th_old)) break;
+                    th_old = th_t;
+                    for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] = asoc * csg[k][i] + gt[k][i];
+                    for (int k = 0; k < N; ++k) for (int i = 0; i < NIQ; ++i) csr[k][i] = asoc * csr[k][i] + rt[k][i];
+                    riccati_solve(&C, W, csg, csr);
+                    asoc = frac_to_boundary(&C, W, W->dU, W->dS, tau);
+                    for (int i = 0; i < nA; ++i) W->Xt[i] = W->X[i] + asoc * W->dX[i];
+                    for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + asoc * W->dU[j];
+                    for (int k = 0; k < N; ++k) for (int i = 0; i < NIQ; ++i) W->St[k][i] = W->S[k][i] + asoc * W->dS[k][i];
+                    th_t = residuals(&C, W->Xt, W->Ut, W->St, gt, rt);
+                    ph_t = barrier_obj(&C, W->Xt, W->Ut, W->St);
+                    if (filter_accept(W, nfilt, th_t, ph_t, th, phi, gTd, alpha, th_max, th_min, &ftype)) {
+                        /* IPOPT takes the SOC solve as the whole step: the slack-row multipliers, the
+                           bound-multiplier directions and their fraction to the boundary follow it */
+                        accepted = 1; alpha = asoc; az = dual_steps(&C, W, nU, tau);
+                        break;
+                    }
                 }
-                if (acc) { accepted = 1; alpha = asoc; free(Sv); break; }
-                /* restore the original direction */
-                memcpy(W->dX, Sv->dX, sizeof W->dX); memcpy(W->dU, Sv->dU, sizeof W->dU);
-                memcpy(W->lamp, Sv->lamp, sizeof W->lamp); memcpy(W->dS, Sv->dS, sizeof W->dS);
+                if (!accepted) {    /* back to the plain direction */
+                    memcpy(W->dX, Sv->dX, sizeof W->dX); memcpy(W->dU, Sv->dU, sizeof W->dU);
+                    memcpy(W->lamp, Sv->lamp, sizeof W->lamp); memcpy(W->dS, Sv->dS, sizeof W->dS);
+                }
                 free(Sv);
-                if (th_t > kap_soc * th_prev) break;
             }
             if (!accepted) alpha *= 0.5;
         }

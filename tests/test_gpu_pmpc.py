@@ -113,6 +113,25 @@ def test_c2_and_c4_batches_match_oracle(dm):
             np.testing.assert_allclose(out["f"], ref["f"], rtol=1e-7, atol=1e-9)
 
 
+def test_scan_and_sequential_riccati_agree(dm):
+    """The launcher runs the quadratic Riccati part as a DPP scan for B <= 1024 and as the sequential
+    sweep beyond (throughput regime).  The same 1152 instances solved as one launch of 2304 (sequential;
+    every instance twice) and as 64 launches of 18 (scan) take the same iterations and agree to 1e-9."""
+    from dart_mpc.workload import pmpc_batch
+    S, T, P = pmpc_batch(64)
+    s = dm.Solver(N=20, Ts=0.002, tol=1e-8, B_max=2 * S.shape[0])
+    big = s.solve_batch(np.concatenate([S, S]), np.concatenate([T, T]), np.concatenate([P, P]))
+    small = [s.solve_batch(S[i:i + 18], T[i:i + 18], P[i:i + 18]) for i in range(0, S.shape[0], 18)]
+    s.close()
+    u_small = np.concatenate([o["u0"] for o in small])
+    it_small = np.concatenate([o["iters"] for o in small])
+    B = S.shape[0]
+    np.testing.assert_array_equal(big["status"], 0)
+    np.testing.assert_array_equal(big["iters"][:B], big["iters"][B:])
+    assert np.mean(big["iters"][:B] == it_small) >= 0.99
+    assert np.max(np.abs(big["u0"][:B] - u_small)) <= 1e-9
+
+
 def test_symmetry_and_rest_properties(dm):
     """Size-independent properties (SURVEY §8c KATs): u*(mirrored) = -u*, u* = 0 at rest on target."""
     from dart_mpc.workload import pmpc_batch

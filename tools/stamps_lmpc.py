@@ -32,5 +32,5 @@ for i, n in enumerate(PHASES):
     print(f"  {n:15s} {int(st[i]):10d}  {100 * st[i] / tot:5.1f}%  per-iter {st[i] / it:9.0f}")
 for i, n in zip((11, 12, 13, 14), ("closed loop", "forward sweep", "eval: rk4+adjoint", "eval: directions")):
     print(f"  {n:15s} {int(st[i]):10d}  {100 * st[i] / tot:5.1f}%  per-iter {st[i] / it:9.0f}")
-print(f"  riccati passes {int(st[9])}, line-search trials {int(st[10])}")
+print(f"  riccati passes {int(st[9])}, line-search trials {int(st[10])}, second-order corrections {int(st[15])}")
 print("batch iters:", out["iters"].tolist())
