@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--rmpc-steps", type=int, default=200, help="launches of the supplementary C3 RMPC line (0 = skip)")
     ap.add_argument("--lmpc-steps", type=int, default=100, help="launches of the supplementary C5 LMPC line (0 = skip)")
     ap.add_argument("--arm-steps", type=int, default=200, help="launches of the supplementary arm-QP line (0 = skip)")
+    ap.add_argument("--c4-steps", type=int, default=50,
+                    help="steps of the supplementary C4 line (1152 instances sharded over the ranks + gather; 0 = skip)")
     ap.add_argument("--saturation-batch", type=int, default=18 * 1024,
                     help="supplementary single-launch batch for the saturated rate (0 = skip)")
     return ap.parse_args()
@@ -125,6 +127,75 @@ def bench_rmpc(args, torch, dev, stream, dart_mpc):
                                "sample": f"C oracle (oracle/rmpc_ipm.c), {solved} cold-start C3 solves in {cdt:.1f} s"}
     s.close()
     return out
+
+
+def bench_c4(args, torch, dev, stream, dart_mpc, world, rank):
+    """C4 (BASELINE.json configs[3]): PMPC 18 configs x 64 seeds = 1152 instances, N=20, sharded over the
+    ranks in contiguous blocks (dart_mpc.parallel.shard_bounds).  One step = every rank solves its block,
+    packs [u0, f, status] and joins one all_gather_into_tensor (RCCL over xGMI) of the padded blocks.
+    The global batch is fixed as ranks are added (strong scaling); the gather is inside the timed region."""
+    import torch.distributed as dist
+    from dart_mpc.parallel import RESULT_COLS, shard_bounds
+    from dart_mpc.workload import pmpc_batch
+    Bg, K, N = 18 * 64, args.c4_steps, args.N
+    S, T, P = pmpc_batch(n_seeds=64, seed0=300000)
+    lo, hi = shard_bounds(Bg, world, rank)
+    per, n = -(-Bg // world), hi - lo
+    dt64 = torch.float64
+    X0 = torch.tensor(S[lo:hi], dtype=dt64, device=dev).contiguous()
+    RF = torch.tensor(T[lo:hi], dtype=dt64, device=dev).contiguous()
+    PR = torch.tensor(P[lo:hi], dtype=dt64, device=dev).contiguous()
+    U0 = torch.empty((n, 2), dtype=dt64, device=dev)
+    FV = torch.empty(n, dtype=dt64, device=dev)
+    ST = torch.empty(n, dtype=torch.int32, device=dev)
+    IT = torch.empty(n, dtype=torch.int32, device=dev)
+    block = torch.zeros((per, RESULT_COLS), dtype=dt64, device=dev)
+    full = torch.zeros((world * per, RESULT_COLS), dtype=dt64, device=dev)
+    solver = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=max(1, n), device=dev.index)
+    sp = stream.cuda_stream
+
+    def step():
+        solver.solve_batch_dev(n, X0.data_ptr(), RF.data_ptr(), PR.data_ptr(), U0.data_ptr(), FV.data_ptr(),
+                               ST.data_ptr(), IT.data_ptr(), stream=sp)
+        with torch.cuda.stream(stream):
+            block[:n, 0:2].copy_(U0)
+            block[:n, 2].copy_(FV)
+            block[:n, 3].copy_(ST)
+            if world > 1:
+                dist.all_gather_into_tensor(full, block)
+            else:
+                full.copy_(block)
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=dt64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t[0])
+    res = full.cpu().numpy()[:Bg]
+    solver.close()
+    if rank != 0:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_lib   # checker only
+    ref = oracle_lib.solve_batch(S[:36], T[:36], P[:36], N=N, Ts=0.002, tol=1e-11, nthreads=4, want_w=False)
+    return {"workload": "C4: PMPC 18 configs x 64 seeds = 1152 instances, N=20, tol 1e-8, cold start, contiguous "
+                        "blocks over the ranks + all_gather_into_tensor of [u0, f, status] (RCCL)",
+            "global_batch": Bg, "per_rank": per, "n_gpus": world, "scaling": "strong", "steps": K,
+            "solves_per_s": Bg * K / dt, "ms_per_step": dt / K * 1e3, "gather_in_timed_region": world > 1,
+            "status_ok_frac": float(np.mean(res[:, 3] == 0)),
+            "max_abs_u0_err_vs_exact_optimum_first36": float(np.max(np.abs(res[:36, 0:2] - ref["u0"])))}
 
 
 def bench_lmpc(args, torch, dev, stream, dart_mpc):
@@ -411,8 +482,21 @@ def main():
         for _ in range(args.host_calls):
             hs.solve_batch(S, T, P)
         hdt = (time.perf_counter() - h0) / args.host_calls
-        host_path = {"batch": B, "ms_per_call": hdt * 1e3, "solves_per_s": B / hdt}
+        # one instance per call: the latency PMPC.solve / mpc_worker sees per control step
+        for _ in range(5):
+            hs.solve_batch(S[:1], T[:1], P[:1])
+        h1 = time.perf_counter()
+        for _ in range(args.host_calls):
+            hs.solve_batch(S[:1], T[:1], P[:1])
+        h1dt = (time.perf_counter() - h1) / args.host_calls
+        host_path = {"batch": B, "ms_per_call": hdt * 1e3, "solves_per_s": B / hdt,
+                     "single_instance_ms_per_call": h1dt * 1e3,
+                     "note": "dart_mpc_solve_batch through the Python Solver: inputs packed into pinned memory, one "
+                             "DMA copy, outputs written by the kernel into mapped pinned memory, stream sync"}
         hs.close()
+
+    # supplementary C4 (BASELINE.json configs[3]): 1152 instances sharded over the ranks + result gather
+    c4 = bench_c4(args, torch, dev, stream, dart_mpc, world, rank) if args.c4_steps > 0 else None
 
     # supplementary C3 (BASELINE.json configs[2]): RMPC batch=18 with the RLS update fused into the launch
     rmpc = None
@@ -466,6 +550,7 @@ def main():
             "iters_mean": float(its.mean()),
             "saturation": saturation,
             "host_path_pcie_inclusive": host_path,
+            "pmpc_c4": c4,
             "rmpc_c3": rmpc,
             "lmpc_c5": lmpc,
             "arm_qp": arm,

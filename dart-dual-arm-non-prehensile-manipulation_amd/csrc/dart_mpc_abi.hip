@@ -7,6 +7,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "dart_mpc.h"
@@ -18,13 +19,123 @@
 
 #include <cmath>
 
+namespace {
+
+// Staging of the host-pointer entries.  The inputs (and the in/out arrays) are packed into pinned
+// host memory and reach HBM with ONE DMA copy; the kernel writes its outputs straight into mapped,
+// coherent pinned host memory (a few bytes per instance, no copy back); in/out arrays return with
+// one more DMA copy.  Against one pageable hipMemcpy per array this removes 5-10 copies per call.
+// Capacities grow on demand; a stage is not thread-safe (one per handle, one per device for the
+// stateless entries behind a mutex).
+struct HostStage {
+    char* hin = nullptr;            // pinned: packed inputs | in/out arrays
+    char* din = nullptr;            // device mirror of hin
+    char* hout = nullptr;           // pinned, mapped, coherent: kernel outputs
+    char* dout = nullptr;           // device address of hout
+    size_t in_cap = 0, out_cap = 0, in_off = 0, out_off = 0, io_first = 0;
+    struct Back { void* dst; size_t off, bytes; };
+    Back back[8];
+    int nback = 0;
+
+    static size_t al(size_t n) { return (n + 255) & ~size_t(255); }
+    hipError_t reserve(size_t in_bytes, size_t out_bytes) {
+        hipError_t e = hipSuccess;
+        if (in_bytes > in_cap) {
+            release_in();
+            e = hipHostMalloc((void**)&hin, in_bytes, hipHostMallocDefault);
+            if (e == hipSuccess) e = hipMalloc((void**)&din, in_bytes);
+            if (e != hipSuccess) { release_in(); return e; }
+            in_cap = in_bytes;
+        }
+        if (out_bytes > out_cap) {
+            release_out();
+            e = hipHostMalloc((void**)&hout, out_bytes, hipHostMallocMapped | hipHostMallocCoherent);
+            if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&dout, hout, 0);
+            if (e != hipSuccess) { release_out(); return e; }
+            out_cap = out_bytes;
+        }
+        return e;
+    }
+    void release_in() {
+        if (hin) (void)hipHostFree(hin);
+        if (din) (void)hipFree(din);
+        hin = din = nullptr; in_cap = 0;
+    }
+    void release_out() {
+        if (hout) (void)hipHostFree(hout);
+        hout = dout = nullptr; out_cap = 0;
+    }
+    void begin() { in_off = out_off = 0; nback = 0; io_first = 0; }
+    // device pointer of an input copied from src (n elements); nullptr stays nullptr
+    template <class T> const T* in(const T* src, size_t n) {
+        if (!src) return nullptr;
+        const size_t off = in_off;
+        std::memcpy(hin + off, src, n * sizeof(T));
+        in_off += al(n * sizeof(T));
+        return reinterpret_cast<const T*>(din + off);
+    }
+    // device pointer of an in/out array (read and updated by the kernel); call these last
+    template <class T> T* inout(T* src, size_t n) {
+        if (!src) return nullptr;
+        if (nback == 0) io_first = in_off;
+        const size_t off = in_off;
+        in(src, n);
+        back[nback++] = Back{src, off, n * sizeof(T)};
+        return reinterpret_cast<T*>(din + off);
+    }
+    // device-visible pointer of an output slot (n elements) in mapped host memory
+    template <class T> T* out(size_t n) {
+        const size_t off = out_off;
+        out_off += al(n * sizeof(T));
+        return reinterpret_cast<T*>(dout + off);
+    }
+    template <class T> const T* host_of(const T* dev_out) const {
+        return reinterpret_cast<const T*>(hout + (reinterpret_cast<const char*>(dev_out) - dout));
+    }
+    hipError_t upload(hipStream_t s) const {
+        return in_off ? hipMemcpyAsync(din, hin, in_off, hipMemcpyHostToDevice, s) : hipSuccess;
+    }
+    hipError_t download_inout(hipStream_t s) const {
+        return nback ? hipMemcpyAsync(hin + io_first, din + io_first, in_off - io_first, hipMemcpyDeviceToHost, s)
+                     : hipSuccess;
+    }
+    // after the stream synchronised: in/out arrays back to the caller, then outputs
+    void finish_inout() const {
+        for (int i = 0; i < nback; ++i) std::memcpy(back[i].dst, hin + back[i].off, back[i].bytes);
+    }
+    template <class T> void take(T* dst, const T* dev_out, size_t n) const {
+        if (dst && dev_out) std::memcpy(dst, host_of(dev_out), n * sizeof(T));
+    }
+    void release() { release_in(); release_out(); }
+};
+
+// stage + stream of the stateless host entries (arm QP, policy step, RLS), one per device
+struct DeviceStage {
+    std::mutex mu;
+    HostStage st;
+    hipStream_t stream = nullptr;
+};
+
+hipError_t device_stage(DeviceStage** out) {
+    static DeviceStage stages[64];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    DeviceStage& d = stages[dev];
+    std::lock_guard<std::mutex> g(d.mu);
+    if (!d.stream) e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking);
+    *out = &d;
+    return e;
+}
+
+}  // namespace
+
 struct dart_mpc_handle {
     dart_mpc_config cfg;
     int device = 0;
     hipStream_t stream = nullptr;
-    double* dbuf = nullptr;        // staged inputs/outputs for the host entry
-    int32_t* ibuf = nullptr;
-    size_t nd = 0, ni = 0;
+    HostStage st;                  // staging of the host-pointer entries
     std::string err;
 };
 
@@ -102,20 +213,23 @@ int dart_mpc_create(const dart_mpc_config* cfg, int device, dart_mpc_handle** ou
     h->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
-    const size_t B = (size_t)cfg->B_max;
+    // staging for B_max instances: inputs (+ in/out arrays) and outputs, 256-byte aligned per array
+    const size_t B = (size_t)cfg->B_max, A = 8 * 256;
+    size_t nin = 0, nout = 0;
     if (cfg->variant == DART_MPC_LMPC) {
         const size_t nw = (size_t)dart_lmpc_nw(cfg->N);
-        h->nd = B * (8 + 2 + dartmpc::LM_NPV + 8 + dartmpc::LM_NPRM + nw + 2 + 1 + nw);
+        nin = B * (8 + 2 + dartmpc::LM_NPV + 8 + dartmpc::LM_NPRM + nw);
+        nout = B * (2 + 1 + nw + 1);
     } else if (cfg->variant == DART_MPC_RMPC) {
         const size_t nw = (size_t)dart_rmpc_nw(cfg->N);
-        h->nd = B * (4 + 2 + 14 + 98 + 7 + 2 + 4 * (cfg->N + 1) + 10 + nw + 2 + 1 + nw);
+        nin = B * (4 + 2 + 14 + 98 + 7 + 2 + 4 * (cfg->N + 1) + 10 + nw);
+        nout = B * (2 + 1 + nw + 1);
     } else {
         const size_t nw = (size_t)dart_mpc_nw(cfg->N);
-        h->nd = B * (6 + 6 + 6 + nw + 2 + 1 + nw);
+        nin = B * (6 + 6 + 6 + nw);
+        nout = B * (2 + 1 + nw + 1);
     }
-    h->ni = B * 2;
-    if (e == hipSuccess) e = hipMalloc(&h->dbuf, h->nd * sizeof(double));
-    if (e == hipSuccess) e = hipMalloc(&h->ibuf, h->ni * sizeof(int32_t));
+    if (e == hipSuccess) e = h->st.reserve(nin * sizeof(double) + A, nout * sizeof(double) + A);
     if (e != hipSuccess) {
         dart_mpc_destroy(h);
         return DART_MPC_EHIP;
@@ -148,28 +262,24 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     if (B == 0) return DART_MPC_OK;
     HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
-    const size_t nw = (size_t)dart_mpc_nw(h->cfg.N), Bm = (size_t)h->cfg.B_max;
-    double* d_x0 = h->dbuf;
-    double* d_ref = d_x0 + Bm * 6;
-    double* d_prm = d_ref + Bm * 6;
-    double* d_ww = d_prm + Bm * 6;
-    double* d_u0 = d_ww + Bm * nw;
-    double* d_f = d_u0 + Bm * 2;
-    double* d_wo = d_f + Bm;
-    int32_t* d_st = h->ibuf;
-    int32_t* d_it = d_st + Bm;
-    HIPCHK(h, hipMemcpyAsync(d_x0, x0, sizeof(double) * 6 * B, hipMemcpyHostToDevice, s), "copy x0");
-    HIPCHK(h, hipMemcpyAsync(d_ref, ref, sizeof(double) * 6 * B, hipMemcpyHostToDevice, s), "copy ref");
-    HIPCHK(h, hipMemcpyAsync(d_prm, prm, sizeof(double) * 6 * B, hipMemcpyHostToDevice, s), "copy prm");
-    if (w_warm) HIPCHK(h, hipMemcpyAsync(d_ww, w_warm, sizeof(double) * nw * B, hipMemcpyHostToDevice, s), "copy w_warm");
-    int rc = launch(h, B, d_x0, d_ref, d_prm, w_warm ? d_ww : nullptr, d_u0, d_f, w_out ? d_wo : nullptr, d_st, d_it, s);
+    const size_t nw = (size_t)dart_mpc_nw(h->cfg.N);
+    HostStage& S = h->st;
+    S.begin();
+    const double* d_x0 = S.in(x0, 6 * B);
+    const double* d_ref = S.in(ref, 6 * B);
+    const double* d_prm = S.in(prm, 6 * B);
+    const double* d_ww = S.in(w_warm, nw * B);
+    double* d_u0 = S.out<double>(2 * B);
+    double* d_f = S.out<double>(B);
+    double* d_wo = w_out ? S.out<double>(nw * B) : nullptr;
+    int32_t* d_st = S.out<int32_t>(B);
+    int32_t* d_it = S.out<int32_t>(B);
+    HIPCHK(h, S.upload(s), "copy inputs");
+    int rc = launch(h, B, d_x0, d_ref, d_prm, d_ww, d_u0, d_f, d_wo, d_st, d_it, s);
     if (rc) return rc;
-    HIPCHK(h, hipMemcpyAsync(u0, d_u0, sizeof(double) * 2 * B, hipMemcpyDeviceToHost, s), "copy u0");
-    HIPCHK(h, hipMemcpyAsync(f, d_f, sizeof(double) * B, hipMemcpyDeviceToHost, s), "copy f");
-    if (w_out) HIPCHK(h, hipMemcpyAsync(w_out, d_wo, sizeof(double) * nw * B, hipMemcpyDeviceToHost, s), "copy w_out");
-    HIPCHK(h, hipMemcpyAsync(status, d_st, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s), "copy status");
-    HIPCHK(h, hipMemcpyAsync(iters, d_it, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s), "copy iters");
     HIPCHK(h, hipStreamSynchronize(s), "hipStreamSynchronize");
+    S.take(u0, d_u0, 2 * B); S.take(f, d_f, B); S.take(w_out, d_wo, nw * B);
+    S.take(status, d_st, B); S.take(iters, d_it, B);
     return DART_MPC_OK;
 }
 
@@ -206,48 +316,33 @@ int dart_rmpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const dou
     if (B == 0) return DART_MPC_OK;
     HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
-    const size_t N = (size_t)h->cfg.N, nw = (size_t)dart_rmpc_nw(h->cfg.N), Bm = (size_t)h->cfg.B_max;
-    double* p = h->dbuf;
-    double* d_x0 = p; p += Bm * 4;
-    double* d_up = p; p += Bm * 2;
-    double* d_th = p; p += Bm * 14;
-    double* d_P = p; p += Bm * 98;
-    double* d_phi = p; p += Bm * 7;
-    double* d_y = p; p += Bm * 2;
-    double* d_R = p; p += Bm * 4 * (N + 1);
-    double* d_prm = p; p += Bm * 10;
-    double* d_ww = p; p += Bm * nw;
-    double* d_u0 = p; p += Bm * 2;
-    double* d_f = p; p += Bm;
-    double* d_wo = p;
-    int32_t* d_st = h->ibuf;
-    int32_t* d_it = d_st + Bm;
-    auto up = [&](double* d, const double* hsrc, size_t n) { return hipMemcpyAsync(d, hsrc, sizeof(double) * n, hipMemcpyHostToDevice, s); };
-    HIPCHK(h, up(d_x0, x0, 4 * B), "copy x0");
-    HIPCHK(h, up(d_up, u_prev, 2 * B), "copy u_prev");
-    HIPCHK(h, up(d_th, theta, 14 * B), "copy theta");
-    if (rls_P) {
-        HIPCHK(h, up(d_P, rls_P, 98 * B), "copy rls_P");
-        HIPCHK(h, up(d_phi, rls_phi, 7 * B), "copy rls_phi");
-        HIPCHK(h, up(d_y, rls_y, 2 * B), "copy rls_y");
-    }
-    HIPCHK(h, up(d_R, Rref, 4 * (N + 1) * B), "copy Rref");
-    HIPCHK(h, up(d_prm, prm, 10 * B), "copy prm");
-    if (w_warm) HIPCHK(h, up(d_ww, w_warm, nw * B), "copy w_warm");
-    int rc = dart_rmpc_solve_batch_dev(h, B, d_x0, d_up, d_th, rls_P ? d_P : nullptr, d_phi, d_y, rls_lambda, d_R, d_prm,
-                                       w_warm ? d_ww : nullptr, d_u0, d_f, w_out ? d_wo : nullptr, d_st, d_it, s);
+    const size_t N = (size_t)h->cfg.N, nw = (size_t)dart_rmpc_nw(h->cfg.N);
+    HostStage& S = h->st;
+    S.begin();
+    const double* d_x0 = S.in(x0, 4 * B);
+    const double* d_up = S.in(u_prev, 2 * B);
+    const double* d_phi = rls_P ? S.in(rls_phi, 7 * B) : nullptr;
+    const double* d_y = rls_P ? S.in(rls_y, 2 * B) : nullptr;
+    const double* d_R = S.in(Rref, 4 * (N + 1) * B);
+    const double* d_prm = S.in(prm, 10 * B);
+    const double* d_ww = S.in(w_warm, nw * B);
+    // theta is updated in place only when the RLS step is fused
+    double* d_th = rls_P ? S.inout(theta, 14 * B) : const_cast<double*>(S.in(theta, 14 * B));
+    double* d_P = rls_P ? S.inout(rls_P, 98 * B) : nullptr;
+    double* d_u0 = S.out<double>(2 * B);
+    double* d_f = S.out<double>(B);
+    double* d_wo = w_out ? S.out<double>(nw * B) : nullptr;
+    int32_t* d_st = S.out<int32_t>(B);
+    int32_t* d_it = S.out<int32_t>(B);
+    HIPCHK(h, S.upload(s), "copy inputs");
+    int rc = dart_rmpc_solve_batch_dev(h, B, d_x0, d_up, d_th, d_P, d_phi, d_y, rls_lambda, d_R, d_prm, d_ww, d_u0, d_f,
+                                       d_wo, d_st, d_it, s);
     if (rc) return rc;
-    auto dn = [&](void* hdst, const void* d, size_t bytes) { return hipMemcpyAsync(hdst, d, bytes, hipMemcpyDeviceToHost, s); };
-    HIPCHK(h, dn(u0, d_u0, sizeof(double) * 2 * B), "copy u0");
-    HIPCHK(h, dn(f, d_f, sizeof(double) * B), "copy f");
-    if (w_out) HIPCHK(h, dn(w_out, d_wo, sizeof(double) * nw * B), "copy w_out");
-    if (rls_P) {
-        HIPCHK(h, dn(theta, d_th, sizeof(double) * 14 * B), "copy theta");
-        HIPCHK(h, dn(rls_P, d_P, sizeof(double) * 98 * B), "copy rls_P");
-    }
-    HIPCHK(h, dn(status, d_st, sizeof(int32_t) * B), "copy status");
-    HIPCHK(h, dn(iters, d_it, sizeof(int32_t) * B), "copy iters");
+    HIPCHK(h, S.download_inout(s), "copy theta / rls_P");
     HIPCHK(h, hipStreamSynchronize(s), "hipStreamSynchronize");
+    S.finish_inout();
+    S.take(u0, d_u0, 2 * B); S.take(f, d_f, B); S.take(w_out, d_wo, nw * B);
+    S.take(status, d_st, B); S.take(iters, d_it, B);
     return DART_MPC_OK;
 }
 
@@ -280,36 +375,26 @@ int dart_lmpc_solve_batch(dart_mpc_handle* h, int B, const double* state, const 
     if (B == 0) return DART_MPC_OK;
     HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
-    const size_t nw = (size_t)dart_lmpc_nw(h->cfg.N), Bm = (size_t)h->cfg.B_max;
-    double* p = h->dbuf;
-    double* d_st0 = p; p += Bm * 8;
-    double* d_up = p; p += Bm * 2;
-    double* d_pv = p; p += Bm * dartmpc::LM_NPV;
-    double* d_tg = p; p += Bm * 8;
-    double* d_prm = p; p += Bm * dartmpc::LM_NPRM;
-    double* d_ww = p; p += Bm * nw;
-    double* d_u0 = p; p += Bm * 2;
-    double* d_f = p; p += Bm;
-    double* d_wo = p;
-    int32_t* d_st = h->ibuf;
-    int32_t* d_it = d_st + Bm;
-    auto up = [&](double* d, const double* hsrc, size_t n) { return hipMemcpyAsync(d, hsrc, sizeof(double) * n, hipMemcpyHostToDevice, s); };
-    HIPCHK(h, up(d_st0, state, 8 * B), "copy state");
-    HIPCHK(h, up(d_up, u_prev, 2 * B), "copy u_prev");
-    HIPCHK(h, up(d_pv, pvec, dartmpc::LM_NPV * B), "copy pvec");
-    HIPCHK(h, up(d_tg, target, 8 * B), "copy target");
-    HIPCHK(h, up(d_prm, prm, dartmpc::LM_NPRM * B), "copy prm");
-    if (w_warm) HIPCHK(h, up(d_ww, w_warm, nw * B), "copy w_warm");
-    int rc = dart_lmpc_solve_batch_dev(h, B, d_st0, d_up, d_pv, d_tg, d_prm, w_warm ? d_ww : nullptr, d_u0, d_f,
-                                       w_out ? d_wo : nullptr, d_st, d_it, s);
+    const size_t nw = (size_t)dart_lmpc_nw(h->cfg.N);
+    HostStage& S = h->st;
+    S.begin();
+    const double* d_st0 = S.in(state, 8 * B);
+    const double* d_up = S.in(u_prev, 2 * B);
+    const double* d_pv = S.in(pvec, dartmpc::LM_NPV * B);
+    const double* d_tg = S.in(target, 8 * B);
+    const double* d_prm = S.in(prm, dartmpc::LM_NPRM * B);
+    const double* d_ww = S.in(w_warm, nw * B);
+    double* d_u0 = S.out<double>(2 * B);
+    double* d_f = S.out<double>(B);
+    double* d_wo = w_out ? S.out<double>(nw * B) : nullptr;
+    int32_t* d_st = S.out<int32_t>(B);
+    int32_t* d_it = S.out<int32_t>(B);
+    HIPCHK(h, S.upload(s), "copy inputs");
+    int rc = dart_lmpc_solve_batch_dev(h, B, d_st0, d_up, d_pv, d_tg, d_prm, d_ww, d_u0, d_f, d_wo, d_st, d_it, s);
     if (rc) return rc;
-    auto dn = [&](void* hdst, const void* d, size_t bytes) { return hipMemcpyAsync(hdst, d, bytes, hipMemcpyDeviceToHost, s); };
-    HIPCHK(h, dn(u0, d_u0, sizeof(double) * 2 * B), "copy u0");
-    HIPCHK(h, dn(f, d_f, sizeof(double) * B), "copy f");
-    if (w_out) HIPCHK(h, dn(w_out, d_wo, sizeof(double) * nw * B), "copy w_out");
-    HIPCHK(h, dn(status, d_st, sizeof(int32_t) * B), "copy status");
-    HIPCHK(h, dn(iters, d_it, sizeof(int32_t) * B), "copy iters");
     HIPCHK(h, hipStreamSynchronize(s), "hipStreamSynchronize");
+    S.take(u0, d_u0, 2 * B); S.take(f, d_f, B); S.take(w_out, d_wo, nw * B);
+    S.take(status, d_st, B); S.take(iters, d_it, B);
     return DART_MPC_OK;
 }
 
@@ -363,46 +448,34 @@ int dart_lmpc_policy_step(const dart_lmpc_policy_config* cfg, int B, const float
     if (B > 0 && (!state || !target || !control || !current_k || !obs_mean || !obs_M2 || !obs_count || !history ||
                   !timestep || !noise || !model_params)) return DART_MPC_EINVAL;
     if (B == 0) return DART_MPC_OK;
-    const size_t nd = (size_t)B * (8 + 8 + 2 + 34 + 52 + 52 + 34);
-    const size_t nf = (size_t)DART_LMPC_POLICY_NWEIGHTS + (size_t)B * (10 * 52 + 34 + 34);
-    double* d = nullptr; float* fl = nullptr; int32_t* iv = nullptr;
-    hipError_t e = hipMalloc(&d, nd * sizeof(double));
-    if (e == hipSuccess) e = hipMalloc(&fl, nf * sizeof(float));
-    if (e == hipSuccess) e = hipMalloc(&iv, (size_t)2 * B * sizeof(int32_t));
-    double *d_st = d, *d_tg = d_st + 8 * B, *d_ct = d_tg + 8 * B, *d_ck = d_ct + 2 * B, *d_mn = d_ck + 34 * B,
-           *d_m2 = d_mn + 52 * B, *d_mp = d_m2 + 52 * B;
-    float *d_w = fl, *d_h = d_w + DART_LMPC_POLICY_NWEIGHTS, *d_nz = d_h + 520 * B, *d_ao = d_nz + 34 * B;
-    int32_t *d_cnt = iv, *d_ts = iv + B;
-    auto up = [&](void* dst, const void* src, size_t bytes) {
-        if (e == hipSuccess) e = hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
-    };
-    auto dn = [&](void* dst, const void* src, size_t bytes) {
-        if (e == hipSuccess) e = hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
-    };
-    up(d_w, weights, sizeof(float) * DART_LMPC_POLICY_NWEIGHTS);
-    up(d_st, state, sizeof(double) * 8 * B); up(d_tg, target, sizeof(double) * 8 * B);
-    up(d_ct, control, sizeof(double) * 2 * B); up(d_ck, current_k, sizeof(double) * 34 * B);
-    up(d_mn, obs_mean, sizeof(double) * 52 * B); up(d_m2, obs_M2, sizeof(double) * 52 * B);
-    up(d_mp, model_params, sizeof(double) * 34 * B); up(d_h, history, sizeof(float) * 520 * B);
-    up(d_nz, noise, sizeof(float) * 34 * B); up(d_cnt, obs_count, sizeof(int32_t) * B);
-    up(d_ts, timestep, sizeof(int32_t) * B);
-    if (e == hipSuccess) {
-        a.w.W1 = d_w; a.w.b1 = d_w + 520 * 64; a.w.W2 = a.w.b1 + 64; a.w.b2 = a.w.W2 + 64 * 64;
-        a.w.W3 = a.w.b2 + 64; a.w.b3 = a.w.W3 + 64 * 34; a.w.log_std = a.w.b3 + 34;
-        a.state = d_st; a.target = d_tg; a.control = d_ct; a.current_k = d_ck; a.obs_mean = d_mn; a.obs_M2 = d_m2;
-        a.obs_count = d_cnt; a.history = d_h; a.timestep = d_ts; a.noise = d_nz; a.model_params = d_mp;
-        a.action_out = d_ao;
-        e = dartmpc_launch_policy(&a, nullptr);
-    }
-    dn(obs_mean, d_mn, sizeof(double) * 52 * B); dn(obs_M2, d_m2, sizeof(double) * 52 * B);
-    dn(model_params, d_mp, sizeof(double) * 34 * B); dn(history, d_h, sizeof(float) * 520 * B);
-    dn(obs_count, d_cnt, sizeof(int32_t) * B); dn(timestep, d_ts, sizeof(int32_t) * B);
-    if (action_out) dn(action_out, d_ao, sizeof(float) * 34 * B);
-    if (d) (void)hipFree(d);
-    if (fl) (void)hipFree(fl);
-    if (iv) (void)hipFree(iv);
-    return e == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
+    DeviceStage* D = nullptr;
+    if (device_stage(&D) != hipSuccess) return DART_MPC_EHIP;
+    std::lock_guard<std::mutex> lock(D->mu);
+    HostStage& S = D->st;
+    const size_t nin = sizeof(float) * ((size_t)DART_LMPC_POLICY_NWEIGHTS + (size_t)B * (34 + 520)) +
+                       sizeof(double) * (size_t)B * (8 + 8 + 2 + 34 + 52 + 52 + 34) + sizeof(int32_t) * 2 * B + 16 * 256;
+    if (S.reserve(nin, sizeof(float) * 34 * B + 256) != hipSuccess) return DART_MPC_EHIP;
+    S.begin();
+    const float* d_w = S.in(weights, (size_t)DART_LMPC_POLICY_NWEIGHTS);
+    a.w.W1 = d_w; a.w.b1 = d_w + 520 * 64; a.w.W2 = a.w.b1 + 64; a.w.b2 = a.w.W2 + 64 * 64;
+    a.w.W3 = a.w.b2 + 64; a.w.b3 = a.w.W3 + 64 * 34; a.w.log_std = a.w.b3 + 34;
+    a.state = S.in(state, 8 * (size_t)B); a.target = S.in(target, 8 * (size_t)B);
+    a.control = S.in(control, 2 * (size_t)B); a.current_k = S.in(current_k, 34 * (size_t)B);
+    a.noise = S.in(noise, 34 * (size_t)B);
+    a.obs_mean = S.inout(obs_mean, 52 * (size_t)B); a.obs_M2 = S.inout(obs_M2, 52 * (size_t)B);
+    a.model_params = S.inout(model_params, 34 * (size_t)B); a.history = S.inout(history, 520 * (size_t)B);
+    a.obs_count = S.inout(obs_count, (size_t)B); a.timestep = S.inout(timestep, (size_t)B);
+    a.action_out = S.out<float>(34 * (size_t)B);
+    hipError_t e = S.upload(D->stream);
+    if (e == hipSuccess) e = dartmpc_launch_policy(&a, D->stream);
+    if (e == hipSuccess) e = S.download_inout(D->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(D->stream);
+    if (e != hipSuccess) return DART_MPC_EHIP;
+    S.finish_inout();
+    S.take(action_out, a.action_out, 34 * (size_t)B);
+    return DART_MPC_OK;
 }
+
 
 int dart_rls_update_batch_dev(int B, double* theta, double* P, const double* phi, const double* y, double lambda,
                               void* stream) {
@@ -413,19 +486,23 @@ int dart_rls_update_batch_dev(int B, double* theta, double* P, const double* phi
 int dart_rls_update_batch(int B, double* theta, double* P, const double* phi, const double* y, double lambda) {
     if (B < 0 || (B > 0 && (!theta || !P || !phi || !y)) || !(lambda > 0.0)) return DART_MPC_EINVAL;
     if (B == 0) return DART_MPC_OK;
-    double* d = nullptr;
-    const size_t n = (size_t)B * (7 + 49 + 7 + 1);
-    if (hipMalloc(&d, n * sizeof(double)) != hipSuccess) return DART_MPC_EHIP;
-    double *dt = d, *dP = dt + 7 * B, *dphi = dP + 49 * B, *dy = dphi + 7 * B;
-    hipError_t e = hipMemcpy(dt, theta, sizeof(double) * 7 * B, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dP, P, sizeof(double) * 49 * B, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dphi, phi, sizeof(double) * 7 * B, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dy, y, sizeof(double) * B, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = dartmpc_launch_rls(B, dt, dP, dphi, dy, lambda, nullptr);
-    if (e == hipSuccess) e = hipMemcpy(theta, dt, sizeof(double) * 7 * B, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(P, dP, sizeof(double) * 49 * B, hipMemcpyDeviceToHost);
-    (void)hipFree(d);
-    return e == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
+    DeviceStage* D = nullptr;
+    if (device_stage(&D) != hipSuccess) return DART_MPC_EHIP;
+    std::lock_guard<std::mutex> lock(D->mu);
+    HostStage& S = D->st;
+    if (S.reserve(sizeof(double) * (size_t)B * (7 + 49 + 7 + 1) + 4 * 256, 256) != hipSuccess) return DART_MPC_EHIP;
+    S.begin();
+    const double* dphi = S.in(phi, 7 * (size_t)B);
+    const double* dy = S.in(y, (size_t)B);
+    double* dt = S.inout(theta, 7 * (size_t)B);
+    double* dP = S.inout(P, 49 * (size_t)B);
+    hipError_t e = S.upload(D->stream);
+    if (e == hipSuccess) e = dartmpc_launch_rls(B, dt, dP, dphi, dy, lambda, D->stream);
+    if (e == hipSuccess) e = S.download_inout(D->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(D->stream);
+    if (e != hipSuccess) return DART_MPC_EHIP;
+    S.finish_inout();
+    return DART_MPC_OK;
 }
 
 int dart_mpc_sync(dart_mpc_handle* h) {
@@ -448,8 +525,7 @@ const char* dart_mpc_last_error(const dart_mpc_handle* h) { return h ? h->err.c_
 
 void dart_mpc_destroy(dart_mpc_handle* h) {
     if (!h) return;
-    if (h->dbuf) (void)hipFree(h->dbuf);
-    if (h->ibuf) (void)hipFree(h->ibuf);
+    h->st.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -498,24 +574,22 @@ int dart_arm_solve_batch(const dart_arm_config* cfg, int B, int n, const double*
     if (!snap || !prm || !qdd || !tau || !loss || !status || !iters) return DART_MPC_EINVAL;
     const size_t SL = (size_t)dartmpc::arm_snap_len(n), PL = (size_t)dartmpc::arm_prm_len(n);
     const size_t np = prm_stride ? PL * B : PL;
-    const size_t nd = SL * B + np + (size_t)B * (2 * n + 1);
-    double* d = nullptr;
-    int32_t* iv = nullptr;
-    hipError_t e = hipMalloc(&d, nd * sizeof(double));
-    if (e == hipSuccess) e = hipMalloc(&iv, (size_t)2 * B * sizeof(int32_t));
-    double *d_s = d, *d_p = d_s + SL * B, *d_q = d_p + np, *d_t = d_q + (size_t)n * B, *d_l = d_t + (size_t)n * B;
-    if (e == hipSuccess) e = hipMemcpy(d_s, snap, sizeof(double) * SL * B, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d_p, prm, sizeof(double) * np, hipMemcpyHostToDevice);
-    if (e == hipSuccess) {
-        a.snap = d_s; a.prm = d_p; a.qdd = d_q; a.tau = d_t; a.loss = d_l; a.status = iv; a.iters = iv + B;
-        e = dartmpc_launch_arm(&a, nullptr);
-    }
-    if (e == hipSuccess) e = hipMemcpy(qdd, d_q, sizeof(double) * n * B, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(tau, d_t, sizeof(double) * n * B, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(loss, d_l, sizeof(double) * B, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(status, iv, sizeof(int32_t) * B, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(iters, iv + B, sizeof(int32_t) * B, hipMemcpyDeviceToHost);
-    if (d) (void)hipFree(d);
-    if (iv) (void)hipFree(iv);
-    return e == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
+    DeviceStage* D = nullptr;
+    if (device_stage(&D) != hipSuccess) return DART_MPC_EHIP;
+    std::lock_guard<std::mutex> lock(D->mu);
+    HostStage& S = D->st;
+    if (S.reserve(sizeof(double) * (SL * B + np) + 2 * 256,
+                  sizeof(double) * (2 * (size_t)n * B + B) + sizeof(int32_t) * 2 * B + 5 * 256) != hipSuccess)
+        return DART_MPC_EHIP;
+    S.begin();
+    a.snap = S.in(snap, SL * B); a.prm = S.in(prm, np);
+    a.qdd = S.out<double>((size_t)n * B); a.tau = S.out<double>((size_t)n * B); a.loss = S.out<double>(B);
+    a.status = S.out<int32_t>(B); a.iters = S.out<int32_t>(B);
+    hipError_t e = S.upload(D->stream);
+    if (e == hipSuccess) e = dartmpc_launch_arm(&a, D->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(D->stream);
+    if (e != hipSuccess) return DART_MPC_EHIP;
+    S.take(qdd, a.qdd, (size_t)n * B); S.take(tau, a.tau, (size_t)n * B); S.take(loss, a.loss, B);
+    S.take(status, a.status, B); S.take(iters, a.iters, B);
+    return DART_MPC_OK;
 }

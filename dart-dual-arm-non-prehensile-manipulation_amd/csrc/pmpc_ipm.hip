@@ -23,6 +23,7 @@
 // no global traffic inside the iteration loop.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "pmpc_ipm.h"
 #include "stamps.h"
@@ -636,7 +637,11 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
     // The quadratic scan shortens the dependent chain but needs more registers (one wave per SIMD
     // instead of two): worth it while every wave has a SIMD of its own (B <= 4 x 256), not beyond.
     const dim3 grid(a.B * a.pack);
-    if (a.N <= 31 && a.B <= 1024)
+    static const int qscan_max_b = [] {     // experiment knob: DART_PMPC_QSCAN_MAX_B (default 1024)
+        const char* e = getenv("DART_PMPC_QSCAN_MAX_B");
+        return e ? atoi(e) : 1024;
+    }();
+    if (a.N <= 31 && a.B <= qscan_max_b)
         hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
     else if (a.N <= 31)
         hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, false>), grid, dim3(dartmpc::kWave), 0, stream, a);

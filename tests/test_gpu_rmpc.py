@@ -155,17 +155,19 @@ def test_closed_loop_driver_matches_oracle_loop(dm):
         up = u
 
 
-def test_same_path_as_oracle_without_soc(dm):
+@pytest.mark.parametrize("soc", [False, True])
+def test_same_path_as_oracle(dm, soc):
     """Exact derivatives in the kernel: against the C oracle with its second-order correction off
-    (the kernel's line search has none) every instance takes the same iterations, ends with the same
-    status and returns the same control at the reference's tol 1e-8."""
+    (the kernel's line search has none) and on (IPOPT's default; it never engages on the C3 workload,
+    test_oracle_rmpc.py) every instance takes the same iterations, ends with the same status and
+    returns the same control at the reference's tol 1e-8."""
     from dart_mpc.workload import rmpc_batch
     D = rmpc_batch(8, seed0=40)
     s = dm.RmpcSolver(N=20, tol=1e-8, B_max=256)
     g = s.solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
     s.close()
     o = oracle_lib.rmpc_solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"], N=20, tol=1e-8,
-                                    nthreads=8, soc=False)
+                                    nthreads=8, soc=soc)
     assert np.array_equal(g["status"], o["status"])
     assert np.mean(g["iters"] == o["iters"]) >= 0.99, (g["iters"], o["iters"])
     assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6

@@ -119,3 +119,18 @@ def test_rmpc_workload_shapes_and_determinism():
     assert a["rls_P"].shape == (18, 2, 7, 7)
     for k in a:
         assert np.array_equal(a[k], b[k]), k
+
+
+def test_second_order_correction_never_engages_on_c3():
+    """IPOPT's second-order correction (max_soc 4) leaves every C3 solve bit-identical to the solve
+    without it (720 instances, tol 1e-8 and 1e-11): on this workload the full step is never rejected
+    with theta(trial) >= theta, so the kernel's line search (no correction) follows IPOPT's path."""
+    from dart_mpc.workload import rmpc_batch
+    D = rmpc_batch(40, seed0=0)
+    args = (D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
+    for tol in (1e-8, 1e-11):
+        a = oracle_lib.rmpc_solve_batch(*args, N=20, tol=tol, nthreads=8, want_w=False, soc=True)
+        b = oracle_lib.rmpc_solve_batch(*args, N=20, tol=tol, nthreads=8, want_w=False, soc=False)
+        np.testing.assert_array_equal(a["u0"], b["u0"])
+        np.testing.assert_array_equal(a["iters"], b["iters"])
+        np.testing.assert_array_equal(a["status"], b["status"])
