@@ -26,6 +26,13 @@ ALGO_BYTES = {"pmpc_ipm_kernel": 18 * 176, "rmpc_ipm_kernel": 18 * (4 + 2 + 14 +
               "arm_qp_kernel": 36 * (206 + 262 + 7 + 7 + 1 + 1) * 8}   # snapshot + (shared) params read per wave + outputs
 
 
+# the headline launch of each kernel (B=18 packed 8 blocks per instance; 36 arms): other dispatches
+# of the same kernel in the bench (C4, saturation runs) are left out of the per-launch figures
+GRID = {"pmpc_ipm_kernel": 18 * 8 * 64, "rmpc_ipm_kernel": 18 * 8 * 64, "lmpc_ipm_kernel": 18 * 8 * 64,
+        "arm_qp_kernel": 36 * 64}
+STATS_NAME = {"pmpc_ipm_kernel": "pmpc_ipm_kernel<1, true>"}   # template instance the C2 launch uses
+
+
 def short(name):
     for k in KERNELS:
         if k in name:
@@ -46,7 +53,7 @@ for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = short(row.get("Kernel_Name", ""))
-                if k is None or row.get("Counter_Name") != ctr:
+                if k is None or row.get("Counter_Name") != ctr or int(row.get("Grid_Size", 0)) != GRID[k]:
                     continue
                 per[k][ctr].append(float(row["Counter_Value"]))
                 meta[k] = {"grid_size": int(row.get("Grid_Size", 0)), "VGPR_Count": int(row.get("VGPR_Count", 0)),
@@ -58,7 +65,7 @@ if stats:
     with open(stats[0]) as fh:
         for row in csv.DictReader(fh):
             k = short(row["Name"])
-            if k:
+            if k and STATS_NAME.get(k, k) in row["Name"]:
                 avg[k] = {"calls": int(row["Calls"]), "average_ns": float(row["AverageNs"])}
 for k, d in per.items():
     fk = sum(d["FETCH_SIZE"]) / max(1, len(d["FETCH_SIZE"]))
