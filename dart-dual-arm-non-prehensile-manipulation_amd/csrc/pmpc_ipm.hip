@@ -65,15 +65,24 @@ __device__ __forceinline__ void z_rk4(double h, double w, double pz, double vz, 
     vzn = vz + h / 6 * (k1v + 2 * k2v + 2 * k3v + k4v);
 }
 
-// DPP move with an explicit fill value for lanes whose source is outside the row / masked out
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ double dpp_fill(double fill, double x) {
+// DPP move with an identity fill (FILL = 0.0 or 1.0) for lanes whose source is outside the row or
+// masked out.  With every row enabled a zero half comes from bound_ctrl (the DPP writes 0 where the
+// source is out of range): no initialising move; 1.0 only needs its high word 0x3ff00000 set first.
+// Rows masked off keep the old value, so a partial ROWMASK initialises both words.
+template <int CTRL, int ROWMASK, int FILL>
+__device__ __forceinline__ double dpp_fill(double x) {
     const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
-    const unsigned long long o = __builtin_bit_cast(unsigned long long, fill);
-    const int rlo = __builtin_amdgcn_update_dpp((int)(unsigned)(o & 0xffffffffu), (int)(unsigned)(b & 0xffffffffu),
-                                                CTRL, ROWMASK, 0xf, false);
-    const int rhi = __builtin_amdgcn_update_dpp((int)(unsigned)(o >> 32), (int)(unsigned)(b >> 32), CTRL, ROWMASK, 0xf,
-                                                false);
+    const int blo = (int)(unsigned)(b & 0xffffffffu), bhi = (int)(unsigned)(b >> 32);
+    constexpr int fhi = FILL ? 0x3ff00000 : 0;
+    int rlo, rhi;
+    if constexpr (ROWMASK == 0xf) {
+        rlo = __builtin_amdgcn_mov_dpp(blo, CTRL, 0xf, 0xf, true);
+        if constexpr (FILL) rhi = __builtin_amdgcn_update_dpp(fhi, bhi, CTRL, 0xf, 0xf, false);
+        else rhi = __builtin_amdgcn_mov_dpp(bhi, CTRL, 0xf, 0xf, true);
+    } else {
+        rlo = __builtin_amdgcn_update_dpp(0, blo, CTRL, ROWMASK, 0xf, false);
+        rhi = __builtin_amdgcn_update_dpp(fhi, bhi, CTRL, ROWMASK, 0xf, false);
+    }
     return __builtin_bit_cast(double, ((unsigned long long)(unsigned)rhi << 32) | (unsigned)rlo);
 }
 // one Hillis-Steele level of an inclusive scan of 2-D affine maps x -> F x + c (later o earlier):
@@ -81,9 +90,9 @@ __device__ __forceinline__ double dpp_fill(double fill, double x) {
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ void affine_scan_level(double& f11, double& f12, double& f21, double& f22, double& c1,
                                                   double& c2) {
-    const double p11 = dpp_fill<CTRL, ROWMASK>(1.0, f11), p12 = dpp_fill<CTRL, ROWMASK>(0.0, f12);
-    const double p21 = dpp_fill<CTRL, ROWMASK>(0.0, f21), p22 = dpp_fill<CTRL, ROWMASK>(1.0, f22);
-    const double q1 = dpp_fill<CTRL, ROWMASK>(0.0, c1), q2 = dpp_fill<CTRL, ROWMASK>(0.0, c2);
+    const double p11 = dpp_fill<CTRL, ROWMASK, 1>(f11), p12 = dpp_fill<CTRL, ROWMASK, 0>(f12);
+    const double p21 = dpp_fill<CTRL, ROWMASK, 0>(f21), p22 = dpp_fill<CTRL, ROWMASK, 1>(f22);
+    const double q1 = dpp_fill<CTRL, ROWMASK, 0>(c1), q2 = dpp_fill<CTRL, ROWMASK, 0>(c2);
     const double n11 = fma(f11, p11, f12 * p21), n12 = fma(f11, p12, f12 * p22);
     const double n21 = fma(f21, p11, f22 * p21), n22 = fma(f21, p12, f22 * p22);
     c1 = fma(f11, q1, fma(f12, q2, c1));
@@ -97,7 +106,7 @@ template <int CTRL>
 __device__ __forceinline__ void mat4_scan_level(double* T) {
     double F[16];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) F[e] = dpp_fill<CTRL, 0xf>((e % 5 == 0) ? 1.0 : 0.0, T[e]);
+    for (int e = 0; e < 16; ++e) F[e] = (e % 5 == 0) ? dpp_fill<CTRL, 0xf, 1>(T[e]) : dpp_fill<CTRL, 0xf, 0>(T[e]);
     double N[16];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -145,6 +154,8 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
     // backward sweep reproduces the terminal value function there without a branch
     const double f11 = uon ? 1.0 : 0.0, a12k = uon ? a12 : 0.0, a22k = uon ? a22 : 0.0;
     const double ai22 = 1.0 / a22, ai12 = -a12 * ai22;        // A^-1 = [[1, ai12], [0, ai22]]
+    // the same per lane for the quadratic scan: identity stage maps on the terminal / idle lanes
+    const double uonf = uon ? 1.0 : 0.0, ai12k = uon ? ai12 : 0.0, ai22k = uon ? ai22 : 1.0, a22i = uon ? a22 : 1.0;
     const double A11k = a12k * a12k, A12k = 2.0 * a12k * a22k, A22k = a22k * a22k;
 
     // per-lane axis slots
@@ -295,15 +306,13 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
             if (use_scan) {
                 const double iR = uon ? frcp(Rt[0]) : 0.0;
                 const double G11 = be1[0] * be1[0] * iR, G12 = be1[0] * be2[0] * iR, G22 = be2[0] * be2[0] * iR;
-                const double g11 = G11 + ai12 * G12, g12 = G12 + ai12 * G22, g21 = ai22 * G12, g22 = ai22 * G22;
-                double T[16] = {1.0, ai12, g11, g12,
-                                0.0, ai22, g21, g22,
-                                X11d, X11d * ai12, fma(X11d, g11, 1.0), X11d * g12,
-                                0.0, X22d * ai22, fma(X22d, g21, a12), fma(X22d, g22, a22)};
-                if (!uon) {
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) T[e] = (e % 5 == 0) ? 1.0 : 0.0;
-                }
+                const double g11 = G11 + ai12k * G12, g12 = G12 + ai12k * G22, g21 = ai22k * G12, g22 = ai22k * G22;
+                // idle / terminal lanes: A^-1 = I, G = 0 (iR = 0), X = 0, A^T = I give T = I without a select
+                const double X11k = X11d * uonf, X22k = X22d * uonf;
+                double T[16] = {1.0, ai12k, g11, g12,
+                                0.0, ai22k, g21, g22,
+                                X11k, X11k * ai12k, fma(X11k, g11, 1.0), X11k * g12,
+                                0.0, X22k * ai22k, fma(X22k, g21, a12k), fma(X22k, g22, a22i)};
                 mat4_scan_level<0x101>(T);
                 mat4_scan_level<0x102>(T);
                 mat4_scan_level<0x104>(T);

@@ -14,7 +14,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
-LIB_PATH = os.path.join(PKG_DIR, "libdartmpc.so")
+# DART_MPC_LIB: file name of an alternative in-tree build (A/B timing of two builds, tools/ab_lib.sh)
+LIB_PATH = os.path.join(PKG_DIR, os.path.basename(os.environ.get("DART_MPC_LIB", "libdartmpc.so")))
 
 SOLVED, ACCEPTABLE, MAXITER, LS_FAIL, INERTIA_FAIL = 0, 1, -1, -2, -3
 STATUS_NAMES = {SOLVED: "Solve_Succeeded", ACCEPTABLE: "Solved_To_Acceptable_Level",

@@ -1,0 +1,24 @@
+#!/bin/bash
+# A/B timing of two in-tree builds of libdartmpc on the GPU box (bench main line + supplementary lines).
+# Usage: bash tools/ab_lib.sh <lib A file name> <lib B file name> [reps] [extra bench args]
+set -o pipefail
+A=${1:-libdartmpc_base.so}
+B=${2:-libdartmpc.so}
+REPS=${3:-3}
+EXTRA=${4:-"--rmpc-steps 0 --lmpc-steps 0 --arm-steps 0"}
+mkdir -p gpurun_out
+ARGS="--steps 2000 --warmup 50 --no-cpu-baseline --saturation-batch 0 --host-calls 0 --c4-steps 0 $EXTRA"
+for r in $(seq 1 $REPS); do
+  for lib in "$A" "$B"; do
+    DART_MPC_LIB=$lib timeout -k 10 180 python bench.py $ARGS > gpurun_out/ab.json 2>gpurun_out/ab.err || exit $?
+    python - "$lib" <<'PY'
+import json, sys
+d = json.load(open("gpurun_out/ab.json"))
+out = [sys.argv[1], "C2", round(d["value"]), round(d["roofline"]["kernel_ms"] * 1e3, 2), "us"]
+for k in ("rmpc_c3", "lmpc_c5", "arm_qp"):
+    if d.get(k):
+        out += [k, round(d[k]["solves_per_s"]), round(d[k]["kernel_ms"] * 1e3, 1), "us"]
+print(*out)
+PY
+  done
+done
