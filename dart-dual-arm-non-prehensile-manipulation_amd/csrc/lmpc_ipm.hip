@@ -6,18 +6,23 @@
 // (:480-489: max_iter, tol, acceptable_tol, acceptable_iter; the 0.05 s wall-clock cap is not
 // reproduced: the solve is deterministic here).  The 34-vector pvec is an input.
 //
-// Method: IPOPT's primal-dual barrier method as in pmpc_ipm.hip / rmpc_ipm.hip (monotone mu,
-// filter line search, inertia correction, bound_relax 1e-8, gradient-based scaling of the
-// objective and of the constraint rows) with IPOPT's optimal / acceptable termination tests.
-// The Delta-u cost couples consecutive controls: the Riccati recursion runs on the augmented
-// state x~_k = [x_k; u_{k-1}] (nx~ = 10), three LDS phases per node (ocp_wave.h, OcpLds3).
-// Exact derivatives as IPOPT gets them from CasADi: per direction of z = [x; u], the RK4 tangent
-// (a column of the step Jacobian) and a second-order adjoint sweep back through the four stages
-// (a column of the exact Hessian of lambda^T x+), from per-stage derivative data staged in LDS.
+// Separable structure: safe_dynamics never mixes the two horizontal directions -- [px, vx,
+// theta_y, omega_y] are driven by tilt a alone (sliding friction, rolling slip vx - r_x omega_y,
+// the omega_y torques, toppling sin theta_y; :352-427), [py, vy, theta_x, omega_x] by tilt b
+// alone -- and Q, Qt, R and the U box are diagonal.  The NLP therefore splits into two
+// independent scalar-input problems, coupled only through IPOPT's global quantities (mu, the
+// step length, the filter, the scalings), all of which are wave-wide reductions here.  The two
+// subsystems share one code path with per-half parameters: half h = lane >> 5 solves subsystem
+// h, lane 32 h + k owns shooting node k (N <= 31).
 //
-// Mapping: one wave64 per instance, lane k = shooting node k (N <= 31) for node-local work;
-// the node-coupled Riccati / forward sweeps run through LDS (ocp_wave.h).  The LDS image
-// (~135 KB) is dynamic shared memory: one instance per CU.
+// Method: IPOPT's primal-dual barrier method as in pmpc_ipm.hip / rmpc_ipm.hip (monotone mu,
+// filter line search with second-order correction, inertia correction, bound_relax 1e-8,
+// gradient-based scaling of the objective and of the constraint rows) with IPOPT's optimal /
+// acceptable termination tests.  The Delta-u cost couples consecutive controls: each half runs
+// the Riccati recursion on its augmented state x~_k = [x_k (4); u_{k-1}] (ocp_wave.h, OcpLdsS,
+// one LDS round trip per node).  Exact derivatives as IPOPT gets them from CasADi: per
+// direction of z = [x; u], the RK4 tangent (a column of the step Jacobian) and a second-order
+// adjoint sweep back through the four stages (a column of the exact Hessian of lambda^T x+).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -28,10 +33,10 @@
 
 namespace dartmpc {
 
-constexpr int LM_NMAXS = 32;      // max shooting nodes (N <= 31)
-constexpr int LM_NSC = 10;        // stage-dependent tangent coefficients per RK stage
+constexpr int LM_NMAXS = 32;      // node slots per half (N <= 31)
+constexpr int LM_NSC = 5;         // stage-dependent tangent coefficients per RK stage
 constexpr double LM_G = 9.81;     // rlmpc2.py:354
-using LmLds = OcpLds3<10, LM_NMAXS>;
+using LmLds = OcpLdsS<5, LM_NMAXS>;
 
 #ifdef DART_STAMPS
 __device__ unsigned long long g_stamp_lm[16];
@@ -41,25 +46,31 @@ struct Strb {           // stribeck_fric parameters (rlmpc2.py:372-376)
     double Fc, dF, B, ivs, ieps;    // dF = F_s - F_c, ivs = 1 / (v_s + 1e-12), ieps = 1 / eps
 };
 
-struct LmModel {
-    double im_x, im_y, m_x, m_y, c_x, c_y, k_x, k_y;
-    Strb sx, sy, srx, sry;
-    double iIx, iIy, r_x, r_y, c_rx, c_ry, tqx, tqy;   // tq = m g h_com (toppling torque scale)
-    double h;                                         // Ts
+// One subsystem, local state [p, v, th, om], input a (x: [px, vx, theta_y, omega_y; a],
+// y: [py, vy, theta_x, omega_x; b]):
+//   pdot = v,  vdot = (m g sin a - c v - k p - Ff(v) - Fr(v + rs om)) / m,
+//   thdot = om, omdot = (-r Fr(v + rs om) - Tn(om) - crot om - tq sin th) / I
+// with rs = -r_x (x) / +r_y (y) the rolling-slip coupling (:391-395) and tq = m g h_com (:413-414).
+struct LmSub {
+    double im, m, c, k;
+    Strb st;                // translational Stribeck: sliding (v) and rolling slip
+    double rs, r, rr2;      // slip = v + rs om; torque -r Fr; rr2 = -r rs
+    double iI, crot;
+    Strb sr;                // rotational Stribeck
+    double tq;
+    double h;               // Ts
 };
 
 struct LmShared {
     LmLds ocp;
-    // per node (row 32: scratch of the idle lanes), per RK stage: d f / d y coefficients, and the
-    // second-derivative data turned into adjoint-weighted curvature coefficients
-    NodeArr<double[4][LM_NSC], LM_NMAXS + 1> SC;
-    NodeArr<double[4][8], LM_NMAXS + 1> SD;
-    NodeArr<double[12], LM_NMAXS + 1> JL;      // J^T lambda_{k+1} staging, primal residual maxima
-    NodeArr<double[14], LM_NMAXS + 1> DL;      // per node: lambda_{k+1}, tilt curvature, g cos(u) for the mirror lanes
-    NodeArr<double[10], LM_NMAXS + 1> CS;      // second-order correction: c_soc rows of node k (incoming defect)
-    NodeArr<double[22], LM_NMAXS + 1> SV;      // second-order correction: the plain step (dx~, lambda+, du) of node k
-    LmModel model;                    // uniform problem data, read at the use sites (keeps VGPRs free)
-    double Q[8], Qt[8], tgt[8];
+    // per node slot, per RK stage: d f / d y coefficients, and the second-derivative data turned
+    // into adjoint-weighted curvature coefficients
+    NodeArr<double[4][LM_NSC], 2 * LM_NMAXS> SC;
+    NodeArr<double[4][4], 2 * LM_NMAXS> SD;
+    NodeArr<double[7], 2 * LM_NMAXS> JL;     // J^T lambda_{k+1} (x 4, u 1), primal residual maxima
+    NodeArr<double[5], 2 * LM_NMAXS> CS;     // second-order correction: c_soc rows of node k (incoming defect)
+    NodeArr<double[11], 2 * LM_NMAXS> SV;    // second-order correction: the plain step (dx~, lambda+, du)
+    LmSub sub[2];                   // uniform problem data of the two halves
 };
 
 __device__ __forceinline__ double sq(double p) { return fabs(p) + 1e-6; }   // squash_param :296-298
@@ -100,410 +111,350 @@ __device__ __forceinline__ void sincos_any(double x, double& s, double& c) {
     else sincos(x, &s, &c);
 }
 
-// safe_dynamics (:260-429): xdot of state y for tilt sines sa, sb
-__device__ __forceinline__ void lm_f(const LmModel& m, const double* y, double sa, double sb, double* f) {
-    const double Ffx = strb(m.sx, y[1]);
-    const double Frx = strb(m.sx, fma(-m.r_x, y[7], y[1]));          // slip vx - r_x om_y
-    const double Ffy = strb(m.sy, y[3]);
-    const double Fry = strb(m.sy, fma(m.r_y, y[5], y[3]));           // slip vy - (-r_y om_x)
-    const double Tnx = strb(m.srx, y[5]);
-    const double Tny = strb(m.sry, y[7]);
-    const double tx = -m.r_y * Fry - Tnx - m.c_rx * y[5] - m.tqx * sin_any(y[4]);
-    const double ty = -m.r_x * Frx - Tny - m.c_ry * y[7] - m.tqy * sin_any(y[6]);
-    const double rx = m.m_x * (LM_G * sa) - m.c_x * y[1] - m.k_x * y[0] - Ffx - Frx;
-    const double ry = m.m_y * (LM_G * sb) - m.c_y * y[3] - m.k_y * y[2] - Ffy - Fry;
-    f[0] = y[1]; f[1] = rx * m.im_x; f[2] = y[3]; f[3] = ry * m.im_y;
-    f[4] = y[5]; f[5] = tx * m.iIx; f[6] = y[7]; f[7] = ty * m.iIy;
+// safe_dynamics (:260-429) of one subsystem: ydot for state y and tilt sine sa
+__device__ __forceinline__ void sub_f(const LmSub& m, const double* y, double sa, double* f) {
+    const double Ff = strb(m.st, y[1]);
+    const double Fr = strb(m.st, fma(m.rs, y[3], y[1]));
+    const double Tn = strb(m.sr, y[3]);
+    f[0] = y[1];
+    f[1] = (m.m * (LM_G * sa) - m.c * y[1] - m.k * y[0] - Ff - Fr) * m.im;
+    f[2] = y[3];
+    f[3] = (-m.r * Fr - Tn - m.crot * y[3] - m.tq * sin_any(y[2])) * m.iI;
 }
 
-__device__ __forceinline__ void lm_rk4(const LmModel& mlds, const double* x, double sa, double sb, double* xn) {
-    const LmModel m = mlds;     // model to registers once (LDS round trips off the stage chains)
-    double k[8], y[8], acc[8];
+__device__ __forceinline__ void sub_rk4(const LmSub& ml, const double* x, double sa, double* xn) {
+    const LmSub m = ml;         // model to registers once (LDS round trips off the stage chains)
+    double k[4], y[4], acc[4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { y[i] = x[i]; acc[i] = 0.0; }
+    for (int i = 0; i < 4; ++i) { y[i] = x[i]; acc[i] = 0.0; }
 #pragma unroll 1
     for (int s = 0; s < 4; ++s) {
         const double wts = (s == 0 || s == 3) ? 1.0 : 2.0, cst = s < 2 ? 0.5 : (s == 2 ? 1.0 : 0.0);
-        lm_f(m, y, sa, sb, k);
+        sub_f(m, y, sa, k);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { acc[i] = fma(wts, k[i], acc[i]); y[i] = fma(cst * m.h, k[i], x[i]); }
+        for (int i = 0; i < 4; ++i) { acc[i] = fma(wts, k[i], acc[i]); y[i] = fma(cst * m.h, k[i], x[i]); }
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) xn[i] = fma(m.h / 6.0, acc[i], x[i]);
+    for (int i = 0; i < 4; ++i) xn[i] = fma(m.h / 6.0, acc[i], x[i]);
 }
 
-// Value pass of RK4 that also stores, per stage s, the tangent coefficients sc[s][10] (the
-// nonzero entries of d f / d y at y_s) and the second-derivative data sd[s][8] = [S''(vx),
-// S''(slip x), S''(vy), S''(slip y), S''(om_x), S''(om_y), sin th_x, sin th_y].
-__device__ __forceinline__ void lm_rk4_lin(const LmModel& mlds, const double* x, double sa, double sb, double* xn,
-                                           double (*sc)[LM_NSC], double (*sd)[8]) {
-    const LmModel m = mlds;     // model to registers once: the stage loop reads every field ~4 times
-    double y[8], acc[8];
+// Value pass of RK4 that also stores, per stage s, the tangent coefficients
+// sc[s] = [dvdot/dv, dvdot/dom, domdot/dv, domdot/dth, domdot/dom] at y_s and the second-derivative
+// data sd[s] = [Ff''(v), Fr''(slip), Tn''(om), sin th].
+__device__ __forceinline__ void sub_rk4_lin(const LmSub& ml, const double* x, double sa, double* xn,
+                                            double (*sc)[LM_NSC], double (*sd)[4]) {
+    const LmSub m = ml;
+    double y[4], acc[4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { y[i] = x[i]; acc[i] = 0.0; }
+    for (int i = 0; i < 4; ++i) { y[i] = x[i]; acc[i] = 0.0; }
 #pragma unroll 1
     for (int s = 0; s < 4; ++s) {
         const double wts = (s == 0 || s == 3) ? 1.0 : 2.0, cst = s < 2 ? 0.5 : (s == 2 ? 1.0 : 0.0);
-        // each friction term's value / slope / curvature goes into k, sc, sd as soon as it exists
-        // (short live ranges: this pass runs under heavy register pressure)
-        double k[8];
-        k[0] = y[1]; k[2] = y[3]; k[4] = y[5]; k[6] = y[7];
-        {
-            double Sfx, Sfx1, Sfx2, Srx, Srx1, Srx2;
-            strb_d(m.sx, y[1], Sfx, Sfx1, Sfx2);
-            strb_d(m.sx, fma(-m.r_x, y[7], y[1]), Srx, Srx1, Srx2);
-            sd[s][0] = Sfx2; sd[s][1] = Srx2;
-            sc[s][0] = (-m.c_x - Sfx1 - Srx1) * m.im_x;
-            sc[s][1] = m.r_x * Srx1 * m.im_x;
-            sc[s][7] = -m.r_x * Srx1 * m.iIy;
-            k[1] = (m.m_x * (LM_G * sa) - m.c_x * y[1] - m.k_x * y[0] - Sfx - Srx) * m.im_x;
-            k[7] = -m.r_x * Srx;                                   // completed below
-            double Sny, Sny1, Sny2, sty, cty;
-            strb_d(m.sry, y[7], Sny, Sny1, Sny2);
-            sincos_any(y[6], sty, cty);
-            sd[s][5] = Sny2; sd[s][7] = sty;
-            sc[s][8] = (m.r_x * m.r_x * Srx1 - Sny1 - m.c_ry) * m.iIy;
-            sc[s][9] = -m.tqy * cty * m.iIy;
-            k[7] = (k[7] - Sny - m.c_ry * y[7] - m.tqy * sty) * m.iIy;
-        }
-        {
-            double Sfy, Sfy1, Sfy2, Sry, Sry1, Sry2;
-            strb_d(m.sy, y[3], Sfy, Sfy1, Sfy2);
-            strb_d(m.sy, fma(m.r_y, y[5], y[3]), Sry, Sry1, Sry2);
-            sd[s][2] = Sfy2; sd[s][3] = Sry2;
-            sc[s][2] = (-m.c_y - Sfy1 - Sry1) * m.im_y;
-            sc[s][3] = -m.r_y * Sry1 * m.im_y;
-            sc[s][4] = -m.r_y * Sry1 * m.iIx;
-            k[3] = (m.m_y * (LM_G * sb) - m.c_y * y[3] - m.k_y * y[2] - Sfy - Sry) * m.im_y;
-            k[5] = -m.r_y * Sry;                                   // completed below
-            double Snx, Snx1, Snx2, stx, ctx;
-            strb_d(m.srx, y[5], Snx, Snx1, Snx2);
-            sincos_any(y[4], stx, ctx);
-            sd[s][4] = Snx2; sd[s][6] = stx;
-            sc[s][5] = (-m.r_y * m.r_y * Sry1 - Snx1 - m.c_rx) * m.iIx;
-            sc[s][6] = -m.tqx * ctx * m.iIx;
-            k[5] = (k[5] - Snx - m.c_rx * y[5] - m.tqx * stx) * m.iIx;
-        }
+        double k[4];
+        k[0] = y[1]; k[2] = y[3];
+        double Sf, Sf1, Sf2, Sr, Sr1, Sr2, Sn, Sn1, Sn2, sth, cth;
+        strb_d(m.st, y[1], Sf, Sf1, Sf2);
+        strb_d(m.st, fma(m.rs, y[3], y[1]), Sr, Sr1, Sr2);
+        sd[s][0] = Sf2; sd[s][1] = Sr2;
+        sc[s][0] = (-m.c - Sf1 - Sr1) * m.im;
+        sc[s][1] = -m.rs * Sr1 * m.im;
+        sc[s][2] = -m.r * Sr1 * m.iI;
+        k[1] = (m.m * (LM_G * sa) - m.c * y[1] - m.k * y[0] - Sf - Sr) * m.im;
+        k[3] = -m.r * Sr;                                          // completed below
+        strb_d(m.sr, y[3], Sn, Sn1, Sn2);
+        sincos_any(y[2], sth, cth);
+        sd[s][2] = Sn2; sd[s][3] = sth;
+        sc[s][3] = -m.tq * cth * m.iI;
+        sc[s][4] = (m.rr2 * Sr1 - Sn1 - m.crot) * m.iI;
+        k[3] = (k[3] - Sn - m.crot * y[3] - m.tq * sth) * m.iI;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] = fma(wts, k[i], acc[i]);
+        for (int i = 0; i < 4; ++i) acc[i] = fma(wts, k[i], acc[i]);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) y[i] = fma(cst * m.h, k[i], x[i]);
+        for (int i = 0; i < 4; ++i) y[i] = fma(cst * m.h, k[i], x[i]);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) xn[i] = fma(m.h / 6.0, acc[i], x[i]);
+    for (int i = 0; i < 4; ++i) xn[i] = fma(m.h / 6.0, acc[i], x[i]);
 }
 
 // q = (d f / d y at stage s)^T v from the stage's tangent coefficients
-__device__ __forceinline__ void lm_jtv(const LmModel& m, const double* c, const double* v, double* q) {
-    const double kx1 = -m.k_x * m.im_x, ky3 = -m.k_y * m.im_y;
+__device__ __forceinline__ void sub_jtv(double kx1, const double* c, const double* v, double* q) {
     q[0] = kx1 * v[1];
-    q[1] = fma(c[0], v[1], fma(c[7], v[7], v[0]));
-    q[2] = ky3 * v[3];
-    q[3] = fma(c[2], v[3], fma(c[4], v[5], v[2]));
-    q[4] = c[6] * v[5];
-    q[5] = fma(c[3], v[3], fma(c[5], v[5], v[4]));
-    q[6] = c[9] * v[7];
-    q[7] = fma(c[1], v[1], fma(c[8], v[7], v[6]));
+    q[1] = fma(c[0], v[1], fma(c[2], v[3], v[0]));
+    q[2] = c[3] * v[3];
+    q[3] = fma(c[1], v[1], fma(c[4], v[3], v[2]));
 }
 
 // First-order adjoint of L = nl^T x+ (nl = -lambda_{k+1}) through the four RK4 stages; converts the
 // stage second-derivative data sd[s] in place into the curvature coefficients of kb_s^T f'' at y_s:
-// [A1, A2, A3, B1, B2, B3, C1, C2] with (vx, om_y) block [[A1, A2], [A2, A3]], (vy, om_x) block
-// [[B1, B2], [B2, B3]], th_x: C1, th_y: C2; returns the tilt curvature huu[2] = sum_s kb_s^T f_uu.
-__device__ __forceinline__ void lm_adjoint_curv(const LmModel& m, const double (*sc)[LM_NSC], double (*sd)[8],
-                                                const double* lamn, double sa, double sb, double* huu) {
-    double kb[8], yb[8];
-    const double h = m.h;
+// [A1, A2, A3, C] with the (v, om) block [[A1, A2], [A2, A3]] and th: C; returns the tilt
+// curvature huu = sum_s kb_s^T f_aa.
+__device__ __forceinline__ double sub_adjoint_curv(const LmSub& m, const double (*sc)[LM_NSC], double (*sd)[4],
+                                                   const double* lamn, double sa) {
+    double kb[4], yb[4];
+    const double h = m.h, kx1 = -m.k * m.im;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) kb[i] = -(h / 6.0) * lamn[i];        // kb_4
-    huu[0] = 0.0; huu[1] = 0.0;
+    for (int i = 0; i < 4; ++i) kb[i] = -(h / 6.0) * lamn[i];        // kb_4
+    double huu = 0.0;
 #pragma unroll 1
     for (int s = 3; s >= 0; --s) {
         double* d = sd[s];
-        const double c_vx = kb[1] * (-d[0] * m.im_x);
-        const double c_sx = kb[1] * (-d[1] * m.im_x) + kb[7] * (-m.r_x * d[1] * m.iIy);
-        const double c_vy = kb[3] * (-d[2] * m.im_y);
-        const double c_sy = kb[3] * (-d[3] * m.im_y) + kb[5] * (-m.r_y * d[3] * m.iIx);
-        const double c_ox = kb[5] * (-d[4] * m.iIx);
-        const double c_oy = kb[7] * (-d[5] * m.iIy);
-        const double c_tx = kb[5] * (m.tqx * d[6] * m.iIx);
-        const double c_ty = kb[7] * (m.tqy * d[7] * m.iIy);
-        d[0] = c_vx + c_sx; d[1] = -m.r_x * c_sx; d[2] = fma(m.r_x * m.r_x, c_sx, c_oy);
-        d[3] = c_vy + c_sy; d[4] = m.r_y * c_sy; d[5] = fma(m.r_y * m.r_y, c_sy, c_ox);
-        d[6] = c_tx; d[7] = c_ty;
-        huu[0] = fma(kb[1], -LM_G * sa, huu[0]);
-        huu[1] = fma(kb[3], -LM_G * sb, huu[1]);
+        const double c_v = kb[1] * (-d[0] * m.im);
+        const double c_s = kb[1] * (-d[1] * m.im) + kb[3] * (-m.r * d[1] * m.iI);
+        const double c_o = kb[3] * (-d[2] * m.iI);
+        const double c_t = kb[3] * (m.tq * d[3] * m.iI);
+        d[0] = c_v + c_s; d[1] = m.rs * c_s; d[2] = fma(m.rs * m.rs, c_s, c_o); d[3] = c_t;
+        huu = fma(kb[1], -LM_G * sa, huu);
         if (s > 0) {      // kb_{s-1} = w_{s-1} h/6 nl + c_s h J_s^T kb_s  (c = 1, 1/2, 1/2 for s = 3, 2, 1)
-            lm_jtv(m, sc[s], kb, yb);
+            sub_jtv(kx1, sc[s], kb, yb);
             const double cs = s == 3 ? h : 0.5 * h, ws = (s == 1 ? 1.0 : 2.0) * h / 6.0;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) kb[i] = fma(cs, yb[i], -ws * lamn[i]);
+            for (int i = 0; i < 4; ++i) kb[i] = fma(cs, yb[i], -ws * lamn[i]);
         }
     }
+    return huu;
 }
 
-// Direction d (0..7 state, 8..9 tilt): tangent of RK4 -> column d of the step Jacobian (written to
+// Direction d (0..3 state, 4 tilt): tangent of RK4 -> column d of the step Jacobian (written to
 // column jc(d) of M~, returns col . lamn), then the second-order adjoint sweep back through the
 // stages -> column d of the exact Hessian of -lambda^T x+ over z = [x; u], written to the packed
 // stage Hessian (rows i >= d).
-__device__ __forceinline__ double lm_direction(const LmModel& m, const double (*sc)[LM_NSC], const double (*cv)[8],
-                                               const double* huu, double gca, double gcb, int d, const double* lamn,
-                                               double* Mk, double* Hk) {
-    double yd[4][8], acc[8], e[8];
+__device__ __forceinline__ double sub_direction(const LmSub& m, const double (*sc)[LM_NSC], const double (*cv)[4],
+                                                double huu, double gca, int d, const double* lamn, double* Mk,
+                                                double* Hk) {
+    double yd[4][4], acc[4], e[4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { e[i] = (i == d) ? 1.0 : 0.0; yd[0][i] = e[i]; acc[i] = 0.0; }
-    const double fa = d == 8 ? gca : 0.0, fb = d == 9 ? gcb : 0.0;
-    const double kx1 = -m.k_x * m.im_x, ky3 = -m.k_y * m.im_y;
+    for (int i = 0; i < 4; ++i) { e[i] = (i == d) ? 1.0 : 0.0; yd[0][i] = e[i]; acc[i] = 0.0; }
+    const double fa = d == 4 ? gca : 0.0;
+    const double kx1 = -m.k * m.im;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const double wts = (s == 0 || s == 3) ? 1.0 : 2.0, cst = s < 2 ? 0.5 : (s == 2 ? 1.0 : 0.0);
         const double* c = sc[s];
         const double* y = yd[s];
-        double k[8];
-        k[0] = y[1]; k[2] = y[3]; k[4] = y[5]; k[6] = y[7];
-        k[1] = fma(kx1, y[0], fma(c[0], y[1], fma(c[1], y[7], fa)));
-        k[3] = fma(ky3, y[2], fma(c[2], y[3], fma(c[3], y[5], fb)));
-        k[5] = fma(c[4], y[3], fma(c[5], y[5], c[6] * y[4]));
-        k[7] = fma(c[7], y[1], fma(c[8], y[7], c[9] * y[6]));
+        double k[4];
+        k[0] = y[1]; k[2] = y[3];
+        k[1] = fma(kx1, y[0], fma(c[0], y[1], fma(c[1], y[3], fa)));
+        k[3] = fma(c[2], y[1], fma(c[4], y[3], c[3] * y[2]));
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] = fma(wts, k[i], acc[i]);
+        for (int i = 0; i < 4; ++i) acc[i] = fma(wts, k[i], acc[i]);
         if (s < 3) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) yd[s + 1][i] = fma(cst * m.h, k[i], e[i]);
+            for (int i = 0; i < 4; ++i) yd[s + 1][i] = fma(cst * m.h, k[i], e[i]);
         }
     }
-    const int jc = d < 8 ? d : d + 2;
+    const int jc = d < 4 ? d : 5;
     double dot = 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 4; ++i) {
         const double col = fma(m.h / 6.0, acc[i], e[i]);
         Mk[jc * LmLds::NC + i] = col;
         dot = fma(col, lamn[i], dot);
     }
-    // second-order adjoint: kbd_s = d/dd kb_s, ybd_s = J_s^T kbd_s + (kb_s^T f'')_s yd_s
-    double kbd[8], hx[8], hu0 = d == 8 ? huu[0] : 0.0, hu1 = d == 9 ? huu[1] : 0.0;
+    // second-order adjoint: kbd_s = d/dd kb_s, q_s = J_s^T kbd_s + (kb_s^T f'')_s yd_s
+    double kbd[4], hx[4], hu = d == 4 ? huu : 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { kbd[i] = 0.0; hx[i] = 0.0; }
+    for (int i = 0; i < 4; ++i) { kbd[i] = 0.0; hx[i] = 0.0; }
 #pragma unroll
     for (int s = 3; s >= 0; --s) {
         const double* cc = cv[s];
         const double* y = yd[s];
-        double q[8];
-        lm_jtv(m, sc[s], kbd, q);
-        q[1] = fma(cc[0], y[1], fma(cc[1], y[7], q[1]));
-        q[7] = fma(cc[1], y[1], fma(cc[2], y[7], q[7]));
-        q[3] = fma(cc[3], y[3], fma(cc[4], y[5], q[3]));
-        q[5] = fma(cc[4], y[3], fma(cc[5], y[5], q[5]));
-        q[4] = fma(cc[6], y[4], q[4]);
-        q[6] = fma(cc[7], y[6], q[6]);
-        hu0 = fma(gca, kbd[1], hu0);
-        hu1 = fma(gcb, kbd[3], hu1);
+        double q[4];
+        sub_jtv(kx1, sc[s], kbd, q);
+        q[1] = fma(cc[0], y[1], fma(cc[1], y[3], q[1]));
+        q[3] = fma(cc[1], y[1], fma(cc[2], y[3], q[3]));
+        q[2] = fma(cc[3], y[2], q[2]);
+        hu = fma(gca, kbd[1], hu);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) hx[i] += q[i];
+        for (int i = 0; i < 4; ++i) hx[i] += q[i];
         const double cs = s == 3 ? m.h : 0.5 * m.h;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) kbd[i] = cs * q[i];
+        for (int i = 0; i < 4; ++i) kbd[i] = cs * q[i];
     }
-    // rows i >= d of column d (z indices: x 0..7, tilt 10, 11)
-    const int zd = jc;
+    // rows i >= d of column d (z indices: x 0..3, up 4, tilt 5)
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-        if (i >= d) Hk[hp(i, zd)] = hx[i];
-    Hk[hp(10, zd)] = hu0;
-    Hk[hp(11, zd)] = hu1;
+    for (int i = 0; i < 4; ++i)
+        if (i >= d) Hk[hp(i, jc)] = hx[i];
+    Hk[hp(5, jc)] = hu;
     return dot;
-}
-
-// all ten directions, one at a time; J^T lambda_{k+1} into jl[10]
-__device__ __forceinline__ void lm_directions(const LmModel& m, const double (*sc)[LM_NSC], const double (*cv)[8],
-                                              const double* huu, double gca, double gcb, const double* lamn, double* Mk,
-                                              double* Hk, double* jl, double* jl_lds) {
-#pragma unroll 1
-    for (int d = 0; d < 10; ++d) jl_lds[d] = lm_direction(m, sc, cv, huu, gca, gcb, d, lamn, Mk, Hk);
-#pragma unroll
-    for (int d = 0; d < 10; ++d) jl[d] = jl_lds[d];
-}
-
-// directions d0 .. d0+4 of one node (the two half-waves of the wave split the ten directions);
-// per-node inputs from LDS: dl = [lambda_{k+1}(10), huu(2), g cos a, g cos b]
-__device__ __forceinline__ void lm_directions_half(const LmModel& m, const double (*sc)[LM_NSC], const double (*cv)[8],
-                                                   const double* dl, int d0, double* Mk, double* Hk, double* jl_lds) {
-    double lamn[10], huu[2];
-#pragma unroll
-    for (int i = 0; i < 10; ++i) lamn[i] = dl[i];
-    huu[0] = dl[10]; huu[1] = dl[11];
-    const double gca = dl[12], gcb = dl[13];
-    const LmModel mr = m;       // model to registers once for the five directions
-#pragma unroll 1
-    for (int d = d0; d < d0 + 5; ++d) jl_lds[d] = lm_direction(mr, sc, cv, huu, gca, gcb, d, lamn, Mk, Hk);
 }
 
 __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     LmShared& SH = *reinterpret_cast<LmShared*>(smem);
     LmLds* S = &SH.ocp;
-    const Riccati3Roles<LmLds> RR = riccati3_roles<LmLds>();
+    const RiccatiSRoles RR = riccati_s_roles<LmLds>();
     STAMP_DECL
     if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
     const int b = blockIdx.x / a.pack;
-    const int k = threadIdx.x;
+    const int lane = threadIdx.x;
+    const int hf = lane >> 5;                  // subsystem: 0 = x [px, vx, th_y, om_y; a], 1 = y [py, vy, th_x, om_x; b]
+    const int k = lane & 31;                   // shooting node
+    const int sl = hf * LM_NMAXS + k;          // node slot of this lane (every lane owns one)
     const int N = a.N;
     const bool xon = k <= N, uon = k < N;
-    const int sr = xon ? k : LM_NMAXS;        // per-node LDS scratch row (idle lanes share row 32)
     constexpr int NC = LmLds::NC;
+    // full-state index of the subsystem's local state i
+    auto gidx = [&](int i) { return hf == 0 ? (i == 0 ? 0 : i == 1 ? 1 : i == 2 ? 6 : 7) : (i == 0 ? 2 : i == 1 ? 3 : i == 2 ? 4 : 5); };
 
-    // ---------------- model parameters (uniform, staged in LDS) -------------------------------
-    if (k == 0) {
-        LmModel& m = SH.model;
+    // ---------------- model parameters (uniform per half, staged in LDS) -----------------------
+    if (lane == 0 || lane == 32) {
+        LmSub& m = SH.sub[hf];
         const double* p = a.pvec + LM_NPV * b;
-        m.m_x = sq(p[0]); m.m_y = sq(p[1]); m.im_x = 1.0 / m.m_x; m.im_y = 1.0 / m.m_y;
-        m.c_x = sq(p[2]); m.c_y = sq(p[3]); m.k_x = sq(p[4]); m.k_y = sq(p[5]);
-        m.sx = make_strb(p[6], p[7], p[8], sq(p[9]), sq(p[10]));
-        m.sy = make_strb(p[11], p[12], p[13], sq(p[14]), sq(p[15]));
-        m.iIx = 1.0 / (sq(p[16]) + 1e-12); m.iIy = 1.0 / (sq(p[17]) + 1e-12);
-        m.r_x = sq(p[18]); m.r_y = sq(p[19]); m.c_rx = sq(p[20]); m.c_ry = sq(p[21]);
-        m.srx = make_strb(p[22], p[23], p[24], sq(p[25]), sq(p[26]));
-        m.sry = make_strb(p[27], p[28], p[29], sq(p[30]), sq(p[31]));
-        m.tqx = m.m_y * LM_G * sq(p[32]); m.tqy = m.m_x * LM_G * sq(p[33]);
-        m.h = a.Ts;
-        for (int i = 0; i < 8; ++i) {
-            SH.Q[i] = a.prm[LM_NPRM * b + i]; SH.Qt[i] = a.prm[LM_NPRM * b + 8 + i]; SH.tgt[i] = a.target[8 * b + i];
+        const double m_x = sq(p[0]), m_y = sq(p[1]);
+        if (hf == 0) {     // x: m_x, c_x, k_x, Stribeck x, I_y, r_x, c_rot_y, rotational Stribeck y, h_com_y
+            m.m = m_x; m.c = sq(p[2]); m.k = sq(p[4]);
+            m.st = make_strb(p[6], p[7], p[8], sq(p[9]), sq(p[10]));
+            m.iI = 1.0 / (sq(p[17]) + 1e-12);
+            m.r = sq(p[18]); m.rs = -m.r; m.crot = sq(p[21]);
+            m.sr = make_strb(p[27], p[28], p[29], sq(p[30]), sq(p[31]));
+            m.tq = m_x * LM_G * sq(p[33]);
+        } else {           // y: m_y, c_y, k_y, Stribeck y, I_x, r_y, c_rot_x, rotational Stribeck x, h_com_x
+            m.m = m_y; m.c = sq(p[3]); m.k = sq(p[5]);
+            m.st = make_strb(p[11], p[12], p[13], sq(p[14]), sq(p[15]));
+            m.iI = 1.0 / (sq(p[16]) + 1e-12);
+            m.r = sq(p[19]); m.rs = m.r; m.crot = sq(p[20]);
+            m.sr = make_strb(p[22], p[23], p[24], sq(p[25]), sq(p[26]));
+            m.tq = m_y * LM_G * sq(p[32]);
         }
+        m.im = 1.0 / m.m;
+        m.rr2 = -m.r * m.rs;
+        m.h = a.Ts;
     }
     __syncthreads();
-    const LmModel& m = SH.model;
-    const double* Q = SH.Q;
-    const double* tgt = SH.tgt;
-    const double* Wq = k < N ? SH.Q : SH.Qt;     // stage or terminal weights (lane N is the terminal node)
-    const double* Qt = SH.Qt;
+    const LmSub& m = SH.sub[hf];
     const double* pr = a.prm + LM_NPRM * b;
-    const double R0 = pr[16], R1 = pr[17], R2 = pr[18], R3 = pr[19];
+    double Wq[4], tg[4], Qtv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int gi = gidx(i);
+        Qtv[i] = pr[8 + gi];
+        Wq[i] = k < N ? pr[gi] : Qtv[i];       // stage or terminal weights (lane N is the terminal node)
+        tg[i] = a.target[8 * b + gi];
+    }
+    const double Ru = pr[16 + hf], Rdu = pr[18 + hf];
     const double ulo = pr[20], uhi = pr[21];
 
     const double lo = ulo - 1e-8 * fmax(1.0, fabs(ulo)), hi = uhi + 1e-8 * fmax(1.0, fabs(uhi));
     const bool poly = fmax(fabs(lo), fabs(hi)) <= 1.0;
 
     // ---------------- constant structure of the stage blocks ------------------------------------
-    double* Mk = &S->M[xon ? k : 0][0][0];
-    double* Hk = S->H[xon ? k : 0];
+    double* Mk = &S->M[sl][0][0];
+    double* Hk = S->H[sl];
     if (uon) {
         for (int e = 0; e < LmLds::ND * NC; ++e) Mk[e] = 0.0;
         for (int e = 0; e < LmLds::NTP; ++e) Hk[e] = 0.0;
-        Mk[10 * NC + 8] = 1.0; Mk[11 * NC + 9] = 1.0;     // up+ = u
-        Mk[12 * NC + 10] = 1.0;                            // homogeneous coordinate
+        Mk[5 * NC + 4] = 1.0;                 // up+ = u
+        Mk[6 * NC + 5] = 1.0;                 // homogeneous coordinate
     }
 
-    // ---------------- initial point (lane k = node k) --------------------------------------------
-    const double* st0 = a.state + 8 * b;
-    const double* upv = a.u_prev + 2 * b;
+    // ---------------- initial point (lane 32 h + k = node k of subsystem h) -----------------------
+    const double* st0g = a.state + 8 * b;
+    double st0[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st0[i] = st0g[gidx(i)];
+    const double upv = a.u_prev[2 * b + hf];
     const int nw = 8 * (N + 1) + 2 * N;
     const double* ww = a.w_warm ? a.w_warm + (size_t)nw * b : nullptr;
-    double x[8], up[2], u[2], lam[10], zl[2], zu[2];
+    double x[4], up, u, lam[5], zl, zu;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = xon && ww ? ww[8 * k + i] : 0.0;   // warm start w0 (zeros first, :492)
+    for (int i = 0; i < 4; ++i) x[i] = xon && ww ? ww[8 * k + gidx(i)] : 0.0;   // warm start w0 (zeros first, :492)
     const double pushl = fmin(1e-2 * fmax(1.0, fabs(lo)), 1e-2 * (hi - lo));
     const double pushu = fmin(1e-2 * fmax(1.0, fabs(hi)), 1e-2 * (hi - lo));
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const double t = uon && ww ? ww[8 * (N + 1) + 2 * k + j] : 0.0;
-        u[j] = uon ? fmin(fmax(t, lo + pushl), hi - pushu) : 0.0;
-        zl[j] = uon ? 1.0 : 0.0; zu[j] = uon ? 1.0 : 0.0;
+    {
+        const double t = uon && ww ? ww[8 * (N + 1) + 2 * k + hf] : 0.0;
+        u = uon ? fmin(fmax(t, lo + pushl), hi - pushu) : 0.0;
+        zl = uon ? 1.0 : 0.0; zu = uon ? 1.0 : 0.0;
     }
     {
-        const double p0 = from_prev(u[0]), p1 = from_prev(u[1]);
-        up[0] = k == 0 ? upv[0] : p0;
-        up[1] = k == 0 ? upv[1] : p1;
+        const double p0 = from_prev(u);
+        up = k == 0 ? upv : p0;
     }
 #pragma unroll
-    for (int i = 0; i < 10; ++i) lam[i] = 0.0;
+    for (int i = 0; i < 5; ++i) lam[i] = 0.0;
 
-    auto cost_grad = [&](const double* xx, const double* uu, const double* pp, double* g) {
+    auto cost_grad = [&](const double* xx, double uu, double pp, double* g) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) g[i] = 2.0 * Wq[i] * (xx[i] - tgt[i]);
-        const double d0 = uu[0] - pp[0], d1 = uu[1] - pp[1];
-        g[8] = uon ? -2.0 * R2 * d0 : 0.0; g[9] = uon ? -2.0 * R3 * d1 : 0.0;
-        g[10] = uon ? fma(2.0 * R0, uu[0], 2.0 * R2 * d0) : 0.0;
-        g[11] = uon ? fma(2.0 * R1, uu[1], 2.0 * R3 * d1) : 0.0;
+        for (int i = 0; i < 4; ++i) g[i] = 2.0 * Wq[i] * (xx[i] - tg[i]);
+        const double d0 = uu - pp;
+        g[4] = uon ? -2.0 * Rdu * d0 : 0.0;
+        g[5] = uon ? fma(2.0 * Ru, uu, 2.0 * Rdu * d0) : 0.0;
     };
-    auto cost_val = [&](const double* xx, const double* uu, const double* pp) {
+    auto cost_val = [&](const double* xx, double uu, double pp) {
         double f = 0.0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) f = fma(Wq[i] * (xx[i] - tgt[i]), xx[i] - tgt[i], f);
-        const double d0 = uu[0] - pp[0], d1 = uu[1] - pp[1];
-        const double fu = R0 * uu[0] * uu[0] + R1 * uu[1] * uu[1] + R2 * d0 * d0 + R3 * d1 * d1;
+        for (int i = 0; i < 4; ++i) f = fma(Wq[i] * (xx[i] - tg[i]), xx[i] - tg[i], f);
+        const double d0 = uu - pp;
+        const double fu = Ru * uu * uu + Rdu * d0 * d0;
         return xon ? f + (uon ? fu : 0.0) : 0.0;
     };
     // incoming augmented defect g_k of node k for a trial point (value-only RK4 of lane k-1)
-    auto defects = [&](const double* xx, const double* pp, const double* uu, double* g) {
-        double sa, ca, sb, cb, xn[8];
-        tilt_sincos(poly, uu[0], sa, ca);
-        tilt_sincos(poly, uu[1], sb, cb);
-        lm_rk4(m, xx, sa, sb, xn);
-        double f[10];
+    auto defects = [&](const double* xx, double pp, double uu, double* g) {
+        double sa, ca, xn[4];
+        tilt_sincos(poly, uu, sa, ca);
+        sub_rk4(m, xx, sa, xn);
+        double f[5];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) f[i] = from_prev(xn[i]);
-        f[8] = from_prev(uu[0]); f[9] = from_prev(uu[1]);
+        for (int i = 0; i < 4; ++i) f[i] = from_prev(xn[i]);
+        f[4] = from_prev(uu);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) g[i] = k == 0 ? xx[i] - st0[i] : xx[i] - f[i];
-        g[8] = k == 0 ? pp[0] - upv[0] : pp[0] - f[8];
-        g[9] = k == 0 ? pp[1] - upv[1] : pp[1] - f[9];
+        for (int i = 0; i < 4; ++i) g[i] = k == 0 ? xx[i] - st0[i] : xx[i] - f[i];
+        g[4] = k == 0 ? pp - upv : pp - f[4];
     };
 
     // objective scaling (max |grad f| at the start point), constraint-row scaling (max |grad g_i|)
     double gmax = 0.0;
     {
-        double g[12];
+        double g[6];
         cost_grad(x, u, up, g);
 #pragma unroll
-        for (int i = 0; i < 12; ++i) gmax = fmax(gmax, xon ? fabs(g[i]) : 0.0);
+        for (int i = 0; i < 6; ++i) gmax = fmax(gmax, xon ? fabs(g[i]) : 0.0);
     }
     gmax = wmax(gmax);
     const double sc = gmax > 100.0 ? 100.0 / gmax : 1.0;
 
-    double dsc[8];          // scaling of the incoming physical defect rows of node k (up rows: 1)
+    double dsc[4];          // scaling of the incoming physical defect rows of node k (up row: 1)
     {
-        double sa, ca, sb, cb, xn[8], huu[2];
-        const double lz[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        tilt_sincos(poly, u[0], sa, ca);
-        tilt_sincos(poly, u[1], sb, cb);
-        lm_rk4_lin(m, x, sa, sb, xn, SH.SC[sr], SH.SD[sr]);
-        lm_adjoint_curv(m, SH.SC[sr], SH.SD[sr], lz, sa, sb, huu);
-        double* Mt = &S->M[xon ? k : 0][0][0];
+        double sa, ca, xn[4];
+        const double lz[5] = {0, 0, 0, 0, 0};
+        tilt_sincos(poly, u, sa, ca);
+        sub_rk4_lin(m, x, sa, xn, SH.SC[sl], SH.SD[sl]);
+        const double huu = sub_adjoint_curv(m, SH.SC[sl], SH.SD[sl], lz, sa);
         if (uon) {
-            double jl0[10];
-            lm_directions(m, SH.SC[sr], SH.SD[sr], huu, LM_G * ca, LM_G * cb, lz, Mt, Hk, jl0, SH.JL[sr]);
+            const LmSub mr = m;
+#pragma unroll 1
+            for (int d = 0; d < 5; ++d) sub_direction(mr, SH.SC[sl], SH.SD[sl], huu, LM_G * ca, d, lz, Mk, Hk);
         }
-        double rs[8];
+        double rs[4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < 4; ++i) {
             double mx = 1.0;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) mx = fmax(mx, fabs(Mt[j * NC + i]));
-            mx = fmax(mx, fmax(fabs(Mt[10 * NC + i]), fabs(Mt[11 * NC + i])));
+            for (int j = 0; j < 4; ++j) mx = fmax(mx, fabs(Mk[j * NC + i]));
+            mx = fmax(mx, fabs(Mk[5 * NC + i]));
             rs[i] = uon ? (mx > 100.0 ? 100.0 / mx : 1.0) : 1.0;
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { const double t = from_prev(rs[i]); dsc[i] = k == 0 ? 1.0 : t; }
+        for (int i = 0; i < 4; ++i) { const double t = from_prev(rs[i]); dsc[i] = k == 0 ? 1.0 : t; }
     }
 
     const double tol = a.tol, mu_min = tol / 10;
-    const double nA = 10.0 * (N + 1), nb = 4.0 * N;
+    const double nA = 10.0 * (N + 1), nb = 4.0 * N;     // IPOPT's counts on the full NLP
     const double gam_th = 1e-5, gam_ph = 1e-8, s_th = 1.1, s_ph = 2.3, eta_ph = 1e-8, gam_al = 0.05;
 
     auto theta_of = [&](const double* g) {
         double t = 0.0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) t = fma(dsc[i], fabs(g[i]), t);
-        return xon ? t + fabs(g[8]) + fabs(g[9]) : 0.0;
+        for (int i = 0; i < 4; ++i) t = fma(dsc[i], fabs(g[i]), t);
+        return xon ? t + fabs(g[4]) : 0.0;
     };
     double theta;
     {
-        double g0[10];
+        double g0[5];
         defects(x, up, u, g0);
         theta = wsum(theta_of(g0));
     }
     const double th_max = 1e4 * fmax(1.0, theta), th_min = 1e-4 * fmax(1.0, theta);
-    double fth = 0.0, fph = 0.0;
+    double fth = 0.0, fph = 0.0;      // filter entry held by lane (slot = lane id)
     int nfilt = 0, acc_count = 0;
     double mu = 0.1, delta_last = 0.0;
     int status = -1, it = 0;
@@ -511,99 +462,82 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     STAMP(0);
     for (it = 0;; ++it) {
         // ---------------- derivatives, residuals, optimality error ---------------------------
-        // The stage data go to LDS as soon as they exist (H without its gradient row, the
-        // columns of M~, the defect column, dx~_0) to keep the register working set small.
-        const double isl0 = uon ? frcp(u[0] - lo) : 0.0, isl1 = uon ? frcp(u[1] - lo) : 0.0;
-        const double isu0 = uon ? frcp(hi - u[0]) : 0.0, isu1 = uon ? frcp(hi - u[1]) : 0.0;
-        double lamn[10];
+        const double isl = uon ? frcp(u - lo) : 0.0, isu = uon ? frcp(hi - u) : 0.0;
+        double lamn[5];
 #pragma unroll
-        for (int i = 0; i < 10; ++i) { const double t = from_next(lam[i]); lamn[i] = uon ? t : 0.0; }
-        double jl[10];      // J^T lambda_{k+1} (x columns 0..7, tilt 8..9)
+        for (int i = 0; i < 5; ++i) { const double t = from_next(lam[i]); lamn[i] = uon ? t : 0.0; }
+        double jl[5];       // J^T lambda_{k+1} (x columns 0..3, tilt 4)
         {
-            double sa, ca, sb, cb;
-            tilt_sincos(poly, u[0], sa, ca);
-            tilt_sincos(poly, u[1], sb, cb);
-            double xn[8];
-            lm_rk4_lin(m, x, sa, sb, xn, SH.SC[sr], SH.SD[sr]);
+            double sa, ca;
+            tilt_sincos(poly, u, sa, ca);
+            double xn[4];
+            sub_rk4_lin(m, x, sa, xn, SH.SC[sl], SH.SD[sl]);
             {
-                double huu[2];
-                lm_adjoint_curv(m, SH.SC[sr], SH.SD[sr], lamn, sa, sb, huu);
-                if (k < 32) {
-#pragma unroll
-                    for (int i = 0; i < 10; ++i) SH.DL[k][i] = lamn[i];
-                    SH.DL[k][10] = huu[0]; SH.DL[k][11] = huu[1]; SH.DL[k][12] = LM_G * ca; SH.DL[k][13] = LM_G * cb;
-                }
-                __syncthreads();
+                const double huu = sub_adjoint_curv(m, SH.SC[sl], SH.SD[sl], lamn, sa);
                 STAMP(13);
-                {   // exact dynamics Hessian (x, u blocks) and the Jacobian columns: lanes k and k + 32 take
-                    // directions 0..4 and 5..9 of node k
-                    const int kn = k & 31;
-                    if (kn < N)
-                        lm_directions_half(m, SH.SC[kn], SH.SD[kn], SH.DL[kn], k < 32 ? 0 : 5, &S->M[kn][0][0], S->H[kn],
-                                           SH.JL[kn]);
-                }
-                __syncthreads();
-                STAMP(14);
+                // exact dynamics Hessian (x, u blocks) and the Jacobian columns of node k
                 if (uon) {
-                    // the cost / barrier terms: z = [x(8), up(2), u(2), 1], gradient row later
+                    const LmSub mr = m;     // model to registers once for the five directions
+#pragma unroll 1
+                    for (int d = 0; d < 5; ++d)
+                        SH.JL[sl][d] = sub_direction(mr, SH.SC[sl], SH.SD[sl], huu, LM_G * ca, d, lamn, Mk, Hk);
 #pragma unroll
-                    for (int i = 0; i < 10; ++i) jl[i] = SH.JL[sr][i];
+                    for (int d = 0; d < 5; ++d) jl[d] = SH.JL[sl][d];
+                    // the cost / barrier terms: z = [x(4), up, u, 1], gradient row later
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) Hk[hp(i, i)] += sc * 2.0 * Q[i];
-                    Hk[hp(8, 8)] = sc * 2.0 * R2; Hk[hp(9, 9)] = sc * 2.0 * R3;
-                    Hk[hp(10, 10)] += sc * 2.0 * (R0 + R2) + zl[0] * isl0 + zu[0] * isu0;
-                    Hk[hp(11, 11)] += sc * 2.0 * (R1 + R3) + zl[1] * isl1 + zu[1] * isu1;
-                    Hk[hp(10, 8)] = -sc * 2.0 * R2; Hk[hp(11, 9)] = -sc * 2.0 * R3;
+                    for (int i = 0; i < 4; ++i) Hk[hp(i, i)] += sc * 2.0 * Wq[i];
+                    Hk[hp(4, 4)] = sc * 2.0 * Rdu;
+                    Hk[hp(5, 5)] += sc * 2.0 * (Ru + Rdu) + zl * isl + zu * isu;
+                    Hk[hp(5, 4)] = -sc * 2.0 * Rdu;
                 } else {
 #pragma unroll
-                    for (int i = 0; i < 10; ++i) jl[i] = 0.0;
+                    for (int i = 0; i < 5; ++i) jl[i] = 0.0;
                 }
+                STAMP(14);
             }
             // outgoing augmented defect c_k = [F(z_k); u_k] - x~_{k+1} -> defect column of M~
-            double cdef[10];
+            double cdef[5];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) { const double t = from_next(x[i]); cdef[i] = xn[i] - t; }
-            { const double t0 = from_next(up[0]), t1 = from_next(up[1]); cdef[8] = u[0] - t0; cdef[9] = u[1] - t1; }
+            for (int i = 0; i < 4; ++i) { const double t = from_next(x[i]); cdef[i] = xn[i] - t; }
+            { const double t0 = from_next(up); cdef[4] = u - t0; }
             if (uon) {
 #pragma unroll
-                for (int r = 0; r < 10; ++r) Mk[12 * NC + r] = cdef[r];
+                for (int r = 0; r < 5; ++r) Mk[6 * NC + r] = cdef[r];
             }
             // incoming defect g_k: primal residuals now, -g_0 = dx~_0 for the forward sweep
             double pl = 0.0, plu = 0.0;
 #pragma unroll
-            for (int i = 0; i < 10; ++i) {
+            for (int i = 0; i < 5; ++i) {
                 const double t = from_prev(cdef[i]);
                 double gi = -t;
-                if (k == 0) gi = i < 8 ? x[i] - st0[i] : up[i - 8] - upv[i - 8];
-                const double d = i < 8 ? dsc[i] : 1.0;
+                if (k == 0) gi = i < 4 ? x[i] - st0[i] : up - upv;
+                const double d = i < 4 ? dsc[i] : 1.0;
                 pl = fmax(pl, xon ? d * fabs(gi) : 0.0);
                 plu = fmax(plu, xon ? fabs(gi) : 0.0);
-                if (k == 0) S->dx0[i] = -gi;
-                SH.CS[sr][i] = gi;       // c(x) for a second-order correction
+                if (k == 0) S->dx0[hf][i] = -gi;
+                SH.CS[sl][i] = gi;       // c(x) for a second-order correction
             }
-            SH.JL[sr][10] = pl; SH.JL[sr][11] = plu;    // primal residual maxima (LDS: frees registers)
+            SH.JL[sl][5] = pl; SH.JL[sl][6] = plu;      // primal residual maxima (LDS: frees registers)
         }
         double dinf = 0.0, c0 = 0.0, cmin = 1e300, suml = 0.0, sumz = 0.0;
-        double pinf = SH.JL[sr][10], pinf_u = SH.JL[sr][11];
+        double pinf = SH.JL[sl][5], pinf_u = SH.JL[sl][6];
         {
-            double gl[12];
+            double gl[6];
             cost_grad(x, u, up, gl);
 #pragma unroll
-            for (int j = 0; j < 12; ++j) gl[j] *= sc;
+            for (int j = 0; j < 6; ++j) gl[j] *= sc;
 #pragma unroll
-            for (int i = 0; i < 10; ++i) gl[i] += lam[i];
+            for (int i = 0; i < 5; ++i) gl[i] += lam[i];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) gl[j] -= jl[j];
-            gl[10] -= jl[8] + lamn[8] + zl[0] - zu[0];
-            gl[11] -= jl[9] + lamn[9] + zl[1] - zu[1];
+            for (int j = 0; j < 4; ++j) gl[j] -= jl[j];
+            gl[5] -= jl[4] + lamn[4] + zl - zu;
 #pragma unroll
-            for (int j = 0; j < 12; ++j) dinf = fmax(dinf, (j < 10 ? xon : uon) ? fabs(gl[j]) : 0.0);
+            for (int j = 0; j < 6; ++j) dinf = fmax(dinf, (j < 5 ? xon : uon) ? fabs(gl[j]) : 0.0);
 #pragma unroll
-            for (int i = 0; i < 10; ++i) suml += xon ? fabs(lam[i]) / (i < 8 ? dsc[i] : 1.0) : 0.0;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) if (uon) {
-                const double cl = zl[j] * (u[j] - lo), cu = zu[j] * (hi - u[j]);
-                c0 = fmax(c0, fmax(cl, cu)); cmin = fmin(cmin, fmin(cl, cu)); sumz += zl[j] + zu[j];
+            for (int i = 0; i < 5; ++i) suml += xon ? fabs(lam[i]) / (i < 4 ? dsc[i] : 1.0) : 0.0;
+            if (uon) {
+                const double cl = zl * (u - lo), cu = zu * (hi - u);
+                c0 = fmax(cl, cu); cmin = fmin(cl, cu); sumz = zl + zu;
             }
         }
         dinf = wmaxf((float)dinf); pinf = wmaxf((float)pinf); pinf_u = wmaxf((float)pinf_u); c0 = wmaxf((float)c0);
@@ -631,22 +565,23 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
 
         // ---------------- gradient rows (they depend on mu) ------------------------------------
         {
-            double gq[12];
+            double gq[6];
             cost_grad(x, u, up, gq);
 #pragma unroll
-            for (int j = 0; j < 12; ++j) gq[j] *= sc;
+            for (int j = 0; j < 6; ++j) gq[j] *= sc;
             if (uon) {
-                gq[10] += -mu * isl0 + mu * isu0; gq[11] += -mu * isl1 + mu * isu1;
+                gq[5] += -mu * isl + mu * isu;
 #pragma unroll
-                for (int j = 0; j < 12; ++j) Hk[hp(12, j)] = gq[j];
+                for (int j = 0; j < 6; ++j) Hk[hp(6, j)] = gq[j];
             }
-            if (k == N) {   // terminal value function [[2 Qt, q_N], [q_N^T, 0]] on x~ (packed, NP = 11)
-                double* PN = S->PK[N];
-                for (int e = 0; e < LmLds::NPT; ++e) PN[e] = 0.0;
+            if (k == N) {   // terminal surrogate G_N: value function [[2 Qt, q_N], [q_N^T, 0]] on x~, Quu = 1
+                double* GN = S->G[sl];
+                for (int e = 0; e < LmLds::NTP; ++e) GN[e] = 0.0;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) PN[hp(i, i)] = sc * 2.0 * Qt[i];
+                for (int i = 0; i < 4; ++i) GN[gszz<5>(i, i)] = sc * 2.0 * Qtv[i];
 #pragma unroll
-                for (int j = 0; j < 10; ++j) PN[hp(10, j)] = gq[j];
+                for (int j = 0; j < 5; ++j) GN[gszz<5>(5, j)] = gq[j];
+                GN[hp(5, 5)] = 1.0;
             }
         }
         __syncthreads();
@@ -658,70 +593,58 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         // kappa_soc 0.99): a rejected full step with theta(trial) >= theta re-solves the system with
         // c_soc <- alpha_soc c_soc + c(x_trial) (from c(x), alpha_soc = alpha) in the defect column of
         // M~ and dx~_0 (H~, incl. the inertia shift, is unchanged) and tries x + alpha_soc d_soc.
-        double dx[10], dU[2], lamp[10], gt[10], dzl[2], dzu[2];
+        double dx[5], dU = 0.0, lamp[5], gt[5], dzl = 0.0, dzu = 0.0;
         double amax = 1.0, az = 1.0, phi = 0.0, gTd = 0.0, amin = 0.0, alpha = 1.0, th_t = 0.0, ph_t = 0.0;
         double th_prev = 0.0;
         float lg_sw = 0.0f;
         bool accepted = false, ftype = false, tiny = false, ok = true;
         int ls = 0, soc = -1;        // soc: -1 plain step, >= 0 second-order-correction pass
-        // the Newton step from the factorised value functions: forward sweep, du = K [dx~; 1], lambda+
+        // the Newton step from the factorised stage QPs: forward sweep, du = K [dx~; 1], lambda+
         auto recover_step = [&]() {
-            forward_sweep(S, N, k, dx);
+            forward_sweep_s(S, N, k, dx);
             STAMP(12);
-            asm volatile("" ::: "memory");     // keep the K / Pt reads below after the sweep (register pressure)
-            const int kk = xon ? k : 0;
-            const double* K0 = S->PK[uon ? k : 0] + LmLds::NPT;
-            const double* K1 = K0 + LmLds::NP;
-            double d0 = K0[10], d1 = K1[10];
+            const double* K = S->KK[uon ? sl : hf * LM_NMAXS];
+            double d0 = K[5];
 #pragma unroll
-            for (int j = 0; j < 10; ++j) { d0 = fma(K0[j], dx[j], d0); d1 = fma(K1[j], dx[j], d1); }
-            dU[0] = uon ? d0 : 0.0; dU[1] = uon ? d1 : 0.0;
-            node_multiplier3(S, kk, dx, lamp);
+            for (int j = 0; j < 5; ++j) d0 = fma(K[j], dx[j], d0);
+            dU = uon ? d0 : 0.0;
+            node_multiplier_s(S, xon ? sl : hf * LM_NMAXS, dx, dU, lamp);
         };
         // primal fraction to the boundary of dU (wave-uniform)
         auto primal_ftb = [&]() {
             double am = 1.0;
             if (uon) {
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    if (dU[j] < 0) am = fmin(am, -tau * (u[j] - lo) / dU[j]);
-                    if (dU[j] > 0) am = fmin(am, tau * (hi - u[j]) / dU[j]);
-                }
+                if (dU < 0) am = fmin(am, -tau * (u - lo) / dU);
+                if (dU > 0) am = fmin(am, tau * (hi - u) / dU);
             }
             return (double)wminf((float)am) * (1.0 - 1.0 / 1048576.0);
         };
         // bound-multiplier directions of dU and their fraction to the boundary (wave-uniform)
         auto dual_step = [&]() {
-            dzl[0] = uon ? mu * isl0 - zl[0] - zl[0] * isl0 * dU[0] : 0.0;
-            dzl[1] = uon ? mu * isl1 - zl[1] - zl[1] * isl1 * dU[1] : 0.0;
-            dzu[0] = uon ? mu * isu0 - zu[0] + zu[0] * isu0 * dU[0] : 0.0;
-            dzu[1] = uon ? mu * isu1 - zu[1] + zu[1] * isu1 * dU[1] : 0.0;
+            dzl = uon ? mu * isl - zl - zl * isl * dU : 0.0;
+            dzu = uon ? mu * isu - zu + zu * isu * dU : 0.0;
             double az_ = 1.0;
             if (uon) {
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    if (dzl[j] < 0) az_ = fmin(az_, -tau * zl[j] / dzl[j]);
-                    if (dzu[j] < 0) az_ = fmin(az_, -tau * zu[j] / dzu[j]);
-                }
+                if (dzl < 0) az_ = fmin(az_, -tau * zl / dzl);
+                if (dzu < 0) az_ = fmin(az_, -tau * zu / dzu);
             }
             return (double)wminf((float)az_) * (1.0 - 1.0 / 1048576.0);
         };
         // trial point x + al d: incoming defects gt of node k, wave-summed theta and barrier objective
         auto trial = [&](double al) {
-            double xt[8], pt[2], ut[2];
+            double xt[4];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) xt[i] = fma(al, dx[i], x[i]);
-            pt[0] = fma(al, dx[8], up[0]); pt[1] = fma(al, dx[9], up[1]);
-            ut[0] = fma(al, dU[0], u[0]); ut[1] = fma(al, dU[1], u[1]);
+            for (int i = 0; i < 4; ++i) xt[i] = fma(al, dx[i], x[i]);
+            const double pt = fma(al, dx[4], up), ut = fma(al, dU, u);
             defects(xt, pt, ut, gt);
             double phl = sc * cost_val(xt, ut, pt);
-            if (uon) phl -= mu * log((ut[0] - lo) * (hi - ut[0]) * (ut[1] - lo) * (hi - ut[1]));
+            if (uon) phl -= mu * log((ut - lo) * (hi - ut));
             th_t = wsum(theta_of(gt)); ph_t = wsum(phl);
         };
         // filter acceptance of (th_t, ph_t) for the step size al_test (IPOPT alpha_primal_test)
         auto acceptable = [&](double al_test, bool& ft) {
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
-            in_filter = in_filter || wany(k < nfilt && th_t >= fth && ph_t >= fph);
+            in_filter = in_filter || wany(lane < nfilt && th_t >= fth && ph_t >= fph);
             if (in_filter) return false;
             const bool sw = gTd < 0.0 && lg2(al_test) > lg_sw;
             if (theta <= th_min && sw) {
@@ -734,14 +657,14 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             // Riccati (one call site): plain step with inertia correction, or a second-order
             // correction with the same factorisation and the defects c_soc
             if (soc >= 0) {
-                double cs[10];
+                double cs[5];
 #pragma unroll
-                for (int i = 0; i < 10; ++i) cs[i] = xon ? SH.CS[sr][i] : 0.0;
+                for (int i = 0; i < 5; ++i) cs[i] = xon ? SH.CS[sl][i] : 0.0;
 #pragma unroll
-                for (int r = 0; r < 10; ++r) {
+                for (int r = 0; r < 5; ++r) {
                     const double t = from_next(cs[r]);
-                    if (uon) Mk[12 * NC + r] = -t;
-                    if (k == 0) S->dx0[r] = -cs[r];
+                    if (uon) Mk[6 * NC + r] = -t;
+                    if (k == 0) S->dx0[hf][r] = -cs[r];
                 }
                 __syncthreads();
                 STAMP_ADD(15, 1);
@@ -750,18 +673,18 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 double delta = 0.0, dapplied = 0.0;
                 int attempt = 0;
                 for (;;) {
-                    ok = riccati3_sweep(S, N, RR);
+                    ok = riccati_s_sweep(S, N, RR);
                     if (ok || soc >= 0 || ++attempt >= 60) break;
                     delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last / 3.0))
                                            : delta * (delta_last == 0.0 ? 100.0 : 8.0);
                     const double dd = delta - dapplied;
                     if (uon) {
 #pragma unroll
-                        for (int j = 0; j < 12; ++j) Hk[hp(j, j)] += dd;
+                        for (int j = 0; j < 6; ++j) Hk[hp(j, j)] += dd;
                     }
                     if (k == N) {
 #pragma unroll
-                        for (int j = 0; j < 10; ++j) S->PK[N][hp(j, j)] += dd;
+                        for (int j = 0; j < 5; ++j) S->G[sl][gszz<5>(j, j)] += dd;
                     }
                     dapplied = delta;
                     __syncthreads();
@@ -772,7 +695,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             }
             STAMP(3);
             if (!ok) break;
-            closed_loop3(S, N);
+            closed_loop_s(S, N);
             STAMP(11);
             recover_step();
             STAMP(4);
@@ -782,13 +705,13 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 az = dual_step();
                 STAMP(5);
                 double phil = sc * cost_val(x, u, up), gtdl = 0.0;
-                if (uon) phil -= mu * log((u[0] - lo) * (hi - u[0]) * (u[1] - lo) * (hi - u[1]));
+                if (uon) phil -= mu * log((u - lo) * (hi - u));
                 {
-                    double gz_[12];
+                    double gz_[6];
                     cost_grad(x, u, up, gz_);
 #pragma unroll
-                    for (int i = 0; i < 10; ++i) gtdl += xon ? sc * gz_[i] * dx[i] : 0.0;
-                    if (uon) gtdl += (sc * gz_[10] - mu * isl0 + mu * isu0) * dU[0] + (sc * gz_[11] - mu * isl1 + mu * isu1) * dU[1];
+                    for (int i = 0; i < 5; ++i) gtdl += xon ? sc * gz_[i] * dx[i] : 0.0;
+                    if (uon) gtdl += (sc * gz_[5] - mu * isl + mu * isu) * dU;
                 }
                 phi = wsum(phil); gTd = wsum(gtdl);
                 const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
@@ -799,14 +722,11 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 amin *= gam_al;
                 float tnl = 0.0f;
 #pragma unroll
-                for (int i = 0; i < 10; ++i) {
-                    const double xi = i < 8 ? x[i] : up[i - 8];
+                for (int i = 0; i < 5; ++i) {
+                    const double xi = i < 4 ? x[i] : up;
                     tnl = fmaxf(tnl, xon ? fabsf((float)dx[i]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)xi)) : 0.0f);
                 }
-                if (uon) {
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) tnl = fmaxf(tnl, fabsf((float)dU[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)u[j])));
-                }
+                if (uon) tnl = fmaxf(tnl, fabsf((float)dU) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)u)));
                 tiny = wmaxf(tnl) < 2.2e-15f;
                 alpha = amax;
                 al_try = alpha;
@@ -823,11 +743,11 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     if (ls == 0 && a.max_soc > 0 && !(th_t < theta)) {
                         if (xon) {      // c_soc = alpha c(x) + c(x_trial); keep the plain step
 #pragma unroll
-                            for (int i = 0; i < 10; ++i) {
-                                SH.CS[sr][i] = fma(alpha, SH.CS[sr][i], gt[i]);
-                                SH.SV[sr][i] = dx[i]; SH.SV[sr][10 + i] = lamp[i];
+                            for (int i = 0; i < 5; ++i) {
+                                SH.CS[sl][i] = fma(alpha, SH.CS[sl][i], gt[i]);
+                                SH.SV[sl][i] = dx[i]; SH.SV[sl][5 + i] = lamp[i];
                             }
-                            SH.SV[sr][20] = dU[0]; SH.SV[sr][21] = dU[1];
+                            SH.SV[sl][10] = dU;
                         }
                         th_prev = th_t; soc = 0; resolve = true;
                         break;
@@ -842,15 +762,15 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     if (soc + 1 < a.max_soc && th_t <= 0.99 * th_prev) {
                         if (xon) {      // c_soc <- alpha_soc c_soc + c(x_soc trial)
 #pragma unroll
-                            for (int i = 0; i < 10; ++i) SH.CS[sr][i] = fma(al_try, SH.CS[sr][i], gt[i]);
+                            for (int i = 0; i < 5; ++i) SH.CS[sl][i] = fma(al_try, SH.CS[sl][i], gt[i]);
                         }
                         th_prev = th_t; ++soc; resolve = true;
                         break;
                     }
                     if (xon) {      // corrections failed: back to the plain step, backtrack
 #pragma unroll
-                        for (int i = 0; i < 10; ++i) { dx[i] = SH.SV[sr][i]; lamp[i] = SH.SV[sr][10 + i]; }
-                        dU[0] = SH.SV[sr][20]; dU[1] = SH.SV[sr][21];
+                        for (int i = 0; i < 5; ++i) { dx[i] = SH.SV[sl][i]; lamp[i] = SH.SV[sl][5 + i]; }
+                        dU = SH.SV[sl][10];
                     }
                     soc = -1;
                 }
@@ -866,24 +786,20 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         STAMP(7);
         if (!accepted) { status = -2; break; }
         if (!ftype && nfilt < kWave) {
-            if (k == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
+            if (lane == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
             ++nfilt;
         }
         // ---------------- accept ------------------------------------------------------------
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = xon ? fma(alpha, dx[i], x[i]) : x[i];
-        up[0] = xon ? fma(alpha, dx[8], up[0]) : up[0];
-        up[1] = xon ? fma(alpha, dx[9], up[1]) : up[1];
+        for (int i = 0; i < 4; ++i) x[i] = xon ? fma(alpha, dx[i], x[i]) : x[i];
+        up = xon ? fma(alpha, dx[4], up) : up;
 #pragma unroll
-        for (int i = 0; i < 10; ++i) lam[i] = xon ? fma(alpha, lamp[i] - lam[i], lam[i]) : 0.0;
+        for (int i = 0; i < 5; ++i) lam[i] = xon ? fma(alpha, lamp[i] - lam[i], lam[i]) : 0.0;
         if (uon) {
-            u[0] = fma(alpha, dU[0], u[0]); u[1] = fma(alpha, dU[1], u[1]);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const double il = frcp(u[j] - lo), iu = frcp(hi - u[j]);
-                zl[j] = fmax(fmin(fma(az, dzl[j], zl[j]), 1e10 * mu * il), 1e-10 * mu * il);
-                zu[j] = fmax(fmin(fma(az, dzu[j], zu[j]), 1e10 * mu * iu), 1e-10 * mu * iu);
-            }
+            u = fma(alpha, dU, u);
+            const double il = frcp(u - lo), iu = frcp(hi - u);
+            zl = fmax(fmin(fma(az, dzl, zl), 1e10 * mu * il), 1e-10 * mu * il);
+            zu = fmax(fmin(fma(az, dzu, zu), 1e10 * mu * iu), 1e-10 * mu * iu);
         }
         theta = th_t;
         STAMP(8);
@@ -891,17 +807,15 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
 
     // ---------------- outputs -------------------------------------------------------------
     const double fval = wsum(cost_val(x, u, up));
-    if (k == 0) {
-        a.u0[2 * b] = u[0]; a.u0[2 * b + 1] = u[1];
-        a.f[b] = fval; a.status[b] = status; a.iters[b] = it;
-    }
+    if (lane == 0) { a.f[b] = fval; a.status[b] = status; a.iters[b] = it; }
+    if (k == 0) a.u0[2 * b + hf] = u;
     if (a.w_out) {
         double* wo = a.w_out + (size_t)nw * b;
         if (xon) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) wo[8 * k + i] = x[i];
+            for (int i = 0; i < 4; ++i) wo[8 * k + gidx(i)] = x[i];
         }
-        if (uon) { wo[8 * (N + 1) + 2 * k] = u[0]; wo[8 * (N + 1) + 2 * k + 1] = u[1]; }
+        if (uon) wo[8 * (N + 1) + 2 * k + hf] = u;
     }
     STAMP_FLUSH_TO(g_stamp_lm, b);
 }

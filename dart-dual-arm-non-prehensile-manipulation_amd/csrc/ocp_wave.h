@@ -242,197 +242,164 @@ __device__ void forward_sweep(L* S, int N, int node, double* dxo) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Three-phase variant with an explicit value function, for wide augmented states (LMPC,
-// NXA = 10): per node (A) T = Pt_{k+1} M_k (NP x ND entries, 11 FMA each), (B) G = Ht + M^T T
-// (packed, 11 FMA each), (C) the 2 x 2 Schur complement -> Pt_k (packed) and [K | k].  Each
-// lane holds only the operands of its own few entries (no uniform block in registers).
+// Scalar-input variant for two independent subsystems per wave (LMPC: the x and y halves of the
+// separable 8-state model, lmpc_ipm.hip).  Half h = lane >> 5 owns node slots 32 h + k; z =
+// [x~ (NXA); u; 1], ND = NXA + 2, so the packed G_k of one subsystem (NT = 28 at NXA = 5) fits a
+// half-wave: lane 32 h + e owns entry e of its half.  Quu is a scalar; the Schur complement is
+// G_k(i, j) = Ht_ij + a_i^T Gzz a_j - (a_i^T Gzu)(Guz a_j) / Quu, one LDS round trip per node.
 template <int NXA_, int NMAXS_>
-struct OcpLds3 {
-    static constexpr int NXA = NXA_, NP = NXA + 1, ND = NXA + 3, NMAXS = NMAXS_;
-    static constexpr int NC = even(NP);
+struct OcpLdsS {
+    static constexpr int NXA = NXA_;          // augmented state dimension of one subsystem
+    static constexpr int NP = NXA + 1;        // value-function dimension (with homogeneous 1)
+    static constexpr int ND = NXA + 2;        // stage vector [x~; u; 1]
+    static constexpr int NMAXS = NMAXS_;      // node slots per half (N + 1 <= NMAXS)
+    static constexpr int NC = even(NP);       // padded column stride of M
     static constexpr int NT = tri(ND), NTP = even(NT);
-    static constexpr int NPT = tri(NP);
-    static constexpr int NPK = even(NPT + 2 * NP);   // [Pt packed | K row 0 | K row 1] per node
     static constexpr int NF = even(NXA + 1);
-    static constexpr int NTT = NP * ND;               // entries of T
-    static constexpr int EA = (NTT + 63) / 64, EB = (NT + 63) / 64, EC = (NPT + 2 * NP + 63) / 64;
-    double M[NMAXS][ND][NC];
-    double H[NMAXS][NTP];
-    double PK[NMAXS][NPK];
-    static constexpr int NPF = even(NP);              // row stride of the full copy of Pt_{k+1}
-    double T[ND][NP + 1];                             // scratch Pt_{k+1} M_k, transposed: T[j][m]
-    double PF[NP][NPF];                               // scratch Pt_{k+1}, full rows (16-byte aligned)
-    double G[NTP];                                    // scratch G_k
-    double F[NMAXS][NXA][NF];
-    double dx0[NC];
+    static_assert(NT <= 32, "one packed entry per half-wave lane");
+    NodeArr<double[ND][NC], 2 * NMAXS> M;     // M[s][j][m] = M_k(m, j), slot s = NMAXS h + k
+    NodeArr<double[NTP], 2 * NMAXS> H;        // stage Hessian + gradient row, packed
+    NodeArr<double[NTP], 2 * NMAXS> G;        // G_k; G[N] = terminal surrogate (Pt_N, Quu = 1)
+    NodeArr<double[NC], 2 * NMAXS> KK;        // [K | k]_k
+    NodeArr<double[NXA][NF], 2 * NMAXS> F;    // closed loop rows [Phi_k(r, :) | f_k(r)]
+    double dx0[2][NC];                        // forward sweep start of each half
+};
+
+template <int NXA>
+__host__ __device__ constexpr int zsi_of_p(int p) { return p < NXA ? p : NXA + 1; }
+template <int NXA>
+__host__ __device__ constexpr int gszz(int p, int q) { return hp(zsi_of_p<NXA>(p), zsi_of_p<NXA>(q)); }
+template <int NXA>
+__host__ __device__ constexpr int gszu(int p) { return hp(zsi_of_p<NXA>(p), NXA); }
+
+struct RiccatiSRoles {
+    int ci, cj;     // column offsets (j * NC) of a_i, a_j in M_k
+    int e;          // packed entry of this lane in its half
+    bool on;
 };
 
 template <class L>
-struct Riccati3Roles {
-    int am[L::EA], aj[L::EA];            // (A) row m of Pt, column offset of a_j
-    bool aon[L::EA];
-    int bi[L::EB], bj[L::EB];            // (B) column offsets of a_i, T column j
-    bool bon[L::EB];
-    int ga0[L::EC], ga1[L::EC], gb0[L::EC], gb1[L::EC], gzz[L::EC];   // (C) packed G offsets
-    bool isK[L::EC], con[L::EC];
-    int ka[L::EC];
-    int fpq[L::EC], fqp[L::EC];          // (C) offsets (p, q) and (q, p) of a value entry in the full copy
-};
-
-template <class L>
-__device__ Riccati3Roles<L> riccati3_roles() {
-    constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, NC = L::NC, NT = L::NT, NPT = L::NPT, NTT = L::NTT;
-    const int lane = threadIdx.x;
-    Riccati3Roles<L> r{};
-#pragma unroll
-    for (int q = 0; q < L::EA; ++q) {
-        const int e0 = lane + 64 * q, e = e0 < NTT ? e0 : 0;
-        r.am[q] = e / ND; r.aj[q] = (e % ND) * NC; r.aon[q] = e0 < NTT;
-    }
-#pragma unroll
-    for (int q = 0; q < L::EB; ++q) {
-        const int e0 = lane + 64 * q, e = e0 < NT ? e0 : 0;
-        int i = 0;
-        while (tri(i + 1) <= e) ++i;
-        const int j = e - tri(i);
-        r.bi[q] = i * NC; r.bj[q] = j; r.bon[q] = e0 < NT;
-    }
-#pragma unroll
-    for (int q = 0; q < L::EC; ++q) {
-        const int e = lane + 64 * q;
-        int zi = 0, zj = 0;
-        r.isK[q] = e >= NPT;
-        r.ka[q] = 0;
-        r.fpq[q] = 0; r.fqp[q] = 0;
-        if (e < NPT) {
-            int p = 0;
-            while (tri(p + 1) <= e) ++p;
-            const int qq = e - tri(p);
-            zi = zi_of_p<NXA>(p); zj = zi_of_p<NXA>(qq);
-            r.fpq[q] = p * L::NPF + qq; r.fqp[q] = qq * L::NPF + p;
-        } else {
-            const int rr = (e - NPT) < 2 * NP ? e - NPT : 0;
-            r.ka[q] = rr / NP;
-            zi = zi_of_p<NXA>(rr % NP); zj = zi;
-        }
-        r.ga0[q] = hp(zi, NXA); r.ga1[q] = hp(zi, NXA + 1);
-        r.gb0[q] = hp(NXA, zj); r.gb1[q] = hp(NXA + 1, zj);
-        r.gzz[q] = hp(zi, zj);
-        r.con[q] = e < NPT + 2 * NP;
-    }
+__device__ RiccatiSRoles riccati_s_roles() {
+    RiccatiSRoles r{};
+    const int e0 = threadIdx.x & 31;
+    r.on = e0 < L::NT;
+    r.e = r.on ? e0 : 0;
+    int i = 0;
+    while (tri(i + 1) <= r.e) ++i;
+    r.ci = i * L::NC; r.cj = (r.e - tri(i)) * L::NC;
     return r;
 }
 
-// Backward sweep; PK[N] (value part) must hold the terminal value function.
+// Backward sweep of both halves over nodes N-1 .. 0; G[slot N] must hold each half's terminal
+// surrogate.  Returns false (wave-uniform) if some Quu of either half is not positive.
 template <class L>
-__device__ bool riccati3_sweep(L* S, int N, const Riccati3Roles<L>& R) {
-    constexpr int NXA = L::NXA, NP = L::NP, NPT = L::NPT;
-    const int lane = threadIdx.x;
+__device__ bool riccati_s_sweep(L* S, int N, const RiccatiSRoles& R) {
+    constexpr int NXA = L::NXA, NP = L::NP;
+    const int base = (threadIdx.x >> 5) * L::NMAXS;
     bool ok = true;
-    {   // full copy of the terminal value function
-        const int i = lane / NP, j = lane % NP;
-        for (int e = lane; e < NP * NP; e += 64) {
-            const int ii = e / NP, jj = e % NP;
-            S->PF[ii][jj] = S->PK[N][ii >= jj ? tri(ii) + jj : tri(jj) + ii];
-        }
-        (void)i; (void)j;
-    }
-    __syncthreads();
     for (int k = N - 1; k >= 0; --k) {
-        // (A) T(m, j) = sum_n Pt_{k+1}(m, n) M_k(n, j): row m of the full copy and column j of M_k are
-        // both contiguous (16-byte aligned), stored transposed for (B)
-        {
-            double tv[L::EA];
+        const double* Gn = S->G[base + k + 1];
+        const double q = Gn[hp(NXA, NXA)];
+        ok = ok && q > 0.0 && isfinite(q);
+        const double iq = frcp(q);
+        const double* Mk = &S->M[base + k][0][0];
+        double vi[NP], vj[NP];
 #pragma unroll
-            for (int q = 0; q < L::EA; ++q) {
-                const double* aj = &S->M[k][0][0] + R.aj[q];
-                const double* pm = S->PF[R.am[q]];
-                double t = 0.0;
+        for (int m = 0; m < NP; ++m) { vi[m] = Mk[R.ci + m]; vj[m] = Mk[R.cj + m]; }
+        double t[NP], b = 0.0, c = 0.0;
 #pragma unroll
-                for (int n = 0; n < NP; ++n) t = fma(pm[n], aj[n], t);
-                tv[q] = t;
-            }
+        for (int m = 0; m < NP; ++m) t[m] = 0.0;
 #pragma unroll
-            for (int q = 0; q < L::EA; ++q)
-                if (R.aon[q]) S->T[(lane + 64 * q) % L::ND][(lane + 64 * q) / L::ND] = tv[q];
+        for (int n = 0; n < NP; ++n) {
+#pragma unroll
+            for (int m = 0; m < NP; ++m) t[m] = fma(Gn[gszz<NXA>(m, n)], vj[n], t[m]);
+            b = fma(vi[n], Gn[gszu<NXA>(n)], b);
+            c = fma(vj[n], Gn[gszu<NXA>(n)], c);
         }
-        __syncthreads();
-        // (B) G(i, j) = Ht(i, j) + sum_m M_k(m, i) T(m, j)
-        {
-            double gv[L::EB];
+        double ga = S->H[base + k][R.e], gb = 0.0;
 #pragma unroll
-            for (int q = 0; q < L::EB; ++q) {
-                const double* ai = &S->M[k][0][0] + R.bi[q];
-                const double* tj = S->T[R.bj[q]];
-                double g = S->H[k][(lane + 64 * q) < L::NT ? lane + 64 * q : 0];
-#pragma unroll
-                for (int mm = 0; mm < NP; ++mm) g = fma(ai[mm], tj[mm], g);
-                gv[q] = g;
-            }
-#pragma unroll
-            for (int q = 0; q < L::EB; ++q)
-                if (R.bon[q]) S->G[lane + 64 * q] = gv[q];
+        for (int m = 0; m < NP; m += 2) {
+            ga = fma(vi[m], t[m], ga);
+            if (m + 1 < NP) gb = fma(vi[m + 1], t[m + 1], gb);
         }
-        __syncthreads();
-        // (C) Schur complement on the u block -> packed Pt_k, gains, and the full copy for node k-1
-        double i00, i01, i11;
-        ok = quu_inverse<NXA>(S->G, i00, i01, i11) && ok;
-        {
-            double cv[L::EC];
-#pragma unroll
-            for (int q = 0; q < L::EC; ++q) {
-                const double b0 = S->G[R.gb0[q]], b1 = S->G[R.gb1[q]];
-                const double w0 = fma(i00, b0, i01 * b1), w1 = fma(i01, b0, i11 * b1);
-                const double a0 = S->G[R.ga0[q]], a1 = S->G[R.ga1[q]], gz = S->G[R.gzz[q]];
-                const double pv = gz - fma(a0, w0, a1 * w1);
-                const double kv = R.ka[q] == 0 ? -w0 : -w1;
-                cv[q] = R.isK[q] ? kv : pv;
-            }
-#pragma unroll
-            for (int q = 0; q < L::EC; ++q) {
-                if (R.con[q]) S->PK[k][lane + 64 * q] = cv[q];
-                if (R.con[q] && !R.isK[q]) {
-                    (&S->PF[0][0])[R.fpq[q]] = cv[q];
-                    (&S->PF[0][0])[R.fqp[q]] = cv[q];
-                }
-            }
-        }
+        const double g = (ga + gb) - b * c * iq;
+        // all reads of G_{k+1} and M_k precede the write of G_k (distinct slots: no hazard)
+        if (R.on) S->G[base + k][R.e] = g;
         __syncthreads();
     }
-    (void)NPT;
-    return ok;
+    const double q0 = S->G[base][hp(NXA, NXA)];
+    ok = ok && q0 > 0.0 && isfinite(q0);
+    return !wany(!ok);
 }
 
-// [Phi | f] of every node from the stored gains, lane per node.  Ends with a barrier.
+// [K | k] = -Guz / Quu and [Phi | f] of every node, lane 32 h + k per node (k < N).  Ends with a barrier.
 template <class L>
-__device__ void closed_loop3(L* S, int N) {
-    constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, NPT = L::NPT;
-    const int k = threadIdx.x;
+__device__ void closed_loop_s(L* S, int N) {
+    constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND;
+    const int k = threadIdx.x & 31, sl = (threadIdx.x >> 5) * L::NMAXS + k;
     if (k < N) {
-        const double* K0 = S->PK[k] + NPT;
-        const double* K1 = K0 + NP;
+        const double* Gk = S->G[sl];
+        const double iq = frcp(Gk[hp(NXA, NXA)]);
+        double K[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) { K[p] = -Gk[gszu<NXA>(p)] * iq; S->KK[sl][p] = K[p]; }
+        const double* Mk = &S->M[sl][0][0];
 #pragma unroll
         for (int r = 0; r < NXA; ++r) {
-            const double b0 = S->M[k][NXA][r], b1 = S->M[k][NXA + 1][r];
+            const double bq = Mk[NXA * L::NC + r];
 #pragma unroll
-            for (int j = 0; j < NXA; ++j) S->F[k][r][j] = fma(b0, K0[j], fma(b1, K1[j], S->M[k][j][r]));
-            S->F[k][r][NXA] = fma(b0, K0[NXA], fma(b1, K1[NXA], S->M[k][ND - 1][r]));
+            for (int j = 0; j < NXA; ++j) S->F[sl][r][j] = fma(bq, K[j], Mk[j * L::NC + r]);
+            S->F[sl][r][NXA] = fma(bq, K[NXA], Mk[(ND - 1) * L::NC + r]);
         }
     }
     __syncthreads();
 }
 
-// lam~_k = -Pt_k [dx~; 1] (first NXA rows), lane per node
+// lam~ = -Pt_k [dx~; 1] (first NXA rows) with Pt_k [dx~; 1] = Gzz [dx~; 1] + Gzu du, read from G of slot sl
 template <class L>
-__device__ __forceinline__ void node_multiplier3(const L* S, int k, const double* dx, double* lam) {
-    constexpr int NXA = L::NXA;
-    const double* Pk = S->PK[k];
+__device__ __forceinline__ void node_multiplier_s(const L* S, int sl, const double* dx, double du, double* lam) {
+    constexpr int NXA = L::NXA, NP = L::NP;
+    const double* Gk = S->G[sl];
 #pragma unroll
     for (int p = 0; p < NXA; ++p) {
-        double t = Pk[hp(NXA, p)];
+        double t = Gk[gszz<NXA>(p, NP - 1)];
 #pragma unroll
-        for (int q = 0; q < NXA; ++q) t = fma(Pk[hp(p, q)], dx[q], t);
-        lam[p] = -t;
+        for (int q = 0; q < NXA; ++q) t = fma(Gk[gszz<NXA>(p, q)], dx[q], t);
+        lam[p] = -fma(Gk[gszu<NXA>(p)], du, t);
+    }
+}
+
+// Forward sweep of both halves: lane 32 h + r (r < NXA) owns row r of its half's chain
+// dx~_{k+1} = Phi_k dx~_k + f_k; the new states are broadcast by readlane (both halves, then a
+// per-half select).  Every lane returns in dxo the step of node `node` of its half.
+template <class L>
+__device__ void forward_sweep_s(L* S, int N, int node, double* dxo) {
+    constexpr int NXA = L::NXA;
+    const int h = threadIdx.x >> 5, base = h * L::NMAXS;
+    const int r = (threadIdx.x & 31) < NXA ? (threadIdx.x & 31) : 0;
+    double d[NXA];
+#pragma unroll
+    for (int i = 0; i < NXA; ++i) { d[i] = S->dx0[h][i]; dxo[i] = d[i]; }
+    double Fc[NXA + 1];
+#pragma unroll
+    for (int j = 0; j <= NXA; ++j) Fc[j] = S->F[base][r][j];
+    for (int k = 0; k < N; ++k) {
+        double Fn[NXA + 1];
+        const int kn = k + 1 < N ? k + 1 : k;
+#pragma unroll
+        for (int j = 0; j <= NXA; ++j) Fn[j] = S->F[base + kn][r][j];
+        double s = Fc[NXA];
+#pragma unroll
+        for (int j = 0; j < NXA; ++j) s = fma(Fc[j], d[j], s);
+        const bool mine = node == k + 1;
+#pragma unroll
+        for (int i = 0; i < NXA; ++i) {
+            const double d0 = readlane(s, i), d1 = readlane(s, 32 + i);
+            d[i] = h ? d1 : d0;
+            dxo[i] = mine ? d[i] : dxo[i];
+        }
+#pragma unroll
+        for (int j = 0; j <= NXA; ++j) Fc[j] = Fn[j];
     }
 }
 
