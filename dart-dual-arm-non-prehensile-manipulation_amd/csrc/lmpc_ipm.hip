@@ -71,6 +71,7 @@ struct LmShared {
     NodeArr<double[5], 2 * LM_NMAXS> CS;     // second-order correction: c_soc rows of node k (incoming defect)
     NodeArr<double[11], 2 * LM_NMAXS> SV;    // second-order correction: the plain step (dx~, lambda+, du)
     LmSub sub[2];                   // uniform problem data of the two halves
+    double W[2][2][4], tg[2][4], st0[2][4];   // [half][stage, terminal] weights, target, x_0 (local order)
 };
 
 __device__ __forceinline__ double sq(double p) { return fabs(p) + 1e-6; }   // squash_param :296-298
@@ -220,7 +221,7 @@ __device__ __forceinline__ double sub_adjoint_curv(const LmSub& m, const double 
 // stage Hessian (rows i >= d).
 __device__ __forceinline__ double sub_direction(const LmSub& m, const double (*sc)[LM_NSC], const double (*cv)[4],
                                                 double huu, double gca, int d, const double* lamn, double* Mk,
-                                                double* Hk) {
+                                                double* Hk, double cadd) {
     double yd[4][4], acc[4], e[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) { e[i] = (i == d) ? 1.0 : 0.0; yd[0][i] = e[i]; acc[i] = 0.0; }
@@ -270,11 +271,12 @@ __device__ __forceinline__ double sub_direction(const LmSub& m, const double (*s
 #pragma unroll
         for (int i = 0; i < 4; ++i) kbd[i] = cs * q[i];
     }
-    // rows i >= d of column d (z indices: x 0..3, up 4, tilt 5)
+    // rows i >= d of column d (z indices: x 0..3, up 4, tilt 5); cadd = the cost / barrier curvature
+    // of the diagonal entry (d, d)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        if (i >= d) Hk[hp(i, jc)] = hx[i];
-    Hk[hp(5, jc)] = hu;
+        if (i >= d) Hk[hp(i, jc)] = i == d ? hx[i] + cadd : hx[i];
+    Hk[hp(5, jc)] = d == 4 ? hu + cadd : hu;
     return dot;
 }
 
@@ -320,17 +322,18 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         m.rr2 = -m.r * m.rs;
         m.h = a.Ts;
     }
+    const double* pr = a.prm + LM_NPRM * b;
+    if (k < 4) {
+        const int gi = gidx(k);
+        SH.W[hf][0][k] = pr[gi]; SH.W[hf][1][k] = pr[8 + gi];
+        SH.tg[hf][k] = a.target[8 * b + gi]; SH.st0[hf][k] = a.state[8 * b + gi];
+    }
     __syncthreads();
     const LmSub& m = SH.sub[hf];
-    const double* pr = a.prm + LM_NPRM * b;
-    double Wq[4], tg[4], Qtv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int gi = gidx(i);
-        Qtv[i] = pr[8 + gi];
-        Wq[i] = k < N ? pr[gi] : Qtv[i];       // stage or terminal weights (lane N is the terminal node)
-        tg[i] = a.target[8 * b + gi];
-    }
+    const double* Wq = SH.W[hf][k < N ? 0 : 1];    // stage or terminal weights (lane N is the terminal node)
+    const double* Qtv = SH.W[hf][1];
+    const double* tg = SH.tg[hf];
+    const double* st0 = SH.st0[hf];
     const double Ru = pr[16 + hf], Rdu = pr[18 + hf];
     const double ulo = pr[20], uhi = pr[21];
 
@@ -348,10 +351,6 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     }
 
     // ---------------- initial point (lane 32 h + k = node k of subsystem h) -----------------------
-    const double* st0g = a.state + 8 * b;
-    double st0[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) st0[i] = st0g[gidx(i)];
     const double upv = a.u_prev[2 * b + hf];
     const int nw = 8 * (N + 1) + 2 * N;
     const double* ww = a.w_warm ? a.w_warm + (size_t)nw * b : nullptr;
@@ -422,7 +421,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         if (uon) {
             const LmSub mr = m;
 #pragma unroll 1
-            for (int d = 0; d < 5; ++d) sub_direction(mr, SH.SC[sl], SH.SD[sl], huu, LM_G * ca, d, lz, Mk, Hk);
+            for (int d = 0; d < 5; ++d) sub_direction(mr, SH.SC[sl], SH.SD[sl], huu, LM_G * ca, d, lz, Mk, Hk, 0.0);
         }
         double rs[4];
 #pragma unroll
@@ -478,16 +477,15 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 // exact dynamics Hessian (x, u blocks) and the Jacobian columns of node k
                 if (uon) {
                     const LmSub mr = m;     // model to registers once for the five directions
+                    // with the cost / barrier terms of z = [x(4), up, u, 1] on the diagonal (gradient row later)
+                    const double cu = sc * 2.0 * (Ru + Rdu) + zl * isl + zu * isu;
 #pragma unroll 1
                     for (int d = 0; d < 5; ++d)
-                        SH.JL[sl][d] = sub_direction(mr, SH.SC[sl], SH.SD[sl], huu, LM_G * ca, d, lamn, Mk, Hk);
+                        SH.JL[sl][d] = sub_direction(mr, SH.SC[sl], SH.SD[sl], huu, LM_G * ca, d, lamn, Mk, Hk,
+                                                     d < 4 ? sc * 2.0 * Wq[d] : cu);
 #pragma unroll
                     for (int d = 0; d < 5; ++d) jl[d] = SH.JL[sl][d];
-                    // the cost / barrier terms: z = [x(4), up, u, 1], gradient row later
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) Hk[hp(i, i)] += sc * 2.0 * Wq[i];
                     Hk[hp(4, 4)] = sc * 2.0 * Rdu;
-                    Hk[hp(5, 5)] += sc * 2.0 * (Ru + Rdu) + zl * isl + zu * isu;
                     Hk[hp(5, 4)] = -sc * 2.0 * Rdu;
                 } else {
 #pragma unroll

@@ -298,14 +298,15 @@ __device__ bool riccati_s_sweep(L* S, int N, const RiccatiSRoles& R) {
     const int base = (threadIdx.x >> 5) * L::NMAXS;
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
-        const double* Gn = S->G[base + k + 1];
-        const double q = Gn[hp(NXA, NXA)];
-        ok = ok && q > 0.0 && isfinite(q);
-        const double iq = frcp(q);
+        // straight-line body, every lane active (lanes past NT recompute entry 0 and store the same
+        // value): the loads of H_k and M_k do not wait on G_{k+1}, and Quu's reciprocal is taken
+        // after the products, so one LDS latency per node stays on the chain
+        const double hk = S->H[base + k][R.e];
         const double* Mk = &S->M[base + k][0][0];
         double vi[NP], vj[NP];
 #pragma unroll
         for (int m = 0; m < NP; ++m) { vi[m] = Mk[R.ci + m]; vj[m] = Mk[R.cj + m]; }
+        const double* Gn = S->G[base + k + 1];
         double t[NP], b = 0.0, c = 0.0;
 #pragma unroll
         for (int m = 0; m < NP; ++m) t[m] = 0.0;
@@ -316,15 +317,17 @@ __device__ bool riccati_s_sweep(L* S, int N, const RiccatiSRoles& R) {
             b = fma(vi[n], Gn[gszu<NXA>(n)], b);
             c = fma(vj[n], Gn[gszu<NXA>(n)], c);
         }
-        double ga = S->H[base + k][R.e], gb = 0.0;
+        double ga = hk, gb = 0.0;
 #pragma unroll
         for (int m = 0; m < NP; m += 2) {
             ga = fma(vi[m], t[m], ga);
             if (m + 1 < NP) gb = fma(vi[m + 1], t[m + 1], gb);
         }
-        const double g = (ga + gb) - b * c * iq;
+        const double q = Gn[hp(NXA, NXA)];
+        ok = ok && q > 0.0 && isfinite(q);
+        const double g = (ga + gb) - b * c * frcp(q);
         // all reads of G_{k+1} and M_k precede the write of G_k (distinct slots: no hazard)
-        if (R.on) S->G[base + k][R.e] = g;
+        S->G[base + k][R.e] = g;
         __syncthreads();
     }
     const double q0 = S->G[base][hp(NXA, NXA)];
@@ -338,18 +341,29 @@ __device__ void closed_loop_s(L* S, int N) {
     constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND;
     const int k = threadIdx.x & 31, sl = (threadIdx.x >> 5) * L::NMAXS + k;
     if (k < N) {
+        // every LDS read before the first write (the compiler cannot prove F, KK and M disjoint and
+        // would otherwise wait out each read before the next write)
         const double* Gk = S->G[sl];
+        const double* Mk = &S->M[sl][0][0];
+        double gu[NP], mk[NXA + 2][NXA];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) gu[p] = Gk[gszu<NXA>(p)];
+#pragma unroll
+        for (int j = 0; j < NXA + 2; ++j)
+#pragma unroll
+            for (int r = 0; r < NXA; ++r) mk[j][r] = Mk[(j < NXA ? j : j == NXA ? NXA : ND - 1) * L::NC + r];
         const double iq = frcp(Gk[hp(NXA, NXA)]);
         double K[NP];
 #pragma unroll
-        for (int p = 0; p < NP; ++p) { K[p] = -Gk[gszu<NXA>(p)] * iq; S->KK[sl][p] = K[p]; }
-        const double* Mk = &S->M[sl][0][0];
+        for (int p = 0; p < NP; ++p) K[p] = -gu[p] * iq;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) S->KK[sl][p] = K[p];
 #pragma unroll
         for (int r = 0; r < NXA; ++r) {
-            const double bq = Mk[NXA * L::NC + r];
+            const double bq = mk[NXA][r];
 #pragma unroll
-            for (int j = 0; j < NXA; ++j) S->F[sl][r][j] = fma(bq, K[j], Mk[j * L::NC + r]);
-            S->F[sl][r][NXA] = fma(bq, K[NXA], Mk[(ND - 1) * L::NC + r]);
+            for (int j = 0; j < NXA; ++j) S->F[sl][r][j] = fma(bq, K[j], mk[j][r]);
+            S->F[sl][r][NXA] = fma(bq, K[NXA], mk[NXA + 1][r]);
         }
     }
     __syncthreads();
@@ -371,7 +385,8 @@ __device__ __forceinline__ void node_multiplier_s(const L* S, int sl, const doub
 
 // Forward sweep of both halves: lane 32 h + r (r < NXA) owns row r of its half's chain
 // dx~_{k+1} = Phi_k dx~_k + f_k; the new states are broadcast by readlane (both halves, then a
-// per-half select).  Every lane returns in dxo the step of node `node` of its half.
+// ds_swizzle broadcast of lane 32 h + i within each half).  Every lane returns in dxo the step of
+// node `node` of its half.
 template <class L>
 __device__ void forward_sweep_s(L* S, int N, int node, double* dxo) {
     constexpr int NXA = L::NXA;
@@ -394,8 +409,7 @@ __device__ void forward_sweep_s(L* S, int N, int node, double* dxo) {
         const bool mine = node == k + 1;
 #pragma unroll
         for (int i = 0; i < NXA; ++i) {
-            const double d0 = readlane(s, i), d1 = readlane(s, 32 + i);
-            d[i] = h ? d1 : d0;
+            d[i] = half_bcast(s, i);
             dxo[i] = mine ? d[i] : dxo[i];
         }
 #pragma unroll

@@ -24,6 +24,27 @@ __device__ __forceinline__ double readlane(double x, int l) {
     const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
+// value of lane 32 (lane / 32) + I in every lane of each 32-lane half: ds_swizzle bitmask mode
+// (and_mask 0, or_mask I) -- a crossbar move through the LDS unit without a memory access
+template <int I>
+__device__ __forceinline__ double half_bcast_c(double x) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+    const int lo = __builtin_amdgcn_ds_swizzle((int)(unsigned)(b & 0xffffffffu), I << 5);
+    const int hi = __builtin_amdgcn_ds_swizzle((int)(unsigned)(b >> 32), I << 5);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double half_bcast(double x, int i) {
+    switch (i) {       // i is a compile-time constant at every (unrolled) call site
+        case 0: return half_bcast_c<0>(x);
+        case 1: return half_bcast_c<1>(x);
+        case 2: return half_bcast_c<2>(x);
+        case 3: return half_bcast_c<3>(x);
+        case 4: return half_bcast_c<4>(x);
+        case 5: return half_bcast_c<5>(x);
+        case 6: return half_bcast_c<6>(x);
+        default: return half_bcast_c<7>(x);
+    }
+}
 constexpr int kWaveShl1 = 0x130;   // lane k <- lane k+1
 constexpr int kWaveShr1 = 0x138;   // lane k <- lane k-1
 __device__ __forceinline__ double from_next(double x) { return dpp<kWaveShl1>(x); }

@@ -1,15 +1,14 @@
 #!/bin/bash
 # A/B timing of two in-tree builds of libdartmpc on the GPU box (bench main line + supplementary lines).
-# Usage: bash tools/ab_lib.sh <lib A file name> <lib B file name> [reps] [extra bench args]
+# Usage: bash tools/ab_lib.sh "<lib file names, space separated>" [reps] [extra bench args]
 set -o pipefail
-A=${1:-libdartmpc_base.so}
-B=${2:-libdartmpc.so}
-REPS=${3:-3}
-EXTRA=${4:-"--rmpc-steps 0 --lmpc-steps 0 --arm-steps 0"}
+LIBS=${1:-"libdartmpc_base.so libdartmpc.so"}
+REPS=${2:-3}
+EXTRA=${3:-"--rmpc-steps 0 --lmpc-steps 0 --arm-steps 0"}
 mkdir -p gpurun_out
 ARGS="--steps 2000 --warmup 50 --no-cpu-baseline --saturation-batch 0 --host-calls 0 --c4-steps 0 $EXTRA"
 for r in $(seq 1 $REPS); do
-  for lib in "$A" "$B"; do
+  for lib in $LIBS; do
     DART_MPC_LIB=$lib timeout -k 10 180 python bench.py $ARGS > gpurun_out/ab.json 2>gpurun_out/ab.err || exit $?
     python - "$lib" <<'PY'
 import json, sys
