@@ -118,13 +118,16 @@ __device__ bool riccati_sweep(L* S, int N, const RiccatiRoles<L::EPL>& R) {
     const int lane = threadIdx.x;
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
+        // straight-line body, every lane active (lanes past NT recompute entry 0 and store the same
+        // value): the loads of H_k and M_k do not wait on G_{k+1}, and Quu^-1 is formed after the
+        // products, so one LDS latency per node stays on the chain
+        double hk[L::EPL];
+#pragma unroll
+        for (int q = 0; q < L::EPL; ++q) hk[q] = S->H[k][R.on[q] ? lane + 64 * q : 0];
         const double* Gn = S->G[k + 1];
-        double i00, i01, i11;
-        ok = quu_inverse<NXA>(Gn, i00, i01, i11) && ok;
-        double gout[L::EPL];
+        double gout[L::EPL], bb0[L::EPL], bb1[L::EPL], cc0[L::EPL], cc1[L::EPL];
 #pragma unroll
         for (int q = 0; q < L::EPL; ++q) {
-            if (!R.on[q]) continue;
             const double* ai = &S->M[k][0][0] + R.ci[q];
             const double* aj = &S->M[k][0][0] + R.cj[q];
             double vi[NP], vj[NP];
@@ -144,19 +147,25 @@ __device__ bool riccati_sweep(L* S, int N, const RiccatiRoles<L::EPL>& R) {
                 c0 = fma(vj[n], Gn[gzu<NXA>(n, 0)], c0);
                 c1 = fma(vj[n], Gn[gzu<NXA>(n, 1)], c1);
             }
-            double ga = S->H[k][lane + 64 * q], gb = 0.0;
+            double ga = hk[q], gb = 0.0;
 #pragma unroll
             for (int m = 0; m < NP; m += 2) {
                 ga = fma(vi[m], t[m], ga);
                 if (m + 1 < NP) gb = fma(vi[m + 1], t[m + 1], gb);
             }
-            const double w0 = fma(i00, c0, i01 * c1), w1 = fma(i01, c0, i11 * c1);
-            gout[q] = (ga + gb) - fma(b0, w0, b1 * w1);
+            gout[q] = ga + gb; bb0[q] = b0; bb1[q] = b1; cc0[q] = c0; cc1[q] = c1;
+        }
+        double i00, i01, i11;
+        ok = quu_inverse<NXA>(Gn, i00, i01, i11) && ok;
+#pragma unroll
+        for (int q = 0; q < L::EPL; ++q) {
+            const double w0 = fma(i00, cc0[q], i01 * cc1[q]), w1 = fma(i01, cc0[q], i11 * cc1[q]);
+            gout[q] -= fma(bb0[q], w0, bb1[q] * w1);
         }
         // all reads of G_{k+1} and M_k precede the writes of G_k (distinct rows: no hazard)
 #pragma unroll
         for (int q = 0; q < L::EPL; ++q)
-            if (R.on[q]) S->G[k][lane + 64 * q] = gout[q];
+            if (q == 0 || R.on[q]) S->G[k][R.on[q] ? lane + 64 * q : 0] = gout[q];
         __syncthreads();
     }
     double i00, i01, i11;
@@ -170,24 +179,31 @@ __device__ void closed_loop(L* S, int N) {
     constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND;
     const int k = threadIdx.x;
     if (k < N) {
+        // LDS reads grouped ahead of the writes (the compiler cannot prove F, KK and M disjoint and
+        // would otherwise wait out each read before the next write)
         const double* Gk = S->G[k];
+        double gu0[NP], gu1[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) { gu0[p] = Gk[gzu<NXA>(p, 0)]; gu1[p] = Gk[gzu<NXA>(p, 1)]; }
         double i00, i01, i11;
         quu_inverse<NXA>(Gk, i00, i01, i11);
         double K0[NP], K1[NP];
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
-            const double c0 = Gk[gzu<NXA>(p, 0)], c1 = Gk[gzu<NXA>(p, 1)];
-            K0[p] = -fma(i00, c0, i01 * c1);
-            K1[p] = -fma(i01, c0, i11 * c1);
-            S->KK[k][0][p] = K0[p];
-            S->KK[k][1][p] = K1[p];
+            K0[p] = -fma(i00, gu0[p], i01 * gu1[p]);
+            K1[p] = -fma(i01, gu0[p], i11 * gu1[p]);
         }
 #pragma unroll
-        for (int r = 0; r < NXA; ++r) {
-            const double b0 = S->M[k][NXA][r], b1 = S->M[k][NXA + 1][r];
+        for (int p = 0; p < NP; ++p) { S->KK[k][0][p] = K0[p]; S->KK[k][1][p] = K1[p]; }
 #pragma unroll
-            for (int j = 0; j < NXA; ++j) S->F[k][r][j] = fma(b0, K0[j], fma(b1, K1[j], S->M[k][j][r]));
-            S->F[k][r][NXA] = fma(b0, K0[NXA], fma(b1, K1[NXA], S->M[k][ND - 1][r]));
+        for (int r = 0; r < NXA; ++r) {      // row r of M_k read whole before row r of F is written
+            double mr[NXA + 3];
+#pragma unroll
+            for (int j = 0; j < NXA + 3; ++j) mr[j] = S->M[k][j < NXA + 2 ? j : ND - 1][r];
+            const double b0 = mr[NXA], b1 = mr[NXA + 1];
+#pragma unroll
+            for (int j = 0; j < NXA; ++j) S->F[k][r][j] = fma(b0, K0[j], fma(b1, K1[j], mr[j]));
+            S->F[k][r][NXA] = fma(b0, K0[NXA], fma(b1, K1[NXA], mr[NXA + 2]));
         }
     }
     __syncthreads();
