@@ -636,7 +636,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             const double pt = fma(al, dx[4], up), ut = fma(al, dU, u);
             defects(xt, pt, ut, gt);
             double phl = sc * cost_val(xt, ut, pt);
-            if (uon) phl -= mu * log((ut - lo) * (hi - ut));
+            if (uon) phl -= mu * log_fast((ut - lo) * (hi - ut));
             th_t = wsum(theta_of(gt)); ph_t = wsum(phl);
         };
         // filter acceptance of (th_t, ph_t) for the step size al_test (IPOPT alpha_primal_test)
@@ -703,7 +703,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 az = dual_step();
                 STAMP(5);
                 double phil = sc * cost_val(x, u, up), gtdl = 0.0;
-                if (uon) phil -= mu * log((u - lo) * (hi - u));
+                if (uon) phil -= mu * log_fast((u - lo) * (hi - u));
                 {
                     double gz_[6];
                     cost_grad(x, u, up, gz_);

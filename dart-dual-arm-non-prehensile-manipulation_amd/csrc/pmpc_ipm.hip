@@ -498,7 +498,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
             const double sl = th[j] - lo, su = hi - th[j];
             phil += xon ? fma(scQp * ep, ep, scQv * ev * ev) : 0.0;
             gtdl += xon ? fma(qp2 * ep, dp[j], qv2 * ev * dv[j]) : 0.0;
-            phil += uon ? fma(scR * th[j], th[j], -mu * log(sl * su)) : 0.0;
+            phil += uon ? fma(scR * th[j], th[j], -mu * log_fast(sl * su)) : 0.0;
             gtdl += uon ? rt[j] * dth[j] : 0.0;
         }
         const double phi = wsum(phil), gTd = wsum(gtdl);
@@ -534,7 +534,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 const double ep = pt - rp[j], ev = vt - rv[j];
                 thl += xon ? fabs(t1) + fabs(t2) : 0.0;
                 phl += xon ? fma(scQp * ep, ep, scQv * ev * ev) : 0.0;
-                phl += uon ? fma(scR * tt, tt, -mu * log((tt - lo) * (hi - tt))) : 0.0;
+                phl += uon ? fma(scR * tt, tt, -mu * log_fast((tt - lo) * (hi - tt))) : 0.0;
             }
             th_t = wsum(thl); ph_t = wsum(phl);
             if (tiny) { accepted = true; ftype = true; break; }

@@ -678,7 +678,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         double phil = sc * cost_val(x, u, up), gtdl = 0.0;
         {
             const double pa = barrier_args(u, s);
-            phil -= uon ? mu * log(pa) : 0.0;
+            phil -= uon ? mu * log_fast(pa) : 0.0;
             double gq[8];
             cost_grad(x, u, up, gq);
 #pragma unroll
@@ -731,7 +731,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 #pragma unroll
             for (int i = 0; i < RM_NIQ; ++i) thl += uon ? fabs(ct[i] - st_[i]) : 0.0;
             double phl = sc * cost_val(xt, ut, pt);
-            phl -= uon ? mu * log(barrier_args(ut, st_)) : 0.0;
+            phl -= uon ? mu * log_fast(barrier_args(ut, st_)) : 0.0;
             th_t = wsum(thl); ph_t = wsum(phl);
             if (tiny) { accepted = true; ftype = true; break; }
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);

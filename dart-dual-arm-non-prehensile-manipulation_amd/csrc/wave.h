@@ -191,6 +191,34 @@ __device__ __forceinline__ double exp_fast(double x) {
     return __builtin_ldexp(__builtin_ldexp(p, n1), n2);
 }
 
+// natural log of x = m 2^e (m = frexp mantissa in [0.5, 1)), fdlibm's e_log.c reduction and
+// minimax polynomial (Lg1..Lg7, < 1 ulp): 1 + f in [sqrt(2)/2, sqrt(2)), s = f / (2 + f),
+// log(1 + f) = f - (hfsq - s (hfsq + R(s^2))).  Shared by the device log_fast and its host check
+// (tools/check_log.cpp); rcp2f(f) supplies 1 / (2 + f).
+template <class Rcp>
+__host__ __device__ __forceinline__ double log_core(double m, int e, Rcp rcp2f) {
+    if (m < 0.70710678118654752440) { m *= 2.0; e -= 1; }
+    const double f = m - 1.0, k = (double)e;
+    const double s = f * rcp2f(f), z = s * s, w = z * z;
+    const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
+    const double t2 = z * fma(w, fma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01),
+                                     2.857142874366239149e-01), 6.666666666666735130e-01);
+    const double R = t2 + t1, hfsq = 0.5 * f * f;
+    return k * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + k * 1.90821492927058770002e-10)) - f);
+}
+struct RcpTwoPlus {     // 1 / (2 + f) for f in [-0.3, 0.42]: v_rcp_f64 + one Newton step
+    __device__ double operator()(double f) const { return frcp(2.0 + f); }
+};
+// log for the barrier terms (positive normal arguments; NaN for x <= 0 or non-finite x, so a
+// trial outside the box is rejected by the filter like with the library log).  About half the
+// instructions of the library log; < 1 ulp (host check).
+__device__ __forceinline__ double log_fast(double x) {
+    const double m = __builtin_amdgcn_frexp_mant(x);
+    const int e = __builtin_amdgcn_frexp_exp(x);
+    const double r = log_core(m, e, RcpTwoPlus());
+    return (x > 0.0 && x < 1.0e308) ? r : __builtin_nan("");
+}
+
 // IPOPT's Compare_le: lhs <= rhs up to 10 machine epsilons of |base| (filter acceptance tests)
 __device__ __forceinline__ bool cmp_le(double lhs, double rhs, double base) {
     return lhs - rhs <= 10.0 * 2.220446049250313e-16 * fabs(base);
