@@ -511,12 +511,12 @@ int dart_mpc_sync(dart_mpc_handle* h) {
     return DART_MPC_OK;
 }
 
-// internal self-test of the wave primitives (not in include/dart_mpc.h): host_out[195]
+// internal self-test of the wave primitives (not in include/dart_mpc.h): host_out[201]
 int dartmpc_selftest(double* host_out) {
     double* d = nullptr;
-    if (hipMalloc(&d, 195 * sizeof(double)) != hipSuccess) return DART_MPC_EHIP;
+    if (hipMalloc(&d, 201 * sizeof(double)) != hipSuccess) return DART_MPC_EHIP;
     hipError_t e = dartmpc_wave_selftest(d, nullptr);
-    if (e == hipSuccess) e = hipMemcpy(host_out, d, 195 * sizeof(double), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(host_out, d, 201 * sizeof(double), hipMemcpyDeviceToHost);
     (void)hipFree(d);
     return e == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
 }

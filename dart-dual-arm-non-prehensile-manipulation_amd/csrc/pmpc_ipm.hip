@@ -625,7 +625,9 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
 
 // self-test of the wave primitives: out[0..63] = from_next(lane), out[64..127] = from_prev(lane),
 // out[128] = wsum(lane), out[129] = wmax(lane), out[130] = wmin(lane + 1),
-// out[131..194] = relative error of the raw v_rcp_f64 on x_i = 1.37^(i-32)*pi (diagnostic)
+// out[131..194] = relative error of the raw v_rcp_f64 on x_i = 1.37^(i-32)*pi (diagnostic),
+// out[195] = wsumf(lane), out[196] = wmaxf(v), out[197] = wminf(v + 0.5) with v = (37 lane) mod 64,
+// out[198] = wmaxf(0 except lane 40: inf), out[199] / out[200] = half_bcast<3>(lane) at lanes 0 / 40
 __global__ __launch_bounds__(kWave) void wave_selftest_kernel(double* out) {
     const double x = (double)threadIdx.x;
     const double n = from_next(x), p = from_prev(x);
@@ -635,6 +637,12 @@ __global__ __launch_bounds__(kWave) void wave_selftest_kernel(double* out) {
     if (threadIdx.x == 0) { out[128] = s; out[129] = mx; out[130] = mn; }
     const double y = 3.141592653589793 * pow(1.37, (double)threadIdx.x - 32.0);
     out[131 + threadIdx.x] = fma(y, __builtin_amdgcn_rcp(y), -1.0);
+    const float v = (float)((37 * threadIdx.x) % 64);
+    const float sf = wsumf((float)threadIdx.x), mxf = wmaxf(v), mnf = wminf(v + 0.5f);
+    const float inf1 = wmaxf(threadIdx.x == 40 ? __builtin_inff() : 0.0f);
+    const double hb = half_bcast_c<3>(x);
+    if (threadIdx.x == 0) { out[195] = sf; out[196] = mxf; out[197] = mnf; out[198] = inf1; out[199] = hb; }
+    if (threadIdx.x == 40) out[200] = hb;
 }
 
 }  // namespace dartmpc

@@ -10,12 +10,14 @@ constexpr int kWave = 64;
 // ---------------------------------------------------------------------------
 // wave primitives (every call site is at wave-uniform control flow: EXEC full)
 // ---------------------------------------------------------------------------
+// DPP move with bound_ctrl: lanes whose source is out of range get 0, rows masked off by ROWMASK
+// are left undefined (no initialising copy of the destination is needed either way)
 template <int CTRL, int ROWMASK = 0xf>
 __device__ __forceinline__ double dpp(double x) {
     const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
     const int lo = (int)(unsigned)(b & 0xffffffffu), hi = (int)(unsigned)(b >> 32);
-    const int rlo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWMASK, 0xf, false);
-    const int rhi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWMASK, 0xf, false);
+    const int rlo = __builtin_amdgcn_mov_dpp(lo, CTRL, ROWMASK, 0xf, true);
+    const int rhi = __builtin_amdgcn_mov_dpp(hi, CTRL, ROWMASK, 0xf, true);
     return __builtin_bit_cast(double, ((unsigned long long)(unsigned)rhi << 32) | (unsigned)rlo);
 }
 __device__ __forceinline__ double readlane(double x, int l) {
@@ -45,8 +47,8 @@ __device__ __forceinline__ double half_bcast(double x, int i) {
         default: return half_bcast_c<7>(x);
     }
 }
-constexpr int kWaveShl1 = 0x130;   // lane k <- lane k+1
-constexpr int kWaveShr1 = 0x138;   // lane k <- lane k-1
+constexpr int kWaveShl1 = 0x130;   // lane k <- lane k+1 (lane 63 <- 0)
+constexpr int kWaveShr1 = 0x138;   // lane k <- lane k-1 (lane 0 <- 0)
 __device__ __forceinline__ double from_next(double x) { return dpp<kWaveShl1>(x); }
 __device__ __forceinline__ double from_prev(double x) { return dpp<kWaveShr1>(x); }
 
@@ -54,21 +56,28 @@ struct OpSum { __device__ double operator()(double a, double b) const { return a
 struct OpMax { __device__ double operator()(double a, double b) const { return fmax(a, b); } };
 struct OpMin { __device__ double operator()(double a, double b) const { return fmin(a, b); } };
 
-// row reduction by quad_perm + row_ror, then the four row totals by readlane: uniform result
+// row reduction by quad_perm + row_ror (every lane of a row holds the row total), then the rows
+// chained by row_bcast:15 (rows 1, 3 take lane 15 / 47) and row_bcast:31 (rows 2, 3 take lane 31):
+// lane 63 holds the wave total, read once (uniform result)
 template <class Op>
 __device__ __forceinline__ double wreduce(double x, Op op) {
     x = op(x, dpp<0xB1>(x));     // quad_perm [1,0,3,2]
     x = op(x, dpp<0x4E>(x));     // quad_perm [2,3,0,1]
     x = op(x, dpp<0x124>(x));    // row_ror:4
     x = op(x, dpp<0x128>(x));    // row_ror:8
-    return op(op(readlane(x, 0), readlane(x, 16)), op(readlane(x, 32), readlane(x, 48)));
+    x = op(x, dpp<0x142, 0xa>(x));   // row_bcast:15
+    x = op(x, dpp<0x143, 0xc>(x));   // row_bcast:31
+    return readlane(x, 63);
 }
 // f32 variant for error measures, scalings and step-length minima (half the DPP traffic):
 // their consumers only compare against tolerances or fractions-to-the-boundary with >= 1 % slack
-template <int CTRL>
+template <int CTRL, int ROWMASK = 0xf>
 __device__ __forceinline__ float dppf(float x) {
-    const int r = __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false);
-    return __builtin_bit_cast(float, r);
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, ROWMASK, 0xf, true));
+}
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ unsigned dppu(unsigned x) {
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)x, CTRL, ROWMASK, 0xf, true);
 }
 __device__ __forceinline__ float readlanef(float x, int l) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
@@ -79,14 +88,32 @@ __device__ __forceinline__ float wreducef(float x, Op op) {
     x = op(x, dppf<0x4E>(x));
     x = op(x, dppf<0x124>(x));
     x = op(x, dppf<0x128>(x));
-    return op(op(readlanef(x, 0), readlanef(x, 16)), op(readlanef(x, 32), readlanef(x, 48)));
+    x = op(x, dppf<0x142, 0xa>(x));
+    x = op(x, dppf<0x143, 0xc>(x));
+    return readlanef(x, 63);
 }
 struct OpSumF { __device__ float operator()(float a, float b) const { return a + b; } };
 struct OpMaxF { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
 struct OpMinF { __device__ float operator()(float a, float b) const { return fminf(a, b); } };
 __device__ __forceinline__ float wsumf(float x) { return wreducef(x, OpSumF()); }
-__device__ __forceinline__ float wmaxf(float x) { return wreducef(x, OpMaxF()); }
-__device__ __forceinline__ float wminf(float x) { return wreducef(x, OpMinF()); }
+// max / min over the wave of NON-NEGATIVE floats (+0, positive, inf; a NaN propagates as the
+// largest): on such values the IEEE order is the unsigned order of the bit patterns, so the steps
+// run on v_max_u32 / v_min_u32, without the NaN-quieting canonicalize fmaxf needs on DPP results
+struct OpMaxU { __device__ unsigned operator()(unsigned a, unsigned b) const { return a > b ? a : b; } };
+struct OpMinU { __device__ unsigned operator()(unsigned a, unsigned b) const { return a < b ? a : b; } };
+template <class Op>
+__device__ __forceinline__ float wreduce_nn(float xf, Op op) {
+    unsigned x = __builtin_bit_cast(unsigned, xf);
+    x = op(x, dppu<0xB1>(x));
+    x = op(x, dppu<0x4E>(x));
+    x = op(x, dppu<0x124>(x));
+    x = op(x, dppu<0x128>(x));
+    x = op(x, dppu<0x142, 0xa>(x));
+    x = op(x, dppu<0x143, 0xc>(x));
+    return __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)x, 63));
+}
+__device__ __forceinline__ float wmaxf(float x) { return wreduce_nn(x, OpMaxU()); }
+__device__ __forceinline__ float wminf(float x) { return wreduce_nn(x, OpMinU()); }
 
 __device__ __forceinline__ double wsum(double x) { return wreduce(x, OpSum()); }
 __device__ __forceinline__ double wmax(double x) { return wreduce(x, OpMax()); }

@@ -143,7 +143,7 @@ def wave_selftest():
     L = lib()
     L.dartmpc_selftest.argtypes = [ctypes.c_void_p]
     L.dartmpc_selftest.restype = ctypes.c_int
-    out = np.zeros(195)
+    out = np.zeros(201)
     rc = L.dartmpc_selftest(ctypes.c_void_p(out.ctypes.data))
     if rc != 0:
         raise DartMPCError(f"dartmpc_selftest failed ({rc})")

@@ -231,5 +231,9 @@ def test_wave_primitives_selftest(dm):
     lanes = np.arange(64.0)
     np.testing.assert_array_equal(out[:63], lanes[1:])        # from_next
     np.testing.assert_array_equal(out[65:128], lanes[:63])    # from_prev
+    assert out[63] == 0.0 and out[64] == 0.0                  # bound_ctrl: out-of-range lanes read 0
     assert out[128] == lanes.sum() and out[129] == 63.0 and out[130] == 1.0
+    # f32 reductions (row_bcast chaining; max / min on the unsigned order of non-negative floats)
+    assert out[195] == lanes.sum() and out[196] == 63.0 and out[197] == 0.5 and np.isinf(out[198])
+    assert out[199] == 3.0 and out[200] == 35.0               # ds_swizzle broadcast within each half
     print("raw v_rcp_f64 max relative error:", np.max(np.abs(out[131:195])))
