@@ -29,6 +29,8 @@
 #include "stamps.h"
 #include "wave.h"
 
+// this kernel runs at the register limit: its double sums use the readlane cross-row step (wsum_rl)
+
 namespace dartmpc {
 
 constexpr int RM_NMAXS = 32;      // max shooting nodes (N <= 31)
@@ -416,7 +418,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         for (int i = 0; i < 6; ++i) th0 += xon ? fabs(gdef[i]) : 0.0;
 #pragma unroll
         for (int i = 0; i < RM_NIQ; ++i) th0 += uon ? fabs(c[i] - s[i]) : 0.0;
-        theta = wsum(th0);
+        theta = wsum_rl(th0);
     }
     const double th_max = 1e4 * fmax(1.0, theta), th_min = 1e-4 * fmax(1.0, theta);
     double fth = 0.0, fph = 0.0;
@@ -691,7 +693,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
                 for (int i = 0; i < RM_NIQ; ++i) gtdl += psi[i] * dS[i];
             }
         }
-        const double phi = wsum(phil), gTd = wsum(gtdl);
+        const double phi = wsum_rl(phil), gTd = wsum_rl(gtdl);
         const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
         const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
         const float lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;
@@ -732,7 +734,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             for (int i = 0; i < RM_NIQ; ++i) thl += uon ? fabs(ct[i] - st_[i]) : 0.0;
             double phl = sc * cost_val(xt, ut, pt);
             phl -= uon ? mu * log_fast(barrier_args(ut, st_)) : 0.0;
-            th_t = wsum(thl); ph_t = wsum(phl);
+            th_t = wsum_rl(thl); ph_t = wsum_rl(phl);
             if (tiny) { accepted = true; ftype = true; break; }
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
             in_filter = in_filter || wany(k < nfilt && th_t >= fth && ph_t >= fph);
@@ -784,7 +786,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     }
 
     // ---------------- outputs -------------------------------------------------------------
-    const double fval = wsum(cost_val(x, u, up));
+    const double fval = wsum_rl(cost_val(x, u, up));
     if (k == 0) {
         a.u0[2 * b] = u[0]; a.u0[2 * b + 1] = u[1];
         a.f[b] = fval; a.status[b] = status; a.iters[b] = it;

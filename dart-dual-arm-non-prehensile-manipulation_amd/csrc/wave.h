@@ -59,12 +59,15 @@ struct OpMin { __device__ double operator()(double a, double b) const { return f
 // row reduction by quad_perm + row_ror (every lane of a row holds the row total), then the rows
 // chained by row_bcast:15 (rows 1, 3 take lane 15 / 47) and row_bcast:31 (rows 2, 3 take lane 31):
 // lane 63 holds the wave total, read once (uniform result)
-template <class Op>
+// (BCAST = false: the four row totals by readlane instead -- fewer VGPRs live across the reduction,
+// for kernels at the register limit)
+template <class Op, bool BCAST = true>
 __device__ __forceinline__ double wreduce(double x, Op op) {
     x = op(x, dpp<0xB1>(x));     // quad_perm [1,0,3,2]
     x = op(x, dpp<0x4E>(x));     // quad_perm [2,3,0,1]
     x = op(x, dpp<0x124>(x));    // row_ror:4
     x = op(x, dpp<0x128>(x));    // row_ror:8
+    if constexpr (!BCAST) return op(op(readlane(x, 0), readlane(x, 16)), op(readlane(x, 32), readlane(x, 48)));
     x = op(x, dpp<0x142, 0xa>(x));   // row_bcast:15
     x = op(x, dpp<0x143, 0xc>(x));   // row_bcast:31
     return readlane(x, 63);
@@ -116,6 +119,7 @@ __device__ __forceinline__ float wmaxf(float x) { return wreduce_nn(x, OpMaxU())
 __device__ __forceinline__ float wminf(float x) { return wreduce_nn(x, OpMinU()); }
 
 __device__ __forceinline__ double wsum(double x) { return wreduce(x, OpSum()); }
+__device__ __forceinline__ double wsum_rl(double x) { return wreduce<OpSum, false>(x, OpSum()); }
 __device__ __forceinline__ double wmax(double x) { return wreduce(x, OpMax()); }
 __device__ __forceinline__ double wmin(double x) { return wreduce(x, OpMin()); }
 __device__ __forceinline__ bool wany(bool p) { return __ballot(p) != 0ull; }
