@@ -200,13 +200,16 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
         g2 = (k == 0) ? vj - svj : vj - iv;
     };
 
-    double g1[NAX], g2[NAX];
+    // sines and defects of the current point: computed here once, then carried over from the
+    // accepted line-search trial (the update x + alpha d repeats the trial's arithmetic exactly)
+    double g1[NAX], g2[NAX], snc[NAX];
     double th0 = 0.0;
 #pragma unroll
     for (int j = 0; j < NAX; ++j) {
         double s0, c0_;
         tilt_sincos(poly, th[j], s0, c0_);
-        defects(p[j], v[j], uon ? s0 : 0.0, sp[j], sv[j], g1[j], g2[j]);
+        snc[j] = uon ? s0 : 0.0;
+        defects(p[j], v[j], snc[j], sp[j], sv[j], g1[j], g2[j]);
         if (xon) th0 += fabs(g1[j]) + fabs(g2[j]);
     }
     double theta = wsum(th0);                                  // filter's constraint violation
@@ -224,10 +227,9 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
         double dinf = 0.0, pinf = 0.0, c0 = 0.0, cmin = 1e300, suml = 0.0, sumz = 0.0;
 #pragma unroll
         for (int j = 0; j < NAX; ++j) {
-            double s_, c_;
-            tilt_sincos(poly, th[j], s_, c_);
-            sn[j] = uon ? s_ : 0.0; cs[j] = uon ? c_ : 0.0;
-            defects(p[j], v[j], sn[j], sp[j], sv[j], g1[j], g2[j]);
+            sn[j] = snc[j];
+            const double c_ = tilt_cos(poly, th[j]);
+            cs[j] = uon ? c_ : 0.0;
             const double ln = from_next(lp[j]), vn = from_next(lv[j]);   // unconditional: EXEC stays full
             lpn[j] = uon ? ln : 0.0; lvn[j] = uon ? vn : 0.0;
             const double sl = th[j] - lo, su = hi - th[j];
@@ -317,11 +319,11 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 mat4_scan_level<0x102>(T);
                 mat4_scan_level<0x104>(T);
                 mat4_scan_level<0x108>(T);
-                {   // rows 0 and 2 of each half: compose with the suffix held by lane 16 (48)
-                    const int src = (lane & 32) | 16;
+                {   // rows 0 and 2 of each half: compose with the suffix held by lane 16 (48), fetched
+                    // by ds_swizzle (bitmask mode, or_mask 16: no address, no LDS access)
                     double F[16];
 #pragma unroll
-                    for (int e = 0; e < 16; ++e) F[e] = __shfl(T[e], src);
+                    for (int e = 0; e < 16; ++e) F[e] = half_bcast_c<16>(T[e]);
                     if ((lane & 16) == 0) {
                         double Nn[16];
 #pragma unroll
@@ -411,9 +413,8 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 affine_scan_level<0x104, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:4
                 affine_scan_level<0x108, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:8
                 {   // rows 0 and 2 compose with the suffix held by the first lane of rows 1 and 3
-                    const int src = (lane & 32) | 16;
                     const bool lo_row = (lane & 16) == 0;
-                    const double r1 = __shfl(c1, src), r2 = __shfl(c2, src);   // only the constant is needed now
+                    const double r1 = half_bcast_c<16>(c1), r2 = half_bcast_c<16>(c2);   // only the constant is needed now
                     if (lo_row) {
                         c1 = fma(m11, r1, fma(m12, r2, c1));
                         c2 = fma(m21, r1, fma(m22, r2, c2));
@@ -522,6 +523,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
         const bool tiny = wmaxf(tnl) < 2.2e-15f;
         STAMP(5);
         int ls = 0;
+        double snt[NAX], g1t[NAX], g2t[NAX];     // the trial's sines and defects (carried on acceptance)
         for (; ls < 80; ++ls) {
             double thl = 0.0, phl = 0.0;
 #pragma unroll
@@ -529,8 +531,10 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 const double pt = fma(alpha, dp[j], p[j]), vt = fma(alpha, dv[j], v[j]), tt = fma(alpha, dth[j], th[j]);
                 double s_, c_;
                 tilt_sincos(poly, tt, s_, c_);
-                double t1, t2;
-                defects(pt, vt, uon ? s_ : 0.0, sp[j], sv[j], t1, t2);
+                snt[j] = uon ? s_ : 0.0;
+                double& t1 = g1t[j];
+                double& t2 = g2t[j];
+                defects(pt, vt, snt[j], sp[j], sv[j], t1, t2);
                 const double ep = pt - rp[j], ev = vt - rv[j];
                 thl += xon ? fabs(t1) + fabs(t2) : 0.0;
                 phl += xon ? fma(scQp * ep, ep, scQv * ev * ev) : 0.0;
@@ -562,6 +566,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
         // -------- accept the step ----------------------------------------------------
 #pragma unroll
         for (int j = 0; j < NAX; ++j) {
+            snc[j] = snt[j]; g1[j] = g1t[j]; g2[j] = g2t[j];
             p[j] = fma(alpha, dp[j], p[j]); v[j] = fma(alpha, dv[j], v[j]);
             lp[j] = fma(alpha, dlp[j], lp[j]); lv[j] = fma(alpha, dlv[j], lv[j]);
             th[j] = fma(alpha, dth[j], th[j]);

@@ -165,6 +165,21 @@ __device__ __forceinline__ void sincos_small(double x, double& s, double& c) {
     pc = fma(pc, y, -0.5);                                   // -1/2!
     c = fma(y, pc, 1.0);
 }
+__device__ __forceinline__ double cos_small(double x) {       // the cosine half of sincos_small
+    const double y = x * x;
+    double pc = 1.0 / 2432902008176640000.0;
+    pc = fma(pc, y, -1.0 / 6402373705728000.0);
+    pc = fma(pc, y, 1.0 / 20922789888000.0);
+    pc = fma(pc, y, -1.0 / 87178291200.0);
+    pc = fma(pc, y, 1.0 / 479001600.0);
+    pc = fma(pc, y, -1.0 / 3628800.0);
+    pc = fma(pc, y, 1.0 / 40320.0);
+    pc = fma(pc, y, -1.0 / 720.0);
+    pc = fma(pc, y, 1.0 / 24.0);
+    pc = fma(pc, y, -0.5);
+    return fma(y, pc, 1.0);
+}
+__device__ __forceinline__ double tilt_cos(bool poly, double x) { return poly ? cos_small(x) : cos(x); }
 __device__ __forceinline__ void tilt_sincos(bool poly, double x, double& s, double& c) {
     if (poly) sincos_small(x, s, c);
     else sincos(x, &s, &c);
