@@ -673,7 +673,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 for (;;) {
                     ok = riccati_s_sweep(S, N, RR);
                     if (ok || soc >= 0 || ++attempt >= 60) break;
-                    delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last / 3.0))
+                    delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))   // IPOPT perturb_dec_fact 1/3
                                            : delta * (delta_last == 0.0 ? 100.0 : 8.0);
                     const double dd = delta - dapplied;
                     if (uon) {

@@ -249,8 +249,8 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
         const double cmin_w = wminf((float)cmin);
         // IPOPT's scalings s_d, s_c (>= 1) as reciprocals: one division each instead of one per test
         const float sz_w = wsumf((float)sumz);
-        const double is_d = 100.0 / fmax(100.0, (double)(wsumf((float)suml) + sz_w) * inv_neb);
-        const double is_c = 100.0 / fmax(100.0, (double)sz_w * inv_nb);
+        const double is_d = 100.0 * frcp(fmax(100.0, (double)(wsumf((float)suml) + sz_w) * inv_neb));
+        const double is_c = 100.0 * frcp(fmax(100.0, (double)sz_w * inv_nb));
         dinf = dinf_w; pinf = pinf_w; c0 = c0_w;
         STAMP(1);
         if (fmax(dinf * is_d, fmax(pinf, c0 * is_c)) <= tol) { status = 0; break; }
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
         int attempt = 0;
         for (; attempt < 60 && !ok; ++attempt) {
             if (attempt > 0)
-                delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last / 3.0))
+                delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))   // IPOPT perturb_dec_fact 1/3
                                        : delta * (delta_last == 0.0 ? 100.0 : 8.0);
             const double X11d = qp2 + delta, X22d = qv2 + delta;
             double Quu[NAX], Rt[NAX];
@@ -508,7 +508,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
         const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
         const float lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;    // log2(theta^s_th / (-gTd)^s_ph)
         double amin = gam_th;
-        if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta / (-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
+        if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta * frcp(-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
         amin *= gam_al;
         double alpha = amax, th_t = 0.0, ph_t = 0.0;
         bool accepted = false, ftype = false;

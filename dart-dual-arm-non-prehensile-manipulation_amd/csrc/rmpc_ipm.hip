@@ -590,7 +590,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         bool ok = riccati_sweep(S, N, RR);
         int attempt = 1;
         for (; attempt < 60 && !ok; ++attempt) {
-            delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last / 3.0))
+            delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))   // IPOPT perturb_dec_fact 1/3
                                    : delta * (delta_last == 0.0 ? 100.0 : 8.0);
             const double dd = delta - dapplied;
             if (uon) {

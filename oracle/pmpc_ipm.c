@@ -417,7 +417,7 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
         double delta = 0.0;
         int ok = riccati_factor(&C, W, 0.0);
         for (int attempt = 0; !ok && attempt < 60; ++attempt) {
-            delta = (attempt == 0) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last / 3.0))
+            delta = (attempt == 0) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))   /* perturb_dec_fact 1/3 */
                                    : delta * (delta_last == 0.0 ? 100.0 : 8.0);
             ok = riccati_factor(&C, W, delta);
         }
