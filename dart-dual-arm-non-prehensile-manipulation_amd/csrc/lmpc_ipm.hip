@@ -532,7 +532,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
 #pragma unroll
             for (int j = 0; j < 6; ++j) dinf = fmax(dinf, (j < 5 ? xon : uon) ? fabs(gl[j]) : 0.0);
 #pragma unroll
-            for (int i = 0; i < 5; ++i) suml += xon ? fabs(lam[i]) / (i < 4 ? dsc[i] : 1.0) : 0.0;
+            for (int i = 0; i < 5; ++i) suml += xon ? fabs(lam[i]) * (i < 4 ? frcp(dsc[i]) : 1.0) : 0.0;
             if (uon) {
                 const double cl = zl * (u - lo), cu = zu * (hi - u);
                 c0 = fmax(cl, cu); cmin = fmin(cl, cu); sumz = zl + zu;
@@ -541,9 +541,10 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         dinf = wmaxf((float)dinf); pinf = wmaxf((float)pinf); pinf_u = wmaxf((float)pinf_u); c0 = wmaxf((float)c0);
         const double cminw = wminf((float)cmin);
         suml = wsumf((float)suml); sumz = wsumf((float)sumz);
-        const double s_d = fmax(100.0, (suml + sumz) / (nA + nb)) / 100.0;
-        const double s_c = fmax(100.0, sumz / nb) / 100.0;
-        const double err = fmax(dinf / s_d, fmax(pinf, c0 / s_c));
+        // IPOPT's scalings s_d, s_c (>= 1) as reciprocals
+        const double is_d = 100.0 * frcp(fmax(100.0, (suml + sumz) * (1.0 / (nA + nb))));
+        const double is_c = 100.0 * frcp(fmax(100.0, sumz * (1.0 / nb)));
+        const double err = fmax(dinf * is_d, fmax(pinf, c0 * is_c));
         // IPOPT OptimalityErrorConvergenceCheck: optimal, then acceptable, then the iteration cap
         if (err <= tol && dinf <= sc && pinf_u <= 1e-4 && c0 <= 1e-4 * sc) { status = 0; break; }
         if (a.acc_iter > 0 && err <= a.acc_tol && pinf_u <= 1e-2 && c0 <= 1e-2 * sc) {
@@ -554,7 +555,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         if (it >= a.max_iter) { status = -1; break; }
         for (;;) {
             const double cmu = fmax(c0 - mu, mu - cminw);
-            if (fmax(dinf / s_d, fmax(pinf, cmu / s_c)) > 10.0 * mu || mu <= mu_min) break;
+            if (fmax(dinf * is_d, fmax(pinf, cmu * is_c)) > 10.0 * mu || mu <= mu_min) break;
             mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
             nfilt = 0;
         }
@@ -612,8 +613,8 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         auto primal_ftb = [&]() {
             double am = 1.0;
             if (uon) {
-                if (dU < 0) am = fmin(am, -tau * (u - lo) / dU);
-                if (dU > 0) am = fmin(am, tau * (hi - u) / dU);
+                if (dU < 0) am = fmin(am, -tau * (u - lo) * frcp(dU));     // reduced in f32 with a 2^-20 margin
+                if (dU > 0) am = fmin(am, tau * (hi - u) * frcp(dU));
             }
             return (double)wminf((float)am) * (1.0 - 1.0 / 1048576.0);
         };
@@ -623,8 +624,8 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             dzu = uon ? mu * isu - zu + zu * isu * dU : 0.0;
             double az_ = 1.0;
             if (uon) {
-                if (dzl < 0) az_ = fmin(az_, -tau * zl / dzl);
-                if (dzu < 0) az_ = fmin(az_, -tau * zu / dzu);
+                if (dzl < 0) az_ = fmin(az_, -tau * zl * frcp(dzl));
+                if (dzu < 0) az_ = fmin(az_, -tau * zu * frcp(dzu));
             }
             return (double)wminf((float)az_) * (1.0 - 1.0 / 1048576.0);
         };
@@ -716,7 +717,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
                 lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;
                 amin = gam_th;
-                if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta / (-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
+                if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta * frcp(-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
                 amin *= gam_al;
                 float tnl = 0.0f;
 #pragma unroll

@@ -51,11 +51,17 @@ struct RmShared {
     double theta[14];
     double rls_Pphi[2][7], rls_phiP[2][7];
     RmModel model;                            // uniform, read at the use sites (keeps VGPRs free)
-    NodeArr<double[4][4], RM_NMAXS + 1> SC;   // per node (row 32: idle lanes), per RK stage: d f1,3 / d vx,vy
+    union {
+        NodeArr<double[4][4], RM_NMAXS + 1> SC;   // per node (row 32: idle lanes), per RK stage: d f1,3 / d vx,vy
+        // [Sigma, psi, r] of the slack rows, parked from the QP build to the slack steps (SC is dead
+        // then; the kernel runs at the register limit)
+        NodeArr<double[3][RM_NIQ], RM_NMAXS + 1> SR;
+    };
     NodeArr<double[4][2], RM_NMAXS + 1> SD;   // tanh curvature per stage -> adjoint-weighted coefficients
     NodeArr<double[8], RM_NMAXS + 1> JL;      // J^T lambda staging, primal residual maxima
     NodeArr<double[10], RM_NMAXS + 1> DL;     // per node: lambda_{k+1}, tilt curvature, g cos(u) for the mirror lanes
 };
+static_assert(sizeof(NodeArr<double[3][RM_NIQ], RM_NMAXS + 1>) <= sizeof(NodeArr<double[4][4], RM_NMAXS + 1>), "SR fits SC");
 
 // continuous model (np_mpc...:178-186); also returns d f / d vx|vy of rows 1, 3 and tanh values
 __device__ __forceinline__ void rm_f(const RmModel& m, const double* y, double sa, double sb, double* f,
@@ -485,8 +491,9 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         for (int i = 0; i < RM_NIQ; ++i) {
             rq[i] = uon ? cz[i] - s[i] : 0.0;
             const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
-            sig[i] = uon ? (i < 2 ? vl[i] / dl : 0.0) + vu[i] / du_ : 0.0;
-            psi[i] = uon ? (i < 2 ? -mu / dl : 0.0) + mu / du_ : 0.0;
+            const double idl = i < 2 ? frcp(dl) : 0.0, idu = frcp(du_);
+            sig[i] = uon ? fma(vl[i], idl, vu[i] * idu) : 0.0;
+            psi[i] = uon ? mu * (idu - idl) : 0.0;
         }
         double dinf = 0.0, pinf = SH.JL[sr][6], c0 = 0.0, cmin = 1e300, suml = 0.0, sumz = 0.0;
         {
@@ -529,18 +536,20 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         dinf = wmaxf((float)dinf); pinf = wmaxf((float)pinf); c0 = wmaxf((float)c0);
         const double cminw = wminf((float)cmin);
         suml = wsumf((float)suml); sumz = wsumf((float)sumz);
-        const double s_d = fmax(100.0, (suml + sumz) / (nA + nI + nb)) / 100.0;
-        const double s_c = fmax(100.0, sumz / nb) / 100.0;
-        if (fmax(dinf / s_d, fmax(pinf, c0 / s_c)) <= tol) { status = 0; break; }
+        // IPOPT's scalings s_d, s_c (>= 1) as reciprocals
+        const double is_d = 100.0 * frcp(fmax(100.0, (suml + sumz) * (1.0 / (nA + nI + nb))));
+        const double is_c = 100.0 * frcp(fmax(100.0, sumz * (1.0 / nb)));
+        if (fmax(dinf * is_d, fmax(pinf, c0 * is_c)) <= tol) { status = 0; break; }
         for (;;) {
             const double cmu = fmax(c0 - mu, mu - cminw);
-            if (fmax(dinf / s_d, fmax(pinf, cmu / s_c)) > 10.0 * mu || mu <= mu_min) break;
+            if (fmax(dinf * is_d, fmax(pinf, cmu * is_c)) > 10.0 * mu || mu <= mu_min) break;
             mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
             nfilt = 0;
 #pragma unroll
             for (int i = 0; i < RM_NIQ; ++i) {
                 const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
-                psi[i] = uon ? (i < 2 ? -mu / dl : 0.0) + mu / du_ : 0.0;
+                const double idl = i < 2 ? frcp(dl) : 0.0, idu = frcp(du_);
+                psi[i] = uon ? mu * (idu - idl) : 0.0;
             }
         }
         const double tau = fmax(0.99, 1.0 - mu);
@@ -572,6 +581,8 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) Hk[hp(8, j)] = gq[j];
             }
+#pragma unroll
+            for (int i = 0; i < RM_NIQ; ++i) { SH.SR[sr][0][i] = sig[i]; SH.SR[sr][1][i] = psi[i]; SH.SR[sr][2][i] = rq[i]; }
             if (k == N) {   // terminal surrogate G_N: value function [[Q_N, q_N], [q_N^T, 0]], Quu = I
                 double* GN = S->G[N];
                 for (int e = 0; e < tri(9); ++e) GN[e] = 0.0;
@@ -634,11 +645,12 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             rm_iq(dzv, 0.0, cdz);
 #pragma unroll
             for (int i = 0; i < RM_NIQ; ++i) {
-                dS[i] = uon ? cdz[i] + rq[i] : 0.0;
-                dY[i] = uon ? sig[i] * dS[i] + psi[i] - yq[i] : 0.0;
+                dS[i] = uon ? cdz[i] + SH.SR[sr][2][i] : 0.0;
+                dY[i] = uon ? SH.SR[sr][0][i] * dS[i] + SH.SR[sr][1][i] - yq[i] : 0.0;
                 const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
-                dvl[i] = uon && i < 2 ? mu / dl - vl[i] - vl[i] / dl * dS[i] : 0.0;
-                dvu[i] = uon ? mu / du_ - vu[i] + vu[i] / du_ * dS[i] : 0.0;
+                const double idl = i < 2 ? frcp(dl) : 0.0, idu = frcp(du_);
+                dvl[i] = uon && i < 2 ? fma(mu, idl, -vl[i]) - vl[i] * idl * dS[i] : 0.0;
+                dvu[i] = uon ? fma(mu, idu, -vu[i]) + vu[i] * idu * dS[i] : 0.0;
             }
             dzl[0] = uon ? mu * isl0 - zl[0] - zl[0] * isl0 * dU[0] : 0.0;
             dzl[1] = uon ? mu * isl1 - zl[1] - zl[1] * isl1 * dU[1] : 0.0;
@@ -649,17 +661,28 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         if (uon) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                if (dU[j] < 0) amax = fmin(amax, -tau * (u[j] - lo) / dU[j]);
-                if (dU[j] > 0) amax = fmin(amax, tau * (hi - u[j]) / dU[j]);
-                if (dzl[j] < 0) az = fmin(az, -tau * zl[j] / dzl[j]);
-                if (dzu[j] < 0) az = fmin(az, -tau * zu[j] / dzu[j]);
+                // fractions to the boundary by frcp: reduced in f32 with a 2^-20 margin below
+                if (dU[j] < 0) amax = fmin(amax, -tau * (u[j] - lo) * frcp(dU[j]));
+                if (dU[j] > 0) amax = fmin(amax, tau * (hi - u[j]) * frcp(dU[j]));
+                if (dzl[j] < 0) az = fmin(az, -tau * zl[j] * frcp(dzl[j]));
+                if (dzu[j] < 0) az = fmin(az, -tau * zu[j] * frcp(dzu[j]));
             }
 #pragma unroll
             for (int i = 0; i < RM_NIQ; ++i) {
-                if (i < 2 && dS[i] < 0) amax = fmin(amax, -tau * (s[i] - sL[i]) / dS[i]);
-                if (dS[i] > 0) amax = fmin(amax, tau * (sU[i] - s[i]) / dS[i]);
-                if (i < 2 && dvl[i] < 0) az = fmin(az, -tau * vl[i] / dvl[i]);
-                if (dvu[i] < 0) az = fmin(az, -tau * vu[i] / dvu[i]);
+                if (i < 2 && dS[i] < 0) amax = fmin(amax, -tau * (s[i] - sL[i]) * frcp(dS[i]));
+                if (dS[i] > 0) amax = fmin(amax, tau * (sU[i] - s[i]) * frcp(dS[i]));
+                if (i < 2 && dvl[i] < 0) az = fmin(az, -tau * vl[i] * frcp(dvl[i]));
+                if (dvu[i] < 0) az = fmin(az, -tau * vu[i] * frcp(dvu[i]));
+            }
+        }
+        // [dY, dvl, dvu] parked until the accept in the node's closed-loop rows (dead after the
+        // forward sweep until the next iteration)
+        double* SY = &S->F[uon ? k : 0][0][0];
+        if (uon) {
+#pragma unroll
+            for (int i = 0; i < RM_NIQ; ++i) {
+                SY[i] = dY[i]; SY[8 + i] = dvu[i];
+                if (i < 2) SY[6 + i] = dvl[i];
             }
         }
         amax = (double)wminf((float)amax) * (1.0 - 1.0 / 1048576.0);
@@ -690,7 +713,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             if (uon) {
                 gtdl += (gq[6] - mu * isl0 + mu * isu0) * dU[0] + (gq[7] - mu * isl1 + mu * isu1) * dU[1];
 #pragma unroll
-                for (int i = 0; i < RM_NIQ; ++i) gtdl += psi[i] * dS[i];
+                for (int i = 0; i < RM_NIQ; ++i) gtdl += SH.SR[sr][1][i] * dS[i];
             }
         }
         const double phi = wsum_rl(phil), gTd = wsum_rl(gtdl);
@@ -698,7 +721,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
         const float lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;
         double amin = gam_th;
-        if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta / (-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
+        if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta * frcp(-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
         amin *= gam_al;
         double alpha = amax, th_t = 0.0, ph_t = 0.0;
         bool accepted = false, ftype = false;
@@ -775,10 +798,11 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 #pragma unroll
             for (int i = 0; i < RM_NIQ; ++i) {
                 s[i] = fma(alpha, dS[i], s[i]);
-                yq[i] = fma(alpha, dY[i], yq[i]);
+                yq[i] = fma(alpha, SY[i], yq[i]);
                 const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
-                if (i < 2) vl[i] = fmax(fmin(fma(az, dvl[i], vl[i]), 1e10 * mu / dl), mu / (1e10 * dl));
-                vu[i] = fmax(fmin(fma(az, dvu[i], vu[i]), 1e10 * mu / du_), mu / (1e10 * du_));
+                const double idl = i < 2 ? frcp(dl) : 0.0, idu = frcp(du_);
+                if (i < 2) vl[i] = fmax(fmin(fma(az, SY[6 + i], vl[i]), 1e10 * mu * idl), 1e-10 * mu * idl);
+                vu[i] = fmax(fmin(fma(az, SY[8 + i], vu[i]), 1e10 * mu * idu), 1e-10 * mu * idu);
             }
         }
         theta = th_t;
