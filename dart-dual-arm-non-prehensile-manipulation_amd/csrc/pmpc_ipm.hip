@@ -245,11 +245,14 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
             cmin = fmin(cmin, uon ? fmin(zl[j] * sl, zu[j] * su) : 1e300);
             sumz += zl[j] + zu[j];
         }
-        const double dinf_w = wmaxf((float)dinf), pinf_w = wmaxf((float)pinf), c0_w = wmaxf((float)c0);
-        const double cmin_w = wminf((float)cmin);
+        float dinf_f = (float)dinf, pinf_f = (float)pinf, c0_f = (float)c0, cmin_f = (float)cmin;
+        float suml_f = (float)suml, sumz_f = (float)sumz;
+        wred_errors(dinf_f, pinf_f, c0_f, cmin_f, suml_f, sumz_f);
+        const double dinf_w = dinf_f, pinf_w = pinf_f, c0_w = c0_f;
+        const double cmin_w = cmin_f;
         // IPOPT's scalings s_d, s_c (>= 1) as reciprocals: one division each instead of one per test
-        const float sz_w = wsumf((float)sumz);
-        const double is_d = 100.0 * frcp(fmax(100.0, (double)(wsumf((float)suml) + sz_w) * inv_neb));
+        const float sz_w = sumz_f;
+        const double is_d = 100.0 * frcp(fmax(100.0, (double)(suml_f + sz_w) * inv_neb));
         const double is_c = 100.0 * frcp(fmax(100.0, (double)sz_w * inv_nb));
         dinf = dinf_w; pinf = pinf_w; c0 = c0_w;
         STAMP(1);
@@ -487,8 +490,10 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
             az = fmin(az, uon ? fmin(czl, czu) : 1.0);
         }
         // f32 minima rounded down: tau <= 0.99 leaves far more slack than the f32 rounding
-        amax = (double)wminf((float)amax) * (1.0 - 1.0 / 1048576.0);
-        az = (double)wminf((float)az) * (1.0 - 1.0 / 1048576.0);
+        float amax_f = (float)amax, az_f = (float)az;
+        wmin2f(amax_f, az_f);
+        amax = (double)amax_f * (1.0 - 1.0 / 1048576.0);
+        az = (double)az_f * (1.0 - 1.0 / 1048576.0);
         STAMP(4);
 
         // -------- filter line search (Waechter & Biegler 2006, Alg. A) -------------
@@ -502,7 +507,8 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
             phil += uon ? fma(scR * th[j], th[j], -mu * log_fast(sl * su)) : 0.0;
             gtdl += uon ? rt[j] * dth[j] : 0.0;
         }
-        const double phi = wsum(phil), gTd = wsum(gtdl);
+        wsum2(phil, gtdl);
+        const double phi = phil, gTd = gtdl;
         // switching condition alpha (-gTd)^s_ph > delta theta^s_th, compared in log2 space
         const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
         const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
@@ -540,7 +546,8 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 phl += xon ? fma(scQp * ep, ep, scQv * ev * ev) : 0.0;
                 phl += uon ? fma(scR * tt, tt, -mu * log_fast((tt - lo) * (hi - tt))) : 0.0;
             }
-            th_t = wsum(thl); ph_t = wsum(phl);
+            wsum2(thl, phl);
+            th_t = thl; ph_t = phl;
             if (tiny) { accepted = true; ftype = true; break; }
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
             in_filter = in_filter || wany(lane < nfilt && th_t >= fth && ph_t >= fph);

@@ -118,6 +118,52 @@ __device__ __forceinline__ float wreduce_nn(float xf, Op op) {
 __device__ __forceinline__ float wmaxf(float x) { return wreduce_nn(x, OpMaxU()); }
 __device__ __forceinline__ float wminf(float x) { return wreduce_nn(x, OpMinU()); }
 
+// Several independent reductions advanced level by level in lock step: the chains interleave, so
+// no DPP read waits on the VALU result just before it and each chain's latency hides behind the
+// others'.  Levels: quad_perm [1,0,3,2], [2,3,0,1], row_ror 4, 8, row_bcast 15 (rows 1, 3),
+// row_bcast 31 (rows 2, 3); the total is read from lane 63.
+template <int CTRL, int RM>
+__device__ __forceinline__ void lvl_sum(double& x) { x += dpp<CTRL, RM>(x); }
+template <int CTRL, int RM>
+__device__ __forceinline__ void lvl_sumf(float& x) { x += dppf<CTRL, RM>(x); }
+template <int CTRL, int RM>
+__device__ __forceinline__ void lvl_maxu(unsigned& x) { const unsigned y = dppu<CTRL, RM>(x); x = x > y ? x : y; }
+template <int CTRL, int RM>
+__device__ __forceinline__ void lvl_minu(unsigned& x) { const unsigned y = dppu<CTRL, RM>(x); x = x < y ? x : y; }
+#define DART_LEVELS(F) F(0xB1, 0xf) F(0x4E, 0xf) F(0x124, 0xf) F(0x128, 0xf) F(0x142, 0xa) F(0x143, 0xc)
+
+// two f64 sums
+__device__ __forceinline__ void wsum2(double& a, double& b) {
+#define DART_L(C, R) lvl_sum<C, R>(a); lvl_sum<C, R>(b);
+    DART_LEVELS(DART_L)
+#undef DART_L
+    a = readlane(a, 63); b = readlane(b, 63);
+}
+// two f32 minima of non-negative values (see wreduce_nn)
+__device__ __forceinline__ void wmin2f(float& a, float& b) {
+    unsigned x = __builtin_bit_cast(unsigned, a), y = __builtin_bit_cast(unsigned, b);
+#define DART_L(C, R) lvl_minu<C, R>(x); lvl_minu<C, R>(y);
+    DART_LEVELS(DART_L)
+#undef DART_L
+    a = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)x, 63));
+    b = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)y, 63));
+}
+// the error-measure reductions of an IPM iteration: three maxima and one minimum of non-negative
+// values, two f32 sums
+__device__ __forceinline__ void wred_errors(float& mx0, float& mx1, float& mx2, float& mn, float& s0, float& s1) {
+    unsigned a = __builtin_bit_cast(unsigned, mx0), b = __builtin_bit_cast(unsigned, mx1);
+    unsigned c = __builtin_bit_cast(unsigned, mx2), d = __builtin_bit_cast(unsigned, mn);
+#define DART_L(C, R) lvl_maxu<C, R>(a); lvl_maxu<C, R>(b); lvl_maxu<C, R>(c); lvl_minu<C, R>(d); \
+    lvl_sumf<C, R>(s0); lvl_sumf<C, R>(s1);
+    DART_LEVELS(DART_L)
+#undef DART_L
+    mx0 = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)a, 63));
+    mx1 = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)b, 63));
+    mx2 = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)c, 63));
+    mn = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)d, 63));
+    s0 = readlanef(s0, 63); s1 = readlanef(s1, 63);
+}
+
 __device__ __forceinline__ double wsum(double x) { return wreduce(x, OpSum()); }
 __device__ __forceinline__ double wsum_rl(double x) { return wreduce<OpSum, false>(x, OpSum()); }
 __device__ __forceinline__ double wmax(double x) { return wreduce(x, OpMax()); }
