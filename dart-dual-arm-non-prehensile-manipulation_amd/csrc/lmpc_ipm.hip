@@ -538,9 +538,12 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 c0 = fmax(cl, cu); cmin = fmin(cl, cu); sumz = zl + zu;
             }
         }
-        dinf = wmaxf((float)dinf); pinf = wmaxf((float)pinf); pinf_u = wmaxf((float)pinf_u); c0 = wmaxf((float)c0);
-        const double cminw = wminf((float)cmin);
-        suml = wsumf((float)suml); sumz = wsumf((float)sumz);
+        float r0 = (float)dinf, r1 = (float)pinf, r2 = (float)pinf_u, r3 = (float)c0, r4 = (float)cmin;
+        float r5 = (float)suml, r6 = (float)sumz;
+        wred_errors4(r0, r1, r2, r3, r4, r5, r6);
+        dinf = r0; pinf = r1; pinf_u = r2; c0 = r3;
+        const double cminw = r4;
+        suml = r5; sumz = r6;
         // IPOPT's scalings s_d, s_c (>= 1) as reciprocals
         const double is_d = 100.0 * frcp(fmax(100.0, (suml + sumz) * (1.0 / (nA + nb))));
         const double is_c = 100.0 * frcp(fmax(100.0, sumz * (1.0 / nb)));
@@ -638,7 +641,9 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             defects(xt, pt, ut, gt);
             double phl = sc * cost_val(xt, ut, pt);
             if (uon) phl -= mu * log_fast((ut - lo) * (hi - ut));
-            th_t = wsum(theta_of(gt)); ph_t = wsum(phl);
+            double thl = theta_of(gt);
+            wsum2(thl, phl);
+            th_t = thl; ph_t = phl;
         };
         // filter acceptance of (th_t, ph_t) for the step size al_test (IPOPT alpha_primal_test)
         auto acceptable = [&](double al_test, bool& ft) {
@@ -712,7 +717,8 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     for (int i = 0; i < 5; ++i) gtdl += xon ? sc * gz_[i] * dx[i] : 0.0;
                     if (uon) gtdl += (sc * gz_[5] - mu * isl + mu * isu) * dU;
                 }
-                phi = wsum(phil); gTd = wsum(gtdl);
+                wsum2(phil, gtdl);
+                phi = phil; gTd = gtdl;
                 const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
                 const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
                 lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;

@@ -533,9 +533,11 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
                 c0 = fmax(c0, fmax(cl, cu)); cmin = fmin(cmin, fmin(cl, cu)); sumz += zl[j] + zu[j];
             }
         }
-        dinf = wmaxf((float)dinf); pinf = wmaxf((float)pinf); c0 = wmaxf((float)c0);
-        const double cminw = wminf((float)cmin);
-        suml = wsumf((float)suml); sumz = wsumf((float)sumz);
+        float r0 = (float)dinf, r1 = (float)pinf, r2 = (float)c0, r3 = (float)cmin, r4 = (float)suml, r5 = (float)sumz;
+        wred_errors(r0, r1, r2, r3, r4, r5);
+        dinf = r0; pinf = r1; c0 = r2;
+        const double cminw = r3;
+        suml = r4; sumz = r5;
         // IPOPT's scalings s_d, s_c (>= 1) as reciprocals
         const double is_d = 100.0 * frcp(fmax(100.0, (suml + sumz) * (1.0 / (nA + nI + nb))));
         const double is_c = 100.0 * frcp(fmax(100.0, sumz * (1.0 / nb)));
@@ -685,8 +687,10 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
                 if (i < 2) SY[6 + i] = dvl[i];
             }
         }
-        amax = (double)wminf((float)amax) * (1.0 - 1.0 / 1048576.0);
-        az = (double)wminf((float)az) * (1.0 - 1.0 / 1048576.0);
+        float amax_f = (float)amax, az_f = (float)az;
+        wmin2f(amax_f, az_f);
+        amax = (double)amax_f * (1.0 - 1.0 / 1048576.0);
+        az = (double)az_f * (1.0 - 1.0 / 1048576.0);
 
         STAMP(5);
         // ---------------- filter line search -------------------------------------------------

@@ -148,6 +148,24 @@ __device__ __forceinline__ void wmin2f(float& a, float& b) {
     a = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)x, 63));
     b = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)y, 63));
 }
+// the error-measure reductions of an IPM iteration: four maxima and one minimum of non-negative
+// values, two f32 sums
+__device__ __forceinline__ void wred_errors4(float& mx0, float& mx1, float& mx2, float& mx3, float& mn, float& s0,
+                                             float& s1) {
+    unsigned a = __builtin_bit_cast(unsigned, mx0), b = __builtin_bit_cast(unsigned, mx1);
+    unsigned c = __builtin_bit_cast(unsigned, mx2), e = __builtin_bit_cast(unsigned, mx3);
+    unsigned d = __builtin_bit_cast(unsigned, mn);
+#define DART_L(C, R) lvl_maxu<C, R>(a); lvl_maxu<C, R>(b); lvl_maxu<C, R>(c); lvl_maxu<C, R>(e); \
+    lvl_minu<C, R>(d); lvl_sumf<C, R>(s0); lvl_sumf<C, R>(s1);
+    DART_LEVELS(DART_L)
+#undef DART_L
+    mx0 = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)a, 63));
+    mx1 = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)b, 63));
+    mx2 = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)c, 63));
+    mx3 = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)e, 63));
+    mn = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)d, 63));
+    s0 = readlanef(s0, 63); s1 = readlanef(s1, 63);
+}
 // the error-measure reductions of an IPM iteration: three maxima and one minimum of non-negative
 // values, two f32 sums
 __device__ __forceinline__ void wred_errors(float& mx0, float& mx1, float& mx2, float& mn, float& s0, float& s1) {
