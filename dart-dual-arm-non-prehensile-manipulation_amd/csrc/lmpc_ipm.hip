@@ -128,7 +128,7 @@ __device__ __forceinline__ void sub_rk4(const LmSub& ml, const double* x, double
     double k[4], y[4], acc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) { y[i] = x[i]; acc[i] = 0.0; }
-#pragma unroll 1
+#pragma unroll
     for (int s = 0; s < 4; ++s) {
         const double wts = (s == 0 || s == 3) ? 1.0 : 2.0, cst = s < 2 ? 0.5 : (s == 2 ? 1.0 : 0.0);
         sub_f(m, y, sa, k);
@@ -148,7 +148,7 @@ __device__ __forceinline__ void sub_rk4_lin(const LmSub& ml, const double* x, do
     double y[4], acc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) { y[i] = x[i]; acc[i] = 0.0; }
-#pragma unroll 1
+#pragma unroll
     for (int s = 0; s < 4; ++s) {
         const double wts = (s == 0 || s == 3) ? 1.0 : 2.0, cst = s < 2 ? 0.5 : (s == 2 ? 1.0 : 0.0);
         double k[4];
@@ -196,7 +196,7 @@ __device__ __forceinline__ double sub_adjoint_curv(const LmSub& m, const double 
 #pragma unroll
     for (int i = 0; i < 4; ++i) kb[i] = -(h / 6.0) * lamn[i];        // kb_4
     double huu = 0.0;
-#pragma unroll 1
+#pragma unroll
     for (int s = 3; s >= 0; --s) {
         double* d = sd[s];
         const double c_v = kb[1] * (-d[0] * m.im);
@@ -479,7 +479,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     const LmSub mr = m;     // model to registers once for the five directions
                     // with the cost / barrier terms of z = [x(4), up, u, 1] on the diagonal (gradient row later)
                     const double cu = sc * 2.0 * (Ru + Rdu) + zl * isl + zu * isu;
-#pragma unroll 1
+#pragma unroll
                     for (int d = 0; d < 5; ++d)
                         SH.JL[sl][d] = sub_direction(mr, SH.SC[sl], SH.SD[sl], huu, LM_G * ca, d, lamn, Mk, Hk,
                                                      d < 4 ? sc * 2.0 * Wq[d] : cu);
