@@ -105,7 +105,7 @@ __device__ __forceinline__ void rm_rk4_lin(const RmModel& mlds, const double* x,
     double y[4], acc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) { y[i] = x[i]; acc[i] = 0.0; }
-#pragma unroll 1
+#pragma unroll
     for (int s = 0; s < 4; ++s) {
         const double wts = (s == 0 || s == 3) ? 1.0 : 2.0, cst = s < 2 ? 0.5 : (s == 2 ? 1.0 : 0.0);
         double k[4], j1vx, j1vy, j3vx, j3vy, tx, ty;
@@ -138,7 +138,7 @@ __device__ __forceinline__ void rm_adjoint_curv(const RmModel& mlds, const doubl
 #pragma unroll
     for (int i = 0; i < 4; ++i) kb[i] = -(h / 6.0) * lamn[i];
     huu[0] = 0.0; huu[1] = 0.0;
-#pragma unroll 1
+#pragma unroll
     for (int s = 3; s >= 0; --s) {
         sd[s][0] = fma(kb[1], m.th[4], kb[3] * m.th[11]) * sd[s][0];
         sd[s][1] = fma(kb[1], m.th[5], kb[3] * m.th[12]) * sd[s][1];
@@ -231,7 +231,7 @@ __device__ __forceinline__ void rm_directions(const RmModel& m, const double (*s
 #pragma unroll
     for (int i = 0; i < 14; ++i) mr.th[i] = m.th[i];
     mr.gz = m.gz; mr.h = m.h; mr.ie = m.ie;
-#pragma unroll 1
+#pragma unroll
     for (int d = d0; d < d0 + 3; ++d) jl_lds[d] = rm_direction(mr, scr, cvr, huu, gca, gcb, d, lamn, Mk, Hk);
 }
 
