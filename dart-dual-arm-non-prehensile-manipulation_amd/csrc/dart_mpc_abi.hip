@@ -32,14 +32,23 @@ struct HostStage {
     char* din = nullptr;            // device mirror of hin
     char* hout = nullptr;           // pinned, mapped, coherent: kernel outputs
     char* dout = nullptr;           // device address of hout
-    size_t in_cap = 0, out_cap = 0, in_off = 0, out_off = 0, io_first = 0;
+    char* hzc = nullptr;            // pinned, mapped, coherent: zero-copy inputs (read by the kernel over PCIe)
+    char* dzc = nullptr;            // device address of hzc
+    size_t in_cap = 0, out_cap = 0, zc_cap = 0, in_off = 0, out_off = 0, zc_off = 0, io_first = 0;
     struct Back { void* dst; size_t off, bytes; };
     Back back[8];
     int nback = 0;
 
     static size_t al(size_t n) { return (n + 255) & ~size_t(255); }
-    hipError_t reserve(size_t in_bytes, size_t out_bytes) {
+    hipError_t reserve(size_t in_bytes, size_t out_bytes, size_t zc_bytes = 0) {
         hipError_t e = hipSuccess;
+        if (zc_bytes > zc_cap) {
+            release_zc();
+            e = hipHostMalloc((void**)&hzc, zc_bytes, hipHostMallocMapped | hipHostMallocCoherent);
+            if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&dzc, hzc, 0);
+            if (e != hipSuccess) { release_zc(); return e; }
+            zc_cap = zc_bytes;
+        }
         if (in_bytes > in_cap) {
             release_in();
             e = hipHostMalloc((void**)&hin, in_bytes, hipHostMallocDefault);
@@ -65,7 +74,20 @@ struct HostStage {
         if (hout) (void)hipHostFree(hout);
         hout = dout = nullptr; out_cap = 0;
     }
-    void begin() { in_off = out_off = 0; nback = 0; io_first = 0; }
+    void release_zc() {
+        if (hzc) (void)hipHostFree(hzc);
+        hzc = dzc = nullptr; zc_cap = 0;
+    }
+    void begin() { in_off = out_off = zc_off = 0; nback = 0; io_first = 0; }
+    // device-visible pointer of an input the kernel reads straight from mapped host memory: no DMA
+    // copy on the call path (for kernels that read their inputs once, at the start)
+    template <class T> const T* in_zc(const T* src, size_t n) {
+        if (!src) return nullptr;
+        const size_t off = zc_off;
+        std::memcpy(hzc + off, src, n * sizeof(T));
+        zc_off += al(n * sizeof(T));
+        return reinterpret_cast<const T*>(dzc + off);
+    }
     // device pointer of an input copied from src (n elements); nullptr stays nullptr
     template <class T> const T* in(const T* src, size_t n) {
         if (!src) return nullptr;
@@ -106,7 +128,7 @@ struct HostStage {
     template <class T> void take(T* dst, const T* dev_out, size_t n) const {
         if (dst && dev_out) std::memcpy(dst, host_of(dev_out), n * sizeof(T));
     }
-    void release() { release_in(); release_out(); }
+    void release() { release_in(); release_out(); release_zc(); }
 };
 
 // stage + stream of the stateless host entries (arm QP, policy step, RLS), one per device
@@ -229,7 +251,10 @@ int dart_mpc_create(const dart_mpc_config* cfg, int device, dart_mpc_handle** ou
         nin = B * (6 + 6 + 6 + nw);
         nout = B * (2 + 1 + nw + 1);
     }
-    if (e == hipSuccess) e = h->st.reserve(nin * sizeof(double) + A, nout * sizeof(double) + A);
+    // PMPC reads its inputs zero-copy (dart_mpc_solve_batch): their pinned buffer is the mapped one
+    const bool zc = cfg->variant == DART_MPC_PMPC;
+    if (e == hipSuccess)
+        e = h->st.reserve(zc ? A : nin * sizeof(double) + A, nout * sizeof(double) + A, zc ? nin * sizeof(double) + A : 0);
     if (e != hipSuccess) {
         dart_mpc_destroy(h);
         return DART_MPC_EHIP;
@@ -265,10 +290,12 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     const size_t nw = (size_t)dart_mpc_nw(h->cfg.N);
     HostStage& S = h->st;
     S.begin();
-    const double* d_x0 = S.in(x0, 6 * B);
-    const double* d_ref = S.in(ref, 6 * B);
-    const double* d_prm = S.in(prm, 6 * B);
-    const double* d_ww = S.in(w_warm, nw * B);
+    // the PMPC kernel reads x0 / ref / prm / w_warm once, at its start: zero-copy from mapped host
+    // memory instead of a DMA copy on the call path
+    const double* d_x0 = S.in_zc(x0, 6 * B);
+    const double* d_ref = S.in_zc(ref, 6 * B);
+    const double* d_prm = S.in_zc(prm, 6 * B);
+    const double* d_ww = S.in_zc(w_warm, nw * B);
     double* d_u0 = S.out<double>(2 * B);
     double* d_f = S.out<double>(B);
     double* d_wo = w_out ? S.out<double>(nw * B) : nullptr;
