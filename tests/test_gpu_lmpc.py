@@ -54,6 +54,25 @@ def test_c5_batch_vs_oracle(dm):
     assert np.allclose(out["f"], ref["f"], rtol=1e-6, atol=1e-9)
 
 
+def test_wide_tilt_box_library_trig_path(dm):
+    """u box [-1.2, 1.2] (library sin/cos for the tilts instead of the Taylor path) against the C
+    oracle at a tight tolerance."""
+    from dart_mpc.workload import lmpc_batch
+    from dart_mpc._lib import LMPC_PRM_DEFAULT
+    D = lmpc_batch(1)
+    prm = np.tile(LMPC_PRM_DEFAULT, (D["state"].shape[0], 1))
+    prm[:, 20] = -1.2; prm[:, 21] = 1.2
+    s = dm.LmpcSolver(N=20, tol=1e-10, max_iter=500, acceptable_iter=0, B_max=64)
+    out = s.solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], prm=prm, want_w=True)
+    s.close()
+    ref = oracle_lib.lmpc_solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], N=20, tol=1e-10, acc_iter=0,
+                                      max_iter=500, nthreads=4, prm=prm)
+    ok = (out["status"] == 0) & (ref["status"] == 0)
+    assert ok.mean() >= 0.9, (out["status"], ref["status"])
+    assert np.array_equal(out["status"], ref["status"])
+    assert np.max(np.abs(out["u0"][ok] - ref["u0"][ok])) <= 1e-6
+
+
 def test_reference_options(dm, lmpc_goldens):
     G = lmpc_goldens
     idx = np.nonzero(G["group"] == "c5")[0]

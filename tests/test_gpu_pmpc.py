@@ -113,6 +113,25 @@ def test_c2_and_c4_batches_match_oracle(dm):
             np.testing.assert_allclose(out["f"], ref["f"], rtol=1e-7, atol=1e-9)
 
 
+def test_wide_tilt_box_library_trig_path(dm):
+    """Tilt boxes wider than 1 rad leave the Taylor sin/cos of the kernel for the library path:
+    u in [-1.2, 1.2] with far targets (controls saturate well past 1 rad), against the C oracle."""
+    import oracle_lib
+    from dart_mpc.workload import pmpc_batch
+    S, T, P = pmpc_batch(1)
+    P = P.copy(); P[:, 4] = -1.2; P[:, 5] = 1.2
+    T = T.copy(); T[:, 0] = np.where(S[:, 0] > 0, -0.6, 0.6); T[:, 2] = np.where(S[:, 2] > 0, -0.5, 0.5)
+    s = dm.Solver(N=20, Ts=0.002, tol=1e-11, B_max=S.shape[0])
+    out = s.solve_batch(S, T, P, want_w=True)
+    s.close()
+    ref = oracle_lib.solve_batch(S, T, P, N=20, Ts=0.002, tol=1e-11, nthreads=8, want_w=True)
+    assert np.all(out["status"] == 0) and np.all(ref["status"] == 0), (out["status"], ref["status"])
+    nX = 6 * 21
+    assert np.max(np.abs(out["w"][:, nX:])) > 1.0                  # the library trig path was exercised
+    assert np.max(np.abs(out["u0"] - ref["u0"])) <= 1e-6
+    np.testing.assert_allclose(out["f"], ref["f"], rtol=1e-7, atol=1e-9)
+
+
 def test_scan_and_sequential_riccati_agree(dm):
     """The launcher runs the quadratic Riccati part as a DPP scan for B <= 1024 and as the sequential
     sweep beyond (throughput regime).  The same 1152 instances solved as one launch of 2304 (sequential;

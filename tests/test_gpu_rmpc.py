@@ -57,6 +57,21 @@ def test_c3_batch_vs_oracle(dm, tol, u0_bound, U_bound):
     assert np.max(np.abs(out["iters"] - ref["iters"])) <= 10, (out["iters"], ref["iters"])
 
 
+def test_wide_tilt_box_library_trig_path(dm):
+    """u box [-1.2, 1.2] (library sin/cos instead of the Taylor path) against the C oracle."""
+    from dart_mpc.workload import rmpc_batch
+    D = rmpc_batch(1)
+    prm = D["prm"].copy(); prm[:, 4] = -1.2; prm[:, 5] = 1.2
+    s = dm.RmpcSolver(N=20, tol=1e-11, max_iter=500, B_max=64)
+    out = s.solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], prm, want_w=True)
+    s.close()
+    ref = oracle_lib.rmpc_solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], prm, N=20, tol=1e-11,
+                                      max_iter=500, nthreads=4)
+    assert np.all(out["status"] == 0) and np.all(ref["status"] == 0), (out["status"], ref["status"])
+    assert np.max(np.abs(out["u0"] - ref["u0"])) <= 1e-6
+    assert np.allclose(out["f"], ref["f"], rtol=1e-6, atol=1e-10)
+
+
 @pytest.mark.parametrize("N", [1, 2, 15, 31])
 def test_horizons(dm, N):
     from dart_mpc.workload import rmpc_batch
