@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--rmpc-steps", type=int, default=200, help="launches of the supplementary C3 RMPC line (0 = skip)")
     ap.add_argument("--lmpc-steps", type=int, default=100, help="launches of the supplementary C5 LMPC line (0 = skip)")
     ap.add_argument("--arm-steps", type=int, default=200, help="launches of the supplementary arm-QP line (0 = skip)")
+    ap.add_argument("--n15-steps", type=int, default=200,
+                    help="launches of the supplementary PMPC line at the driver's horizon N=15 (0 = skip)")
     ap.add_argument("--c4-steps", type=int, default=50,
                     help="steps of the supplementary C4 line (1152 instances sharded over the ranks + gather; 0 = skip)")
     ap.add_argument("--saturation-batch", type=int, default=18 * 1024,
@@ -127,6 +129,46 @@ def bench_rmpc(args, torch, dev, stream, dart_mpc):
                                "sample": f"C oracle (oracle/rmpc_ipm.c), {solved} cold-start C3 solves in {cdt:.1f} s"}
     s.close()
     return out
+
+
+def bench_pmpc_driver_horizon(args, torch, dev, stream, dart_mpc, N=15):
+    """PMPC at the DART driver's own horizon (N = 15 for every object, main_parallel_enhanced.py:171-196),
+    batch 18, fresh instances per launch, inputs in HBM.  At N <= 15 each axis fits one 16-lane DPP row
+    and the scans skip their cross-row steps."""
+    from dart_mpc.workload import pmpc_batch
+    B, K = 18, args.n15_steps
+    steps = [pmpc_batch(1, seed0=600000 + 1000 * i) for i in range(K + 5)]
+    T = lambda j: torch.tensor(np.stack([st[j] for st in steps]), dtype=torch.float64, device=dev).contiguous()
+    X0, RF, PR = T(0), T(1), T(2)
+    U0 = torch.empty((K + 5, B, 2), dtype=torch.float64, device=dev)
+    FV = torch.empty((K + 5, B), dtype=torch.float64, device=dev)
+    ST = torch.empty((K + 5, B), dtype=torch.int32, device=dev)
+    IT = torch.empty((K + 5, B), dtype=torch.int32, device=dev)
+    s = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=B, device=dev.index)
+    sp = stream.cuda_stream
+
+    def launch(i):
+        s.solve_batch_dev(B, X0[i].data_ptr(), RF[i].data_ptr(), PR[i].data_ptr(), U0[i].data_ptr(), FV[i].data_ptr(),
+                          ST[i].data_ptr(), IT[i].data_ptr(), stream=sp)
+
+    for i in range(5):
+        launch(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for j in range(K):
+            launch(5 + j)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = ST[5:].cpu().numpy()
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_lib   # checker only
+    S0, T0, P0 = steps[5]
+    ref = oracle_lib.solve_batch(S0, T0, P0, N=N, Ts=0.002, tol=1e-11, nthreads=4, want_w=False)
+    s.close()
+    return {"workload": f"PMPC batch=18, N={N} (the DART driver's horizon), tol {args.tol:g}, cold start",
+            "solves_per_s": B * K / dt, "ms_per_step": dt / K * 1e3, "status_ok_frac": float(np.mean(st == 0)),
+            "max_abs_u0_err_vs_exact_optimum": float(np.max(np.abs(U0[5].cpu().numpy() - ref["u0"])))}
 
 
 def bench_c4(args, torch, dev, stream, dart_mpc, world, rank):
@@ -503,6 +545,11 @@ def main():
     # supplementary C4 (BASELINE.json configs[3]): 1152 instances sharded over the ranks + result gather
     c4 = bench_c4(args, torch, dev, stream, dart_mpc, world, rank) if args.c4_steps > 0 else None
 
+    # supplementary PMPC line at the DART driver's horizon (N = 15)
+    n15 = None
+    if rank == 0 and args.n15_steps > 0:
+        n15 = bench_pmpc_driver_horizon(args, torch, dev, stream, dart_mpc)
+
     # supplementary C3 (BASELINE.json configs[2]): RMPC batch=18 with the RLS update fused into the launch
     rmpc = None
     if rank == 0 and args.rmpc_steps > 0:
@@ -556,6 +603,7 @@ def main():
             "saturation": saturation,
             "host_path_pcie_inclusive": host_path,
             "pmpc_c4": c4,
+            "pmpc_n15": n15,
             "rmpc_c3": rmpc,
             "lmpc_c5": lmpc,
             "arm_qp": arm,

@@ -124,7 +124,9 @@ __device__ __forceinline__ void mat4_scan_level(double* T) {
 // ---------------------------------------------------------------------------
 //   QSCAN: compile the quadratic-Riccati scan (latency regime); without it the kernel fits 2 waves
 //   per SIMD (throughput regime)
-template <int NAX, bool QSCAN>
+//   ONEROW: N <= 15, every axis fits one 16-lane DPP row and the scans need no cross-row step (the
+//   DART driver's default horizon is 15, main_parallel_enhanced.py:171-196)
+template <int NAX, bool QSCAN, bool ONEROW = false>
 __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
     STAMP_DECL
     // small batches: the launcher deals 8 blocks per instance and only every 8th works, so all
@@ -136,6 +138,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
     const int ax0 = NAX == 1 ? (lane >> 5) : 0;               // axis of slot 0 (NAX == 1)
     const int N = a.N;
     const bool xon = k <= N, uon = k < N;
+    constexpr bool one_row = ONEROW;
     const double h = a.Ts;
 
     const double* st = a.x0 + 6 * b;
@@ -322,8 +325,8 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 mat4_scan_level<0x102>(T);
                 mat4_scan_level<0x104>(T);
                 mat4_scan_level<0x108>(T);
-                {   // rows 0 and 2 of each half: compose with the suffix held by lane 16 (48), fetched
-                    // by ds_swizzle (bitmask mode, or_mask 16: no address, no LDS access)
+                if constexpr (!one_row) {   // rows 0 and 2 of each half: compose with the suffix held by lane 16 (48),
+                    // fetched by ds_swizzle (bitmask mode, or_mask 16: no address, no LDS access)
                     double F[16];
 #pragma unroll
                     for (int e = 0; e < 16; ++e) F[e] = half_bcast_c<16>(T[e]);
@@ -415,7 +418,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 affine_scan_level<0x102, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:2
                 affine_scan_level<0x104, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:4
                 affine_scan_level<0x108, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:8
-                {   // rows 0 and 2 compose with the suffix held by the first lane of rows 1 and 3
+                if constexpr (!one_row) {   // rows 0 and 2 compose with the suffix held by the first lane of rows 1 and 3
                     const bool lo_row = (lane & 16) == 0;
                     const double r1 = half_bcast_c<16>(c1), r2 = half_bcast_c<16>(c2);   // only the constant is needed now
                     if (lo_row) {
@@ -452,7 +455,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
             affine_scan_level<0x112, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:2
             affine_scan_level<0x114, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:4
             affine_scan_level<0x118, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:8
-            affine_scan_level<0x142, 0xa>(f11, f12, f21, f22, c1, c2);   // row_bcast:15 -> rows 1, 3
+            if constexpr (!one_row) affine_scan_level<0x142, 0xa>(f11, f12, f21, f22, c1, c2);   // row_bcast:15 -> rows 1, 3
             dp[0] = c1; dv[0] = c2;
         } else
         for (int step = 0; step < N; ++step) {
@@ -670,7 +673,9 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
         const char* e = getenv("DART_PMPC_QSCAN_MAX_B");
         return e ? atoi(e) : 1024;
     }();
-    if (a.N <= 31 && a.B <= qscan_max_b)
+    if (a.N <= 15 && a.B <= qscan_max_b)
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+    else if (a.N <= 31 && a.B <= qscan_max_b)
         hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
     else if (a.N <= 31)
         hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, false>), grid, dim3(dartmpc::kWave), 0, stream, a);
