@@ -325,28 +325,28 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 mat4_scan_level<0x102>(T);
                 mat4_scan_level<0x104>(T);
                 mat4_scan_level<0x108>(T);
-                if constexpr (!one_row) {   // rows 0 and 2 of each half: compose with the suffix held by lane 16 (48),
+                // [U; Y] = T [I; X] of the row-local suffix
+                double W[8] = {fma(T[2], X11d, T[0]), fma(T[3], X22d, T[1]), fma(T[6], X11d, T[4]),
+                               fma(T[7], X22d, T[5]), fma(T[10], X11d, T[8]), fma(T[11], X22d, T[9]),
+                               fma(T[14], X11d, T[12]), fma(T[15], X22d, T[13])};
+                if constexpr (!one_row) {
+                    // rows 0 and 2 of each half: [U; Y]_k = T_k(row) [U; Y]_16, the 4 x 2 of lane 16 (48)
                     // fetched by ds_swizzle (bitmask mode, or_mask 16: no address, no LDS access)
-                    double F[16];
+                    double F[8];
 #pragma unroll
-                    for (int e = 0; e < 16; ++e) F[e] = half_bcast_c<16>(T[e]);
+                    for (int e = 0; e < 8; ++e) F[e] = half_bcast_c<16>(W[e]);
                     if ((lane & 16) == 0) {
-                        double Nn[16];
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
 #pragma unroll
-                            for (int jj = 0; jj < 4; ++jj)
-                                Nn[4 * i + jj] = fma(T[4 * i], F[jj], fma(T[4 * i + 1], F[4 + jj],
-                                                     fma(T[4 * i + 2], F[8 + jj], T[4 * i + 3] * F[12 + jj])));
-#pragma unroll
-                        for (int e = 0; e < 16; ++e) T[e] = Nn[e];
+                            for (int jj = 0; jj < 2; ++jj)
+                                W[2 * i + jj] = fma(T[4 * i], F[jj], fma(T[4 * i + 1], F[2 + jj],
+                                                    fma(T[4 * i + 2], F[4 + jj], T[4 * i + 3] * F[6 + jj])));
                     }
                 }
-                // [U; Y] = T [I; X], P = Y U^-1 (symmetrised)
-                const double U11 = fma(T[2], X11d, T[0]), U12 = fma(T[3], X22d, T[1]);
-                const double U21 = fma(T[6], X11d, T[4]), U22 = fma(T[7], X22d, T[5]);
-                const double Y11 = fma(T[10], X11d, T[8]), Y12 = fma(T[11], X22d, T[9]);
-                const double Y21 = fma(T[14], X11d, T[12]), Y22 = fma(T[15], X22d, T[13]);
+                // P = Y U^-1 (symmetrised)
+                const double U11 = W[0], U12 = W[1], U21 = W[2], U22 = W[3];
+                const double Y11 = W[4], Y12 = W[5], Y21 = W[6], Y22 = W[7];
                 const double idet = frcp(fma(U11, U22, -U12 * U21));
                 const double q11 = fma(Y11, U22, -Y12 * U21) * idet, q12 = fma(Y12, U11, -Y11 * U12) * idet;
                 const double q21 = fma(Y21, U22, -Y22 * U21) * idet, q22 = fma(Y22, U11, -Y21 * U12) * idet;
