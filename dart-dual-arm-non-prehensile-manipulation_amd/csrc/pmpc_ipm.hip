@@ -126,7 +126,9 @@ __device__ __forceinline__ void mat4_scan_level(double* T) {
 //   per SIMD (throughput regime)
 //   ONEROW: N <= 15, every axis fits one 16-lane DPP row and the scans need no cross-row step (the
 //   DART driver's default horizon is 15, main_parallel_enhanced.py:171-196)
-template <int NAX, bool QSCAN, bool ONEROW = false>
+//   SHORT2: 16 <= N <= 23, the suffix of node 16 spans at most 8 lanes, so the quadratic scan stops
+//   after 3 in-row levels and finishes rows 0 / 2 with two 4 x 2 compositions (no 4th 4 x 4 level)
+template <int NAX, bool QSCAN, bool ONEROW = false, bool SHORT2 = false>
 __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
     STAMP_DECL
     // small batches: the launcher deals 8 blocks per instance and only every 8th works, so all
@@ -139,6 +141,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
     const int N = a.N;
     const bool xon = k <= N, uon = k < N;
     constexpr bool one_row = ONEROW;
+    constexpr bool short2 = SHORT2 && !ONEROW;
     const double h = a.Ts;
 
     const double* st = a.x0 + 6 * b;
@@ -324,12 +327,37 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 mat4_scan_level<0x101>(T);
                 mat4_scan_level<0x102>(T);
                 mat4_scan_level<0x104>(T);
-                mat4_scan_level<0x108>(T);
+                if constexpr (!short2) mat4_scan_level<0x108>(T);
                 // [U; Y] = T [I; X] of the row-local suffix
                 double W[8] = {fma(T[2], X11d, T[0]), fma(T[3], X22d, T[1]), fma(T[6], X11d, T[4]),
                                fma(T[7], X22d, T[5]), fma(T[10], X11d, T[8]), fma(T[11], X22d, T[9]),
                                fma(T[14], X11d, T[12]), fma(T[15], X22d, T[13])};
-                if constexpr (!one_row) {
+                if constexpr (short2) {
+                    // after 3 levels lane k holds S_k ... S_{min(k+7, row end)}: lanes 16-23 (48-55)
+                    // already reach the terminal (N <= 23), lanes 8-15 the row end.  Lanes 8-15 compose
+                    // with the 4 x 2 of lane 16 (ds_swizzle), then lanes 0-7 with that of lane k + 8 (DPP)
+                    double F[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) F[e] = half_bcast_c<16>(W[e]);
+                    if ((lane & 16) == 0) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+#pragma unroll
+                            for (int jj = 0; jj < 2; ++jj)
+                                W[2 * i + jj] = fma(T[4 * i], F[jj], fma(T[4 * i + 1], F[2 + jj],
+                                                    fma(T[4 * i + 2], F[4 + jj], T[4 * i + 3] * F[6 + jj])));
+                    }
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) F[e] = dpp_fill<0x108, 0xf, 0>(W[e]);
+                    if ((lane & 24) == 0) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+#pragma unroll
+                            for (int jj = 0; jj < 2; ++jj)
+                                W[2 * i + jj] = fma(T[4 * i], F[jj], fma(T[4 * i + 1], F[2 + jj],
+                                                    fma(T[4 * i + 2], F[4 + jj], T[4 * i + 3] * F[6 + jj])));
+                    }
+                } else if constexpr (!one_row) {
                     // rows 0 and 2 of each half: [U; Y]_k = T_k(row) [U; Y]_16, the 4 x 2 of lane 16 (48)
                     // fetched by ds_swizzle (bitmask mode, or_mask 16: no address, no LDS access)
                     double F[8];
@@ -675,6 +703,8 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
     }();
     if (a.N <= 15 && a.B <= qscan_max_b)
         hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+    else if (a.N <= 23 && a.B <= qscan_max_b)
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
     else if (a.N <= 31 && a.B <= qscan_max_b)
         hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
     else if (a.N <= 31)

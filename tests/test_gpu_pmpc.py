@@ -168,7 +168,7 @@ def test_symmetry_and_rest_properties(dm):
     s.close()
 
 
-@pytest.mark.parametrize("N", [1, 2, 15, 31, 40, 63])
+@pytest.mark.parametrize("N", [1, 2, 15, 16, 23, 24, 31, 40, 63])
 def test_horizons_match_oracle(dm, N):
     import oracle_lib
     from dart_mpc.workload import pmpc_batch
