@@ -44,7 +44,9 @@ stats = glob.glob(os.path.join(SRC, "trace", "**", "*kernel_stats.csv"), recursi
 if stats:
     shutil.copy(stats[0], os.path.join(DST, "kernel_stats.csv"))
 summary = {"note": "FETCH_SIZE / WRITE_SIZE from separate rocprofv3 --pmc passes (tools/profile_round.sh), KB; "
-                   "traffic_bytes_per_launch = (2*FETCH + WRITE)*1024 (gfx950 FETCH correction, MI355X_MICROARCH.md)",
+                   "traffic_bytes_per_launch = (2*FETCH + WRITE)*1024 (gfx950 FETCH correction, MI355X_MICROARCH.md); "
+                   "VGPR_Count / Accum_VGPR_Count / LDS_Block_Size are copied as the kernel trace reports them (they "
+                   "do not follow the compiler's arch-VGPR + AGPR split; DESIGN.md §4 quotes -Rpass-analysis counts)",
            "kernels": {}}
 per = defaultdict(lambda: defaultdict(list))
 meta = {}
