@@ -102,17 +102,31 @@ __device__ __forceinline__ void affine_scan_level(double& f11, double& f12, doub
 
 // One level of a suffix scan of 4x4 matrices (T <- T * F, F fetched from lane k + d by DPP
 // row_shl:d, identity where out of range)
-template <int CTRL>
+template <int CTRL, bool FIRST = false>
 __device__ __forceinline__ void mat4_scan_level(double* T) {
+    // FIRST: T is a lane's own stage map, whose column 0 is (1, 0, X11, 0), and so is that of the
+    // neighbour's map or of the identity fill: those entries are not fetched and their products
+    // with 0 / 1 are dropped (the compiler keeps 0 * x for NaN semantics)
+    constexpr bool fz[16] = {FIRST, false, false, false, FIRST, false, false, false,
+                             false, false, false, false, FIRST, false, false, false};
     double F[16];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) F[e] = (e % 5 == 0) ? dpp_fill<CTRL, 0xf, 1>(T[e]) : dpp_fill<CTRL, 0xf, 0>(T[e]);
+    for (int e = 0; e < 16; ++e)
+        F[e] = fz[e] ? (e == 0 ? 1.0 : 0.0)
+                     : (e % 5 == 0) ? dpp_fill<CTRL, 0xf, 1>(T[e]) : dpp_fill<CTRL, 0xf, 0>(T[e]);
     double N[16];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            N[4 * i + j] = fma(T[4 * i], F[j], fma(T[4 * i + 1], F[4 + j], fma(T[4 * i + 2], F[8 + j], T[4 * i + 3] * F[12 + j])));
+        for (int j = 0; j < 4; ++j) {
+            double acc = T[4 * i + 3] * F[12 + j];
+            if (fz[12 + j]) acc = 0.0;
+            acc = fma(T[4 * i + 2], F[8 + j], acc);
+            if (!fz[4 + j]) acc = fma(T[4 * i + 1], F[4 + j], acc);
+            if (FIRST && i == 0) acc += F[j];                                  // T[0] = 1
+            else if (!(FIRST && (i == 1 || i == 3))) acc = fma(T[4 * i], F[j], acc);   // T[4] = T[12] = 0
+            N[4 * i + j] = acc;
+        }
 #pragma unroll
     for (int e = 0; e < 16; ++e) T[e] = N[e];
 }
@@ -324,7 +338,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                                 0.0, ai22k, g21, g22,
                                 X11k, X11k * ai12k, fma(X11k, g11, 1.0), X11k * g12,
                                 0.0, X22k * ai22k, fma(X22k, g21, a12k), fma(X22k, g22, a22i)};
-                mat4_scan_level<0x101>(T);
+                mat4_scan_level<0x101, true>(T);
                 mat4_scan_level<0x102>(T);
                 mat4_scan_level<0x104>(T);
                 if constexpr (!short2) mat4_scan_level<0x108>(T);
@@ -445,6 +459,20 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 affine_scan_level<0x101, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:1
                 affine_scan_level<0x102, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:2
                 affine_scan_level<0x104, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:4
+                if constexpr (short2) {
+                    // N <= 23: lanes 16-23 (48-55) are final after 3 levels; lanes 8-15 compose with the
+                    // constant of lane 16, then lanes 0-7 with the (final) constant of lane k + 8
+                    const double r1 = half_bcast_c<16>(c1), r2 = half_bcast_c<16>(c2);
+                    if ((lane & 24) == 8) {
+                        c1 = fma(m11, r1, fma(m12, r2, c1));
+                        c2 = fma(m21, r1, fma(m22, r2, c2));
+                    }
+                    const double s1 = dpp_fill<0x108, 0xf, 0>(c1), s2 = dpp_fill<0x108, 0xf, 0>(c2);
+                    if ((lane & 24) == 0) {
+                        c1 = fma(m11, s1, fma(m12, s2, c1));
+                        c2 = fma(m21, s1, fma(m22, s2, c2));
+                    }
+                } else {
                 affine_scan_level<0x108, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:8
                 if constexpr (!one_row) {   // rows 0 and 2 compose with the suffix held by the first lane of rows 1 and 3
                     const bool lo_row = (lane & 16) == 0;
@@ -453,6 +481,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                         c1 = fma(m11, r1, fma(m12, r2, c1));
                         c2 = fma(m21, r1, fma(m22, r2, c2));
                     }
+                }
                 }
                 p1[0] = c1; p2[0] = c2;
                 // feed-forward k_k = -(e^T h + rt) / Q with h = p_{k+1} - P_{k+1} g_{k+1}
