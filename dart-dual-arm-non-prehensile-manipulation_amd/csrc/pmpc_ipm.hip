@@ -100,6 +100,16 @@ __device__ __forceinline__ void affine_scan_level(double& f11, double& f12, doub
     f11 = n11; f12 = n12; f21 = n21; f22 = n22;
 }
 
+// A composition level whose source lanes already hold pure constants (their map is 0 because
+// their window reaches node 0 of an inclusive prefix scan): only the constant is fetched, c <- F q + c
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void affine_scan_const(double f11, double f12, double f21, double f22, double& c1,
+                                                  double& c2) {
+    const double q1 = dpp_fill<CTRL, ROWMASK, 0>(c1), q2 = dpp_fill<CTRL, ROWMASK, 0>(c2);
+    c1 = fma(f11, q1, fma(f12, q2, c1));
+    c2 = fma(f21, q1, fma(f22, q2, c2));
+}
+
 // One level of a suffix scan of 4x4 matrices (T <- T * F, F fetched from lane k + d by DPP
 // row_shl:d, identity where out of range)
 template <int CTRL, bool FIRST = false>
@@ -511,8 +521,12 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
             affine_scan_level<0x111, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:1
             affine_scan_level<0x112, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:2
             affine_scan_level<0x114, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:4
-            affine_scan_level<0x118, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:8
-            if constexpr (!one_row) affine_scan_level<0x142, 0xa>(f11, f12, f21, f22, c1, c2);   // row_bcast:15 -> rows 1, 3
+            // after 3 levels the windows of lanes 0-7 reach node 0 (map 0, a constant): with N <= 23
+            // the row_shr:8 level only moves constants (row 1's lanes 16-23 read nothing); lane 15 is
+            // a constant once row 0 is done, so the row_bcast:15 level into rows 1 / 3 is one too
+            if constexpr (one_row || short2) affine_scan_const<0x118, 0xf>(f11, f12, f21, f22, c1, c2);
+            else affine_scan_level<0x118, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:8
+            if constexpr (!one_row) affine_scan_const<0x142, 0xa>(f11, f12, f21, f22, c1, c2);   // row_bcast:15 -> rows 1, 3
             dp[0] = c1; dv[0] = c2;
         } else
         for (int step = 0; step < N; ++step) {
