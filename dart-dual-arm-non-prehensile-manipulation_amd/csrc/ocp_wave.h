@@ -59,8 +59,48 @@ struct OcpLds {
     NodeArr<double[NTP], NMAXS> G;            // G_k; G[N] = terminal surrogate (Pt_N, Quu = I)
     NodeArr<double[2][NC], NMAXS> KK;         // [K | k]_k rows
     NodeArr<double[NXA][NF], NMAXS> F;        // closed loop: F[k][r] = [Phi_k(r, :) | f_k(r)]
+    NodeArr<double[NXA][NF], NMAXS / 2> F2;   // two-node maps of nodes 2q, 2q + 1 (compose_pairs)
     double dx0[NC];                           // forward sweep start dx~_0
 };
+
+// Two-node closed-loop maps F2[q] = [Phi_{2q+1} Phi_{2q} | Phi_{2q+1} f_{2q} + f_{2q+1}] of every
+// node pair of each of H independent chains (slot of node k of chain h: h * SLOTS + k; pair slot
+// h * SLOTS / 2 + q), one row per task, tasks spread over the wave.  The forward sweep then runs
+// N / 2 dependent steps instead of N.  Ends with a barrier.
+template <int H, int SLOTS, int NXA, int RPT, class FA, class F2A>
+__device__ __forceinline__ void compose_pairs(FA& F, F2A& F2, int N) {
+    // task = RPT rows of one pair: RPT trades rounds over the wave against work per lane
+    constexpr int NB = (NXA + RPT - 1) / RPT;
+    const int np2 = N >> 1, per = np2 * NB;
+    for (int t = threadIdx.x; t < H * per; t += 64) {
+        const int h = H == 1 ? 0 : t / per, rem = t - h * per, q = rem / NB, r0 = (rem - q * NB) * RPT;
+        const int s0 = h * SLOTS + 2 * q;
+        double b[NXA][NXA + 1];
+#pragma unroll
+        for (int m = 0; m < NXA; ++m)
+#pragma unroll
+            for (int j = 0; j <= NXA; ++j) b[m][j] = F[s0][m][j];
+#pragma unroll
+        for (int rr = 0; rr < RPT; ++rr) {
+            const int r = r0 + rr < NXA ? r0 + rr : NXA - 1;
+            double a[NXA + 1];
+#pragma unroll
+            for (int j = 0; j <= NXA; ++j) a[j] = F[s0 + 1][r][j];
+            double o[NXA + 1];
+#pragma unroll
+            for (int j = 0; j <= NXA; ++j) o[j] = j < NXA ? a[0] * b[0][j] : fma(a[0], b[0][j], a[NXA]);
+#pragma unroll
+            for (int m = 1; m < NXA; ++m)
+#pragma unroll
+                for (int j = 0; j <= NXA; ++j) o[j] = fma(a[m], b[m][j], o[j]);
+            if (r0 + rr < NXA) {
+#pragma unroll
+                for (int j = 0; j <= NXA; ++j) F2[h * (SLOTS / 2) + q][r][j] = o[j];
+            }
+        }
+    }
+    __syncthreads();
+}
 
 // z index of value-function index p (the homogeneous coordinate sits last in both)
 template <int NXA>
@@ -207,6 +247,7 @@ __device__ void closed_loop(L* S, int N) {
         }
     }
     __syncthreads();
+    compose_pairs<1, L::NMAXS, NXA, 1>(S->F, S->F2, N);   // 6 N / 2 tasks: one round
 }
 
 // Multiplier of the dynamics row into node k: lam~_k = -Pt_k [dx~; 1] (first NXA rows), with
@@ -226,10 +267,12 @@ __device__ __forceinline__ void node_multiplier(const L* S, int k, const double*
     }
 }
 
-// Forward sweep: lane r < NXA owns row r of the chain dx~_{k+1} = Phi_k dx~_k + f_k; the new
-// state is broadcast to every lane by readlane (scalar registers), and row r's closed-loop data
-// for node k+1 is prefetched while node k is processed.  Every lane returns in dxo the state step
-// of node `node` (lane-per-node use; node > N keeps dx~_0).  S->dx0 must hold dx~_0.
+// Forward sweep over node pairs: lane r < NXA owns row r of the two-node chain
+// dx~_{2q+2} = F2[q] [dx~_{2q}; 1]; the states are broadcast by readlane (scalar registers), and
+// the rows of the next pair are prefetched while this one is processed.  An odd N ends with one
+// single-node step; the odd nodes in between follow afterwards, lane per node, from their even
+// predecessor (off the chain).  Lane-per-node use: every lane returns in dxo the state step of
+// node `node` = its lane (node > N keeps dx~_0).  S->dx0 must hold dx~_0; compose_pairs must have run.
 template <class L>
 __device__ void forward_sweep(L* S, int N, int node, double* dxo) {
     constexpr int NXA = L::NXA;
@@ -238,22 +281,49 @@ __device__ void forward_sweep(L* S, int N, int node, double* dxo) {
     double d[NXA];
 #pragma unroll
     for (int i = 0; i < NXA; ++i) { d[i] = S->dx0[i]; dxo[i] = d[i]; }
+    const int np2 = N >> 1;
     double Fc[NXA + 1];
 #pragma unroll
-    for (int j = 0; j <= NXA; ++j) Fc[j] = S->F[0][r][j];
-    for (int k = 0; k < N; ++k) {
+    for (int j = 0; j <= NXA; ++j) Fc[j] = S->F2[0][r][j];
+    for (int q = 0; q < np2; ++q) {
         double Fn[NXA + 1];
-        const int kn = k + 1 < N ? k + 1 : k;
+        const int qn = q + 1 < np2 ? q + 1 : q;
 #pragma unroll
-        for (int j = 0; j <= NXA; ++j) Fn[j] = S->F[kn][r][j];
-        double s = Fc[NXA];
+        for (int j = 0; j <= NXA; ++j) Fn[j] = S->F2[qn][r][j];
+        double s0 = Fc[NXA], s1 = 0.0;       // two accumulators: half the dependent FMA depth
 #pragma unroll
-        for (int j = 0; j < NXA; ++j) s = fma(Fc[j], d[j], s);
-        const bool mine = node == k + 1;
+        for (int j = 0; j < NXA; j += 2) {
+            s0 = fma(Fc[j], d[j], s0);
+            if (j + 1 < NXA) s1 = fma(Fc[j + 1], d[j + 1], s1);
+        }
+        const double s = s0 + s1;
+        const bool m = node == 2 * q + 2;
 #pragma unroll
-        for (int i = 0; i < NXA; ++i) { d[i] = readlane(s, i); dxo[i] = mine ? d[i] : dxo[i]; }
+        for (int i = 0; i < NXA; ++i) { d[i] = readlane(s, i); dxo[i] = m ? d[i] : dxo[i]; }
 #pragma unroll
         for (int j = 0; j <= NXA; ++j) Fc[j] = Fn[j];
+    }
+    if (N & 1) {
+        const double* row = S->F[N - 1][r];
+        double s = row[NXA];
+#pragma unroll
+        for (int j = 0; j < NXA; ++j) s = fma(row[j], d[j], s);
+        const bool m = node == N;
+#pragma unroll
+        for (int i = 0; i < NXA; ++i) { d[i] = readlane(s, i); dxo[i] = m ? d[i] : dxo[i]; }
+    }
+    double pv[NXA];
+#pragma unroll
+    for (int i = 0; i < NXA; ++i) pv[i] = from_prev(dxo[i]);
+    if ((node & 1) && node < 2 * np2) {
+#pragma unroll
+        for (int rr = 0; rr < NXA; ++rr) {
+            const double* row = S->F[node - 1][rr];
+            double s = row[NXA];
+#pragma unroll
+            for (int j = 0; j < NXA; ++j) s = fma(row[j], pv[j], s);
+            dxo[rr] = s;
+        }
     }
 }
 
@@ -278,6 +348,7 @@ struct OcpLdsS {
     NodeArr<double[NTP], 2 * NMAXS> G;        // G_k; G[N] = terminal surrogate (Pt_N, Quu = 1)
     NodeArr<double[NC], 2 * NMAXS> KK;        // [K | k]_k
     NodeArr<double[NXA][NF], 2 * NMAXS> F;    // closed loop rows [Phi_k(r, :) | f_k(r)]
+    NodeArr<double[NXA][NF], NMAXS> F2;       // two-node maps, pair slot (NMAXS / 2) h + q (compose_pairs)
     double dx0[2][NC];                        // forward sweep start of each half
 };
 
@@ -383,6 +454,7 @@ __device__ void closed_loop_s(L* S, int N) {
         }
     }
     __syncthreads();
+    compose_pairs<2, L::NMAXS, NXA, 3>(S->F, S->F2, N);   // 2 x 2 x N / 2 tasks: one round
 }
 
 // lam~ = -Pt_k [dx~; 1] (first NXA rows) with Pt_k [dx~; 1] = Gzz [dx~; 1] + Gzu du, read from G of slot sl
@@ -399,37 +471,63 @@ __device__ __forceinline__ void node_multiplier_s(const L* S, int sl, const doub
     }
 }
 
-// Forward sweep of both halves: lane 32 h + r (r < NXA) owns row r of its half's chain
-// dx~_{k+1} = Phi_k dx~_k + f_k; the new states are broadcast by readlane (both halves, then a
-// ds_swizzle broadcast of lane 32 h + i within each half).  Every lane returns in dxo the step of
-// node `node` of its half.
+// Forward sweep of both halves over node pairs: lane 32 h + r (r < NXA) owns row r of its half's
+// two-node chain dx~_{2q+2} = F2 [dx~_{2q}; 1]; the states are broadcast by ds_swizzle within each
+// half.  An odd N ends with one single-node step; the odd nodes in between follow afterwards, lane
+// per node, from their even predecessor.  Every lane returns in dxo the step of node `node`
+// (= lane & 31) of its half.
 template <class L>
 __device__ void forward_sweep_s(L* S, int N, int node, double* dxo) {
     constexpr int NXA = L::NXA;
-    const int h = threadIdx.x >> 5, base = h * L::NMAXS;
-    const int r = (threadIdx.x & 31) < NXA ? (threadIdx.x & 31) : 0;
+    const int h = threadIdx.x >> 5, base = h * L::NMAXS, pbase = h * (L::NMAXS / 2);
+    const int li = threadIdx.x & 31;
+    const int r = li < NXA ? li : 0;
     double d[NXA];
 #pragma unroll
     for (int i = 0; i < NXA; ++i) { d[i] = S->dx0[h][i]; dxo[i] = d[i]; }
+    const int np2 = N >> 1;
     double Fc[NXA + 1];
 #pragma unroll
-    for (int j = 0; j <= NXA; ++j) Fc[j] = S->F[base][r][j];
-    for (int k = 0; k < N; ++k) {
+    for (int j = 0; j <= NXA; ++j) Fc[j] = S->F2[pbase][r][j];
+    for (int q = 0; q < np2; ++q) {
         double Fn[NXA + 1];
-        const int kn = k + 1 < N ? k + 1 : k;
+        const int qn = q + 1 < np2 ? q + 1 : q;
 #pragma unroll
-        for (int j = 0; j <= NXA; ++j) Fn[j] = S->F[base + kn][r][j];
-        double s = Fc[NXA];
+        for (int j = 0; j <= NXA; ++j) Fn[j] = S->F2[pbase + qn][r][j];
+        double s0 = Fc[NXA], s1 = 0.0;
 #pragma unroll
-        for (int j = 0; j < NXA; ++j) s = fma(Fc[j], d[j], s);
-        const bool mine = node == k + 1;
-#pragma unroll
-        for (int i = 0; i < NXA; ++i) {
-            d[i] = half_bcast(s, i);
-            dxo[i] = mine ? d[i] : dxo[i];
+        for (int j = 0; j < NXA; j += 2) {
+            s0 = fma(Fc[j], d[j], s0);
+            if (j + 1 < NXA) s1 = fma(Fc[j + 1], d[j + 1], s1);
         }
+        const double s = s0 + s1;
+        const bool m = node == 2 * q + 2;
+#pragma unroll
+        for (int i = 0; i < NXA; ++i) { d[i] = half_bcast(s, i); dxo[i] = m ? d[i] : dxo[i]; }
 #pragma unroll
         for (int j = 0; j <= NXA; ++j) Fc[j] = Fn[j];
+    }
+    if (N & 1) {
+        const double* row = S->F[base + N - 1][r];
+        double s = row[NXA];
+#pragma unroll
+        for (int j = 0; j < NXA; ++j) s = fma(row[j], d[j], s);
+        const bool m = node == N;
+#pragma unroll
+        for (int i = 0; i < NXA; ++i) { d[i] = half_bcast(s, i); dxo[i] = m ? d[i] : dxo[i]; }
+    }
+    double pv[NXA];
+#pragma unroll
+    for (int i = 0; i < NXA; ++i) pv[i] = from_prev(dxo[i]);
+    if ((node & 1) && node < 2 * np2) {
+#pragma unroll
+        for (int rr = 0; rr < NXA; ++rr) {
+            const double* row = S->F[base + node - 1][rr];
+            double s = row[NXA];
+#pragma unroll
+            for (int j = 0; j < NXA; ++j) s = fma(row[j], pv[j], s);
+            dxo[rr] = s;
+        }
     }
 }
 

@@ -36,7 +36,7 @@ __device__ __forceinline__ double half_bcast_c(double x) {
     return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ double half_bcast(double x, int i) {
-    switch (i) {       // i is a compile-time constant at every (unrolled) call site
+    switch (i) {       // i (< 16) is a compile-time constant at every (unrolled) call site
         case 0: return half_bcast_c<0>(x);
         case 1: return half_bcast_c<1>(x);
         case 2: return half_bcast_c<2>(x);
@@ -44,7 +44,15 @@ __device__ __forceinline__ double half_bcast(double x, int i) {
         case 4: return half_bcast_c<4>(x);
         case 5: return half_bcast_c<5>(x);
         case 6: return half_bcast_c<6>(x);
-        default: return half_bcast_c<7>(x);
+        case 7: return half_bcast_c<7>(x);
+        case 8: return half_bcast_c<8>(x);
+        case 9: return half_bcast_c<9>(x);
+        case 10: return half_bcast_c<10>(x);
+        case 11: return half_bcast_c<11>(x);
+        case 12: return half_bcast_c<12>(x);
+        case 13: return half_bcast_c<13>(x);
+        case 14: return half_bcast_c<14>(x);
+        default: return half_bcast_c<15>(x);
     }
 }
 constexpr int kWaveShl1 = 0x130;   // lane k <- lane k+1 (lane 63 <- 0)
