@@ -351,16 +351,19 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 mat4_scan_level<0x101, true>(T);
                 mat4_scan_level<0x102>(T);
                 mat4_scan_level<0x104>(T);
-                if constexpr (!short2) mat4_scan_level<0x108>(T);
+                if constexpr (!short2 && !one_row) mat4_scan_level<0x108>(T);
                 // [U; Y] = T [I; X] of the row-local suffix
                 double W[8] = {fma(T[2], X11d, T[0]), fma(T[3], X22d, T[1]), fma(T[6], X11d, T[4]),
                                fma(T[7], X22d, T[5]), fma(T[10], X11d, T[8]), fma(T[11], X22d, T[9]),
                                fma(T[14], X11d, T[12]), fma(T[15], X22d, T[13])};
-                if constexpr (short2) {
+                if constexpr (short2 || one_row) {
                     // after 3 levels lane k holds S_k ... S_{min(k+7, row end)}: lanes 16-23 (48-55)
-                    // already reach the terminal (N <= 23), lanes 8-15 the row end.  Lanes 8-15 compose
-                    // with the 4 x 2 of lane 16 (ds_swizzle), then lanes 0-7 with that of lane k + 8 (DPP)
+                    // already reach the terminal (N <= 23), lanes 8-15 the row end (and the terminal
+                    // when N <= 15).  Lanes 8-15 compose with the 4 x 2 of lane 16 (ds_swizzle; not
+                    // for N <= 15), then lanes 0-7 with that of lane k + 8 (DPP).  Lanes past the
+                    // terminal hold [I; X], so a suffix that is already complete stays unchanged.
                     double F[8];
+                    if constexpr (short2) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e) F[e] = half_bcast_c<16>(W[e]);
                     if ((lane & 16) == 0) {
@@ -370,6 +373,7 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                             for (int jj = 0; jj < 2; ++jj)
                                 W[2 * i + jj] = fma(T[4 * i], F[jj], fma(T[4 * i + 1], F[2 + jj],
                                                     fma(T[4 * i + 2], F[4 + jj], T[4 * i + 3] * F[6 + jj])));
+                    }
                     }
 #pragma unroll
                     for (int e = 0; e < 8; ++e) F[e] = dpp_fill<0x108, 0xf, 0>(W[e]);
@@ -469,13 +473,16 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
                 affine_scan_level<0x101, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:1
                 affine_scan_level<0x102, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:2
                 affine_scan_level<0x104, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:4
-                if constexpr (short2) {
+                if constexpr (short2 || one_row) {
                     // N <= 23: lanes 16-23 (48-55) are final after 3 levels; lanes 8-15 compose with the
-                    // constant of lane 16, then lanes 0-7 with the (final) constant of lane k + 8
-                    const double r1 = half_bcast_c<16>(c1), r2 = half_bcast_c<16>(c2);
-                    if ((lane & 24) == 8) {
-                        c1 = fma(m11, r1, fma(m12, r2, c1));
-                        c2 = fma(m21, r1, fma(m22, r2, c2));
+                    // constant of lane 16 (N <= 15: already final), then lanes 0-7 with the (final)
+                    // constant of lane k + 8
+                    if constexpr (short2) {
+                        const double r1 = half_bcast_c<16>(c1), r2 = half_bcast_c<16>(c2);
+                        if ((lane & 24) == 8) {
+                            c1 = fma(m11, r1, fma(m12, r2, c1));
+                            c2 = fma(m21, r1, fma(m22, r2, c2));
+                        }
                     }
                     const double s1 = dpp_fill<0x108, 0xf, 0>(c1), s2 = dpp_fill<0x108, 0xf, 0>(c2);
                     if ((lane & 24) == 0) {
