@@ -54,6 +54,9 @@ def parse():
                     help="launches of the supplementary PMPC line at the driver's horizon N=15 (0 = skip)")
     ap.add_argument("--c4-steps", type=int, default=50,
                     help="steps of the supplementary C4 line (1152 instances sharded over the ranks + gather; 0 = skip)")
+    ap.add_argument("--dist-backend", default=None,
+                    help="torch.distributed backend for N > 1 (default nccl = RCCL over xGMI); 'gloo' with every rank "
+                         "on the card(s) present rehearses the multi-rank path on a one-GPU box")
     ap.add_argument("--saturation-batch", type=int, default=18 * 1024,
                     help="supplementary single-launch batch for the saturated rate (0 = skip)")
     return ap.parse_args()
@@ -171,7 +174,15 @@ def bench_pmpc_driver_horizon(args, torch, dev, stream, dart_mpc, N=15):
             "max_abs_u0_err_vs_exact_optimum": float(np.max(np.abs(U0[5].cpu().numpy() - ref["u0"])))}
 
 
-def bench_c4(args, torch, dev, stream, dart_mpc, world, rank):
+def _max_over_ranks(vals, dev, host_coll):
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(vals, dtype=torch.float64, device="cpu" if host_coll else dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.cpu()]
+
+
+def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False):
     """C4 (BASELINE.json configs[3]): PMPC 18 configs x 64 seeds = 1152 instances, N=20, sharded over the
     ranks in contiguous blocks (dart_mpc.parallel.shard_bounds).  One step = every rank solves its block,
     packs [u0, f, status] and joins one all_gather_into_tensor (RCCL over xGMI) of the padded blocks.
@@ -203,7 +214,11 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank):
             block[:n, 0:2].copy_(U0)
             block[:n, 2].copy_(FV)
             block[:n, 3].copy_(ST)
-            if world > 1:
+            if world > 1 and host_coll:
+                fh = full.cpu()     # gloo rehearsal: the gather runs on host copies
+                dist.all_gather_into_tensor(fh, block.cpu())
+                full.copy_(fh)
+            elif world > 1:
                 dist.all_gather_into_tensor(full, block)
             else:
                 full.copy_(block)
@@ -222,10 +237,12 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank):
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=dt64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t[0])
+        dt = _max_over_ranks([dt], dev, host_coll)[0]
     res = full.cpu().numpy()[:Bg]
+    # every rank finds its own block, bit for bit, at its offset of the gathered result
+    mine = bool(np.array_equal(res[lo:hi], block[:n].cpu().numpy()))
+    if world > 1:
+        mine = _max_over_ranks([0.0 if mine else 1.0], dev, host_coll)[0] == 0.0
     solver.close()
     if rank != 0:
         return None
@@ -236,7 +253,7 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank):
                         "blocks over the ranks + all_gather_into_tensor of [u0, f, status] (RCCL)",
             "global_batch": Bg, "per_rank": per, "n_gpus": world, "scaling": "strong", "steps": K,
             "solves_per_s": Bg * K / dt, "ms_per_step": dt / K * 1e3, "gather_in_timed_region": world > 1,
-            "status_ok_frac": float(np.mean(res[:, 3] == 0)),
+            "status_ok_frac": float(np.mean(res[:, 3] == 0)), "rank_blocks_consistent": mine,
             "max_abs_u0_err_vs_exact_optimum_first36": float(np.max(np.abs(res[:36, 0:2] - ref["u0"])))}
 
 
@@ -402,8 +419,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = args.dist_backend or ("nccl" if torch.cuda.is_available() else "gloo")
+    host_coll = backend == "gloo"
     if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend)
+    # one rank per GPU; a gloo rehearsal with more ranks than cards shares them round robin
+    ndev = max(1, torch.cuda.device_count())
+    local = local % ndev if host_coll else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -455,9 +477,7 @@ def main():
     elapsed = t1 - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev.values()]))
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        elapsed, kern_ms = _max_over_ranks([elapsed, kern_ms], dev, host_coll)
 
     st = ST[W:].cpu().numpy()
     its = IT[W:].cpu().numpy()
@@ -538,12 +558,13 @@ def main():
         h1dt = (time.perf_counter() - h1) / args.host_calls
         host_path = {"batch": B, "ms_per_call": hdt * 1e3, "solves_per_s": B / hdt,
                      "single_instance_ms_per_call": h1dt * 1e3,
-                     "note": "dart_mpc_solve_batch through the Python Solver: inputs packed into pinned memory, one "
-                             "DMA copy, outputs written by the kernel into mapped pinned memory, stream sync"}
+                     "note": "dart_mpc_solve_batch through the Python Solver: inputs packed into mapped, coherent "
+                             "pinned host memory that the kernel reads zero-copy at its start (no DMA copy on the "
+                             "call path), outputs written by the kernel into mapped pinned memory, stream sync"}
         hs.close()
 
     # supplementary C4 (BASELINE.json configs[3]): 1152 instances sharded over the ranks + result gather
-    c4 = bench_c4(args, torch, dev, stream, dart_mpc, world, rank) if args.c4_steps > 0 else None
+    c4 = bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll) if args.c4_steps > 0 else None
 
     # supplementary PMPC line at the DART driver's horizon (N = 15)
     n15 = None
@@ -590,7 +611,8 @@ def main():
             "data": "synthetic (seeded SURVEY §8d workload, fresh instances every step)",
             "config": {"workload": "C2: PMPC batch=18 object configs (3 shapes x 2 masses x 3 frictions), "
                                    "N=20, Ts=0.002, cold start, IPOPT tol 1e-8; one rank per GPU",
-                       "batch_per_gpu": B, "N": N, "parallelism": f"instance-sharded x{world}"},
+                       "batch_per_gpu": B, "N": N, "parallelism": f"instance-sharded x{world}",
+                       **({"dist_backend": backend} if world > 1 else {})},
             "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "kernel": "pmpc_ipm_kernel", "kernel_ms": kern_ms,

@@ -159,6 +159,11 @@ struct dart_mpc_handle {
     hipStream_t stream = nullptr;
     HostStage st;                  // staging of the host-pointer entries
     std::string err;
+    // Serialises the entries on this handle: the host-pointer entries share the pinned staging
+    // buffers and the handle's stream, and every entry may write err.  Concurrent callers (the
+    // reference runs controllers on background threads, RMPC/dev_dual/controller/convimp.py:435)
+    // are safe but take turns; one handle per thread runs them side by side.
+    std::recursive_mutex mu;     // recursive: the host entries call their _dev twins
 };
 
 namespace {
@@ -267,6 +272,7 @@ int dart_mpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* x0, const 
                              const double* w_warm, double* u0, double* f, double* w_out, int32_t* status,
                              int32_t* iters, void* stream) {
     if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
     if (h->cfg.variant != DART_MPC_PMPC) return fail(h, DART_MPC_EINVAL, "handle is not a PMPC handle");
     if (B < 0 || (B > 0 && (!x0 || !ref || !prm || !u0 || !f || !status || !iters)))
         return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
@@ -280,6 +286,7 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
                          const double* w_warm, double* u0, double* f, double* w_out, int32_t* status,
                          int32_t* iters, void* stream) {
     if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
     if (h->cfg.variant != DART_MPC_PMPC) return fail(h, DART_MPC_EINVAL, "handle is not a PMPC handle");
     if (B < 0 || (B > 0 && (!x0 || !ref || !prm || !u0 || !f || !status || !iters)))
         return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
@@ -315,6 +322,7 @@ int dart_rmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* x0, const
                               const double* Rref, const double* prm, const double* w_warm, double* u0, double* f,
                               double* w_out, int32_t* status, int32_t* iters, void* stream) {
     if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
     if (h->cfg.variant != DART_MPC_RMPC) return fail(h, DART_MPC_EINVAL, "handle is not an RMPC handle");
     if (B < 0 || (B > 0 && (!x0 || !u_prev || !theta || !Rref || !prm || !u0 || !f || !status || !iters)))
         return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
@@ -335,6 +343,7 @@ int dart_rmpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const dou
                           const double* Rref, const double* prm, const double* w_warm, double* u0, double* f,
                           double* w_out, int32_t* status, int32_t* iters, void* stream) {
     if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
     if (h->cfg.variant != DART_MPC_RMPC) return fail(h, DART_MPC_EINVAL, "handle is not an RMPC handle");
     if (B < 0 || (B > 0 && (!x0 || !u_prev || !theta || !Rref || !prm || !u0 || !f || !status || !iters)))
         return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
@@ -377,6 +386,7 @@ int dart_lmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* state, co
                               const double* pvec, const double* target, const double* prm, const double* w_warm,
                               double* u0, double* f, double* w_out, int32_t* status, int32_t* iters, void* stream) {
     if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
     if (h->cfg.variant != DART_MPC_LMPC) return fail(h, DART_MPC_EINVAL, "handle is not an LMPC handle");
     if (B < 0 || (B > 0 && (!state || !u_prev || !pvec || !target || !prm || !u0 || !f || !status || !iters)))
         return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
@@ -395,6 +405,7 @@ int dart_lmpc_solve_batch(dart_mpc_handle* h, int B, const double* state, const 
                           const double* target, const double* prm, const double* w_warm, double* u0, double* f,
                           double* w_out, int32_t* status, int32_t* iters, void* stream) {
     if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
     if (h->cfg.variant != DART_MPC_LMPC) return fail(h, DART_MPC_EINVAL, "handle is not an LMPC handle");
     if (B < 0 || (B > 0 && (!state || !u_prev || !pvec || !target || !prm || !u0 || !f || !status || !iters)))
         return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
@@ -534,6 +545,7 @@ int dart_rls_update_batch(int B, double* theta, double* P, const double* phi, co
 
 int dart_mpc_sync(dart_mpc_handle* h) {
     if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
     HIPCHK(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
     return DART_MPC_OK;
 }

@@ -247,7 +247,7 @@ __device__ void closed_loop(L* S, int N) {
         }
     }
     __syncthreads();
-    compose_pairs<1, L::NMAXS, NXA, 1>(S->F, S->F2, N);   // 6 N / 2 tasks: one round
+    compose_pairs<1, L::NMAXS, NXA, 1>(S->F, S->F2, N);   // NXA floor(N / 2) tasks: one round over the wave for N <= 21 (RMPC), two beyond
 }
 
 // Multiplier of the dynamics row into node k: lam~_k = -Pt_k [dx~; 1] (first NXA rows), with

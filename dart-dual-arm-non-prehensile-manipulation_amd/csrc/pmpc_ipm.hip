@@ -172,6 +172,11 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
     const double* rf = a.ref + 6 * b;
     const double* pr = a.prm + 6 * b;
     const double mu_f = pr[0], Qp = pr[1], Qv = pr[2], R = pr[3], ulo = pr[4], uhi = pr[5];
+    // every input is read here, at the start (the host entry hands them over in mapped host memory,
+    // dart_mpc_abi.hip); pz / vz are only needed by the final z rollout, so they wait in LDS rather
+    // than in registers through the iteration loop
+    __shared__ double z0[2];
+    if (a.w_out && lane < 2) z0[lane] = st[4 + lane];
 
     // RK4 map of the linear axis model applied to the basis: exact Phi = [[1,a12],[0,a22]], Gamma = [b1,b2]
     double a12, a22, b1, b2;
@@ -696,7 +701,8 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
     if (a.w_out) {
         // z sub-state follows the final controls through the reference RK4 (mpc_3d.py:93-97, :99-104)
         const double w = uon ? -a.g * (tx * tx + ty * ty) : 0.0;
-        double pz = st[4], vz = st[5];
+        __syncthreads();
+        double pz = z0[0], vz = z0[1];
         for (int step = 0; step < N; ++step) {
             double pzn, vzn;
             z_rk4(h, w, pz, vz, pzn, vzn);

@@ -11,20 +11,27 @@ read ``model.opt.gravity[2]`` (mpc_3d.py:23) and the object state
 """
 from __future__ import annotations
 
+import threading
+
 import numpy as np
 
 from ._lib import Solver
 
+# Controllers with the same configuration share one handle.  The library serialises calls on a
+# handle (its mutex, include/dart_mpc.h), so controllers on different threads stay correct; the
+# cache itself is guarded here.
 _SOLVERS = {}
+_SOLVERS_LOCK = threading.Lock()
 
 
 def _solver(N, Ts, tol, max_iter, device, gravity, B_max):
     key = (int(N), float(Ts), float(tol), int(max_iter), int(device), float(gravity))
-    s = _SOLVERS.get(key)
-    if s is None or s.cfg.B_max < B_max:
-        s = Solver(N=N, Ts=Ts, tol=tol, max_iter=max_iter, B_max=max(B_max, 1024), device=device, gravity=gravity)
-        _SOLVERS[key] = s
-    return s
+    with _SOLVERS_LOCK:
+        s = _SOLVERS.get(key)
+        if s is None or s.cfg.B_max < B_max:
+            s = Solver(N=N, Ts=Ts, tol=tol, max_iter=max_iter, B_max=max(B_max, 1024), device=device, gravity=gravity)
+            _SOLVERS[key] = s
+        return s
 
 
 class PMPC:

@@ -15,20 +15,27 @@ arithmetic, kept on the host as in the reference.
 """
 from __future__ import annotations
 
+import threading
+
 import numpy as np
 
 from ._lib import RmpcSolver, rls_update_batch
 
+# Controllers with the same configuration share one handle.  The library serialises calls on a
+# handle (its mutex, include/dart_mpc.h), so controllers on different threads stay correct; the
+# cache itself is guarded here.
 _SOLVERS = {}
+_SOLVERS_LOCK = threading.Lock()
 
 
 def _solver(N, Ts, tol, max_iter, device, gravity, B):
     key = (int(N), float(Ts), float(tol), int(max_iter), int(device), float(gravity))
-    s = _SOLVERS.get(key)
-    if s is None or s.cfg.B_max < B:
-        s = RmpcSolver(N=N, Ts=Ts, tol=tol, max_iter=max_iter, B_max=max(B, 256), device=device, gravity=gravity)
-        _SOLVERS[key] = s
-    return s
+    with _SOLVERS_LOCK:
+        s = _SOLVERS.get(key)
+        if s is None or s.cfg.B_max < B:
+            s = RmpcSolver(N=N, Ts=Ts, tol=tol, max_iter=max_iter, B_max=max(B, 256), device=device, gravity=gravity)
+            _SOLVERS[key] = s
+        return s
 
 
 class RLS:

@@ -44,7 +44,12 @@
  *
  * Errors: every int-returning call returns 0 on success or a negative
  * DART_MPC_E* code; dart_mpc_last_error() describes the last failure.
- * Threading: a handle is not thread-safe; use one handle per host thread.
+ * Threading: every entry taking a handle locks the handle's mutex, so several
+ * host threads may share one handle (the reference calls its controllers from
+ * background threads, RMPC/dev_dual/controller/convimp.py:435): their calls
+ * take turns on the handle's staging buffers and stream.  For calls that run
+ * side by side, give each thread its own handle.  The stateless entries (RLS,
+ * arm QP, policy step) lock a per-device stage the same way.
  */
 #ifndef DART_MPC_H
 #define DART_MPC_H

@@ -132,13 +132,16 @@ def test_wide_tilt_box_library_trig_path(dm):
     np.testing.assert_allclose(out["f"], ref["f"], rtol=1e-7, atol=1e-9)
 
 
-def test_scan_and_sequential_riccati_agree(dm):
+@pytest.mark.parametrize("N", [15, 16, 20, 23, 24, 31])
+def test_scan_and_sequential_riccati_agree(dm, N):
     """The launcher runs the quadratic Riccati part as a DPP scan for B <= 1024 and as the sequential
     sweep beyond (throughput regime).  The same 1152 instances solved as one launch of 2304 (sequential;
-    every instance twice) and as 64 launches of 18 (scan) take the same iterations and agree to 1e-9."""
+    every instance twice) and as 64 launches of 18 (scan) take the same iterations and agree to 1e-9.
+    N covers every scan instantiation: one-row (N <= 15, the DART driver's horizon), SHORT2
+    (16 <= N <= 23, both ends) and the full scan (N = 24, 31)."""
     from dart_mpc.workload import pmpc_batch
     S, T, P = pmpc_batch(64)
-    s = dm.Solver(N=20, Ts=0.002, tol=1e-8, B_max=2 * S.shape[0])
+    s = dm.Solver(N=N, Ts=0.002, tol=1e-8, B_max=2 * S.shape[0])
     big = s.solve_batch(np.concatenate([S, S]), np.concatenate([T, T]), np.concatenate([P, P]))
     small = [s.solve_batch(S[i:i + 18], T[i:i + 18], P[i:i + 18]) for i in range(0, S.shape[0], 18)]
     s.close()
@@ -256,3 +259,34 @@ def test_wave_primitives_selftest(dm):
     assert out[195] == lanes.sum() and out[196] == 63.0 and out[197] == 0.5 and np.isinf(out[198])
     assert out[199] == 3.0 and out[200] == 35.0               # ds_swizzle broadcast within each half
     print("raw v_rcp_f64 max relative error:", np.max(np.abs(out[131:195])))
+
+
+def test_controllers_on_two_threads(dm):
+    """PMPC controllers of the same configuration share one library handle (dart_mpc.pmpc._SOLVERS).
+    Two threads calling PMPC.solve at once must each get their own instance's answer: the handle's
+    mutex serialises the host-pointer path (shared pinned staging buffers and stream)."""
+    import threading
+    import oracle_lib
+    from dart_mpc.workload import pmpc_batch
+    S, T, P = pmpc_batch(2)
+    ref = oracle_lib.solve_batch(S, T, P, N=20, Ts=0.002, tol=1e-8, want_w=False)
+    errs, fails = [0.0, 0.0], []
+
+    def run(tid):
+        try:
+            for rep in range(25):
+                for i in range(tid, S.shape[0], 2):
+                    mu, Qp, Qv, R, lo, hi = P[i]
+                    c = dm.PMPC(N=20, Qp=Qp, Qv=Qv, R=R, mu=mu, u_bounds=(lo, hi))
+                    u, _ = c.solve(T[i], state=S[i])
+                    errs[tid] = max(errs[tid], float(np.max(np.abs(u - ref["u0"][i]))))
+        except Exception as e:   # pragma: no cover - reported below
+            fails.append(repr(e))
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not fails, fails
+    assert max(errs) <= U0_TOL, errs
