@@ -6,6 +6,8 @@ Drop-in for the reference's MPC hot path:
   - ``AdaptiveNPMPCSmooth``, ``RLS`` <- RMPC/dev_dual/controller/np_mpc_adaptive_with_linear_regressor.py
   - ``RMPCStep``        <- RMPC/dev_dual/rob_ctrl.py:331-352 (RLS fused into the solve launch)
   - ``RLMPC``, ``LmpcPolicy``, ``LmpcSolver`` <- LMPC/src/controller/rlmpc2.py (solver worker, policy worker, front-end)
+  - ``RLMPCAsync``, ``lmpc_solver_worker``, ``lmpc_policy_worker`` <- the same with the reference's shared-memory /
+                           Event process topology (rlmpc2.py:110-164, 229-533, 537-769, 986-1021)
   - ``ArmControl``, ``ArmSolver`` <- ARMCONTROL (PMPC/src/controller/arm.py), the per-arm impedance QP
   - ``harness``         <- the closed loops of main_parallel_enhanced.py / rob_ctrl.py without MuJoCo, and the
                            reference's result formats (logger.py npz + metrics, rob_ctrl.py episode JSON)
@@ -16,8 +18,9 @@ from .pmpc import PMPC, tilt_to_quat  # noqa: F401
 from .worker import mpc_worker  # noqa: F401
 from .rmpc import AdaptiveNPMPCSmooth, RLS, RMPCStep  # noqa: F401
 from .lmpc import RLMPC, LmpcPolicy, init_policy_weights  # noqa: F401
+from .lmpc_shm import RLMPCAsync, lmpc_policy_worker, lmpc_solver_worker  # noqa: F401
 from .arm import ArmControl, ArmSolver  # noqa: F401
 from . import harness, workload  # noqa: F401
 
-__all__ = ["PMPC", "mpc_worker", "Solver", "RmpcSolver", "LmpcSolver", "RLMPC", "LmpcPolicy", "init_policy_weights", "ArmControl", "ArmSolver", "AdaptiveNPMPCSmooth", "RLS", "RMPCStep", "DartMPCError",
+__all__ = ["PMPC", "mpc_worker", "Solver", "RmpcSolver", "LmpcSolver", "RLMPC", "LmpcPolicy", "init_policy_weights", "RLMPCAsync", "lmpc_solver_worker", "lmpc_policy_worker", "ArmControl", "ArmSolver", "AdaptiveNPMPCSmooth", "RLS", "RMPCStep", "DartMPCError",
            "build", "lib", "rls_update_batch", "tilt_to_quat", "workload", "harness"]
