@@ -11,10 +11,10 @@
 //   G = M^T Pt M + Ht                               stage QP incl. gradient (last row/column)
 //   Pt' = Schur complement of G on the u block      ->  gains K (2 x NXA), feed-forward k (2)
 //
-// One LDS round trip per node: lane e owns packed entry (i, j) of G_k and forms it from the
-// columns a_i, a_j of M_k (lane-private reads) and all of G_{k+1} (broadcast reads), with the
-// Schur complement that defines Pt_{k+1} folded into the bilinear form.  The gains [K | k] and
-// the multipliers are recovered from the stored G_k afterwards, lane per node, in parallel.
+// One LDS round trip per node (riccati_sweep_aug): lanes 8 g + s form u_g = Pt_{k+1} a_g row by
+// row from G_{k+1} (the Schur complement that defines Pt_{k+1} folded in), exchange it inside their
+// 8-lane group by DPP and write the packed entries of G_k = M_k^T Pt_{k+1} M_k + Ht_k.  The gains
+// [K | k] and the multipliers are recovered from the stored G_k afterwards, lane per node.
 //
 // The forward sweep dx~_{k+1} = Phi_k dx~_k + f_k (Phi = A + B K, f = c + B k, formed for all
 // nodes in parallel, lane per node) runs redundantly in every lane: no exchange on the chain.
@@ -53,7 +53,6 @@ struct OcpLds {
     static constexpr int NT = tri(ND);        // packed entries of G / Ht
     static constexpr int NTP = even(NT);
     static constexpr int NF = even(NXA + 1);  // closed-loop row stride [Phi row | f]
-    static constexpr int EPL = (NT + 63) / 64;     // packed entries of G per lane
     NodeArr<double[ND][NC], NMAXS> M;         // M[k][j][m] = M_k(m, j): column j of M_k
     NodeArr<double[NTP], NMAXS> H;            // stage Hessian + gradient, packed symmetric
     NodeArr<double[NTP], NMAXS> G;            // G_k; G[N] = terminal surrogate (Pt_N, Quu = I)
@@ -61,6 +60,7 @@ struct OcpLds {
     NodeArr<double[NXA][NF], NMAXS> F;        // closed loop: F[k][r] = [Phi_k(r, :) | f_k(r)]
     NodeArr<double[NXA][NF], NMAXS / 2> F2;   // two-node maps of nodes 2q, 2q + 1 (compose_pairs)
     double dx0[NC];                           // forward sweep start dx~_0
+    alignas(16) double Gc[NTP];               // riccati_sweep_aug: G_{k+1} of the node step in flight
 };
 
 // Two-node closed-loop maps F2[q] = [Phi_{2q+1} Phi_{2q} | Phi_{2q+1} f_{2q} + f_{2q+1}] of every
@@ -112,31 +112,6 @@ __host__ __device__ constexpr int gzz(int p, int q) { return hp(zi_of_p<NXA>(p),
 template <int NXA>
 __host__ __device__ constexpr int gzu(int p, int a) { return hp(zi_of_p<NXA>(p), NXA + a); }
 
-// Per-lane roles of the backward sweep (packed entries e = lane + 64 r of G), decoded once.
-template <int EPL>
-struct RiccatiRoles {
-    int ci[EPL], cj[EPL];   // column offsets (j * NC) of a_i, a_j in M_k
-    bool on[EPL];           // lane owns entry r
-};
-
-template <class L>
-__device__ RiccatiRoles<L::EPL> riccati_roles() {
-    constexpr int NT = L::NT, NC = L::NC;
-    const int lane = threadIdx.x;
-    RiccatiRoles<L::EPL> r{};
-#pragma unroll
-    for (int q = 0; q < L::EPL; ++q) {
-        const int e0 = lane + 64 * q;
-        const int e = e0 < NT ? e0 : 0;
-        int i = 0;
-        while (tri(i + 1) <= e) ++i;
-        const int j = e - tri(i);
-        r.ci[q] = i * NC; r.cj[q] = j * NC;
-        r.on[q] = e0 < NT;
-    }
-    return r;
-}
-
 // Quu of a packed G, its positive-definiteness and its inverse (wave-uniform values)
 template <int NXA>
 __device__ __forceinline__ bool quu_inverse(const double* Gk, double& i00, double& i01, double& i11) {
@@ -147,65 +122,104 @@ __device__ __forceinline__ bool quu_inverse(const double* Gk, double& i00, doubl
     return (g00 > 0.0) && (det > 0.0) && isfinite(det);
 }
 
-// Backward Riccati sweep over nodes N-1 .. 0, one LDS round trip per node.  With
-// Pt_{k+1} = Gzz - Gzu Quu^-1 Guz (the Schur complement of G_{k+1}) folded in,
-//   G_k(i, j) = Ht_ij + a_i^T Gzz a_j - (a_i^T Gzu) Quu^-1 (Guz a_j),
-// lane e owning packed entry (i, j).  G[N] must hold the terminal surrogate.  Returns false
-// (wave-uniform) if some Quu is not positive definite (inertia correction needed).
+// Backward sweep for the Delta-u-augmented stage (x~ = [x (NXA - 2); u_prev (2)], z = [x~; u; 1]):
+// the u_prev columns of M_k are zero (x~+ does not depend on u_{k-1}), so G_k = H_k on every entry
+// with a u_prev index, and the products need only the NP non-zero columns c(g) = [x, u, 1] of M_k.
+// The node step runs in two register phases with one DPP exchange between them, instead of every
+// lane forming a whole NP x NP bilinear form:
+//   phase 1, lane 8 g + s:  u_g[s] = (Pt_{k+1} a_g)[s] = (Gzz a_g)[s] - Gzu(s, :) Quu^-1 (Guz a_g)
+//   phase 2, lane 8 g + s:  G_k(c(g), c(s)) = H_k + sum_m a_s[m] u_g[m]  for s <= g, with the eight
+//                           u_g[m] of its group gathered by quad_perm / row_half_mirror DPP moves
+// (m = s ^ x, x = 0..7; row 7 of every M column is the zero pad).  The 17 entries with a u_prev
+// index are copied from H_k by lanes that write no product entry.  G[N] must hold the terminal
+// surrogate.  Returns false (wave-uniform) if some Quu is not positive definite (inertia correction).
 template <class L>
-__device__ bool riccati_sweep(L* S, int N, const RiccatiRoles<L::EPL>& R) {
-    constexpr int NXA = L::NXA, NP = L::NP;
+__device__ bool riccati_sweep_aug(L* S, int N) {
+    constexpr int NXA = L::NXA, NP = L::NP, NC = L::NC, ND = L::ND, NX = NXA - 2;
+    static_assert(ND == NXA + 3 && NP <= 8 && NC == 8, "two inputs, value dimension <= 8, M columns padded to 8");
     const int lane = threadIdx.x;
+    const int g = lane >> 3, s = lane & 7;
+    const int ge = g < NP ? g : NP - 1, se = s < NP ? s : NP - 1;          // clamped (idle lanes stay finite)
+    const int cg = ge < NX ? ge : ge + 2, cs = se < NX ? se : se + 2;     // z columns of the groups
+    const int zs = se < NXA ? se : ND - 1;                                // z index of value index s
+    // the packed entry this lane writes: a product entry (c(g), c(s)), s <= g < NP; or a u_prev entry
+    // copied from H_k (q-th of the 17, enumerated row by row); or none
+    const bool prod = g < NP && s <= g;
+    int q = -1;
+    if (g >= NP) q = s;                                                   // lanes 56..63: q = 0..7
+    else if (s > g) q = 8 + g * 7 - g * (g - 1) / 2 + (s - g - 1);        // upper-triangle lanes
+    int ecopy = -1;
+    if (q >= 0) {
+        int n = 0;
+        for (int i = 0; i < ND; ++i)
+            for (int j = 0; j <= i; ++j)
+                if (i == NX || i == NX + 1 || j == NX || j == NX + 1) {
+                    if (n == q) ecopy = hp(i, j);
+                    ++n;
+                }
+    }
+    // lanes with no entry write the pad slot NT (straight-line stores, no exec masking)
+    static_assert(L::NTP > L::NT, "a pad slot after the packed entries");
+    const int e = prod ? hp(cg, cs) : (ecopy >= 0 ? ecopy : L::NT);
+    // G_{k+1}(zs, z(n)) of the value indices n: packed row zs for z(n) <= zs, else column zs of row z(n)
+    int goff[NP];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+        const int zn = n < NXA ? n : ND - 1;
+        goff[n] = zn <= zs ? tri(zs) + zn : tri(zn) + zs;
+    }
+    const int gsu0 = hp(NXA, zs), gsu1 = hp(NXA + 1, zs);                 // Gzu(s, 0), Gzu(s, 1)
+    // the chain reads G_{k+1} from one fixed slot (loop-invariant addresses); each step rewrites it
+    // with G_k after its reads (one wave: its LDS instructions complete in order)
+    for (int t = lane; t < L::NT; t += 64) S->Gc[t] = S->G[N][t];
+    __syncthreads();
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
-        // straight-line body, every lane active (lanes past NT recompute entry 0 and store the same
-        // value): the loads of H_k and M_k do not wait on G_{k+1}, and Quu^-1 is formed after the
-        // products, so one LDS latency per node stays on the chain
-        double hk[L::EPL];
+        // off the chain: the two M columns and the H entry of this lane
+        const double* Mk = &S->M[k][0][0];
+        double a[NP], b[8];
 #pragma unroll
-        for (int q = 0; q < L::EPL; ++q) hk[q] = S->H[k][R.on[q] ? lane + 64 * q : 0];
-        const double* Gn = S->G[k + 1];
-        double gout[L::EPL], bb0[L::EPL], bb1[L::EPL], cc0[L::EPL], cc1[L::EPL];
+        for (int m = 0; m < NP; ++m) a[m] = Mk[cg * NC + m];
 #pragma unroll
-        for (int q = 0; q < L::EPL; ++q) {
-            const double* ai = &S->M[k][0][0] + R.ci[q];
-            const double* aj = &S->M[k][0][0] + R.cj[q];
-            double vi[NP], vj[NP];
+        for (int x = 0; x < 8; ++x) b[x] = Mk[cs * NC + (s ^ x)];
+        const double hk = S->H[k][e];
+        // phase 1: every read of G_{k+1} issued before the first product
+        const double* Gn = S->Gc;
+        double gz[NP], gu0[NP], gu1[NP];
 #pragma unroll
-            for (int m = 0; m < NP; ++m) { vi[m] = ai[m]; vj[m] = aj[m]; }
-            // NP + 4 independent accumulators updated round-robin: dependency distance NP + 4
-            double t[NP];
-            double b0 = 0.0, b1 = 0.0, c0 = 0.0, c1 = 0.0;
+        for (int n = 0; n < NP; ++n) { gu0[n] = Gn[gzu<NXA>(n, 0)]; gu1[n] = Gn[gzu<NXA>(n, 1)]; }
 #pragma unroll
-            for (int m = 0; m < NP; ++m) t[m] = 0.0;
+        for (int n = 0; n < NP; ++n) gz[n] = Gn[goff[n]];
+        const double gs0 = Gn[gsu0], gs1 = Gn[gsu1];
+        const double q00 = Gn[hp(NXA, NXA)], q01 = Gn[hp(NXA + 1, NXA)], q11 = Gn[hp(NXA + 1, NXA + 1)];
+        double t0 = 0.0, t1 = 0.0, w0 = 0.0, w1 = 0.0;
 #pragma unroll
-            for (int n = 0; n < NP; ++n) {
-#pragma unroll
-                for (int m = 0; m < NP; ++m) t[m] = fma(Gn[gzz<NXA>(m, n)], vj[n], t[m]);
-                b0 = fma(vi[n], Gn[gzu<NXA>(n, 0)], b0);
-                b1 = fma(vi[n], Gn[gzu<NXA>(n, 1)], b1);
-                c0 = fma(vj[n], Gn[gzu<NXA>(n, 0)], c0);
-                c1 = fma(vj[n], Gn[gzu<NXA>(n, 1)], c1);
-            }
-            double ga = hk[q], gb = 0.0;
-#pragma unroll
-            for (int m = 0; m < NP; m += 2) {
-                ga = fma(vi[m], t[m], ga);
-                if (m + 1 < NP) gb = fma(vi[m + 1], t[m + 1], gb);
-            }
-            gout[q] = ga + gb; bb0[q] = b0; bb1[q] = b1; cc0[q] = c0; cc1[q] = c1;
+        for (int n = 0; n < NP; ++n) {
+            w0 = fma(gu0[n], a[n], w0);
+            w1 = fma(gu1[n], a[n], w1);
         }
-        double i00, i01, i11;
-        ok = quu_inverse<NXA>(Gn, i00, i01, i11) && ok;
 #pragma unroll
-        for (int q = 0; q < L::EPL; ++q) {
-            const double w0 = fma(i00, cc0[q], i01 * cc1[q]), w1 = fma(i01, cc0[q], i11 * cc1[q]);
-            gout[q] -= fma(bb0[q], w0, bb1[q] * w1);
+        for (int n = 0; n < NP; ++n) {
+            if (n & 1) t1 = fma(gz[n], a[n], t1);
+            else t0 = fma(gz[n], a[n], t0);
         }
-        // all reads of G_{k+1} and M_k precede the writes of G_k (distinct rows: no hazard)
+        // r = Quu^-1 Guz(:, s) depends on G_{k+1} alone: it runs beside the products with a_g
+        const double det = fma(q00, q11, -q01 * q01);
+        ok = ok && (q00 > 0.0) && (det > 0.0) && isfinite(det);
+        const double idet = frcp(det);
+        const double r0 = fma(q11, gs0, -q01 * gs1) * idet, r1 = fma(q00, gs1, -q01 * gs0) * idet;
+        const double u = (t0 + t1) - fma(r0, w0, r1 * w1);
+        // phase 2: u_g[s ^ x] of the 8-lane group
+        const double m7 = dpp<0x141>(u);                                 // row_half_mirror: lane s <- 7 - s
+        const double ux[8] = {u, dpp<0xB1>(u), dpp<0x4E>(u), dpp<0x1B>(u), dpp<0x1B>(m7), dpp<0x4E>(m7),
+                              dpp<0xB1>(m7), m7};
+        double p0 = hk, p1 = 0.0;
 #pragma unroll
-        for (int q = 0; q < L::EPL; ++q)
-            if (q == 0 || R.on[q]) S->G[k][R.on[q] ? lane + 64 * q : 0] = gout[q];
+        for (int x = 0; x < 8; x += 2) { p0 = fma(b[x], ux[x], p0); p1 = fma(b[x + 1], ux[x + 1], p1); }
+        // all reads of G_{k+1} and M_k precede the write of G_k (distinct rows: no hazard)
+        const double gk = prod ? p0 + p1 : hk;
+        S->G[k][e] = gk;
+        S->Gc[e] = gk;
         __syncthreads();
     }
     double i00, i01, i11;

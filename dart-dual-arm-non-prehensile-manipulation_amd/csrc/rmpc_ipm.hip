@@ -248,7 +248,6 @@ __device__ __forceinline__ void rm_iq(const double* z, double vmax, double* c) {
 __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     __shared__ RmShared SH;
     RmLds* S = &SH.ocp;
-    const RiccatiRoles<RmLds::EPL> RR = riccati_roles<RmLds>();
     STAMP_DECL
     if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
     const int b = blockIdx.x / a.pack;
@@ -600,7 +599,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 
         // ---------------- Newton step: Riccati with inertia correction -----------------------
         double delta = 0.0, dapplied = 0.0;
-        bool ok = riccati_sweep(S, N, RR);
+        bool ok = riccati_sweep_aug(S, N);
         int attempt = 1;
         for (; attempt < 60 && !ok; ++attempt) {
             delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))   // IPOPT perturb_dec_fact 1/3
@@ -617,7 +616,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             }
             dapplied = delta;
             __syncthreads();
-            ok = riccati_sweep(S, N, RR);
+            ok = riccati_sweep_aug(S, N);
         }
         STAMP_ADD(9, attempt);
         STAMP(3);
