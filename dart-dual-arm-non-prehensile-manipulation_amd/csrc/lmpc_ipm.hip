@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "lmpc_ipm.h"
 #include "ocp_wave.h"
 #include "stamps.h"
@@ -832,13 +834,22 @@ extern "C" size_t dartmpc_lmpc_lds_bytes(void) { return sizeof(dartmpc::LmShared
 extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStream_t stream) {
     if (args->B <= 0) return hipSuccess;
     if (args->N < 1 || args->N >= dartmpc::LM_NMAXS) return hipErrorInvalidValue;
-    static bool attr_set = false;
+    // the dynamic-LDS opt-in is per device: set once for every device a launch goes to (thread-safe)
+    static std::mutex mu;
+    static bool attr_set[64] = {};
     const size_t lds = sizeof(dartmpc::LmShared);
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)dartmpc::lmpc_ipm_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (!attr_set[dev]) {
+            e = hipFuncSetAttribute((const void*)dartmpc::lmpc_ipm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds);
+            if (e != hipSuccess) return e;
+            attr_set[dev] = true;
+        }
     }
     dartmpc::LmpcArgs a = *args;
     a.pack = (a.B <= 32) ? 8 : 1;            // one XCD (and its L2) for the code of a small batch

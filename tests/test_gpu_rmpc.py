@@ -72,7 +72,7 @@ def test_wide_tilt_box_library_trig_path(dm):
     assert np.allclose(out["f"], ref["f"], rtol=1e-6, atol=1e-10)
 
 
-@pytest.mark.parametrize("N", [1, 2, 15, 31])
+@pytest.mark.parametrize("N", [1, 2, 15, 21, 22, 31])
 def test_horizons(dm, N):
     from dart_mpc.workload import rmpc_batch
     D = rmpc_batch(1, seed0=3, N=N)
