@@ -29,9 +29,12 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "dart-dual-arm-non-prehensile-manipulation_amd"))
 
-F_ITER_PMPC = 6.0e4          # FLOP per IPM iteration per instance, PMPC N=20
-BYTES_PER_SOLVE = 176        # 18 fp64 in + u0, f, status, iters out
-FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 (vector = matrix), spec
+sys.path.insert(0, ROOT)
+from bench import roofline as RL   # noqa: E402  frozen roofline constants
+
+F_ITER_PMPC = RL.F_ITER["pmpc_n20"]          # FLOP per IPM iteration per instance, PMPC N=20
+BYTES_PER_SOLVE = RL.BYTES_PER_SOLVE["pmpc"]  # 18 fp64 in + u0, f, status, iters out
+FP64_PEAK_TFLOPS = RL.FP64_PEAK_TFLOPS       # MI355X FP64 (vector = matrix), spec
 EVERY = 10                   # kernel-duration sampling stride inside the timed region
 METRIC = "MPC solves/sec (horizon N=20, batch=18 objects) at 1/2/4/8 GPUs; max |u−u_ref|"
 
@@ -110,7 +113,9 @@ def bench_rmpc(args, torch, dev, stream, dart_mpc):
     out = {"workload": "C3: RMPC batch=18, N=20, Ts=0.002, RLS update (2 filters, p=7) fused, cold start, tol "
                        f"{args.tol:g}", "solves_per_s": B * K / dt, "ms_per_step": dt / K * 1e3, "kernel_ms": kern_ms,
            "status_ok_frac": float(np.mean(st == 0)), "iters_mean": float(its.mean()),
-           "max_abs_u0_err_vs_exact_optimum": max_du}
+           "max_abs_u0_err_vs_exact_optimum": max_du,
+           "roofline": RL.roofline(float(its.sum(axis=1).mean()), RL.F_ITER["rmpc_n20"], kern_ms * 1e-3,
+                                   note="sum(iters) x 7.3e4 FLOP per launch / mean kernel time")}
     if not args.no_cpu_baseline:
         try:
             ncores = len(os.sched_getaffinity(0))
@@ -310,6 +315,8 @@ def bench_lmpc(args, torch, dev, stream, dart_mpc):
                        "(tol 1e-4, max_iter 50, acceptable 1e-3 x 5), cold start",
            "solves_per_s": B * K / dt, "ms_per_step": dt / K * 1e3, "kernel_ms": kern_ms,
            "status_ok_frac": float(np.mean(st >= 0)), "iters_mean": float(its.mean()),
+           "roofline": RL.roofline(float(its.sum(axis=1).mean()), RL.F_ITER["lmpc_n30"], kern_ms * 1e-3,
+                                   note="sum(iters) x 3.7e5 FLOP per launch / mean kernel time"),
            "max_abs_u0_err_vs_oracle_same_options": float(np.max(np.abs(u0 - ref["u0"]))),
            "max_abs_u0_err_vs_exact_optimum": float(np.max(np.abs(u0[ok] - exact["u0"][ok]))) if ok.any() else None}
     if not args.no_cpu_baseline:
@@ -508,7 +515,8 @@ def main():
                 solved += Sb.shape[0]
             cdt = time.perf_counter() - c0
             cpu_baseline = {"value": solved / cdt, "unit": "solves/s", "cores": nthreads, "kind": "port",
-                            "sample": f"C oracle IPM (oracle/pmpc_ipm.c, full 6-state NLP, filter line search, "
+                            "sample": f"CPU restatement, not CasADi/IPOPT (neither is installed): C oracle IPM "
+                                      f"(oracle/pmpc_ipm.c, IPOPT's algorithm on the full 6-state NLP, filter line search, "
                                       f"tol {args.tol:g}), {solved} cold-start solves of seeded 18-config batches "
                                       f"(N={N}) in {cdt:.1f} s on {nthreads} OpenMP threads"}
 
@@ -591,6 +599,16 @@ def main():
     if pmc:
         with open(pmc[-1]) as fh:
             traffic = json.load(fh).get("traffic_bytes_per_launch")
+    # latency regime: with one wave per instance the launch is bound by the wave's own instruction
+    # issue; the committed SQ counters of this build (tools/pmc_sq.sh) give the busy fraction
+    issue = None
+    sq = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "sq_summary.json")))
+    if sq:
+        with open(sq[-1]) as fh:
+            pi = json.load(fh)["kernels"]["PMPC C2"]["per_instance"]
+        issue = {"bound": "VALU issue of one wave per instance", "valu_busy_frac": pi["valu_busy_frac"],
+                 "valu_insts_per_solve": pi["valu_insts"], "cycles_per_valu_inst": pi["cycles_per_valu_inst"],
+                 "source": os.path.relpath(sq[-1], ROOT)}
 
     if rank == 0:
         value = world * B * K / elapsed
@@ -614,7 +632,7 @@ def main():
                        **({"dist_backend": backend} if world > 1 else {})},
             "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel": "pmpc_ipm_kernel", "kernel_ms": kern_ms,
+                         "kernel": "pmpc_ipm_kernel", "kernel_ms": kern_ms, "issue": issue,
                          "note": "FP64 compute roof (vector = matrix on gfx950); algorithmic FLOP = "
                                  "sum(iters) x 6.0e4; algorithmic HBM bytes = 176 per solve"},
             "cpu_baseline": cpu_baseline,

@@ -60,7 +60,6 @@ struct OcpLds {
     NodeArr<double[NXA][NF], NMAXS> F;        // closed loop: F[k][r] = [Phi_k(r, :) | f_k(r)]
     NodeArr<double[NXA][NF], NMAXS / 2> F2;   // two-node maps of nodes 2q, 2q + 1 (compose_pairs)
     double dx0[NC];                           // forward sweep start dx~_0
-    alignas(16) double Gc[NTP];               // riccati_sweep_aug: G_{k+1} of the node step in flight
 };
 
 // Two-node closed-loop maps F2[q] = [Phi_{2q+1} Phi_{2q} | Phi_{2q+1} f_{2q} + f_{2q+1}] of every
@@ -169,10 +168,6 @@ __device__ bool riccati_sweep_aug(L* S, int N) {
         goff[n] = zn <= zs ? tri(zs) + zn : tri(zn) + zs;
     }
     const int gsu0 = hp(NXA, zs), gsu1 = hp(NXA + 1, zs);                 // Gzu(s, 0), Gzu(s, 1)
-    // the chain reads G_{k+1} from one fixed slot (loop-invariant addresses); each step rewrites it
-    // with G_k after its reads (one wave: its LDS instructions complete in order)
-    for (int t = lane; t < L::NT; t += 64) S->Gc[t] = S->G[N][t];
-    __syncthreads();
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
         // off the chain: the two M columns and the H entry of this lane
@@ -184,7 +179,7 @@ __device__ bool riccati_sweep_aug(L* S, int N) {
         for (int x = 0; x < 8; ++x) b[x] = Mk[cs * NC + (s ^ x)];
         const double hk = S->H[k][e];
         // phase 1: every read of G_{k+1} issued before the first product
-        const double* Gn = S->Gc;
+        const double* Gn = S->G[k + 1];
         double gz[NP], gu0[NP], gu1[NP];
 #pragma unroll
         for (int n = 0; n < NP; ++n) { gu0[n] = Gn[gzu<NXA>(n, 0)]; gu1[n] = Gn[gzu<NXA>(n, 1)]; }
@@ -217,9 +212,7 @@ __device__ bool riccati_sweep_aug(L* S, int N) {
 #pragma unroll
         for (int x = 0; x < 8; x += 2) { p0 = fma(b[x], ux[x], p0); p1 = fma(b[x + 1], ux[x + 1], p1); }
         // all reads of G_{k+1} and M_k precede the write of G_k (distinct rows: no hazard)
-        const double gk = prod ? p0 + p1 : hk;
-        S->G[k][e] = gk;
-        S->Gc[e] = gk;
+        S->G[k][e] = prod ? p0 + p1 : hk;
         __syncthreads();
     }
     double i00, i01, i11;
