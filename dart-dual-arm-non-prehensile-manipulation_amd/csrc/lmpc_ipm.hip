@@ -65,10 +65,6 @@ struct LmSub {
 
 struct LmShared {
     LmLds ocp;
-    // per node slot, per RK stage: d f / d y coefficients, and the second-derivative data turned
-    // into adjoint-weighted curvature coefficients
-    NodeArr<double[4][LM_NSC], 2 * LM_NMAXS> SC;
-    NodeArr<double[4][4], 2 * LM_NMAXS> SD;
     NodeArr<double[7], 2 * LM_NMAXS> JL;     // J^T lambda_{k+1} (x 4, u 1), primal residual maxima
     NodeArr<double[5], 2 * LM_NMAXS> CS;     // second-order correction: c_soc rows of node k (incoming defect)
     NodeArr<double[11], 2 * LM_NMAXS> SV;    // second-order correction: the plain step (dx~, lambda+, du)
@@ -418,12 +414,13 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         double sa, ca, xn[4];
         const double lz[5] = {0, 0, 0, 0, 0};
         tilt_sincos(poly, u, sa, ca);
-        sub_rk4_lin(m, x, sa, xn, SH.SC[sl], SH.SD[sl]);
-        const double huu = sub_adjoint_curv(m, SH.SC[sl], SH.SD[sl], lz, sa);
+        double scr[4][LM_NSC], cvr[4][4];
+        sub_rk4_lin(m, x, sa, xn, scr, cvr);
+        const double huu = sub_adjoint_curv(m, scr, cvr, lz, sa);
         if (uon) {
             const LmSub mr = m;
 #pragma unroll 1
-            for (int d = 0; d < 5; ++d) sub_direction(mr, SH.SC[sl], SH.SD[sl], huu, LM_G * ca, d, lz, Mk, Hk, 0.0);
+            for (int d = 0; d < 5; ++d) sub_direction(mr, scr, cvr, huu, LM_G * ca, d, lz, Mk, Hk, 0.0);
         }
         double rs[4];
 #pragma unroll
@@ -472,9 +469,11 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             double sa, ca;
             tilt_sincos(poly, u, sa, ca);
             double xn[4];
-            sub_rk4_lin(m, x, sa, xn, SH.SC[sl], SH.SD[sl]);
+            // stage data of the RK4 pass stay in registers through the adjoint and the five directions
+            double scr[4][LM_NSC], cvr[4][4];
+            sub_rk4_lin(m, x, sa, xn, scr, cvr);
             {
-                const double huu = sub_adjoint_curv(m, SH.SC[sl], SH.SD[sl], lamn, sa);
+                const double huu = sub_adjoint_curv(m, scr, cvr, lamn, sa);
                 STAMP(13);
                 // exact dynamics Hessian (x, u blocks) and the Jacobian columns of node k
                 if (uon) {
@@ -483,7 +482,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     const double cu = sc * 2.0 * (Ru + Rdu) + zl * isl + zu * isu;
 #pragma unroll
                     for (int d = 0; d < 5; ++d)
-                        SH.JL[sl][d] = sub_direction(mr, SH.SC[sl], SH.SD[sl], huu, LM_G * ca, d, lamn, Mk, Hk,
+                        SH.JL[sl][d] = sub_direction(mr, scr, cvr, huu, LM_G * ca, d, lamn, Mk, Hk,
                                                      d < 4 ? sc * 2.0 * Wq[d] : cu);
 #pragma unroll
                     for (int d = 0; d < 5; ++d) jl[d] = SH.JL[sl][d];
