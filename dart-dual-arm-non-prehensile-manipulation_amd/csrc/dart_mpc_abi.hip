@@ -159,6 +159,9 @@ struct dart_mpc_handle {
     hipStream_t stream = nullptr;
     HostStage st;                  // staging of the host-pointer entries
     std::string err;
+    int32_t seq = 0;               // completion-word sequence of the host-pointer PMPC entry
+    int32_t* hdone = nullptr;      // PMPC: B_max completion words, mapped host memory (only ever
+    int32_t* ddone = nullptr;      //   hold sequence numbers of earlier calls) and their device address
     // Serialises the entries on this handle: the host-pointer entries share the pinned staging
     // buffers and the handle's stream, and every entry may write err.  Concurrent callers (the
     // reference runs controllers on background threads, RMPC/dev_dual/controller/convimp.py:435)
@@ -200,7 +203,26 @@ int launch(dart_mpc_handle* h, int B, const double* x0, const double* ref, const
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter; a.g = h->cfg.gravity;
     a.x0 = x0; a.ref = ref; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
+    a.done = nullptr; a.seq = 0;
     HIPCHK(h, dartmpc_launch_pmpc(&a, s), "kernel launch");
+    return DART_MPC_OK;
+}
+
+// Wait for the B completion words of a host-pointer PMPC launch (mapped host memory, written last by
+// every instance with a system-scope release).  Spinning on them returns as soon as the last store
+// lands, without the stream-completion round trip; the stream is queried now and then, and if it is
+// done (or failed) without every word set, the stream's own status decides.
+int wait_done(dart_mpc_handle* h, hipStream_t s, const volatile int32_t* done, int B, int32_t seq) {
+    for (unsigned n = 1;; ++n) {
+        int b = 0;
+        while (b < B && __atomic_load_n(done + b, __ATOMIC_ACQUIRE) == seq) ++b;
+        if (b == B) return DART_MPC_OK;
+        if ((n & 255) == 0 && hipStreamQuery(s) != hipErrorNotReady) break;
+        __builtin_ia32_pause();
+    }
+    HIPCHK(h, hipStreamSynchronize(s), "hipStreamSynchronize");
+    for (int b = 0; b < B; ++b)
+        if (__atomic_load_n(done + b, __ATOMIC_ACQUIRE) != seq) return fail(h, DART_MPC_EHIP, "kernel did not complete");
     return DART_MPC_OK;
 }
 
@@ -260,6 +282,13 @@ int dart_mpc_create(const dart_mpc_config* cfg, int device, dart_mpc_handle** ou
     const bool zc = cfg->variant == DART_MPC_PMPC;
     if (e == hipSuccess)
         e = h->st.reserve(zc ? A : nin * sizeof(double) + A, nout * sizeof(double) + A, zc ? nin * sizeof(double) + A : 0);
+    if (e == hipSuccess && zc) {
+        e = hipHostMalloc((void**)&h->hdone, sizeof(int32_t) * B, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) {
+            std::memset(h->hdone, 0, sizeof(int32_t) * B);
+            e = hipHostGetDevicePointer((void**)&h->ddone, h->hdone, 0);
+        }
+    }
     if (e != hipSuccess) {
         dart_mpc_destroy(h);
         return DART_MPC_EHIP;
@@ -308,10 +337,16 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     double* d_wo = w_out ? S.out<double>(nw * B) : nullptr;
     int32_t* d_st = S.out<int32_t>(B);
     int32_t* d_it = S.out<int32_t>(B);
+    int32_t* d_done = h->ddone;
     HIPCHK(h, S.upload(s), "copy inputs");
-    int rc = launch(h, B, d_x0, d_ref, d_prm, d_ww, d_u0, d_f, d_wo, d_st, d_it, s);
+    dartmpc::PmpcArgs a;
+    a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter; a.g = h->cfg.gravity;
+    a.x0 = d_x0; a.ref = d_ref; a.prm = d_prm; a.w_warm = d_ww;
+    a.u0 = d_u0; a.f = d_f; a.w_out = d_wo; a.status = d_st; a.iters = d_it;
+    a.done = d_done; a.seq = ++h->seq;
+    HIPCHK(h, dartmpc_launch_pmpc(&a, s), "kernel launch");
+    const int rc = wait_done(h, s, h->hdone, B, a.seq);
     if (rc) return rc;
-    HIPCHK(h, hipStreamSynchronize(s), "hipStreamSynchronize");
     S.take(u0, d_u0, 2 * B); S.take(f, d_f, B); S.take(w_out, d_wo, nw * B);
     S.take(status, d_st, B); S.take(iters, d_it, B);
     return DART_MPC_OK;
@@ -564,7 +599,9 @@ const char* dart_mpc_last_error(const dart_mpc_handle* h) { return h ? h->err.c_
 
 void dart_mpc_destroy(dart_mpc_handle* h) {
     if (!h) return;
+    if (h->stream) (void)hipStreamSynchronize(h->stream);    // no launch may still use the buffers below
     h->st.release();
+    if (h->hdone) (void)hipHostFree(h->hdone);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }

@@ -19,6 +19,11 @@ struct PmpcArgs {
     double* w_out;          // [B][nw] or nullptr
     int32_t* status;        // [B]
     int32_t* iters;         // [B]
+    // host-pointer entry only: completion word per instance in mapped host memory, set to `seq`
+    // after every other output of the instance is visible system-wide (the host polls it instead of
+    // waiting for the stream); nullptr on the device entry
+    int32_t* done;          // [B] or nullptr
+    int32_t seq;
 };
 
 }  // namespace dartmpc

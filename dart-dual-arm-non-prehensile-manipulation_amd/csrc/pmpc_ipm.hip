@@ -718,6 +718,11 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
         }
         if (xon && (NAX == 2 || ax0 == 0)) { wo[6 * k + 4] = pz; wo[6 * k + 5] = vz; }
     }
+    if (a.done) {
+        // release at system scope: the wave's output stores (any lane) are visible before the word
+        __threadfence_system();
+        if (lane == 0) __hip_atomic_store(a.done + b, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     STAMP(8);
     STAMP_FLUSH(b);
 }

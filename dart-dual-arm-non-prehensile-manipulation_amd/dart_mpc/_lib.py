@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes
 import os
 import subprocess
+import threading
 
 import numpy as np
 
@@ -194,6 +195,25 @@ class Solver:
         if rc != 0:
             self._err(rc, "dart_mpc_solve_batch")
         return dict(u0=u0, f=f, w=w, status=st, iters=it)
+
+    def solve_one(self, x0, ref, prm, want_w=False):
+        """One instance (the per-control-step call of PMPC.solve / mpc_worker): the rows are copied
+        into buffers allocated once, whose pointers are cached, so the Python side of a call is a few
+        slice copies and one ctypes call.  Returns (u0[2], f, status, iters, w or None); the arrays
+        are fresh copies."""
+        one = getattr(self, "_one", None)
+        if one is None:
+            bufs = [np.empty(6), np.empty(6), np.empty(6), np.empty(2), np.empty(1), np.empty(self.nw),
+                    np.empty(1, np.int32), np.empty(1, np.int32)]
+            one = self._one = (threading.Lock(), bufs, [_ptr(b) for b in bufs])
+        lock, (bx, br, bp, bu, bf, bw, bs, bi), ptrs = one
+        with lock:
+            bx[:] = x0; br[:] = ref; bp[:] = prm
+            rc = lib().dart_mpc_solve_batch(self._h, 1, ptrs[0], ptrs[1], ptrs[2], None, ptrs[3], ptrs[4],
+                                            ptrs[5] if want_w else None, ptrs[6], ptrs[7], None)
+            if rc != 0:
+                self._err(rc, "dart_mpc_solve_batch")
+            return bu.copy(), float(bf[0]), int(bs[0]), int(bi[0]), (bw.copy() if want_w else None)
 
     def solve_batch_dev(self, B, x0, ref, prm, u0, f, status, iters, w_warm=0, w_out=0, stream=0):
         """Device pointers (ints) in/out, asynchronous on ``stream`` (an int hipStream_t, 0 = own)."""

@@ -64,6 +64,10 @@ class PMPC:
         self.last_iters = None
 
     # -- parameter row of the C ABI -----------------------------------------
+    @property
+    def _prm(self):
+        return np.array([self.mu, self.Qp, self.Qv, self.R, self.u_bounds[0], self.u_bounds[1]])
+
     def params(self):
         return np.array([self.mu, self.Qp, self.Qv, self.R, self.u_bounds[0], self.u_bounds[1]])
 
@@ -81,13 +85,11 @@ class PMPC:
 
     def solve(self, target, state=None):
         """Reference semantics (mpc_3d.py:115-138): cold start, returns (U_opt[0], loss)."""
-        x = self.get_state() if state is None else np.asarray(state, float)
-        out = self._engine(1).solve_batch(x[None, :], np.asarray(target, float)[None, :], self.params()[None, :],
-                                          want_w=True)
-        self.w0 = out["w"][0]                                                    # mpc_3d.py:135
-        self.last_status = int(out["status"][0])
-        self.last_iters = int(out["iters"][0])
-        return out["u0"][0].copy(), np.array([out["f"][0]])
+        x = self.get_state() if state is None else state
+        u, f, st, it, w = self._engine(1).solve_one(x, target, self._prm, want_w=True)
+        self.w0 = w                                                              # mpc_3d.py:135
+        self.last_status, self.last_iters = st, it
+        return u, np.array([f])
 
     # -- new API ----------------------------------------------------------------
     def step(self, state, target):
