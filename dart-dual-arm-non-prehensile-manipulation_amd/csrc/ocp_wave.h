@@ -274,8 +274,9 @@ __device__ __forceinline__ void node_multiplier(const L* S, int k, const double*
     }
 }
 
-// Forward sweep over node pairs: lane r < NXA owns row r of the two-node chain
-// dx~_{2q+2} = F2[q] [dx~_{2q}; 1]; the states are broadcast by readlane (scalar registers), and
+// Forward sweep over node pairs: lane 16 w + r (r < NXA) of every row w owns row r of the two-node
+// chain dx~_{2q+2} = F2[q] [dx~_{2q}; 1] -- the four rows run the same chain, so each row
+// broadcasts the new state to itself by 64-bit DPP row_newbcast (no scalar round trip) -- and
 // the rows of the next pair are prefetched while this one is processed.  An odd N ends with one
 // single-node step; the odd nodes in between follow afterwards, lane per node, from their even
 // predecessor (off the chain).  Lane-per-node use: every lane returns in dxo the state step of
@@ -283,8 +284,8 @@ __device__ __forceinline__ void node_multiplier(const L* S, int k, const double*
 template <class L>
 __device__ void forward_sweep(L* S, int N, int node, double* dxo) {
     constexpr int NXA = L::NXA;
-    const int lane = threadIdx.x;
-    const int r = lane < NXA ? lane : 0;
+    const int lr = threadIdx.x & 15;
+    const int r = lr < NXA ? lr : 0;
     double d[NXA];
 #pragma unroll
     for (int i = 0; i < NXA; ++i) { d[i] = S->dx0[i]; dxo[i] = d[i]; }
@@ -306,7 +307,7 @@ __device__ void forward_sweep(L* S, int N, int node, double* dxo) {
         const double s = s0 + s1;
         const bool m = node == 2 * q + 2;
 #pragma unroll
-        for (int i = 0; i < NXA; ++i) { d[i] = readlane(s, i); dxo[i] = m ? d[i] : dxo[i]; }
+        for (int i = 0; i < NXA; ++i) { d[i] = row_bcast(s, i); dxo[i] = m ? d[i] : dxo[i]; }
 #pragma unroll
         for (int j = 0; j <= NXA; ++j) Fc[j] = Fn[j];
     }
@@ -317,7 +318,7 @@ __device__ void forward_sweep(L* S, int N, int node, double* dxo) {
         for (int j = 0; j < NXA; ++j) s = fma(row[j], d[j], s);
         const bool m = node == N;
 #pragma unroll
-        for (int i = 0; i < NXA; ++i) { d[i] = readlane(s, i); dxo[i] = m ? d[i] : dxo[i]; }
+        for (int i = 0; i < NXA; ++i) { d[i] = row_bcast(s, i); dxo[i] = m ? d[i] : dxo[i]; }
     }
     double pv[NXA];
 #pragma unroll
@@ -478,17 +479,17 @@ __device__ __forceinline__ void node_multiplier_s(const L* S, int sl, const doub
     }
 }
 
-// Forward sweep of both halves over node pairs: lane 32 h + r (r < NXA) owns row r of its half's
-// two-node chain dx~_{2q+2} = F2 [dx~_{2q}; 1]; the states are broadcast by ds_swizzle within each
-// half.  An odd N ends with one single-node step; the odd nodes in between follow afterwards, lane
-// per node, from their even predecessor.  Every lane returns in dxo the step of node `node`
-// (= lane & 31) of its half.
+// Forward sweep of both halves over node pairs: lane 16 w + r (r < NXA) owns row r of the two-node
+// chain dx~_{2q+2} = F2 [dx~_{2q}; 1] of half h = w / 2 (both rows of a half run it, so each row
+// broadcasts the new state to itself by 64-bit DPP row_newbcast).  An odd N ends with one
+// single-node step; the odd nodes in between follow afterwards, lane per node, from their even
+// predecessor.  Every lane returns in dxo the step of node `node` (= lane & 31) of its half.
 template <class L>
 __device__ void forward_sweep_s(L* S, int N, int node, double* dxo) {
     constexpr int NXA = L::NXA;
     const int h = threadIdx.x >> 5, base = h * L::NMAXS, pbase = h * (L::NMAXS / 2);
-    const int li = threadIdx.x & 31;
-    const int r = li < NXA ? li : 0;
+    const int lr = threadIdx.x & 15;
+    const int r = lr < NXA ? lr : 0;
     double d[NXA];
 #pragma unroll
     for (int i = 0; i < NXA; ++i) { d[i] = S->dx0[h][i]; dxo[i] = d[i]; }
@@ -510,7 +511,7 @@ __device__ void forward_sweep_s(L* S, int N, int node, double* dxo) {
         const double s = s0 + s1;
         const bool m = node == 2 * q + 2;
 #pragma unroll
-        for (int i = 0; i < NXA; ++i) { d[i] = half_bcast(s, i); dxo[i] = m ? d[i] : dxo[i]; }
+        for (int i = 0; i < NXA; ++i) { d[i] = row_bcast(s, i); dxo[i] = m ? d[i] : dxo[i]; }
 #pragma unroll
         for (int j = 0; j <= NXA; ++j) Fc[j] = Fn[j];
     }
@@ -521,7 +522,7 @@ __device__ void forward_sweep_s(L* S, int N, int node, double* dxo) {
         for (int j = 0; j < NXA; ++j) s = fma(row[j], d[j], s);
         const bool m = node == N;
 #pragma unroll
-        for (int i = 0; i < NXA; ++i) { d[i] = half_bcast(s, i); dxo[i] = m ? d[i] : dxo[i]; }
+        for (int i = 0; i < NXA; ++i) { d[i] = row_bcast(s, i); dxo[i] = m ? d[i] : dxo[i]; }
     }
     double pv[NXA];
 #pragma unroll

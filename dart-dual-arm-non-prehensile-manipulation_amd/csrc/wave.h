@@ -26,6 +26,24 @@ __device__ __forceinline__ double readlane(double x, int l) {
     const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
+// value of lane 16 (lane / 16) + I in every lane of each 16-lane row: one v_mov_b64_dpp
+// row_newbcast (the 64-bit DPP control of gfx950), no scalar round trip and no LDS crossbar
+template <int I>
+__device__ __forceinline__ double row_bcast(double x) {
+    return __builtin_amdgcn_update_dpp(0.0, x, 0x150 + I, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double row_bcast(double x, int i) {
+    switch (i) {       // i (< 8) is a compile-time constant at every (unrolled) call site
+        case 0: return row_bcast<0>(x);
+        case 1: return row_bcast<1>(x);
+        case 2: return row_bcast<2>(x);
+        case 3: return row_bcast<3>(x);
+        case 4: return row_bcast<4>(x);
+        case 5: return row_bcast<5>(x);
+        case 6: return row_bcast<6>(x);
+        default: return row_bcast<7>(x);
+    }
+}
 // value of lane 32 (lane / 32) + I in every lane of each 32-lane half: ds_swizzle bitmask mode
 // (and_mask 0, or_mask I) -- a crossbar move through the LDS unit without a memory access
 template <int I>
