@@ -18,6 +18,7 @@ full 6-state NLP), timed on rank 0 over a bounded sample.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import glob
 import json
 import os
@@ -339,6 +340,85 @@ def bench_lmpc(args, torch, dev, stream, dart_mpc):
     return out
 
 
+def bench_lmpc_policy(args, torch, dev, stream, dart_mpc):
+    """C5 with the learned parameter net in the launch (BASELINE.json configs[4]): 18 LMPC controllers,
+    N=30; one step = the policy step of every controller (Welford-normalised 10-step history, MLP
+    520-64-64-34 fp32, rsample, logit update every 8th step, EMA + soft clip) and the solve with the
+    parameters it wrote, as ONE launch (dart_lmpc_policy_solve_batch_dev).  Also timed: the same step
+    as two launches (policy kernel, then solve), and the check that both give identical results."""
+    from dart_mpc.lmpc import NWEIGHTS, PolicyConfig, init_policy_weights, policy_config  # noqa: F401
+    from dart_mpc.workload import lmpc_batch
+    from dart_mpc._lib import LMPC_PRM_DEFAULT, lib
+    B, K, N = 18, args.lmpc_steps, 30
+    D = [lmpc_batch(1, seed0=7000 + i) for i in range(K + 3)]
+    f64 = lambda a: torch.tensor(np.asarray(a), dtype=torch.float64, device=dev).contiguous()
+    ST0 = f64(np.stack([d["state"] for d in D])); TG = f64(np.stack([d["target"] for d in D]))
+    UP = f64(np.stack([d["u_prev"] for d in D]))
+    rng = np.random.default_rng(17)
+    NZ = torch.tensor(rng.standard_normal((K + 3, B, 34)), dtype=torch.float32, device=dev)
+    PR = f64(np.tile(LMPC_PRM_DEFAULT, (B, 1)))
+    W = torch.tensor(init_policy_weights(0), dtype=torch.float32, device=dev)
+    cfg = policy_config()
+    k0 = np.clip(0.5 * cfg.k_max + np.random.default_rng(1).uniform(-0.05, 0.05, (B, 34)) * cfg.k_max, cfg.min_k,
+                 cfg.k_max - cfg.k_ceiling_margin)
+
+    def state():
+        return dict(ck=f64(k0), mean=torch.zeros((B, 52), dtype=torch.float64, device=dev),
+                    M2=torch.zeros((B, 52), dtype=torch.float64, device=dev),
+                    cnt=torch.zeros(B, dtype=torch.int32, device=dev),
+                    hist=torch.zeros((B, 10, 52), dtype=torch.float32, device=dev),
+                    ts=torch.zeros(B, dtype=torch.int32, device=dev), mp=f64(k0))
+
+    out = {k: torch.empty((K + 3, B, 2), dtype=torch.float64, device=dev) for k in ("u0_f", "u0_s")}
+    FV = torch.empty((K + 3, B), dtype=torch.float64, device=dev)
+    SS = torch.empty((K + 3, B), dtype=torch.int32, device=dev)
+    IT = torch.empty((K + 3, B), dtype=torch.int32, device=dev)
+    s = dart_mpc.LmpcSolver(N=N, B_max=B, device=dev.index)
+    sp = stream.cuda_stream
+    A, Bst = state(), state()
+
+    def fused(i, P=A):
+        s.policy_solve_batch_dev(cfg, B, W.data_ptr(), ST0[i].data_ptr(), UP[i].data_ptr(), TG[i].data_ptr(),
+                                 P["ck"].data_ptr(), P["mean"].data_ptr(), P["M2"].data_ptr(), P["cnt"].data_ptr(),
+                                 P["hist"].data_ptr(), P["ts"].data_ptr(), NZ[i].data_ptr(), P["mp"].data_ptr(),
+                                 PR.data_ptr(), out["u0_f"][i].data_ptr(), FV[i].data_ptr(), SS[i].data_ptr(),
+                                 IT[i].data_ptr(), stream=sp)
+
+    def two_launch(i, P=Bst):
+        rc = lib().dart_lmpc_policy_step_dev(ctypes.byref(cfg), B, W.data_ptr(), ST0[i].data_ptr(), TG[i].data_ptr(),
+                                             UP[i].data_ptr(), P["ck"].data_ptr(), P["mean"].data_ptr(),
+                                             P["M2"].data_ptr(), P["cnt"].data_ptr(), P["hist"].data_ptr(),
+                                             P["ts"].data_ptr(), NZ[i].data_ptr(), P["mp"].data_ptr(), None, sp)
+        assert rc == 0
+        s.solve_batch_dev(B, ST0[i].data_ptr(), UP[i].data_ptr(), P["mp"].data_ptr(), TG[i].data_ptr(), PR.data_ptr(),
+                          out["u0_s"][i].data_ptr(), FV[i].data_ptr(), SS[i].data_ptr(), IT[i].data_ptr(), stream=sp)
+
+    res = {}
+    for name, fn in (("fused", fused), ("two_launch", two_launch)):
+        for i in range(3):
+            fn(i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(stream):
+            for j in range(K):
+                fn(3 + j)
+        torch.cuda.synchronize()
+        res[name] = (time.perf_counter() - t0) / K
+    same = bool(torch.equal(out["u0_f"], out["u0_s"])) and all(torch.equal(A[k], Bst[k]) for k in A)
+    kern_ms = _event_ms(torch, stream, lambda j: fused(3 + j), min(K, 50))
+    s.close()
+    return {"workload": "C5 with the parameter policy in the launch: 18 LMPC controllers, N=30, reference IPOPT "
+                        "options, policy step (MLP 520-64-64-34 fp32, logit update every 8th step) as the prologue "
+                        "of the solve kernel, fresh states every step, weights = Policy._init_weights (checkpoints "
+                        "not loaded)",
+            "solves_per_s": B / res["fused"], "ms_per_step": res["fused"] * 1e3, "kernel_ms": kern_ms,
+            "two_launch_ms_per_step": res["two_launch"] * 1e3,
+            "status_ok_frac": float((SS[3:] >= 0).float().mean()), "iters_mean": float(IT[3:].double().mean()),
+            "fused_equals_two_launch": same,
+            "note": "pvec comes from the policy (current_k mid-range +-5 %, then logit updates), not from the "
+                    "U(0.01, 1.9) draws of the plain C5 line, so these NLPs are easier (fewer iterations)"}
+
+
 def bench_arm(args, torch, dev, stream, dart_mpc):
     """Per-arm impedance QP (ARMCONTROL.solver_worker): 36 arm snapshots per launch
     (18 object configs x 2 arms = one dual-arm simulation step of the C2 batch), fresh synthetic
@@ -587,6 +667,7 @@ def main():
     lmpc = None
     if rank == 0 and args.lmpc_steps > 0:
         lmpc = bench_lmpc(args, torch, dev, stream, dart_mpc)
+        lmpc["policy_fused"] = bench_lmpc_policy(args, torch, dev, stream, dart_mpc)
 
     # supplementary: per-arm impedance QP
     arm = None

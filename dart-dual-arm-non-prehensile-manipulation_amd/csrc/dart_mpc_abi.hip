@@ -432,6 +432,7 @@ int dart_lmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* state, co
     a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc;
     a.state = state; a.u_prev = u_prev; a.pvec = pvec; a.target = target; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
+    a.fuse_policy = 0;
     HIPCHK(h, dartmpc_launch_lmpc(&a, stream ? (hipStream_t)stream : h->stream), "kernel launch");
     return DART_MPC_OK;
 }
@@ -549,6 +550,94 @@ int dart_lmpc_policy_step(const dart_lmpc_policy_config* cfg, int B, const float
     return DART_MPC_OK;
 }
 
+
+// fused policy step + LMPC solve: one launch (lmpc_ipm.hip prologue = policy_step_wave)
+int dart_lmpc_policy_solve_batch_dev(dart_mpc_handle* h, const dart_lmpc_policy_config* pcfg, int B,
+                                     const float* weights, const double* state, const double* u_prev,
+                                     const double* target, const double* current_k, double* obs_mean, double* obs_M2,
+                                     int32_t* obs_count, float* history, int32_t* timestep, const float* noise,
+                                     double* model_params, float* action_out, const double* prm, const double* w_warm,
+                                     double* u0, double* f, double* w_out, int32_t* status, int32_t* iters,
+                                     void* stream) {
+    if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
+    if (h->cfg.variant != DART_MPC_LMPC) return fail(h, DART_MPC_EINVAL, "handle is not an LMPC handle");
+    dartmpc::LmpcArgs a;
+    if (policy_args(pcfg, B, weights, a.pol) != DART_MPC_OK) return fail(h, DART_MPC_EINVAL, "bad policy config");
+    if (B > 0 && (!state || !u_prev || !target || !current_k || !obs_mean || !obs_M2 || !obs_count || !history ||
+                  !timestep || !noise || !model_params || !prm || !u0 || !f || !status || !iters))
+        return fail(h, DART_MPC_EINVAL, "null pointer");
+    if (B == 0) return DART_MPC_OK;
+    HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    a.pol.state = state; a.pol.target = target; a.pol.control = u_prev; a.pol.current_k = current_k;
+    a.pol.obs_mean = obs_mean; a.pol.obs_M2 = obs_M2; a.pol.obs_count = obs_count; a.pol.history = history;
+    a.pol.timestep = timestep; a.pol.noise = noise; a.pol.model_params = model_params; a.pol.action_out = action_out;
+    a.fuse_policy = 1;
+    a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter;
+    a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc;
+    a.state = state; a.u_prev = u_prev; a.pvec = nullptr; a.target = target; a.prm = prm; a.w_warm = w_warm;
+    a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
+    HIPCHK(h, dartmpc_launch_lmpc(&a, stream ? (hipStream_t)stream : h->stream), "kernel launch");
+    return DART_MPC_OK;
+}
+
+int dart_lmpc_policy_solve_batch(dart_mpc_handle* h, const dart_lmpc_policy_config* pcfg, int B, const float* weights,
+                                 const double* state, const double* u_prev, const double* target,
+                                 const double* current_k, double* obs_mean, double* obs_M2, int32_t* obs_count,
+                                 float* history, int32_t* timestep, const float* noise, double* model_params,
+                                 float* action_out, const double* prm, const double* w_warm, double* u0, double* f,
+                                 double* w_out, int32_t* status, int32_t* iters, void* stream) {
+    if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
+    if (h->cfg.variant != DART_MPC_LMPC) return fail(h, DART_MPC_EINVAL, "handle is not an LMPC handle");
+    dartmpc::PolicyArgs chk;
+    if (policy_args(pcfg, B, weights, chk) != DART_MPC_OK) return fail(h, DART_MPC_EINVAL, "bad policy config");
+    if (B > 0 && (!state || !u_prev || !target || !current_k || !obs_mean || !obs_M2 || !obs_count || !history ||
+                  !timestep || !noise || !model_params || !prm || !u0 || !f || !status || !iters))
+        return fail(h, DART_MPC_EINVAL, "null pointer");
+    if (B > h->cfg.B_max) return fail(h, DART_MPC_EINVAL, "batch larger than B_max");
+    if (B == 0) return DART_MPC_OK;
+    HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    const size_t nw = (size_t)dart_lmpc_nw(h->cfg.N), Bz = (size_t)B;
+    HostStage& S = h->st;
+    const size_t nin = sizeof(float) * ((size_t)DART_LMPC_POLICY_NWEIGHTS + Bz * (34 + 520)) +
+                       sizeof(double) * Bz * (8 + 2 + 8 + 34 + dartmpc::LM_NPRM + nw + 52 + 52 + 34) +
+                       sizeof(int32_t) * 2 * Bz + 24 * 256;
+    const size_t nout = sizeof(double) * Bz * (2 + 1 + nw) + sizeof(int32_t) * 2 * Bz + sizeof(float) * 34 * Bz + 8 * 256;
+    HIPCHK(h, S.reserve(nin, nout), "staging buffers");
+    S.begin();
+    const float* d_w = S.in(weights, (size_t)DART_LMPC_POLICY_NWEIGHTS);
+    const double* d_st0 = S.in(state, 8 * Bz);
+    const double* d_up = S.in(u_prev, 2 * Bz);
+    const double* d_tg = S.in(target, 8 * Bz);
+    const double* d_ck = S.in(current_k, 34 * Bz);
+    const float* d_nz = S.in(noise, 34 * Bz);
+    const double* d_prm = S.in(prm, dartmpc::LM_NPRM * Bz);
+    const double* d_ww = S.in(w_warm, nw * Bz);
+    double* d_mean = S.inout(obs_mean, 52 * Bz);
+    double* d_M2 = S.inout(obs_M2, 52 * Bz);
+    double* d_mp = S.inout(model_params, 34 * Bz);
+    float* d_hist = S.inout(history, 520 * Bz);
+    int32_t* d_cnt = S.inout(obs_count, Bz);
+    int32_t* d_ts = S.inout(timestep, Bz);
+    double* d_u0 = S.out<double>(2 * Bz);
+    double* d_f = S.out<double>(Bz);
+    double* d_wo = w_out ? S.out<double>(nw * Bz) : nullptr;
+    int32_t* d_stt = S.out<int32_t>(Bz);
+    int32_t* d_it = S.out<int32_t>(Bz);
+    float* d_act = action_out ? S.out<float>(34 * Bz) : nullptr;
+    HIPCHK(h, S.upload(s), "copy inputs");
+    int rc = dart_lmpc_policy_solve_batch_dev(h, pcfg, B, d_w, d_st0, d_up, d_tg, d_ck, d_mean, d_M2, d_cnt, d_hist, d_ts,
+                                              d_nz, d_mp, d_act, d_prm, d_ww, d_u0, d_f, d_wo, d_stt, d_it, s);
+    if (rc) return rc;
+    HIPCHK(h, S.download_inout(s), "copy policy state");
+    HIPCHK(h, hipStreamSynchronize(s), "hipStreamSynchronize");
+    S.finish_inout();
+    S.take(u0, d_u0, 2 * Bz); S.take(f, d_f, Bz); S.take(w_out, d_wo, nw * Bz);
+    S.take(status, d_stt, Bz); S.take(iters, d_it, Bz); S.take(action_out, d_act, 34 * Bz);
+    return DART_MPC_OK;
+}
 
 int dart_rls_update_batch_dev(int B, double* theta, double* P, const double* phi, const double* y, double lambda,
                               void* stream) {

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "lmpc_policy.h"
+
 namespace dartmpc {
 
 constexpr int LM_NPRM = 22;   // [Q(8), Qt(8), R(4), u_lo, u_hi]
@@ -25,6 +27,10 @@ struct LmpcArgs {
     double* w_out;           // [B][8(N+1)+2N] nullable
     int32_t* status;         // [B]
     int32_t* iters;          // [B]
+    // fused policy + solve (dart_lmpc_policy_solve_batch): every instance first runs its policy step
+    // (policy_step_wave) and solves with the parameters it leaves in pol.model_params; pvec unused
+    int fuse_policy;
+    PolicyArgs pol;
 };
 
 }  // namespace dartmpc

@@ -4,7 +4,8 @@
 // :239-491 with the model safe_dynamics :260-429 (index map :301-344), RK4 :431-436, cost
 // :444-464 (Q, Qt on the state error, R on [u; Delta u]), U box, and IPOPT's options
 // (:480-489: max_iter, tol, acceptable_tol, acceptable_iter; the 0.05 s wall-clock cap is not
-// reproduced: the solve is deterministic here).  The 34-vector pvec is an input.
+// reproduced: the solve is deterministic here).  The 34-vector pvec is an input, or, in the fused
+// launch (dart_lmpc_policy_solve_batch), the output of the policy step run as the kernel's prologue.
 //
 // Separable structure: safe_dynamics never mixes the two horizontal directions -- [px, vx,
 // theta_y, omega_y] are driven by tilt a alone (sliding friction, rolling slip vx - r_x omega_y,
@@ -71,6 +72,10 @@ struct LmShared {
     LmSub sub[2];                   // uniform problem data of the two halves
     double W[2][2][4], tg[2][4], st0[2][4];   // [half][stage, terminal] weights, target, x_0 (local order)
 };
+
+// dynamic LDS: LmShared, then (fused launches) the policy step's PolicyLds
+constexpr size_t kLmPolicyLdsOff = (sizeof(LmShared) + 15) & ~size_t(15);
+constexpr size_t kLmLdsBytes = kLmPolicyLdsOff + sizeof(PolicyLds);
 
 __device__ __forceinline__ double sq(double p) { return fabs(p) + 1e-6; }   // squash_param :296-298
 
@@ -291,6 +296,14 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     const int k = lane & 31;                   // shooting node
     const int sl = hf * LM_NMAXS + k;          // node slot of this lane (every lane owns one)
     const int N = a.N;
+    // fused policy step (C5: the learned parameter net in the same launch as the shooting defects it
+    // parameterises): its LDS sits after LmShared, its output vector is this solve's pvec
+    const double* pvec = a.fuse_policy ? nullptr : a.pvec + LM_NPV * b;
+    if (a.fuse_policy) {
+        PolicyLds& PL = *reinterpret_cast<PolicyLds*>(smem + kLmPolicyLdsOff);
+        policy_step_wave(a.pol, b, PL);
+        pvec = PL.pv;
+    }
     const bool xon = k <= N, uon = k < N;
     constexpr int NC = LmLds::NC;
     // full-state index of the subsystem's local state i
@@ -299,7 +312,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     // ---------------- model parameters (uniform per half, staged in LDS) -----------------------
     if (lane == 0 || lane == 32) {
         LmSub& m = SH.sub[hf];
-        const double* p = a.pvec + LM_NPV * b;
+        const double* p = pvec;
         const double m_x = sq(p[0]), m_y = sq(p[1]);
         if (hf == 0) {     // x: m_x, c_x, k_x, Stribeck x, I_y, r_x, c_rot_y, rotational Stribeck y, h_com_y
             m.m = m_x; m.c = sq(p[2]); m.k = sq(p[4]);
@@ -828,7 +841,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
 
 }  // namespace dartmpc
 
-extern "C" size_t dartmpc_lmpc_lds_bytes(void) { return sizeof(dartmpc::LmShared); }
+extern "C" size_t dartmpc_lmpc_lds_bytes(void) { return dartmpc::kLmLdsBytes; }
 
 extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStream_t stream) {
     if (args->B <= 0) return hipSuccess;
@@ -836,7 +849,7 @@ extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStre
     // the dynamic-LDS opt-in is per device: set once for every device a launch goes to (thread-safe)
     static std::mutex mu;
     static bool attr_set[64] = {};
-    const size_t lds = sizeof(dartmpc::LmShared);
+    const size_t lds = dartmpc::kLmLdsBytes;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;

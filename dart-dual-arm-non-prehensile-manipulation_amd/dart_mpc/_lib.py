@@ -30,10 +30,11 @@ EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch",
            "dart_rls_update_batch", "dart_rls_update_batch_dev",
            "dart_lmpc_solve_batch", "dart_lmpc_solve_batch_dev", "dart_lmpc_nw",
            "dart_lmpc_policy_config_default", "dart_lmpc_policy_step", "dart_lmpc_policy_step_dev",
+           "dart_lmpc_policy_solve_batch", "dart_lmpc_policy_solve_batch_dev",
            "dart_arm_config_default", "dart_arm_snapshot_len", "dart_arm_param_len", "dart_arm_solve_batch",
            "dart_arm_solve_batch_dev")
 VARIANT_PMPC, VARIANT_RMPC, VARIANT_LMPC = 0, 1, 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class DartMPCError(RuntimeError):
@@ -117,6 +118,11 @@ def lib():
     L.dart_lmpc_policy_step.restype = ctypes.c_int
     L.dart_lmpc_policy_step_dev.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 14
     L.dart_lmpc_policy_step_dev.restype = ctypes.c_int
+    psig = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 21
+    L.dart_lmpc_policy_solve_batch.argtypes = psig
+    L.dart_lmpc_policy_solve_batch.restype = ctypes.c_int
+    L.dart_lmpc_policy_solve_batch_dev.argtypes = psig
+    L.dart_lmpc_policy_solve_batch_dev.restype = ctypes.c_int
     L.dart_rls_update_batch.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_double]
     L.dart_rls_update_batch.restype = ctypes.c_int
     L.dart_rls_update_batch_dev.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_double, ctypes.c_void_p]
@@ -328,6 +334,18 @@ class LmpcSolver(Solver):
                                              w_out or None, status, iters, stream or None)
         if rc != 0:
             self._err(rc, "dart_lmpc_solve_batch_dev")
+
+    def policy_solve_batch_dev(self, pcfg, B, weights, state, u_prev, target, current_k, obs_mean, obs_M2, obs_count,
+                               history, timestep, noise, model_params, prm, u0, f, status, iters, action_out=0,
+                               w_warm=0, w_out=0, stream=0):
+        """Fused policy step + solve (dart_lmpc_policy_solve_batch_dev), device pointers, asynchronous;
+        ``pcfg`` is a ``dart_mpc.lmpc.PolicyConfig``."""
+        rc = lib().dart_lmpc_policy_solve_batch_dev(
+            self._h, ctypes.byref(pcfg), int(B), weights, state, u_prev, target, current_k, obs_mean, obs_M2, obs_count,
+            history, timestep, noise, model_params, action_out or None, prm, w_warm or None, u0, f, w_out or None,
+            status, iters, stream or None)
+        if rc != 0:
+            self._err(rc, "dart_lmpc_policy_solve_batch_dev")
 
 
 def rls_update_batch(theta, P, phi, y, lam=0.995):

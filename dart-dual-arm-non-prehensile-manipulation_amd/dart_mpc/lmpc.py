@@ -9,7 +9,9 @@ Mirrors LMPC/src/controller/rlmpc2.py:
   - ``RLMPC``: ``RLMPC.solve(target)`` (:986-1021) run synchronously: state from MjData, one
     policy step producing pvec, one warm-started LMPC solve (the worker loop :494-524), returns
     ``(U_opt[0], loss)``.  The reference runs the three parts in separate processes; here they
-    are two launches on one stream.
+    are one launch (``dart_lmpc_policy_solve_batch``: the policy step is the prologue of the
+    solve kernel), or two launches on one stream with ``fused=False``.
+  - ``policy_solve_batch``: the fused policy step + solve for B controllers.
 """
 from __future__ import annotations
 
@@ -101,10 +103,38 @@ class LmpcPolicy:
         return act
 
 
+def policy_solve_batch(solver: LmpcSolver, policy: LmpcPolicy, state, u_prev, target, prm=None, w_warm=None,
+                       want_w=False, noise=None, rng=None):
+    """One LMPC control step for ``policy.B`` controllers in ONE launch: the policy step (control =
+    u_prev, :650 / :505) updates the policy state and ``policy.model_params``, then the solve uses
+    those parameters as pvec (:506).  Same results as ``policy.step`` followed by
+    ``solver.solve_batch``.  Returns the solve dict plus ``action`` (raw actions [B, 34])."""
+    B = policy.B
+    c = lambda a, n: np.ascontiguousarray(a, np.float64).reshape(B, n)
+    state, u_prev, target = c(state, 8), c(u_prev, 2), c(target, 8)
+    prm = c(np.tile(LMPC_PRM_DEFAULT, (B, 1)) if prm is None else prm, 22)
+    ww = None if w_warm is None else c(w_warm, solver.nw)
+    if noise is None:
+        noise = (rng or np.random.default_rng()).standard_normal((B, PA))
+    noise = np.ascontiguousarray(noise, np.float32).reshape(B, PA)
+    act = np.empty((B, PA), np.float32)
+    u0 = np.empty((B, 2)); f = np.empty(B)
+    w = np.empty((B, solver.nw)) if want_w else None
+    st = np.empty(B, np.int32); it = np.empty(B, np.int32)
+    rc = lib().dart_lmpc_policy_solve_batch(
+        solver._h, ctypes.byref(policy.cfg), B, _ptr(policy.weights), _ptr(state), _ptr(u_prev), _ptr(target),
+        _ptr(policy.current_k), _ptr(policy.obs_mean), _ptr(policy.obs_M2), _ptr(policy.obs_count),
+        _ptr(policy.history), _ptr(policy.timestep), _ptr(noise), _ptr(policy.model_params), _ptr(act), _ptr(prm),
+        _ptr(ww), _ptr(u0), _ptr(f), _ptr(w), _ptr(st), _ptr(it), None)
+    if rc != 0:
+        solver._err(rc, "dart_lmpc_policy_solve_batch")
+    return dict(u0=u0, f=f, w=w, status=st, iters=it, action=act)
+
+
 class RLMPC:
     """Front-end of RLMPC (:110-226, :986-1021) with the solver and policy on the GPU."""
 
-    def __init__(self, model=None, data=None, params=None, *, policy_weights=None, seed=0, device=0):
+    def __init__(self, model=None, data=None, params=None, *, policy_weights=None, seed=0, device=0, fused=True):
         p = dict(Ts=0.002, nx=8, nu=2, N=20, Q=LMPC_PRM_DEFAULT[:8], Qt=LMPC_PRM_DEFAULT[8:16], R=LMPC_PRM_DEFAULT[16:20],
                  u_bounds=tuple(LMPC_PRM_DEFAULT[20:22]), body_name="cube2", max_param_abs=2.0, max_delta_abs=0.02)
         p.update(params or {})
@@ -121,6 +151,7 @@ class RLMPC:
         self.last_control = np.zeros(2)
         self.loss = np.zeros(1)
         self._rng = np.random.default_rng(seed + 2)
+        self.fused = bool(fused)
 
     def get_state(self):
         """[px, vx, py, vy, theta_x, omega_x, theta_y, omega_y] (:1034-1042)."""
@@ -133,9 +164,14 @@ class RLMPC:
 
     def solve(self, target, state=None):
         state = self.get_state() if state is None else np.asarray(state, float)
-        self.policy.step(state, target, self.last_control, rng=self._rng)
-        out = self.solver.solve_batch(state[None], self.last_control[None], self.policy.model_params,
-                                      np.asarray(target, float)[None], self.prm, w_warm=self.w0[None], want_w=True)
+        tg = np.asarray(target, float)[None]
+        if self.fused:
+            out = policy_solve_batch(self.solver, self.policy, state[None], self.last_control[None], tg, self.prm,
+                                     w_warm=self.w0[None], want_w=True, rng=self._rng)
+        else:
+            self.policy.step(state, target, self.last_control, rng=self._rng)
+            out = self.solver.solve_batch(state[None], self.last_control[None], self.policy.model_params, tg,
+                                          self.prm, w_warm=self.w0[None], want_w=True)
         self.w0 = out["w"][0]
         self.loss = out["f"].copy()
         self.last_control = out["u0"][0].copy()

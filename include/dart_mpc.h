@@ -19,6 +19,9 @@
  *                             and warm start :510-520), fed by RLMPC.solve :986-1021
  *   dart_lmpc_policy_step(_dev) <- the inference / parameter-write half of RLMPC._rl_worker
  *                             rlmpc2.py:537-769 (Policy :33-80, write_params_to_shm :606-616)
+ *   dart_lmpc_policy_solve_batch(_dev) <- one control step of the LMPC stack: the policy step
+ *                             above, then the solve with the parameters it wrote
+ *                             (views["model_params"], rlmpc2.py:506-515), in ONE launch
  *   dart_arm_solve_batch(_dev) <- ARMCONTROL.solver_worker, the per-arm impedance QP
  *                             PMPC/src/controller/arm.py:266-457 (same code in
  *                             RMPC/dev_dual/controller/parallel.py, LMPC/src/controller/parallel.py),
@@ -60,7 +63,7 @@
 extern "C" {
 #endif
 
-#define DART_MPC_ABI_VERSION 3
+#define DART_MPC_ABI_VERSION 4
 
 enum dart_mpc_variant {
     DART_MPC_PMPC = 0,      /* PMPC/src/controller/mpc_3d.py, N <= 63 */
@@ -225,6 +228,33 @@ int dart_lmpc_policy_step(const dart_lmpc_policy_config *cfg, int B, const float
                           const double *current_k, double *obs_mean, double *obs_M2, int32_t *obs_count,
                           float *history, int32_t *timestep, const float *noise, double *model_params,
                           float *action_out);
+
+/* Fused LMPC control step (handle of variant DART_MPC_LMPC): for every instance, the policy
+ * step of dart_lmpc_policy_step with control = u_prev (views["control"] is both the policy's
+ * observation input, rlmpc2.py:650, and the solver's u_prev, :505), then the LMPC solve of
+ * dart_lmpc_solve_batch with pvec = the model_params the step leaves behind (:506) -- one
+ * kernel launch; the learned parameter net runs in the prologue of the kernel that evaluates the
+ * shooting defects it parameterises (BASELINE.json config C5).  Results equal a policy step
+ * followed by a solve.  Policy state arrays (obs_mean, obs_M2, obs_count, history, timestep,
+ * model_params) are in/out as in dart_lmpc_policy_step; action_out nullable. */
+int dart_lmpc_policy_solve_batch_dev(dart_mpc_handle *h, const dart_lmpc_policy_config *pcfg, int B,
+                                     const float *weights, const double *state, const double *u_prev,
+                                     const double *target, const double *current_k, double *obs_mean,
+                                     double *obs_M2, int32_t *obs_count, float *history, int32_t *timestep,
+                                     const float *noise, double *model_params, float *action_out,
+                                     const double *prm, const double *w_warm,
+                                     double *u0, double *f, double *w_out,
+                                     int32_t *status, int32_t *iters, void *hip_stream);
+
+/* Host pointers (stages through the handle's pinned buffers and blocks). */
+int dart_lmpc_policy_solve_batch(dart_mpc_handle *h, const dart_lmpc_policy_config *pcfg, int B,
+                                 const float *weights, const double *state, const double *u_prev,
+                                 const double *target, const double *current_k, double *obs_mean,
+                                 double *obs_M2, int32_t *obs_count, float *history, int32_t *timestep,
+                                 const float *noise, double *model_params, float *action_out,
+                                 const double *prm, const double *w_warm,
+                                 double *u0, double *f, double *w_out,
+                                 int32_t *status, int32_t *iters, void *hip_stream);
 
 /* Batched standalone RLS.update (np_mpc...:17-27) for B independent p = 7 filters:
  * theta [B][7] and P [B][7][7] updated in place with regressors phi [B][7], targets y [B],

@@ -53,3 +53,61 @@ def test_rlmpc_front_end_step():
         w0 = o["w"][0]; uprev = o["u0"][0]
         assert np.allclose(ctl.policy.model_params[0], st.model_params, atol=1e-6)
         assert np.max(np.abs(out["u0"][0] - o["u0"][0])) <= 1e-6, k
+
+
+def test_fused_policy_solve_equals_policy_step_then_solve():
+    """dart_lmpc_policy_solve_batch (policy step as the prologue of the solve launch, C5) against the
+    two-launch chain on the same inputs over 10 steps (the logit update fires at steps 0 and 8):
+    every output and every piece of policy state bit for bit."""
+    import dart_mpc
+    B, T, N = 6, 10, 20
+    rng = np.random.default_rng(21)
+    fa, fb = dart_mpc.LmpcPolicy(B, seed=3), dart_mpc.LmpcPolicy(B, seed=3)
+    sa = dart_mpc.LmpcSolver(N=N, B_max=B)
+    sb = dart_mpc.LmpcSolver(N=N, B_max=B)
+    wa = wb = None
+    up = np.zeros((B, 2))
+    for t in range(T):
+        state = np.concatenate([rng.uniform(-0.1, 0.1, (B, 4)), rng.uniform(-0.05, 0.05, (B, 4))], axis=1)
+        target = np.zeros((B, 8)); target[:, 0] = rng.uniform(-0.1, 0.1, B); target[:, 2] = rng.uniform(-0.1, 0.1, B)
+        eps = rng.standard_normal((B, 34)).astype(np.float32)
+        oa = dart_mpc.policy_solve_batch(sa, fa, state, up, target, w_warm=wa, want_w=True, noise=eps)
+        act = fb.step(state, target, up, noise=eps)
+        ob = sb.solve_batch(state, up, fb.model_params, target, w_warm=wb, want_w=True)
+        for k in ("u0", "f", "w", "status", "iters"):
+            assert np.array_equal(oa[k], ob[k]), (t, k)
+        assert np.array_equal(oa["action"], act), t
+        for k in ("model_params", "obs_mean", "obs_M2", "obs_count", "history", "timestep"):
+            assert np.array_equal(getattr(fa, k), getattr(fb, k)), (t, k)
+        wa, wb, up = oa["w"], ob["w"], oa["u0"]
+
+
+def test_rlmpc_fused_front_end_matches_oracle_chain():
+    """RLMPC.solve with the fused launch (the default) against the restated policy + C solver chain."""
+    import dart_mpc
+    ctl = dart_mpc.RLMPC(None, None, dict(N=20), seed=4)
+    assert ctl.fused
+    st = lp.PolicyState(ctl.policy.current_k[0])
+    rng = np.random.default_rng(9)
+    state = np.array([0.02, 0.0, -0.01, 0.0, 0.0, 0.0, 0.0, 0.0]); target = np.array([0.1, 0, -0.05, 0, 0, 0, 0, 0])
+    w0 = np.zeros(8 * 21 + 40); uprev = np.zeros(2)
+    for k in range(4):
+        eps = rng.standard_normal(34).astype(np.float32)
+        ctl._rng = _FixedNormal(eps)
+        u, loss = ctl.solve(target, state=state)
+        lp.policy_step(st, ctl.policy.weights, state, target, uprev, eps)
+        o = oracle_lib.lmpc_solve_batch(state[None], uprev[None], st.model_params[None], target[None], N=20,
+                                        w_init=w0[None], soc=False)
+        w0 = o["w"][0]; uprev = o["u0"][0]
+        assert np.allclose(ctl.policy.model_params[0], st.model_params, atol=1e-6)
+        assert np.max(np.abs(u - o["u0"][0])) <= 1e-6, k
+
+
+class _FixedNormal:
+    """Stand-in for the front-end's generator: hands out the given standard-normal draws."""
+
+    def __init__(self, eps):
+        self.eps = eps
+
+    def standard_normal(self, shape):
+        return np.asarray(self.eps, np.float32).reshape(shape)
