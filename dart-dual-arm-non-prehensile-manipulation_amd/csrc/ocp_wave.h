@@ -60,6 +60,7 @@ struct OcpLds {
     NodeArr<double[NXA][NF], NMAXS> F;        // closed loop: F[k][r] = [Phi_k(r, :) | f_k(r)]
     NodeArr<double[NXA][NF], NMAXS / 2> F2;   // two-node maps of nodes 2q, 2q + 1 (compose_pairs)
     double dx0[NC];                           // forward sweep start dx~_0
+    double dxs[NMAXS / 2 + 1][NF];            // forward sweep: dx~ of node 2q + 2 (slot q), odd node N (slot N / 2)
 };
 
 // Two-node closed-loop maps F2[q] = [Phi_{2q+1} Phi_{2q} | Phi_{2q+1} f_{2q} + f_{2q+1}] of every
@@ -274,52 +275,94 @@ __device__ __forceinline__ void node_multiplier(const L* S, int k, const double*
     }
 }
 
+// One step of a paired forward chain: s = row r of F [d; 1], parked (every lane of a row holds the
+// same s; all lanes store, no EXEC masking), then broadcast within the row into d.
+template <int NXA>
+__device__ __forceinline__ void pair_step(const double* F, double* d, double* park) {
+    double s0 = F[NXA], s1 = 0.0;       // two accumulators: half the dependent FMA depth
+#pragma unroll
+    for (int j = 0; j < NXA; j += 2) {
+        s0 = fma(F[j], d[j], s0);
+        if (j + 1 < NXA) s1 = fma(F[j + 1], d[j + 1], s1);
+    }
+    const double s = s0 + s1;
+    *park = s;
+#pragma unroll
+    for (int i = 0; i < NXA; ++i) d[i] = row_bcast_over(s, i, d[i]);
+}
+
+// The chain over the np2 pair maps of one half (pair slots p0 .. p0 + np2 - 1, row r), two pairs per
+// trip with ping-pong rows: the rows of the next pair are loaded before the current step and held
+// in registers across it (PREFETCH; the empty asm keeps the compiler from sinking the loads into the
+// next step, where every step would wait out an LDS latency), else loaded when needed.
+template <int NXA, bool PREFETCH, class F2A, class PA>
+__device__ __forceinline__ void pair_chain(const F2A& F2, int p0, int np2, int r, double* d, PA park) {
+    double Fa[NXA + 1], Fb[NXA + 1];
+#pragma unroll
+    for (int j = 0; j <= NXA; ++j) Fa[j] = F2[p0][r][j];
+    for (int q = 0; q < np2; q += 2) {
+        const bool two = q + 1 < np2;
+        if constexpr (PREFETCH) {
+#pragma unroll
+            for (int j = 0; j <= NXA; ++j) Fb[j] = F2[p0 + (two ? q + 1 : q)][r][j];
+        }
+        pair_step<NXA>(Fa, d, park(q));
+        if (!two) break;
+        if constexpr (PREFETCH) {
+#pragma unroll
+            for (int j = 0; j <= NXA; ++j) asm volatile("" : "+v"(Fb[j]));
+            const int qn = q + 2 < np2 ? q + 2 : q + 1;
+#pragma unroll
+            for (int j = 0; j <= NXA; ++j) Fa[j] = F2[p0 + qn][r][j];
+        } else {
+#pragma unroll
+            for (int j = 0; j <= NXA; ++j) Fb[j] = F2[p0 + q + 1][r][j];
+        }
+        pair_step<NXA>(Fb, d, park(q + 1));
+        if constexpr (PREFETCH) {
+#pragma unroll
+            for (int j = 0; j <= NXA; ++j) asm volatile("" : "+v"(Fa[j]));
+        } else if (q + 2 < np2) {
+#pragma unroll
+            for (int j = 0; j <= NXA; ++j) Fa[j] = F2[p0 + q + 2][r][j];
+        }
+    }
+}
+
 // Forward sweep over node pairs: lane 16 w + r (r < NXA) of every row w owns row r of the two-node
 // chain dx~_{2q+2} = F2[q] [dx~_{2q}; 1] -- the four rows run the same chain, so each row
-// broadcasts the new state to itself by 64-bit DPP row_newbcast (no scalar round trip) -- and
-// the rows of the next pair are prefetched while this one is processed.  An odd N ends with one
-// single-node step; the odd nodes in between follow afterwards, lane per node, from their even
-// predecessor (off the chain).  Lane-per-node use: every lane returns in dxo the state step of
-// node `node` = its lane (node > N keeps dx~_0).  S->dx0 must hold dx~_0; compose_pairs must have run.
-template <class L>
+// broadcasts the new state to itself by 64-bit DPP row_newbcast (no scalar round trip).  The rows of
+// pair q + 1 are loaded while pair q is processed (held in registers across the step by an empty asm,
+// or the compiler sinks the loads into the next step and every step waits out an LDS latency), and
+// row 0 parks each new state in S->dxs instead of every lane selecting it into its own slot.  An odd
+// N ends with one single-node step; the odd nodes in between follow afterwards, lane per node, from
+// their even predecessor (off the chain).  Lane-per-node use: every lane returns in dxo the state step
+// of node `node` = its lane (node > N keeps dx~_0).  S->dx0 must hold dx~_0; compose_pairs must have
+// run.  Ends with a barrier.
+template <class L, bool PREFETCH = true>
 __device__ void forward_sweep(L* S, int N, int node, double* dxo) {
     constexpr int NXA = L::NXA;
     const int lr = threadIdx.x & 15;
     const int r = lr < NXA ? lr : 0;
     double d[NXA];
 #pragma unroll
-    for (int i = 0; i < NXA; ++i) { d[i] = S->dx0[i]; dxo[i] = d[i]; }
+    for (int i = 0; i < NXA; ++i) d[i] = S->dx0[i];
     const int np2 = N >> 1;
-    double Fc[NXA + 1];
-#pragma unroll
-    for (int j = 0; j <= NXA; ++j) Fc[j] = S->F2[0][r][j];
-    for (int q = 0; q < np2; ++q) {
-        double Fn[NXA + 1];
-        const int qn = q + 1 < np2 ? q + 1 : q;
-#pragma unroll
-        for (int j = 0; j <= NXA; ++j) Fn[j] = S->F2[qn][r][j];
-        double s0 = Fc[NXA], s1 = 0.0;       // two accumulators: half the dependent FMA depth
-#pragma unroll
-        for (int j = 0; j < NXA; j += 2) {
-            s0 = fma(Fc[j], d[j], s0);
-            if (j + 1 < NXA) s1 = fma(Fc[j + 1], d[j + 1], s1);
-        }
-        const double s = s0 + s1;
-        const bool m = node == 2 * q + 2;
-#pragma unroll
-        for (int i = 0; i < NXA; ++i) { d[i] = row_bcast(s, i); dxo[i] = m ? d[i] : dxo[i]; }
-#pragma unroll
-        for (int j = 0; j <= NXA; ++j) Fc[j] = Fn[j];
-    }
+    pair_chain<NXA, PREFETCH>(S->F2, 0, np2, r, d, [&](int q) { return &S->dxs[q][r]; });
     if (N & 1) {
         const double* row = S->F[N - 1][r];
         double s = row[NXA];
 #pragma unroll
         for (int j = 0; j < NXA; ++j) s = fma(row[j], d[j], s);
-        const bool m = node == N;
-#pragma unroll
-        for (int i = 0; i < NXA; ++i) { d[i] = row_bcast(s, i); dxo[i] = m ? d[i] : dxo[i]; }
+        S->dxs[np2][r] = s;
     }
+    __syncthreads();
+    // even nodes 2 .. 2 np2 and an odd terminal node from the parked states, node 0 from dx~_0
+    const bool even_n = !(node & 1) && node >= 2 && node <= 2 * np2;
+    const bool odd_end = (N & 1) && node == N;
+    const int slot = even_n ? (node >> 1) - 1 : np2;
+#pragma unroll
+    for (int i = 0; i < NXA; ++i) dxo[i] = (even_n || odd_end) ? S->dxs[slot][i] : S->dx0[i];
     double pv[NXA];
 #pragma unroll
     for (int i = 0; i < NXA; ++i) pv[i] = from_prev(dxo[i]);
@@ -358,6 +401,7 @@ struct OcpLdsS {
     NodeArr<double[NXA][NF], 2 * NMAXS> F;    // closed loop rows [Phi_k(r, :) | f_k(r)]
     NodeArr<double[NXA][NF], NMAXS> F2;       // two-node maps, pair slot (NMAXS / 2) h + q (compose_pairs)
     double dx0[2][NC];                        // forward sweep start of each half
+    double dxs[2][NMAXS / 2 + 1][NF];         // forward sweep of each half: dx~ of node 2q + 2 (slot q), odd node N
 };
 
 template <int NXA>
@@ -481,10 +525,12 @@ __device__ __forceinline__ void node_multiplier_s(const L* S, int sl, const doub
 
 // Forward sweep of both halves over node pairs: lane 16 w + r (r < NXA) owns row r of the two-node
 // chain dx~_{2q+2} = F2 [dx~_{2q}; 1] of half h = w / 2 (both rows of a half run it, so each row
-// broadcasts the new state to itself by 64-bit DPP row_newbcast).  An odd N ends with one
-// single-node step; the odd nodes in between follow afterwards, lane per node, from their even
-// predecessor.  Every lane returns in dxo the step of node `node` (= lane & 31) of its half.
-template <class L>
+// broadcasts the new state to itself by 64-bit DPP row_newbcast); the next pair's rows are loaded
+// during the step and rows 0 / 2 park each new state in S->dxs (as forward_sweep).  An odd N ends with
+// one single-node step; the odd nodes in between follow afterwards, lane per node, from their even
+// predecessor.  Every lane returns in dxo the step of node `node` (= lane & 31) of its half.  Ends
+// with a barrier.
+template <class L, bool PREFETCH = true>
 __device__ void forward_sweep_s(L* S, int N, int node, double* dxo) {
     constexpr int NXA = L::NXA;
     const int h = threadIdx.x >> 5, base = h * L::NMAXS, pbase = h * (L::NMAXS / 2);
@@ -492,38 +538,22 @@ __device__ void forward_sweep_s(L* S, int N, int node, double* dxo) {
     const int r = lr < NXA ? lr : 0;
     double d[NXA];
 #pragma unroll
-    for (int i = 0; i < NXA; ++i) { d[i] = S->dx0[h][i]; dxo[i] = d[i]; }
+    for (int i = 0; i < NXA; ++i) d[i] = S->dx0[h][i];
     const int np2 = N >> 1;
-    double Fc[NXA + 1];
-#pragma unroll
-    for (int j = 0; j <= NXA; ++j) Fc[j] = S->F2[pbase][r][j];
-    for (int q = 0; q < np2; ++q) {
-        double Fn[NXA + 1];
-        const int qn = q + 1 < np2 ? q + 1 : q;
-#pragma unroll
-        for (int j = 0; j <= NXA; ++j) Fn[j] = S->F2[pbase + qn][r][j];
-        double s0 = Fc[NXA], s1 = 0.0;
-#pragma unroll
-        for (int j = 0; j < NXA; j += 2) {
-            s0 = fma(Fc[j], d[j], s0);
-            if (j + 1 < NXA) s1 = fma(Fc[j + 1], d[j + 1], s1);
-        }
-        const double s = s0 + s1;
-        const bool m = node == 2 * q + 2;
-#pragma unroll
-        for (int i = 0; i < NXA; ++i) { d[i] = row_bcast(s, i); dxo[i] = m ? d[i] : dxo[i]; }
-#pragma unroll
-        for (int j = 0; j <= NXA; ++j) Fc[j] = Fn[j];
-    }
+    pair_chain<NXA, PREFETCH>(S->F2, pbase, np2, r, d, [&](int q) { return &S->dxs[h][q][r]; });
     if (N & 1) {
         const double* row = S->F[base + N - 1][r];
         double s = row[NXA];
 #pragma unroll
         for (int j = 0; j < NXA; ++j) s = fma(row[j], d[j], s);
-        const bool m = node == N;
-#pragma unroll
-        for (int i = 0; i < NXA; ++i) { d[i] = row_bcast(s, i); dxo[i] = m ? d[i] : dxo[i]; }
+        S->dxs[h][np2][r] = s;
     }
+    __syncthreads();
+    const bool even_n = !(node & 1) && node >= 2 && node <= 2 * np2;
+    const bool odd_end = (N & 1) && node == N;
+    const int slot = even_n ? (node >> 1) - 1 : np2;
+#pragma unroll
+    for (int i = 0; i < NXA; ++i) dxo[i] = (even_n || odd_end) ? S->dxs[h][slot][i] : S->dx0[h][i];
     double pv[NXA];
 #pragma unroll
     for (int i = 0; i < NXA; ++i) pv[i] = from_prev(dxo[i]);

@@ -32,6 +32,25 @@ template <int I>
 __device__ __forceinline__ double row_bcast(double x) {
     return __builtin_amdgcn_update_dpp(0.0, x, 0x150 + I, 0xf, 0xf, false);
 }
+// the same with the destination's dead previous value as the DPP "old" operand: every lane reads a
+// valid source under row_newbcast, so old never shows, and tying it to the destination spares the
+// initialising move that an explicit old value costs
+template <int I>
+__device__ __forceinline__ double row_bcast_over(double x, double dead) {
+    return __builtin_amdgcn_update_dpp(dead, x, 0x150 + I, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double row_bcast_over(double x, int i, double dead) {
+    switch (i) {       // i (< 8) is a compile-time constant at every (unrolled) call site
+        case 0: return row_bcast_over<0>(x, dead);
+        case 1: return row_bcast_over<1>(x, dead);
+        case 2: return row_bcast_over<2>(x, dead);
+        case 3: return row_bcast_over<3>(x, dead);
+        case 4: return row_bcast_over<4>(x, dead);
+        case 5: return row_bcast_over<5>(x, dead);
+        case 6: return row_bcast_over<6>(x, dead);
+        default: return row_bcast_over<7>(x, dead);
+    }
+}
 __device__ __forceinline__ double row_bcast(double x, int i) {
     switch (i) {       // i (< 8) is a compile-time constant at every (unrolled) call site
         case 0: return row_bcast<0>(x);
