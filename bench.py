@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--host-calls", type=int, default=200, help="calls of the host-pointer (PCIe-inclusive) path")
     ap.add_argument("--rmpc-steps", type=int, default=200, help="launches of the supplementary C3 RMPC line (0 = skip)")
     ap.add_argument("--lmpc-steps", type=int, default=100, help="launches of the supplementary C5 LMPC line (0 = skip)")
+    ap.add_argument("--lmpc-policy-steps", type=int, default=100,
+                    help="launches of the supplementary C5 line with the policy step fused into the launch (0 = skip)")
     ap.add_argument("--arm-steps", type=int, default=200, help="launches of the supplementary arm-QP line (0 = skip)")
     ap.add_argument("--n15-steps", type=int, default=200,
                     help="launches of the supplementary PMPC line at the driver's horizon N=15 (0 = skip)")
@@ -349,7 +351,7 @@ def bench_lmpc_policy(args, torch, dev, stream, dart_mpc):
     from dart_mpc.lmpc import NWEIGHTS, PolicyConfig, init_policy_weights, policy_config  # noqa: F401
     from dart_mpc.workload import lmpc_batch
     from dart_mpc._lib import LMPC_PRM_DEFAULT, lib
-    B, K, N = 18, args.lmpc_steps, 30
+    B, K, N = 18, args.lmpc_policy_steps, 30
     D = [lmpc_batch(1, seed0=7000 + i) for i in range(K + 3)]
     f64 = lambda a: torch.tensor(np.asarray(a), dtype=torch.float64, device=dev).contiguous()
     ST0 = f64(np.stack([d["state"] for d in D])); TG = f64(np.stack([d["target"] for d in D]))
@@ -667,7 +669,8 @@ def main():
     lmpc = None
     if rank == 0 and args.lmpc_steps > 0:
         lmpc = bench_lmpc(args, torch, dev, stream, dart_mpc)
-        lmpc["policy_fused"] = bench_lmpc_policy(args, torch, dev, stream, dart_mpc)
+        if args.lmpc_policy_steps > 0:
+            lmpc["policy_fused"] = bench_lmpc_policy(args, torch, dev, stream, dart_mpc)
 
     # supplementary: per-arm impedance QP
     arm = None

@@ -6,7 +6,7 @@ LIBS=${1:-"libdartmpc_base.so libdartmpc.so"}
 REPS=${2:-3}
 EXTRA=${3:-"--rmpc-steps 0 --lmpc-steps 0 --arm-steps 0"}
 mkdir -p gpurun_out
-ARGS="--steps 2000 --warmup 50 --no-cpu-baseline --saturation-batch 0 --host-calls 0 --c4-steps 0 --n15-steps 0 $EXTRA"
+ARGS="--steps 2000 --warmup 50 --no-cpu-baseline --saturation-batch 0 --host-calls 0 --c4-steps 0 --n15-steps 0 --lmpc-policy-steps 0 $EXTRA"
 for r in $(seq 1 $REPS); do
   for lib in $LIBS; do
     DART_MPC_LIB=$lib timeout -k 10 180 python bench.py $ARGS > gpurun_out/ab.json 2>gpurun_out/ab.err || exit $?

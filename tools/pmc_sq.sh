@@ -9,5 +9,5 @@ export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM \
     --kernel-trace -d $OUT -o run --output-format csv -- \
     python3 bench.py --steps 30 --warmup 3 --no-cpu-baseline --saturation-batch 0 --host-calls 0 --c4-steps 0 --n15-steps 0 \
-    --rmpc-steps 30 --lmpc-steps 30 --arm-steps 30 > $OUT/bench.json 2> $OUT/err.log || exit $?
+    --rmpc-steps 30 --lmpc-steps 30 --lmpc-policy-steps 0 --arm-steps 30 > $OUT/bench.json 2> $OUT/err.log || exit $?
 echo sq_done
