@@ -56,7 +56,7 @@ _lib = None
 
 def build(verbose: bool = False) -> str:
     """Compile libdartmpc.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
-    r = subprocess.run(["make", "-C", CSRC_DIR], capture_output=not verbose, text=True)
+    r = subprocess.run(["make", "-j6", "-C", CSRC_DIR], capture_output=not verbose, text=True)
     if r.returncode != 0:
         raise DartMPCError("building libdartmpc.so failed:\n" + (r.stdout or "") + (r.stderr or ""))
     return LIB_PATH
