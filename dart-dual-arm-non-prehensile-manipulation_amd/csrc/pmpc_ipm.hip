@@ -256,7 +256,13 @@ __global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
     int status = -1, it = 0;
     STAMP(0);
 
+#ifdef DART_STAMPS
+    const unsigned long long t_loop0 = __builtin_amdgcn_s_memtime();
+#endif
     for (it = 0; it < a.max_iter; ++it) {
+#ifdef DART_STAMPS
+        if (it == 1) t_acc_[12] = __builtin_amdgcn_s_memtime() - t_loop0;      // the first iteration (cold code)
+#endif
         // -------- point quantities and optimality error (IPOPT eq. 5) ------------
         double sn[NAX], cs[NAX], isl[NAX], isu[NAX], lpn[NAX], lvn[NAX];
         double dinf = 0.0, pinf = 0.0, c0 = 0.0, cmin = 1e300, suml = 0.0, sumz = 0.0;

@@ -30,5 +30,7 @@ print(f"block0 iters={out['iters'][0]} total cycles={tot:.0f}")
 for i, n in enumerate(PHASES):
     print(f"  {n:12s} {int(st[i]):10d}  {100 * st[i] / tot:5.1f}%  per-iter {st[i] / max(1, out['iters'][0]):9.0f}")
 print(f"  scan-path Riccati passes {int(st[11])}")
+it0 = int(st[0:9].sum() - st[0] - st[8])
+print(f"  first iteration {int(st[12])} cycles, mean iteration {it0 / max(1, out['iters'][0]):.0f} cycles")
 print(f"  riccati passes {int(st[9])}, line-search trials {int(st[10])}")
 print("batch iters:", out["iters"].tolist())
