@@ -152,8 +152,12 @@ __device__ __forceinline__ void mat4_scan_level(double* T) {
 //   DART driver's default horizon is 15, main_parallel_enhanced.py:171-196)
 //   SHORT2: 16 <= N <= 23, the suffix of node 16 spans at most 8 lanes, so the quadratic scan stops
 //   after 3 in-row levels and finishes rows 0 / 2 with two 4 x 2 compositions (no 4th 4 x 4 level)
+//   Occupancy: the sequential NAX == 1 build is the throughput variant and must fit two waves per
+//   SIMD (<= 256 registers); the ILP-oriented scheduler of this file (Makefile) would otherwise spend
+//   the whole register file on one wave
 template <int NAX, bool QSCAN, bool ONEROW = false, bool SHORT2 = false>
-__global__ __launch_bounds__(kWave) void pmpc_ipm_kernel(PmpcArgs a) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu((QSCAN || NAX == 2) ? 1 : 2)))
+void pmpc_ipm_kernel(PmpcArgs a) {
     STAMP_DECL
     // small batches: the launcher deals 8 blocks per instance and only every 8th works, so all
     // instances land on one XCD (blocks go round-robin over the 8 XCDs) and share its L2 for the code
