@@ -31,10 +31,21 @@
 
 namespace dartmpc {
 
+// This file is compiled twice (Makefile): as is, it holds the scan instantiations for N > 15, the
+// launcher and the self-test; with -DPMPC_SEQ, the one-row instantiation (N <= 15) and the
+// sequential (throughput) ones behind dartmpc_launch_pmpc_seq, so that each set gets the
+// optimisation level that is fastest for it.
 #ifdef DART_STAMPS
+#ifndef PMPC_SEQ
 __device__ unsigned long long g_stamp[16];
-#endif
 #define STAMP_FLUSH(b) STAMP_FLUSH_TO(g_stamp, b)
+#else
+__device__ unsigned long long g_stamp_seq[16];
+#define STAMP_FLUSH(b) STAMP_FLUSH_TO(g_stamp_seq, b)
+#endif
+#else
+#define STAMP_FLUSH(b) STAMP_FLUSH_TO(g_stamp, b)
+#endif
 
 // ---------------------------------------------------------------------------
 // model pieces
@@ -737,6 +748,7 @@ void pmpc_ipm_kernel(PmpcArgs a) {
     STAMP_FLUSH(b);
 }
 
+#ifndef PMPC_SEQ
 // self-test of the wave primitives: out[0..63] = from_next(lane), out[64..127] = from_prev(lane),
 // out[128] = wsum(lane), out[129] = wmax(lane), out[130] = wmin(lane + 1),
 // out[131..194] = relative error of the raw v_rcp_f64 on x_i = 1.37^(i-32)*pi (diagnostic),
@@ -759,7 +771,26 @@ __global__ __launch_bounds__(kWave) void wave_selftest_kernel(double* out) {
     if (threadIdx.x == 40) out[200] = hb;
 }
 
+#endif  // PMPC_SEQ
+
 }  // namespace dartmpc
+
+#ifdef PMPC_SEQ
+// one-row scan build (onerow != 0, N <= 15), else the sequential (throughput) builds: two waves per
+// SIMD, used once B exceeds the scan limit or N > 31
+extern "C" hipError_t dartmpc_launch_pmpc_seq(const dartmpc::PmpcArgs* a, unsigned grid, hipStream_t stream,
+                                              int onerow) {
+    if (onerow)
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, true>), dim3(grid), dim3(dartmpc::kWave), 0, stream, *a);
+    else if (a->N <= 31)
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, false>), dim3(grid), dim3(dartmpc::kWave), 0, stream, *a);
+    else
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<2, false>), dim3(grid), dim3(dartmpc::kWave), 0, stream, *a);
+    return hipGetLastError();
+}
+#else
+extern "C" hipError_t dartmpc_launch_pmpc_seq(const dartmpc::PmpcArgs* a, unsigned grid, hipStream_t stream,
+                                              int onerow);
 
 extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStream_t stream) {
     if (args->B <= 0) return hipSuccess;
@@ -773,15 +804,13 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
         return e ? atoi(e) : 1024;
     }();
     if (a.N <= 15 && a.B <= qscan_max_b)
-        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+        return dartmpc_launch_pmpc_seq(&a, grid.x, stream, 1);
     else if (a.N <= 23 && a.B <= qscan_max_b)
         hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
     else if (a.N <= 31 && a.B <= qscan_max_b)
         hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
-    else if (a.N <= 31)
-        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, false>), grid, dim3(dartmpc::kWave), 0, stream, a);
     else
-        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<2, false>), grid, dim3(dartmpc::kWave), 0, stream, a);
+        return dartmpc_launch_pmpc_seq(&a, grid.x, stream, 0);
     return hipGetLastError();
 }
 
@@ -798,3 +827,4 @@ extern "C" hipError_t dartmpc_read_stamps(unsigned long long* host_out) {
                                hipMemcpyDeviceToHost);
 }
 #endif
+#endif  // PMPC_SEQ
