@@ -348,7 +348,7 @@ def bench_lmpc_policy(args, torch, dev, stream, dart_mpc):
     520-64-64-34 fp32, rsample, logit update every 8th step, EMA + soft clip) and the solve with the
     parameters it wrote, as ONE launch (dart_lmpc_policy_solve_batch_dev).  Also timed: the same step
     as two launches (policy kernel, then solve), and the check that both give identical results."""
-    from dart_mpc.lmpc import NWEIGHTS, PolicyConfig, init_policy_weights, policy_config  # noqa: F401
+    from dart_mpc.lmpc import init_policy_weights, policy_config
     from dart_mpc.workload import lmpc_batch
     from dart_mpc._lib import LMPC_PRM_DEFAULT, lib
     B, K, N = 18, args.lmpc_policy_steps, 30
