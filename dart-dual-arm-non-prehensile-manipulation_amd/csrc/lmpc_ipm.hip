@@ -106,12 +106,12 @@ __device__ __forceinline__ void strb_d(const Strb& p, double v, double& S, doubl
 
 __device__ __forceinline__ double sin_any(double x) {
     double s, c;
-    if (fabs(x) <= 1.0) sincos_small(x, s, c);
+    if (fabs(x) <= 1.0) sincos_econ(x, s, c);
     else s = sin(x);
     return s;
 }
 __device__ __forceinline__ void sincos_any(double x, double& s, double& c) {
-    if (fabs(x) <= 1.0) sincos_small(x, s, c);
+    if (fabs(x) <= 1.0) sincos_econ(x, s, c);
     else sincos(x, &s, &c);
 }
 
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     // incoming augmented defect g_k of node k for a trial point (value-only RK4 of lane k-1)
     auto defects = [&](const double* xx, double pp, double uu, double* g) {
         double sa, ca, xn[4];
-        tilt_sincos(poly, uu, sa, ca);
+        tilt_sincos_econ(poly, uu, sa, ca);
         sub_rk4(m, xx, sa, xn);
         double f[5];
 #pragma unroll
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     {
         double sa, ca, xn[4];
         const double lz[5] = {0, 0, 0, 0, 0};
-        tilt_sincos(poly, u, sa, ca);
+        tilt_sincos_econ(poly, u, sa, ca);
         double scr[4][LM_NSC], cvr[4][4];
         sub_rk4_lin(m, x, sa, xn, scr, cvr);
         const double huu = sub_adjoint_curv(m, scr, cvr, lz, sa);
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         double jl[5];       // J^T lambda_{k+1} (x columns 0..3, tilt 4)
         {
             double sa, ca;
-            tilt_sincos(poly, u, sa, ca);
+            tilt_sincos_econ(poly, u, sa, ca);
             double xn[4];
             // stage data of the RK4 pass stay in registers through the adjoint and the five directions
             double scr[4][LM_NSC], cvr[4][4];

@@ -288,9 +288,46 @@ __device__ __forceinline__ double cos_small(double x) {       // the cosine half
     pc = fma(pc, y, -0.5);
     return fma(y, pc, 1.0);
 }
+// sin/cos for |x| <= 1.0 (bound-relaxed tilt range): the Taylor series to x^23 / x^22, economised
+// on [-1, 1] by Chebyshev polynomials to degree 15 (sin) / 16 (cos): truncation <= 4.3e-20 /
+// 2.1e-21, <= 1.05 ulp in double with fma Horner -- the accuracy of the degree-19 / 20 Taylor
+// polynomials above with two terms fewer each (tests/test_math.py re-derives the coefficients and
+// checks the error).  Used by the LMPC kernel (+1 % on C5); PMPC / RMPC keep the Taylor form, which
+// their register allocation prefers (A/B: -0.6 % / -0.4 % with this one).
+#define DART_SIN_COEFFS -0.16666666666666663, 0.00833333333333285, -0.0001984126984096554, 2.755731912250289e-06, \
+                        -2.505208918178363e-08, 1.6056973209300557e-10, -7.52855132478024e-13
+#define DART_COS_COEFFS -0.5, 0.041666666666666664, -0.0013888888888888367, 2.480158730131862e-05, \
+                        -2.7557319146330464e-07, 2.087674380080511e-09, -1.1469439869437463e-11, 4.709676860456087e-14
+__device__ __forceinline__ double sin_poly_(double y) {      // (sin x - x) / x^3 as a polynomial in y = x^2
+    constexpr double c[7] = {DART_SIN_COEFFS};
+    double p = c[6];
+#pragma unroll
+    for (int i = 5; i >= 0; --i) p = fma(p, y, c[i]);
+    return p;
+}
+__device__ __forceinline__ double cos_poly_(double y) {      // (cos x - 1) / x^2 as a polynomial in y = x^2
+    constexpr double c[8] = {DART_COS_COEFFS};
+    double p = c[7];
+#pragma unroll
+    for (int i = 6; i >= 0; --i) p = fma(p, y, c[i]);
+    return p;
+}
+__device__ __forceinline__ void sincos_econ(double x, double& s, double& c) {
+    const double y = x * x;
+    s = fma(x * y, sin_poly_(y), x);
+    c = fma(y, cos_poly_(y), 1.0);
+}
+__device__ __forceinline__ double cos_econ(double x) {       // the cosine half of sincos_econ
+    const double y = x * x;
+    return fma(y, cos_poly_(y), 1.0);
+}
 __device__ __forceinline__ double tilt_cos(bool poly, double x) { return poly ? cos_small(x) : cos(x); }
 __device__ __forceinline__ void tilt_sincos(bool poly, double x, double& s, double& c) {
     if (poly) sincos_small(x, s, c);
+    else sincos(x, &s, &c);
+}
+__device__ __forceinline__ void tilt_sincos_econ(bool poly, double x, double& s, double& c) {
+    if (poly) sincos_econ(x, s, c);
     else sincos(x, &s, &c);
 }
 
