@@ -87,15 +87,15 @@ __device__ __forceinline__ Strb make_strb(double Fs, double Fc, double B, double
 
 // value of the friction law: tanh(v/eps) (F_c + (F_s - F_c) exp(-|v|/(v_s + 1e-12))) + B v
 __device__ __forceinline__ double strb(const Strb& p, double v) {
-    const double e = exp_fast(-fabs(v) * p.ivs);
-    const double T = tanh_fast(v * p.ieps);
+    const double e = exp_econ(-fabs(v) * p.ivs);
+    const double T = tanh_econ(v * p.ieps);
     return fma(T, fma(p.dF, e, p.Fc), p.B * v);
 }
 // value, first and second derivative (d|v|/dv = sign(v), sign(0) = 0, as CasADi)
 __device__ __forceinline__ void strb_d(const Strb& p, double v, double& S, double& S1, double& S2) {
     const double sg = (v > 0.0) ? 1.0 : ((v < 0.0) ? -1.0 : 0.0);
-    const double e = exp_fast(-fabs(v) * p.ivs);
-    const double T = tanh_fast(v * p.ieps);
+    const double e = exp_econ(-fabs(v) * p.ivs);
+    const double T = tanh_econ(v * p.ieps);
     const double C = fma(p.dF, e, p.Fc);
     const double T1 = (1.0 - T * T) * p.ieps, C1 = -p.dF * e * sg * p.ivs;
     const double T2 = -2.0 * T * T1 * p.ieps, C2 = p.dF * e * (sg * sg) * p.ivs * p.ivs;

@@ -383,6 +383,42 @@ __device__ __forceinline__ double exp_fast(double x) {
     return __builtin_ldexp(__builtin_ldexp(p, n1), n2);
 }
 
+// exp / tanh for the LMPC kernel: the reductions of exp_fast / tanh_fast with P(r) = (e^r - 1 - r) / r^2
+// as the degree-19 Taylor polynomial economised by Chebyshev polynomials on |r| <= 0.3467 to degree 10
+// (one term fewer than the degree-11 Taylor P above; the same 0.99 ulp for exp and 1.08 ulp for expm1
+// in double, tests/test_math.py)
+#define DART_EXPM1_COEFFS 0.5, 0.1666666666666667, 0.04166666666666668, 0.008333333333326119, \
+                          0.0013888888888879054, 0.0001984126987487566, 2.4801587336499025e-05, \
+                          2.7557255330683724e-06, 2.755726321849137e-07, 2.5105245845597674e-08, 2.0918160101597142e-09
+__device__ __forceinline__ double expm1_poly_(double r) {
+    constexpr double c[11] = {DART_EXPM1_COEFFS};
+    double p = c[10];
+#pragma unroll
+    for (int i = 9; i >= 0; --i) p = fma(p, r, c[i]);
+    return p;
+}
+__device__ __forceinline__ double tanh_econ(double x) {
+    const double y = fmin(fmax(2.0 * x, -80.0), 80.0);
+    const double n = __builtin_rint(y * 1.4426950408889634);
+    double r = fma(-n, 6.93147180369123816490e-01, y);
+    r = fma(-n, 1.90821492927058770002e-10, r);
+    const double q = fma(expm1_poly_(r) * r, r, r);
+    const double sc = __builtin_ldexp(1.0, (int)n);
+    const double em = fma(sc, q, sc - 1.0);
+    return em * frcp(em + 2.0);
+}
+__device__ __forceinline__ double exp_econ(double x) {
+    const double y = fmin(fmax(x, -745.0), 709.0);
+    const double n = __builtin_rint(y * 1.4426950408889634);
+    double r = fma(-n, 6.93147180369123816490e-01, y);
+    r = fma(-n, 1.90821492927058770002e-10, r);
+    double p = expm1_poly_(r);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    const int ni = (int)n, n1 = ni / 2, n2 = ni - n1;
+    return __builtin_ldexp(__builtin_ldexp(p, n1), n2);
+}
+
 // natural log of x = m 2^e (m = frexp mantissa in [0.5, 1)), fdlibm's e_log.c reduction and
 // minimax polynomial (Lg1..Lg7, < 1 ulp): 1 + f in [sqrt(2)/2, sqrt(2)), s = f / (2 + f),
 // log(1 + f) = f - (hfsq - s (hfsq + R(s^2))).  Shared by the device log_fast and its host check

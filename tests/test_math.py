@@ -91,3 +91,51 @@ def test_sincos_small_coefficients_and_accuracy():
         worst_c = max(worst_c, abs(float((mpmath.mpf(co) - tc) / tc)))
     ulp = 2.220446049250313e-16 / 2
     assert worst_s <= 1.1 * ulp and worst_c <= 1.1 * ulp, (worst_s / ulp, worst_c / ulp)
+
+
+def test_expm1_econ_coefficients_and_accuracy():
+    """exp_econ / tanh_econ's P(r) = (e^r - 1 - r) / r^2 (wave.h, LMPC) is the degree-19 Taylor P
+    economised on |r| <= 0.3467 (the Cody-Waite range ln2 / 2) to degree 10; with fma Horner in
+    double (emulated exactly) exp = 1 + r (1 + r P) and expm1 = r + r^2 P stay within 1 / 1.1 ulp,
+    as with the degree-11 Taylor P of exp_fast / tanh_fast."""
+    mpmath = pytest.importorskip("mpmath")
+    from fractions import Fraction as F
+    from math import factorial
+    src = open(WAVE_H).read()
+    m = re.search(r"#define DART_EXPM1_COEFFS (.*?)\n(?!\s)", src, re.S)
+    assert m
+    coef = [float(t) for t in m.group(1).replace("\\", " ").replace("\n", " ").split(",")]
+    a = F(3467, 10000)
+    n = 19
+    T = [[F(1)], [F(0), F(1)]]
+    for k in range(2, n + 1):
+        u = [F(0)] + [2 * c for c in T[k - 1]]
+        v = T[k - 2] + [F(0)] * (len(u) - len(T[k - 2]))
+        T.append([x - y for x, y in zip(u, v)])
+    mono = [F(1, factorial(k + 2)) * a ** k for k in range(n + 1)]
+    cheb, rem = [F(0)] * (n + 1), mono[:]
+    for k in range(n, -1, -1):
+        cheb[k] = rem[k] / T[k][k]
+        for i, t in enumerate(T[k]):
+            rem[i] -= cheb[k] * t
+    out = [F(0)] * 11
+    for k in range(11):
+        for i, t in enumerate(T[k]):
+            if i < 11:
+                out[i] += cheb[k] * t
+    assert coef == [float(out[k] / a ** k) for k in range(11)]
+    mpmath.mp.dps = 40
+    fma = lambda x, y, z: float(mpmath.mpf(x) * mpmath.mpf(y) + mpmath.mpf(z))
+    we = wm = 0.0
+    for i in range(-600, 601):
+        r = 0.3467 * i / 600
+        p = coef[-1]
+        for c in reversed(coef[:-1]):
+            p = fma(p, r, c)
+        e, em = fma(fma(p, r, 1.0), r, 1.0), fma(p * r, r, r)
+        te, tm = mpmath.exp(mpmath.mpf(r)), mpmath.expm1(mpmath.mpf(r))
+        we = max(we, abs(float((mpmath.mpf(e) - te) / te)))
+        if tm != 0:
+            wm = max(wm, abs(float((mpmath.mpf(em) - tm) / tm)))
+    ulp = 2.220446049250313e-16 / 2
+    assert we <= 1.0 * ulp and wm <= 1.1 * ulp, (we / ulp, wm / ulp)
