@@ -284,7 +284,7 @@ void pmpc_ipm_kernel(PmpcArgs a) {
 #pragma unroll
         for (int j = 0; j < NAX; ++j) {
             sn[j] = snc[j];
-            const double c_ = tilt_cos(poly, th[j]);
+            const double c_ = tilt_cos_econ(poly, th[j]);
             cs[j] = uon ? c_ : 0.0;
             const double ln = from_next(lp[j]), vn = from_next(lv[j]);   // unconditional: EXEC stays full
             lpn[j] = uon ? ln : 0.0; lvn[j] = uon ? vn : 0.0;

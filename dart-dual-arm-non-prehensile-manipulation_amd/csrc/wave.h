@@ -292,8 +292,9 @@ __device__ __forceinline__ double cos_small(double x) {       // the cosine half
 // on [-1, 1] by Chebyshev polynomials to degree 15 (sin) / 16 (cos): truncation <= 4.3e-20 /
 // 2.1e-21, <= 1.05 ulp in double with fma Horner -- the accuracy of the degree-19 / 20 Taylor
 // polynomials above with two terms fewer each (tests/test_math.py re-derives the coefficients and
-// checks the error).  Used by the LMPC kernel (+1 % on C5); PMPC / RMPC keep the Taylor form, which
-// their register allocation prefers (A/B: -0.6 % / -0.4 % with this one).
+// checks the error).  Used by the LMPC kernel (+1 % on C5) and for PMPC's cosine at the iterate
+// (+0.4 % on C2); PMPC's line-search sincos and RMPC keep the Taylor form, which their register
+// allocation prefers (A/B: -0.6 % / -0.4 % with this one).
 #define DART_SIN_COEFFS -0.16666666666666663, 0.00833333333333285, -0.0001984126984096554, 2.755731912250289e-06, \
                         -2.505208918178363e-08, 1.6056973209300557e-10, -7.52855132478024e-13
 #define DART_COS_COEFFS -0.5, 0.041666666666666664, -0.0013888888888888367, 2.480158730131862e-05, \
@@ -326,6 +327,7 @@ __device__ __forceinline__ void tilt_sincos(bool poly, double x, double& s, doub
     if (poly) sincos_small(x, s, c);
     else sincos(x, &s, &c);
 }
+__device__ __forceinline__ double tilt_cos_econ(bool poly, double x) { return poly ? cos_econ(x) : cos(x); }
 __device__ __forceinline__ void tilt_sincos_econ(bool poly, double x, double& s, double& c) {
     if (poly) sincos_econ(x, s, c);
     else sincos(x, &s, &c);
