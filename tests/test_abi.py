@@ -50,6 +50,9 @@ def test_create_rejects_bad_config_without_touching_a_gpu():
     assert _lib.lib().dart_rmpc_solve_batch(None, 1, *([None] * 6), 0.995, *([None] * 9)) == -1
     assert _lib.lib().dart_rls_update_batch(-1, None, None, None, None, 0.995) == -1
     assert _lib.lib().dart_lmpc_solve_batch(None, 1, *([None] * 12)) == -1
+    # the fused LMPC control step: no handle, then a handle-free config check (both before any GPU work)
+    assert _lib.lib().dart_lmpc_policy_solve_batch(None, None, 1, *([None] * 21)) == -1
+    assert _lib.lib().dart_lmpc_policy_solve_batch_dev(None, None, 1, *([None] * 21)) == -1
 
 
 def test_rmpc_shim_validates_like_reference():

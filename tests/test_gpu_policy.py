@@ -111,3 +111,23 @@ class _FixedNormal:
 
     def standard_normal(self, shape):
         return np.asarray(self.eps, np.float32).reshape(shape)
+
+
+def test_rlmpc_fused_and_two_launch_front_ends_agree():
+    """RLMPC(fused=True) and RLMPC(fused=False) on the same states and draws: bit-identical controls,
+    losses, plans and policy state over 9 steps (the logit update fires at steps 0 and 8)."""
+    import dart_mpc
+    ctl = [dart_mpc.RLMPC(None, None, dict(N=20), seed=7, fused=f) for f in (True, False)]
+    rng = np.random.default_rng(31)
+    for k in range(9):
+        state = np.concatenate([rng.uniform(-0.08, 0.08, 4), rng.uniform(-0.03, 0.03, 4)])
+        target = np.array([0.1, 0, -0.05, 0, 0, 0, 0, 0])
+        eps = rng.standard_normal(34).astype(np.float32)
+        outs = []
+        for c in ctl:
+            c._rng = _FixedNormal(eps)
+            outs.append(c.solve(target, state=state))
+        assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1]), k
+        assert np.array_equal(ctl[0].w0, ctl[1].w0), k
+        for a in ("model_params", "obs_mean", "obs_M2", "history", "timestep", "obs_count"):
+            assert np.array_equal(getattr(ctl[0].policy, a), getattr(ctl[1].policy, a)), (k, a)
