@@ -66,8 +66,8 @@ static_assert(sizeof(NodeArr<double[3][RM_NIQ], RM_NMAXS + 1>) <= sizeof(NodeArr
 // continuous model (np_mpc...:178-186); also returns d f / d vx|vy of rows 1, 3 and tanh values
 __device__ __forceinline__ void rm_f(const RmModel& m, const double* y, double sa, double sb, double* f,
                                      double& j1vx, double& j1vy, double& j3vx, double& j3vy, double& tx, double& ty) {
-    tx = tanh_fast(y[1] * m.ie);
-    ty = tanh_fast(y[3] * m.ie);
+    tx = tanh_econ(y[1] * m.ie);
+    ty = tanh_econ(y[3] * m.ie);
     const double* a = m.th;
     const double* c = m.th + 7;
     f[0] = y[1];

@@ -333,62 +333,11 @@ __device__ __forceinline__ void tilt_sincos_econ(bool poly, double x, double& s,
     else sincos(x, &s, &c);
 }
 
-// tanh(x) = em / (em + 2), em = expm1(2x) by Cody-Waite reduction and a degree-13 Taylor
-// polynomial on |r| <= ln2/2: <= 5e-16 relative error (host-checked against libm over
-// [-6, 6] and [-1e-3, 1e-3]), about a third of the instructions of the library tanh.
-__device__ __forceinline__ double tanh_fast(double x) {
-    const double y = fmin(fmax(2.0 * x, -80.0), 80.0);
-    const double n = __builtin_rint(y * 1.4426950408889634);
-    double r = fma(-n, 6.93147180369123816490e-01, y);
-    r = fma(-n, 1.90821492927058770002e-10, r);
-    double p = 1.0 / 6227020800.0;
-    p = fma(p, r, 1.0 / 479001600.0);
-    p = fma(p, r, 1.0 / 39916800.0);
-    p = fma(p, r, 1.0 / 3628800.0);
-    p = fma(p, r, 1.0 / 362880.0);
-    p = fma(p, r, 1.0 / 40320.0);
-    p = fma(p, r, 1.0 / 5040.0);
-    p = fma(p, r, 1.0 / 720.0);
-    p = fma(p, r, 1.0 / 120.0);
-    p = fma(p, r, 1.0 / 24.0);
-    p = fma(p, r, 1.0 / 6.0);
-    p = fma(p, r, 0.5);
-    const double q = fma(p * r, r, r);
-    const double sc = __builtin_ldexp(1.0, (int)n);
-    const double em = fma(sc, q, sc - 1.0);
-    return em * frcp(em + 2.0);                 // em + 2 in [1, 6e34]: frcp (rcp + Newton) to ~4e-16
-}
-
-// exp(x) by Cody-Waite reduction and a degree-13 Taylor polynomial on |r| <= ln2/2:
-// <= 2.3e-16 relative error over [-200, 5] (host-checked against libm); underflows to the
+// exp / tanh (LMPC, RMPC) by Cody-Waite reduction to |r| <= ln2/2 and P(r) = (e^r - 1 - r) / r^2 as the
+// degree-19 Taylor polynomial economised by Chebyshev polynomials on |r| <= 0.3467 to degree 10 (one term
+// fewer than the degree-11 Taylor P the kernels used before; the same 0.99 ulp for exp and 1.08 ulp for
+// expm1 in double, tests/test_math.py).  tanh(x) = em / (em + 2), em = expm1(2x); exp underflows to the
 // subnormals and 0 like libm.
-__device__ __forceinline__ double exp_fast(double x) {
-    const double y = fmin(fmax(x, -745.0), 709.0);
-    const double n = __builtin_rint(y * 1.4426950408889634);
-    double r = fma(-n, 6.93147180369123816490e-01, y);
-    r = fma(-n, 1.90821492927058770002e-10, r);
-    double p = 1.0 / 6227020800.0;
-    p = fma(p, r, 1.0 / 479001600.0);
-    p = fma(p, r, 1.0 / 39916800.0);
-    p = fma(p, r, 1.0 / 3628800.0);
-    p = fma(p, r, 1.0 / 362880.0);
-    p = fma(p, r, 1.0 / 40320.0);
-    p = fma(p, r, 1.0 / 5040.0);
-    p = fma(p, r, 1.0 / 720.0);
-    p = fma(p, r, 1.0 / 120.0);
-    p = fma(p, r, 1.0 / 24.0);
-    p = fma(p, r, 1.0 / 6.0);
-    p = fma(p, r, 0.5);
-    p = fma(p, r, 1.0);
-    p = fma(p, r, 1.0);
-    const int ni = (int)n, n1 = ni / 2, n2 = ni - n1;       // two halves: exact down to the subnormals
-    return __builtin_ldexp(__builtin_ldexp(p, n1), n2);
-}
-
-// exp / tanh for the LMPC kernel: the reductions of exp_fast / tanh_fast with P(r) = (e^r - 1 - r) / r^2
-// as the degree-19 Taylor polynomial economised by Chebyshev polynomials on |r| <= 0.3467 to degree 10
-// (one term fewer than the degree-11 Taylor P above; the same 0.99 ulp for exp and 1.08 ulp for expm1
-// in double, tests/test_math.py)
 #define DART_EXPM1_COEFFS 0.5, 0.1666666666666667, 0.04166666666666668, 0.008333333333326119, \
                           0.0013888888888879054, 0.0001984126987487566, 2.4801587336499025e-05, \
                           2.7557255330683724e-06, 2.755726321849137e-07, 2.5105245845597674e-08, 2.0918160101597142e-09

@@ -94,10 +94,10 @@ def test_sincos_small_coefficients_and_accuracy():
 
 
 def test_expm1_econ_coefficients_and_accuracy():
-    """exp_econ / tanh_econ's P(r) = (e^r - 1 - r) / r^2 (wave.h, LMPC) is the degree-19 Taylor P
+    """exp_econ / tanh_econ's P(r) = (e^r - 1 - r) / r^2 (wave.h, LMPC and RMPC) is the degree-19 Taylor P
     economised on |r| <= 0.3467 (the Cody-Waite range ln2 / 2) to degree 10; with fma Horner in
     double (emulated exactly) exp = 1 + r (1 + r P) and expm1 = r + r^2 P stay within 1 / 1.1 ulp,
-    as with the degree-11 Taylor P of exp_fast / tanh_fast."""
+    as with the degree-11 Taylor P the kernels used before."""
     mpmath = pytest.importorskip("mpmath")
     from fractions import Fraction as F
     from math import factorial
