@@ -203,7 +203,8 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False):
     """C4 (BASELINE.json configs[3]): PMPC 18 configs x 64 seeds = 1152 instances, N=20, sharded over the
     ranks in contiguous blocks (dart_mpc.parallel.shard_bounds).  One step = every rank solves its block,
     packs [u0, f, status] and joins one all_gather_into_tensor (RCCL over xGMI) of the padded blocks.
-    The global batch is fixed as ranks are added (strong scaling); the gather is inside the timed region."""
+    The global batch is fixed as ranks are added (strong scaling); the gather is inside the timed region
+    of `solves_per_s`; `solves_per_s_without_gather` times the solves alone."""
     import torch.distributed as dist
     from dart_mpc.parallel import RESULT_COLS, shard_bounds
     from dart_mpc.workload import pmpc_batch
@@ -224,9 +225,11 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False):
     solver = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=max(1, n), device=dev.index)
     sp = stream.cuda_stream
 
-    def step():
+    def step(gather=True):
         solver.solve_batch_dev(n, X0.data_ptr(), RF.data_ptr(), PR.data_ptr(), U0.data_ptr(), FV.data_ptr(),
                                ST.data_ptr(), IT.data_ptr(), stream=sp)
+        if not gather:
+            return
         with torch.cuda.stream(stream):
             block[:n, 0:2].copy_(U0)
             block[:n, 2].copy_(FV)
@@ -240,21 +243,24 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False):
             else:
                 full.copy_(block)
 
-    for _ in range(3):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(K):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        dt = _max_over_ranks([dt], dev, host_coll)[0]
+    def timed(gather):
+        for _ in range(3):
+            step(gather)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(K):
+            step(gather)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t = time.perf_counter() - t0
+        return _max_over_ranks([t], dev, host_coll)[0] if world > 1 else t
+
+    dt_solve = timed(False)      # the solves alone (with and without the gather)
+    dt = timed(True)
     res = full.cpu().numpy()[:Bg]
     # every rank finds its own block, bit for bit, at its offset of the gathered result
     mine = bool(np.array_equal(res[lo:hi], block[:n].cpu().numpy()))
@@ -270,6 +276,7 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False):
                         "blocks over the ranks + all_gather_into_tensor of [u0, f, status] (RCCL)",
             "global_batch": Bg, "per_rank": per, "n_gpus": world, "scaling": "strong", "steps": K,
             "solves_per_s": Bg * K / dt, "ms_per_step": dt / K * 1e3, "gather_in_timed_region": world > 1,
+            "solves_per_s_without_gather": Bg * K / dt_solve, "ms_per_step_without_gather": dt_solve / K * 1e3,
             "status_ok_frac": float(np.mean(res[:, 3] == 0)), "rank_blocks_consistent": mine,
             "max_abs_u0_err_vs_exact_optimum_first36": float(np.max(np.abs(res[:36, 0:2] - ref["u0"])))}
 

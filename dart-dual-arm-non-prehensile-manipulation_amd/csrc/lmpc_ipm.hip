@@ -422,6 +422,8 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     gmax = wmax(gmax);
     const double sc = gmax > 100.0 ? 100.0 / gmax : 1.0;
 
+    // the derivative pass of iteration 0 runs here, once: its Jacobian columns give the constraint-row
+    // scaling, and the loop's first iteration (same point, lambda = 0) takes M~, H~ and x+ as they stand
     double dsc[4];          // scaling of the incoming physical defect rows of node k (up row: 1)
     {
         double sa, ca, xn[4];
@@ -432,9 +434,16 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         const double huu = sub_adjoint_curv(m, scr, cvr, lz, sa);
         if (uon) {
             const LmSub mr = m;
+            const double isl = frcp(u - lo), isu = frcp(hi - u);
+            const double cu = sc * 2.0 * (Ru + Rdu) + zl * isl + zu * isu;
 #pragma unroll 1
-            for (int d = 0; d < 5; ++d) sub_direction(mr, scr, cvr, huu, LM_G * ca, d, lz, Mk, Hk, 0.0);
+            for (int d = 0; d < 5; ++d)
+                sub_direction(mr, scr, cvr, huu, LM_G * ca, d, lz, Mk, Hk, d < 4 ? sc * 2.0 * Wq[d] : cu);
+            Hk[hp(4, 4)] = sc * 2.0 * Rdu;
+            Hk[hp(5, 4)] = -sc * 2.0 * Rdu;
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) SH.CS[sl][i] = xn[i];       // x+ of iteration 0 (CS is free until then)
         double rs[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -479,9 +488,15 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         for (int i = 0; i < 5; ++i) { const double t = from_next(lam[i]); lamn[i] = uon ? t : 0.0; }
         double jl[5];       // J^T lambda_{k+1} (x columns 0..3, tilt 4)
         {
+            double xn[4];
+            if (it == 0) {      // the setup's derivative pass (lambda = 0: J^T lambda = 0)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xn[i] = SH.CS[sl][i];
+#pragma unroll
+                for (int i = 0; i < 5; ++i) jl[i] = 0.0;
+            } else {
             double sa, ca;
             tilt_sincos_econ(poly, u, sa, ca);
-            double xn[4];
             // stage data of the RK4 pass stay in registers through the adjoint and the five directions
             double scr[4][LM_NSC], cvr[4][4];
             sub_rk4_lin(m, x, sa, xn, scr, cvr);
@@ -506,6 +521,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     for (int i = 0; i < 5; ++i) jl[i] = 0.0;
                 }
                 STAMP(14);
+            }
             }
             // outgoing augmented defect c_k = [F(z_k); u_k] - x~_{k+1} -> defect column of M~
             double cdef[5];
