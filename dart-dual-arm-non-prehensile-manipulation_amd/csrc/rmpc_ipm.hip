@@ -18,9 +18,11 @@
 // gets them from CasADi: per direction the RK4 tangent (a Jacobian column) and a second-order
 // adjoint sweep through the four stages (a column of the exact Hessian of lambda^T x+).
 //
-// Mapping: one wave64 per instance; lane k owns shooting node k (N <= 31) for everything that is
-// node-local (model evaluation, slacks, multipliers, line search); the node-coupled Riccati and
-// forward sweeps run through LDS with the lanes sharing each node's dense algebra (ocp_wave.h).
+// Mapping: one wave64 per instance; lane k and its mirror lane k + 32 own shooting node k (N <= 31):
+// both run the node-local work (model evaluation, multipliers, line search) and they split the six
+// slack rows of the node three and three (slacks, slack multipliers, their steps and barrier terms);
+// the node-coupled Riccati and forward sweeps run through LDS with the lanes sharing each node's dense
+// algebra (ocp_wave.h).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -35,6 +37,7 @@ namespace dartmpc {
 
 constexpr int RM_NMAXS = 32;      // max shooting nodes (N <= 31)
 constexpr int RM_NIQ = 6;         // inequality rows per node: du_x, du_y, vx-vmax, -vx-vmax, vy-vmax, -vy-vmax
+constexpr int RM_NQ = 3;          // of them per lane: rows 0..2 on lane k, rows 3..5 on its mirror lane k + 32
 using RmLds = OcpLds<6, RM_NMAXS>;
 
 #ifdef DART_STAMPS
@@ -235,14 +238,12 @@ __device__ __forceinline__ void rm_directions(const RmModel& m, const double (*s
     for (int d = d0; d < d0 + 3; ++d) jl_lds[d] = rm_direction(mr, scr, cvr, huu, gca, gcb, d, lamn, Mk, Hk);
 }
 
-// z = [px vx py vy upx upy ux uy]: inequality row values C z (np_mpc...:114-127)
-__device__ __forceinline__ void rm_iq(const double* z, double vmax, double* c) {
-    c[0] = z[6] - z[4];
-    c[1] = z[7] - z[5];
-    c[2] = z[1] - vmax;
-    c[3] = -z[1] - vmax;
-    c[4] = z[3] - vmax;
-    c[5] = -z[3] - vmax;
+// z = [px vx py vy upx upy ux uy]: the inequality row values C z (np_mpc...:114-127) of one lane's three
+// rows: du_x, du_y, vx - vmax on the node lane; -vx - vmax, vy - vmax, -vy - vmax on the mirror lane
+__device__ __forceinline__ void rm_iq3(const double* z, double vmax, bool mir, double* c) {
+    c[0] = mir ? -z[1] - vmax : z[6] - z[4];
+    c[1] = mir ? z[3] - vmax : z[7] - z[5];
+    c[2] = mir ? -z[3] - vmax : z[1] - vmax;
 }
 
 __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
@@ -251,7 +252,12 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     STAMP_DECL
     if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
     const int b = blockIdx.x / a.pack;
-    const int k = threadIdx.x;
+    // lane k and its mirror lane k + 32 both own node k: the node work runs on both, the slack rows are
+    // split (rm_iq3), and sums over the wave count the node terms on the node lanes only
+    const int lane = threadIdx.x;
+    const int k = lane & 31;
+    const bool mir = lane >= 32, nod = !mir;
+    const int q0 = mir ? RM_NQ : 0;           // first slack row of this lane
     const int N = a.N;
     const bool xon = k <= N, uon = k < N;
     const double* pr = a.prm + 10 * b;
@@ -263,10 +269,10 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         double* Pg = a.rls_P + 98 * b;
         const double* ph = a.rls_phi + 7 * b;
         const double lamr = a.rls_lambda;
-        if (k < 28) {
-            const int ax = (k % 14) / 7, i = k % 7;
+        if (lane < 28) {
+            const int ax = (lane % 14) / 7, i = lane % 7;
             double s = 0.0;
-            if (k < 14) { for (int j = 0; j < 7; ++j) s = fma(Pg[49 * ax + 7 * i + j], ph[j], s); SH.rls_Pphi[ax][i] = s; }
+            if (lane < 14) { for (int j = 0; j < 7; ++j) s = fma(Pg[49 * ax + 7 * i + j], ph[j], s); SH.rls_Pphi[ax][i] = s; }
             else { for (int j = 0; j < 7; ++j) s = fma(ph[j], Pg[49 * ax + 7 * j + i], s); SH.rls_phiP[ax][i] = s; }
         }
         __syncthreads();
@@ -281,7 +287,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         int idx[2];
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
-            const int e = k + 64 * r;
+            const int e = lane + 64 * r;
             idx[r] = e;
             if (e < 98) {
                 const int ax = e / 49, i = (e % 49) / 7, j = e % 7;
@@ -290,21 +296,21 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             }
         }
         double thn = 0.0;
-        if (k < 14) {
-            const int ax = k / 7, i = k % 7;
-            thn = a.theta[14 * b + k] + SH.rls_Pphi[ax][i] / den[ax] * err[ax];
+        if (lane < 14) {
+            const int ax = lane / 7, i = lane % 7;
+            thn = a.theta[14 * b + lane] + SH.rls_Pphi[ax][i] / den[ax] * err[ax];
         }
         __syncthreads();          // every lane has read P, theta before anyone writes
 #pragma unroll
         for (int r = 0; r < 2; ++r) if (idx[r] < 98) Pg[idx[r]] = pnew[r];
-        if (k < 14) { a.theta[14 * b + k] = thn; SH.theta[k] = thn; }
-    } else if (k < 14) {
-        SH.theta[k] = a.theta[14 * b + k];
+        if (lane < 14) { a.theta[14 * b + lane] = thn; SH.theta[lane] = thn; }
+    } else if (lane < 14) {
+        SH.theta[lane] = a.theta[14 * b + lane];
     }
     __syncthreads();
 
-    if (k < 14) SH.model.th[k] = SH.theta[k];
-    if (k == 0) { SH.model.gz = a.g; SH.model.h = a.Ts; SH.model.ie = 1.0 / veps; }
+    if (lane < 14) SH.model.th[lane] = SH.theta[lane];
+    if (lane == 0) { SH.model.gz = a.g; SH.model.h = a.Ts; SH.model.ie = 1.0 / veps; }
     __syncthreads();
     const RmModel& m = SH.model;
     const int sr = xon ? k : RM_NMAXS;        // per-node LDS scratch row (idle lanes share row 32)
@@ -318,21 +324,25 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     }
 
     const double lo = ulo - 1e-8 * fmax(1.0, fabs(ulo)), hi = uhi + 1e-8 * fmax(1.0, fabs(uhi));
-    double sL[RM_NIQ], sU[RM_NIQ];            // relaxed slack bounds (lower only on the du rows)
-    sL[0] = sL[1] = dulo - 1e-8 * fmax(1.0, fabs(dulo));
-    sU[0] = sU[1] = duhi + 1e-8 * fmax(1.0, fabs(duhi));
+    // relaxed bounds of this lane's slack rows: lower bounds only on the du rows (slots 0, 1 of the node lanes)
+    double sL[RM_NQ], sU[RM_NQ];
+    bool tw[RM_NQ];
 #pragma unroll
-    for (int i = 2; i < RM_NIQ; ++i) { sL[i] = -1e300; sU[i] = 1e-8; }
+    for (int i = 0; i < RM_NQ; ++i) {
+        tw[i] = nod && i < 2;
+        sL[i] = tw[i] ? dulo - 1e-8 * fmax(1.0, fabs(dulo)) : -1e300;
+        sU[i] = tw[i] ? duhi + 1e-8 * fmax(1.0, fabs(duhi)) : 1e-8;
+    }
     const bool poly = fmax(fabs(lo), fabs(hi)) <= 1.0;
 
-    // ---------------- iterate (lane k = node k) -------------------------------------------------
+    // ---------------- iterate (lanes k and k + 32 = node k) ---------------------------------------
     const double* x0 = a.x0 + 4 * b;
     const double* upv = a.u_prev + 2 * b;
     const double* rr = a.Rref + 4 * (N + 1) * b + 4 * (xon ? k : 0);
     const double r0 = rr[0], r1 = rr[1], r2 = rr[2], r3 = rr[3];
     const int nw = 4 * (N + 1) + 2 * N;
     const double* ww = a.w_warm ? a.w_warm + (size_t)nw * b : nullptr;
-    double x[4], up[2], u[2], lam[6], zl[2], zu[2], s[RM_NIQ], yq[RM_NIQ], vl[RM_NIQ], vu[RM_NIQ];
+    double x[4], up[2], u[2], lam[6], zl[2], zu[2], s[RM_NQ], yq[RM_NQ], vl[RM_NQ], vu[RM_NQ];
 #pragma unroll
     for (int i = 0; i < 4; ++i) x[i] = xon && ww ? ww[4 * k + i] : 0.0;   // reference warm start, zeros first call (:168)
     const double pushl = fmin(1e-2 * fmax(1.0, fabs(lo)), 1e-2 * (hi - lo));
@@ -351,21 +361,19 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 #pragma unroll
     for (int i = 0; i < 6; ++i) lam[i] = 0.0;
     {   // slacks: s = C z pushed into the relaxed bounds; multipliers 1
-        double z[8] = {x[0], x[1], x[2], x[3], up[0], up[1], u[0], u[1]}, c[RM_NIQ];
-        rm_iq(z, vmax, c);
+        double z[8] = {x[0], x[1], x[2], x[3], up[0], up[1], u[0], u[1]}, c[RM_NQ];
+        rm_iq3(z, vmax, mir, c);
 #pragma unroll
-        for (int i = 0; i < RM_NIQ; ++i) {
-            double v;
+        for (int i = 0; i < RM_NQ; ++i) {
+            double v = fmin(c[i], sU[i] - 1e-2 * fmax(1.0, fabs(sU[i])));
             if (i < 2) {
                 const double pl = fmin(1e-2 * fmax(1.0, fabs(sL[i])), 1e-2 * (sU[i] - sL[i]));
                 const double pu = fmin(1e-2 * fmax(1.0, fabs(sU[i])), 1e-2 * (sU[i] - sL[i]));
-                v = fmin(fmax(c[i], sL[i] + pl), sU[i] - pu);
-            } else {
-                v = fmin(c[i], sU[i] - 1e-2 * fmax(1.0, fabs(sU[i])));
+                v = tw[i] ? fmin(fmax(c[i], sL[i] + pl), sU[i] - pu) : v;
             }
             s[i] = uon ? v : 0.0;
             yq[i] = 0.0;
-            vl[i] = uon && i < 2 ? 1.0 : 0.0;
+            vl[i] = uon && tw[i] ? 1.0 : 0.0;
             vu[i] = uon ? 1.0 : 0.0;
         }
     }
@@ -417,12 +425,12 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     double theta;
     {
         defects(x, up, u, gdef);
-        double zz[8] = {x[0], x[1], x[2], x[3], up[0], up[1], u[0], u[1]}, c[RM_NIQ], th0 = 0.0;
-        rm_iq(zz, vmax, c);
+        double zz[8] = {x[0], x[1], x[2], x[3], up[0], up[1], u[0], u[1]}, c[RM_NQ], th0 = 0.0;
+        rm_iq3(zz, vmax, mir, c);
 #pragma unroll
-        for (int i = 0; i < 6; ++i) th0 += xon ? fabs(gdef[i]) : 0.0;
+        for (int i = 0; i < 6; ++i) th0 += nod && xon ? fabs(gdef[i]) : 0.0;
 #pragma unroll
-        for (int i = 0; i < RM_NIQ; ++i) th0 += uon ? fabs(c[i] - s[i]) : 0.0;
+        for (int i = 0; i < RM_NQ; ++i) th0 += uon ? fabs(c[i] - s[i]) : 0.0;
         theta = wsum_rl(th0);
     }
     const double th_max = 1e4 * fmax(1.0, theta), th_min = 1e-4 * fmax(1.0, theta);
@@ -447,19 +455,15 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             double xn[4], huu[2];
             rm_rk4_lin(m, x, sa, sb, xn, SH.SC[sr], SH.SD[sr]);
             rm_adjoint_curv(m, SH.SC[sr], SH.SD[sr], lamn, sa, sb, huu);
-            if (k < 32) {
+            if (nod) {
 #pragma unroll
                 for (int i = 0; i < 6; ++i) SH.DL[k][i] = lamn[i];
                 SH.DL[k][6] = huu[0]; SH.DL[k][7] = huu[1]; SH.DL[k][8] = m.gz * ca; SH.DL[k][9] = m.gz * cb;
             }
             __syncthreads();
             STAMP(11);
-            {   // lanes k and k + 32 own directions 0..2 and 3..5 of node k
-                const int kn = k & 31;
-                if (kn < N)
-                    rm_directions(m, SH.SC[kn], SH.SD[kn], SH.DL[kn], k < 32 ? 0 : 3, &S->M[kn][0][0], S->H[kn],
-                                  SH.JL[kn]);
-            }
+            // lanes k and k + 32 own directions 0..2 and 3..5 of node k
+            if (uon) rm_directions(m, SH.SC[k], SH.SD[k], SH.DL[k], mir ? 3 : 0, &S->M[k][0][0], S->H[k], SH.JL[k]);
             __syncthreads();
             STAMP(12);
 #pragma unroll
@@ -484,13 +488,13 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             SH.JL[sr][6] = pl;
         }
         const double zz[8] = {x[0], x[1], x[2], x[3], up[0], up[1], u[0], u[1]};
-        double cz[RM_NIQ], rq[RM_NIQ], sig[RM_NIQ], psi[RM_NIQ];
-        rm_iq(zz, vmax, cz);
+        double cz[RM_NQ], rq[RM_NQ], sig[RM_NQ], psi[RM_NQ];
+        rm_iq3(zz, vmax, mir, cz);
 #pragma unroll
-        for (int i = 0; i < RM_NIQ; ++i) {
+        for (int i = 0; i < RM_NQ; ++i) {
             rq[i] = uon ? cz[i] - s[i] : 0.0;
             const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
-            const double idl = i < 2 ? frcp(dl) : 0.0, idu = frcp(du_);
+            const double idl = tw[i] ? frcp(dl) : 0.0, idu = frcp(du_);
             sig[i] = uon ? fma(vl[i], idl, vu[i] * idu) : 0.0;
             psi[i] = uon ? mu * (idu - idl) : 0.0;
         }
@@ -506,28 +510,31 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) gl[j] -= jl[j];
             gl[6] -= jl[4] + lamn[4]; gl[7] -= jl[5] + lamn[5];
-            // + C^T y
+            // + C^T y, rows 3..5 from the mirror lane; the node's residual counts on the node lanes
+            double yo[RM_NQ];
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) yo[i] = __shfl_xor(yq[i], 32);
             gl[6] += yq[0]; gl[4] -= yq[0]; gl[7] += yq[1]; gl[5] -= yq[1];
-            gl[1] += yq[2] - yq[3]; gl[3] += yq[4] - yq[5];
+            gl[1] += yq[2] - yo[0]; gl[3] += yo[1] - yo[2];
             gl[6] += -zl[0] + zu[0]; gl[7] += -zl[1] + zu[1];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) dinf = fmax(dinf, (j < 6 ? xon : uon) ? fabs(gl[j]) : 0.0);
+            for (int j = 0; j < 8; ++j) dinf = fmax(dinf, nod && (j < 6 ? xon : uon) ? fabs(gl[j]) : 0.0);
 #pragma unroll
-            for (int i = 0; i < RM_NIQ; ++i) dinf = fmax(dinf, uon ? fabs(-yq[i] - vl[i] + vu[i]) : 0.0);
+            for (int i = 0; i < RM_NQ; ++i) dinf = fmax(dinf, uon ? fabs(-yq[i] - vl[i] + vu[i]) : 0.0);
 #pragma unroll
-            for (int i = 0; i < 6; ++i) suml += xon ? fabs(lam[i]) : 0.0;
+            for (int i = 0; i < 6; ++i) suml += nod && xon ? fabs(lam[i]) : 0.0;
 #pragma unroll
-            for (int i = 0; i < RM_NIQ; ++i) {
+            for (int i = 0; i < RM_NQ; ++i) {
                 pinf = fmax(pinf, fabs(rq[i]));
                 suml += fabs(yq[i]);
                 if (uon) {
                     const double cu = vu[i] * (sU[i] - s[i]);
                     c0 = fmax(c0, cu); cmin = fmin(cmin, cu); sumz += vu[i];
-                    if (i < 2) { const double cl = vl[i] * (s[i] - sL[i]); c0 = fmax(c0, cl); cmin = fmin(cmin, cl); sumz += vl[i]; }
+                    if (tw[i]) { const double cl = vl[i] * (s[i] - sL[i]); c0 = fmax(c0, cl); cmin = fmin(cmin, cl); sumz += vl[i]; }
                 }
             }
 #pragma unroll
-            for (int j = 0; j < 2; ++j) if (uon) {
+            for (int j = 0; j < 2; ++j) if (uon && nod) {
                 const double cl = zl[j] * (u[j] - lo), cu = zu[j] * (hi - u[j]);
                 c0 = fmax(c0, fmax(cl, cu)); cmin = fmin(cmin, fmin(cl, cu)); sumz += zl[j] + zu[j];
             }
@@ -547,9 +554,9 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
             nfilt = 0;
 #pragma unroll
-            for (int i = 0; i < RM_NIQ; ++i) {
+            for (int i = 0; i < RM_NQ; ++i) {
                 const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
-                const double idl = i < 2 ? frcp(dl) : 0.0, idu = frcp(du_);
+                const double idl = tw[i] ? frcp(dl) : 0.0, idu = frcp(du_);
                 psi[i] = uon ? mu * (idu - idl) : 0.0;
             }
         }
@@ -566,15 +573,20 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             cost_grad(x, u, up, gq);
 #pragma unroll
             for (int j = 0; j < 8; ++j) gq[j] *= sc;
-            if (uon) {
+            // Sigma and Sigma r + psi of rows 3..5 from the mirror lane; the node lane writes the stage
+            double tq[RM_NQ], so[RM_NQ], to[RM_NQ];
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) tq[i] = sig[i] * rq[i] + psi[i];
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) { so[i] = __shfl_xor(sig[i], 32); to[i] = __shfl_xor(tq[i], 32); }
+            if (uon && nod) {
                 gq[6] += -mu * isl0 + mu * isu0; gq[7] += -mu * isl1 + mu * isu1;
-                const double t0 = sig[0] * rq[0] + psi[0], t1 = sig[1] * rq[1] + psi[1];
-                gq[6] += t0; gq[4] -= t0; gq[7] += t1; gq[5] -= t1;
-                gq[1] += (sig[2] * rq[2] + psi[2]) - (sig[3] * rq[3] + psi[3]);
-                gq[3] += (sig[4] * rq[4] + psi[4]) - (sig[5] * rq[5] + psi[5]);
+                gq[6] += tq[0]; gq[4] -= tq[0]; gq[7] += tq[1]; gq[5] -= tq[1];
+                gq[1] += tq[2] - to[0];
+                gq[3] += to[1] - to[2];
                 Hk[hp(0, 0)] += sc * 2 * Qp; Hk[hp(2, 2)] += sc * 2 * Qp;
-                Hk[hp(1, 1)] += sc * 2 * Qv + sig[2] + sig[3];
-                Hk[hp(3, 3)] += sc * 2 * Qv + sig[4] + sig[5];
+                Hk[hp(1, 1)] += sc * 2 * Qv + sig[2] + so[0];
+                Hk[hp(3, 3)] += sc * 2 * Qv + so[1] + so[2];
                 Hk[hp(6, 6)] += sc * 2 * (Ru + Rdu) + zl[0] * isl0 + zu[0] * isu0 + sig[0];
                 Hk[hp(7, 7)] += sc * 2 * (Ru + Rdu) + zl[1] * isl1 + zu[1] * isu1 + sig[1];
                 Hk[hp(4, 4)] = sc * 2 * Rdu + sig[0]; Hk[hp(5, 5)] = sc * 2 * Rdu + sig[1];
@@ -583,8 +595,10 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
                 for (int j = 0; j < 8; ++j) Hk[hp(8, j)] = gq[j];
             }
 #pragma unroll
-            for (int i = 0; i < RM_NIQ; ++i) { SH.SR[sr][0][i] = sig[i]; SH.SR[sr][1][i] = psi[i]; SH.SR[sr][2][i] = rq[i]; }
-            if (k == N) {   // terminal surrogate G_N: value function [[Q_N, q_N], [q_N^T, 0]], Quu = I
+            for (int i = 0; i < RM_NQ; ++i) {
+                SH.SR[sr][0][q0 + i] = sig[i]; SH.SR[sr][1][q0 + i] = psi[i]; SH.SR[sr][2][q0 + i] = rq[i];
+            }
+            if (k == N && nod) {   // terminal surrogate G_N: value function [[Q_N, q_N], [q_N^T, 0]], Quu = I
                 double* GN = S->G[N];
                 for (int e = 0; e < tri(9); ++e) GN[e] = 0.0;
                 GN[hp(0, 0)] = sc * 2 * Qp; GN[hp(2, 2)] = sc * 2 * Qp;
@@ -605,11 +619,11 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))   // IPOPT perturb_dec_fact 1/3
                                    : delta * (delta_last == 0.0 ? 100.0 : 8.0);
             const double dd = delta - dapplied;
-            if (uon) {
+            if (uon && nod) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) Hk[hp(j, j)] += dd;
             }
-            if (k == N) {
+            if (k == N && nod) {
                 // the sweep never overwrites the terminal surrogate: add delta on its x~ block
 #pragma unroll
                 for (int j = 0; j < 6; ++j) S->G[N][hp(j, j)] += dd;
@@ -639,18 +653,18 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         }
         STAMP(4);
         // slack and multiplier steps
-        double dS[RM_NIQ], dY[RM_NIQ], dvl[RM_NIQ], dvu[RM_NIQ], dzl[2], dzu[2];
+        double dS[RM_NQ], dY[RM_NQ], dvl[RM_NQ], dvu[RM_NQ], dzl[2], dzu[2];
         {
             const double dzv[8] = {dx[0], dx[1], dx[2], dx[3], dx[4], dx[5], dU[0], dU[1]};
-            double cdz[RM_NIQ];
-            rm_iq(dzv, 0.0, cdz);
+            double cdz[RM_NQ];
+            rm_iq3(dzv, 0.0, mir, cdz);
 #pragma unroll
-            for (int i = 0; i < RM_NIQ; ++i) {
-                dS[i] = uon ? cdz[i] + SH.SR[sr][2][i] : 0.0;
-                dY[i] = uon ? SH.SR[sr][0][i] * dS[i] + SH.SR[sr][1][i] - yq[i] : 0.0;
+            for (int i = 0; i < RM_NQ; ++i) {
+                dS[i] = uon ? cdz[i] + SH.SR[sr][2][q0 + i] : 0.0;
+                dY[i] = uon ? SH.SR[sr][0][q0 + i] * dS[i] + SH.SR[sr][1][q0 + i] - yq[i] : 0.0;
                 const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
-                const double idl = i < 2 ? frcp(dl) : 0.0, idu = frcp(du_);
-                dvl[i] = uon && i < 2 ? fma(mu, idl, -vl[i]) - vl[i] * idl * dS[i] : 0.0;
+                const double idl = tw[i] ? frcp(dl) : 0.0, idu = frcp(du_);
+                dvl[i] = uon && tw[i] ? fma(mu, idl, -vl[i]) - vl[i] * idl * dS[i] : 0.0;
                 dvu[i] = uon ? fma(mu, idu, -vu[i]) + vu[i] * idu * dS[i] : 0.0;
             }
             dzl[0] = uon ? mu * isl0 - zl[0] - zl[0] * isl0 * dU[0] : 0.0;
@@ -669,10 +683,10 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
                 if (dzu[j] < 0) az = fmin(az, -tau * zu[j] * frcp(dzu[j]));
             }
 #pragma unroll
-            for (int i = 0; i < RM_NIQ; ++i) {
-                if (i < 2 && dS[i] < 0) amax = fmin(amax, -tau * (s[i] - sL[i]) * frcp(dS[i]));
+            for (int i = 0; i < RM_NQ; ++i) {
+                if (tw[i] && dS[i] < 0) amax = fmin(amax, -tau * (s[i] - sL[i]) * frcp(dS[i]));
                 if (dS[i] > 0) amax = fmin(amax, tau * (sU[i] - s[i]) * frcp(dS[i]));
-                if (i < 2 && dvl[i] < 0) az = fmin(az, -tau * vl[i] * frcp(dvl[i]));
+                if (tw[i] && dvl[i] < 0) az = fmin(az, -tau * vl[i] * frcp(dvl[i]));
                 if (dvu[i] < 0) az = fmin(az, -tau * vu[i] * frcp(dvu[i]));
             }
         }
@@ -681,9 +695,9 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         double* SY = &S->F[uon ? k : 0][0][0];
         if (uon) {
 #pragma unroll
-            for (int i = 0; i < RM_NIQ; ++i) {
-                SY[i] = dY[i]; SY[8 + i] = dvu[i];
-                if (i < 2) SY[6 + i] = dvl[i];
+            for (int i = 0; i < RM_NQ; ++i) {
+                SY[q0 + i] = dY[i]; SY[8 + q0 + i] = dvu[i];
+                if (tw[i]) SY[6 + i] = dvl[i];
             }
         }
         float amax_f = (float)amax, az_f = (float)az;
@@ -695,15 +709,15 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         // ---------------- filter line search -------------------------------------------------
         auto barrier_args = [&](const double* uu, const double* ss) {
             double pa = 1.0;
-            if (uon) {
-                pa = (uu[0] - lo) * (hi - uu[0]) * (uu[1] - lo) * (hi - uu[1]);
-                pa *= (ss[0] - sL[0]) * (sU[0] - ss[0]) * (ss[1] - sL[1]) * (sU[1] - ss[1]);
+            if (uon) {   // the tilt box and the du rows' lower bounds on the node lane, upper bounds of its rows on each
+                const double pb = (uu[0] - lo) * (hi - uu[0]) * (uu[1] - lo) * (hi - uu[1]) * ((ss[0] - sL[0]) * (ss[1] - sL[1]));
+                pa = nod ? pb : 1.0;
 #pragma unroll
-                for (int i = 2; i < RM_NIQ; ++i) pa *= sU[i] - ss[i];
+                for (int i = 0; i < RM_NQ; ++i) pa *= sU[i] - ss[i];
             }
             return pa;
         };
-        double phil = sc * cost_val(x, u, up), gtdl = 0.0;
+        double phil = nod ? sc * cost_val(x, u, up) : 0.0, gtdl = 0.0;
         {
             const double pa = barrier_args(u, s);
             phil -= uon ? mu * log_fast(pa) : 0.0;
@@ -712,11 +726,11 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) gq[j] *= sc;
 #pragma unroll
-            for (int i = 0; i < 6; ++i) gtdl += xon ? gq[i] * dx[i] : 0.0;
+            for (int i = 0; i < 6; ++i) gtdl += nod && xon ? gq[i] * dx[i] : 0.0;
             if (uon) {
-                gtdl += (gq[6] - mu * isl0 + mu * isu0) * dU[0] + (gq[7] - mu * isl1 + mu * isu1) * dU[1];
+                if (nod) gtdl += (gq[6] - mu * isl0 + mu * isu0) * dU[0] + (gq[7] - mu * isl1 + mu * isu1) * dU[1];
 #pragma unroll
-                for (int i = 0; i < RM_NIQ; ++i) gtdl += SH.SR[sr][1][i] * dS[i];
+                for (int i = 0; i < RM_NQ; ++i) gtdl += SH.SR[sr][1][q0 + i] * dS[i];
             }
         }
         const double phi = wsum_rl(phil), gTd = wsum_rl(gtdl);
@@ -737,33 +751,33 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) tnl = fmaxf(tnl, fabsf((float)dU[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)u[j])));
 #pragma unroll
-            for (int i = 0; i < RM_NIQ; ++i) tnl = fmaxf(tnl, fabsf((float)dS[i]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)s[i])));
+            for (int i = 0; i < RM_NQ; ++i) tnl = fmaxf(tnl, fabsf((float)dS[i]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)s[i])));
         }
         const bool tiny = wmaxf(tnl) < 2.2e-15f;
         STAMP(6);
         int ls = 0;
         for (; ls < 80; ++ls) {
-            double xt[4], pt[2], ut[2], st_[RM_NIQ], gt[6];
+            double xt[4], pt[2], ut[2], st_[RM_NQ], gt[6];
 #pragma unroll
             for (int i = 0; i < 4; ++i) xt[i] = fma(alpha, dx[i], x[i]);
             pt[0] = fma(alpha, dx[4], up[0]); pt[1] = fma(alpha, dx[5], up[1]);
             ut[0] = fma(alpha, dU[0], u[0]); ut[1] = fma(alpha, dU[1], u[1]);
 #pragma unroll
-            for (int i = 0; i < RM_NIQ; ++i) st_[i] = fma(alpha, dS[i], s[i]);
+            for (int i = 0; i < RM_NQ; ++i) st_[i] = fma(alpha, dS[i], s[i]);
             defects(xt, pt, ut, gt);
-            double zt[8] = {xt[0], xt[1], xt[2], xt[3], pt[0], pt[1], ut[0], ut[1]}, ct[RM_NIQ];
-            rm_iq(zt, vmax, ct);
+            double zt[8] = {xt[0], xt[1], xt[2], xt[3], pt[0], pt[1], ut[0], ut[1]}, ct[RM_NQ];
+            rm_iq3(zt, vmax, mir, ct);
             double thl = 0.0;
 #pragma unroll
-            for (int i = 0; i < 6; ++i) thl += xon ? fabs(gt[i]) : 0.0;
+            for (int i = 0; i < 6; ++i) thl += nod && xon ? fabs(gt[i]) : 0.0;
 #pragma unroll
-            for (int i = 0; i < RM_NIQ; ++i) thl += uon ? fabs(ct[i] - st_[i]) : 0.0;
-            double phl = sc * cost_val(xt, ut, pt);
+            for (int i = 0; i < RM_NQ; ++i) thl += uon ? fabs(ct[i] - st_[i]) : 0.0;
+            double phl = nod ? sc * cost_val(xt, ut, pt) : 0.0;
             phl -= uon ? mu * log_fast(barrier_args(ut, st_)) : 0.0;
             th_t = wsum_rl(thl); ph_t = wsum_rl(phl);
             if (tiny) { accepted = true; ftype = true; break; }
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
-            in_filter = in_filter || wany(k < nfilt && th_t >= fth && ph_t >= fph);
+            in_filter = in_filter || wany(lane < nfilt && th_t >= fth && ph_t >= fph);
             if (!in_filter) {
                 const bool sw = gTd < 0.0 && lg2(alpha) > lg_sw;
                 if (theta <= th_min && sw) {
@@ -780,7 +794,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         STAMP(7);
         if (!accepted) { status = -2; break; }
         if (!ftype && nfilt < kWave) {
-            if (k == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
+            if (lane == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
             ++nfilt;
         }
         // ---------------- accept ------------------------------------------------------------
@@ -799,13 +813,13 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
                 zu[j] = fmax(fmin(fma(az, dzu[j], zu[j]), 1e10 * mu * iu), 1e-10 * mu * iu);
             }
 #pragma unroll
-            for (int i = 0; i < RM_NIQ; ++i) {
+            for (int i = 0; i < RM_NQ; ++i) {
                 s[i] = fma(alpha, dS[i], s[i]);
-                yq[i] = fma(alpha, SY[i], yq[i]);
+                yq[i] = fma(alpha, SY[q0 + i], yq[i]);
                 const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
-                const double idl = i < 2 ? frcp(dl) : 0.0, idu = frcp(du_);
-                if (i < 2) vl[i] = fmax(fmin(fma(az, SY[6 + i], vl[i]), 1e10 * mu * idl), 1e-10 * mu * idl);
-                vu[i] = fmax(fmin(fma(az, SY[8 + i], vu[i]), 1e10 * mu * idu), 1e-10 * mu * idu);
+                const double idl = tw[i] ? frcp(dl) : 0.0, idu = frcp(du_);
+                if (tw[i]) vl[i] = fmax(fmin(fma(az, SY[6 + i], vl[i]), 1e10 * mu * idl), 1e-10 * mu * idl);
+                vu[i] = fmax(fmin(fma(az, SY[8 + q0 + i], vu[i]), 1e10 * mu * idu), 1e-10 * mu * idu);
             }
         }
         theta = th_t;
@@ -813,18 +827,18 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     }
 
     // ---------------- outputs -------------------------------------------------------------
-    const double fval = wsum_rl(cost_val(x, u, up));
-    if (k == 0) {
+    const double fval = wsum_rl(nod ? cost_val(x, u, up) : 0.0);
+    if (lane == 0) {
         a.u0[2 * b] = u[0]; a.u0[2 * b + 1] = u[1];
         a.f[b] = fval; a.status[b] = status; a.iters[b] = it;
     }
     if (a.w_out) {
         double* wo = a.w_out + (size_t)nw * b;
-        if (xon) {
+        if (nod && xon) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) wo[4 * k + i] = x[i];
         }
-        if (uon) { wo[4 * (N + 1) + 2 * k] = u[0]; wo[4 * (N + 1) + 2 * k + 1] = u[1]; }
+        if (nod && uon) { wo[4 * (N + 1) + 2 * k] = u[0]; wo[4 * (N + 1) + 2 * k + 1] = u[1]; }
     }
     STAMP_FLUSH_TO(g_stamp_rm, b);
 }
