@@ -220,12 +220,13 @@ __device__ bool riccati_sweep_aug(L* S, int N) {
     return quu_inverse<NXA>(S->G[0], i00, i01, i11) && ok;
 }
 
-// Gains and closed-loop matrices for the forward sweep, lane per node (lanes 0..N-1):
-// [K | k] = -Quu^-1 Guz, Phi_k = A_k + B_k K_k, f_k = c_k + B_k k_k.  Ends with a barrier.
+// Gains and closed-loop matrices for the forward sweep, lanes k and k + 32 per node (N <= 32): both
+// form [K | k] = -Quu^-1 Guz, lane k writes it, and the rows of Phi_k = A_k + B_k K_k, f_k = c_k + B_k k_k
+// split between them.  Ends with a barrier.
 template <class L>
 __device__ void closed_loop(L* S, int N) {
-    constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND;
-    const int k = threadIdx.x;
+    constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, RH = (NXA + 1) / 2;
+    const int k = threadIdx.x & 31, rb = threadIdx.x >= 32 ? RH : 0;
     if (k < N) {
         // LDS reads grouped ahead of the writes (the compiler cannot prove F, KK and M disjoint and
         // would otherwise wait out each read before the next write)
@@ -241,10 +242,13 @@ __device__ void closed_loop(L* S, int N) {
             K0[p] = -fma(i00, gu0[p], i01 * gu1[p]);
             K1[p] = -fma(i01, gu0[p], i11 * gu1[p]);
         }
+        if (rb == 0) {
 #pragma unroll
-        for (int p = 0; p < NP; ++p) { S->KK[k][0][p] = K0[p]; S->KK[k][1][p] = K1[p]; }
+            for (int p = 0; p < NP; ++p) { S->KK[k][0][p] = K0[p]; S->KK[k][1][p] = K1[p]; }
+        }
 #pragma unroll
-        for (int r = 0; r < NXA; ++r) {      // row r of M_k read whole before row r of F is written
+        for (int rr = 0; rr < RH; ++rr) {    // row r of M_k read whole before row r of F is written
+            const int r = rb + rr < NXA ? rb + rr : NXA - 1;
             double mr[NXA + 3];
 #pragma unroll
             for (int j = 0; j < NXA + 3; ++j) mr[j] = S->M[k][j < NXA + 2 ? j : ND - 1][r];
