@@ -797,11 +797,13 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
     dartmpc::PmpcArgs a = *args;
     a.pack = (a.B <= 32) ? 8 : 1;          // <= 32 waves fit one XCD's CUs
     // The quadratic scan shortens the dependent chain but needs more registers (one wave per SIMD
-    // instead of two): worth it while every wave has a SIMD of its own (B <= 4 x 256), not beyond.
+    // instead of two): worth it while every wave has a SIMD of its own (B <= 4 x 256) and, measured
+    // (tools/c4_ab.sh), up to ~1.7 k instances, where its second round of waves still finishes before
+    // one round of sequential waves at two per SIMD (B = 1152: 80 against 89 us; 1792: 100 against 97).
     const dim3 grid(a.B * a.pack);
-    static const int qscan_max_b = [] {     // experiment knob: DART_PMPC_QSCAN_MAX_B (default 1024)
+    static const int qscan_max_b = [] {     // experiment knob: DART_PMPC_QSCAN_MAX_B (default 1664)
         const char* e = getenv("DART_PMPC_QSCAN_MAX_B");
-        return e ? atoi(e) : 1024;
+        return e ? atoi(e) : 1664;
     }();
     if (a.N <= 15 && a.B <= qscan_max_b)
         return dartmpc_launch_pmpc_seq(&a, grid.x, stream, 1);

@@ -134,7 +134,7 @@ def test_wide_tilt_box_library_trig_path(dm):
 
 @pytest.mark.parametrize("N", [15, 16, 20, 23, 24, 31])
 def test_scan_and_sequential_riccati_agree(dm, N):
-    """The launcher runs the quadratic Riccati part as a DPP scan for B <= 1024 and as the sequential
+    """The launcher runs the quadratic Riccati part as a DPP scan for B <= 1664 and as the sequential
     sweep beyond (throughput regime).  The same 1152 instances solved as one launch of 2304 (sequential;
     every instance twice) and as 64 launches of 18 (scan) take the same iterations and agree to 1e-9.
     N covers every scan instantiation: one-row (N <= 15, the DART driver's horizon), SHORT2
