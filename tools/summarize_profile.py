@@ -68,7 +68,19 @@ if stats:
         for row in csv.DictReader(fh):
             k = short(row["Name"])
             if k and STATS_NAME.get(k, k) in row["Name"]:
-                avg[k] = {"calls": int(row["Calls"]), "average_ns": float(row["AverageNs"])}
+                avg[k] = {"calls_all_grids": int(row["Calls"]), "average_ns_all_grids": float(row["AverageNs"])}
+# the per-launch duration of the headline launches alone (the stats line of a template instance also
+# counts other batch sizes that use it, e.g. C4's 1152 instances on the PMPC scan build)
+traces = glob.glob(os.path.join(SRC, "trace", "**", "*kernel_trace.csv"), recursive=True)
+if traces:
+    dur = defaultdict(list)
+    with open(traces[0]) as fh:
+        for row in csv.DictReader(fh):
+            k = short(row["Kernel_Name"])
+            if k and STATS_NAME.get(k, k) in row["Kernel_Name"] and int(row["Grid_Size_X"]) == GRID[k]:
+                dur[k].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    for k, v in dur.items():
+        avg.setdefault(k, {}).update(calls=len(v), average_ns=sum(v) / len(v))
 for k, d in per.items():
     fk = sum(d["FETCH_SIZE"]) / max(1, len(d["FETCH_SIZE"]))
     wk = sum(d["WRITE_SIZE"]) / max(1, len(d["WRITE_SIZE"]))
