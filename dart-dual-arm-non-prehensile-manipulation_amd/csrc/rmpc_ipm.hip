@@ -54,17 +54,11 @@ struct RmShared {
     double theta[14];
     double rls_Pphi[2][7], rls_phiP[2][7];
     RmModel model;                            // uniform, read at the use sites (keeps VGPRs free)
-    union {
-        NodeArr<double[4][4], RM_NMAXS + 1> SC;   // per node (row 32: idle lanes), per RK stage: d f1,3 / d vx,vy
-        // [Sigma, psi, r] of the slack rows, parked from the QP build to the slack steps (SC is dead
-        // then; the kernel runs at the register limit)
-        NodeArr<double[3][RM_NIQ], RM_NMAXS + 1> SR;
-    };
-    NodeArr<double[4][2], RM_NMAXS + 1> SD;   // tanh curvature per stage -> adjoint-weighted coefficients
+    // [Sigma, psi, r] of the slack rows (node lane: rows 0..2, mirror lane: 3..5), parked from the QP
+    // build to the slack steps (the kernel runs at the register limit)
+    NodeArr<double[3][RM_NIQ], RM_NMAXS + 1> SR;
     NodeArr<double[8], RM_NMAXS + 1> JL;      // J^T lambda staging, primal residual maxima
-    NodeArr<double[10], RM_NMAXS + 1> DL;     // per node: lambda_{k+1}, tilt curvature, g cos(u) for the mirror lanes
 };
-static_assert(sizeof(NodeArr<double[3][RM_NIQ], RM_NMAXS + 1>) <= sizeof(NodeArr<double[4][4], RM_NMAXS + 1>), "SR fits SC");
 
 // continuous model (np_mpc...:178-186); also returns d f / d vx|vy of rows 1, 3 and tanh values
 __device__ __forceinline__ void rm_f(const RmModel& m, const double* y, double sa, double sb, double* f,
@@ -215,21 +209,11 @@ __device__ __forceinline__ double rm_direction(const RmModel& m, const double (*
     return dot;
 }
 
-// directions d0 .. d0+2 of one node (the two half-waves of the wave split the six directions);
-// per-node inputs from LDS: dl = [lambda_{k+1}(6), huu(2), g cos a, g cos b]
-__device__ __forceinline__ void rm_directions(const RmModel& m, const double (*sc)[4], const double (*cv)[2],
-                                              const double* dl, int d0, double* Mk, double* Hk, double* jl_lds) {
-    double lamn[6], huu[2], scr[4][4], cvr[4][2];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) lamn[i] = dl[i];
-    huu[0] = dl[6]; huu[1] = dl[7];
-    const double gca = dl[8], gcb = dl[9];
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {       // stage data to registers once for the three directions
-#pragma unroll
-        for (int i = 0; i < 4; ++i) scr[st][i] = sc[st][i];
-        cvr[st][0] = cv[st][0]; cvr[st][1] = cv[st][1];
-    }
+// directions d0 .. d0+2 of one node (the node and mirror lanes split the six directions), from the
+// stage data of this lane's RK4 pass
+__device__ __forceinline__ void rm_directions(const RmModel& m, const double (*scr)[4], const double (*cvr)[2],
+                                              const double* lamn, const double* huu, double gca, double gcb, int d0,
+                                              double* Mk, double* Hk, double* jl_lds) {
     RmModel mr;
 #pragma unroll
     for (int i = 0; i < 14; ++i) mr.th[i] = m.th[i];
@@ -452,18 +436,14 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             double sa, ca, sb, cb;
             tilt_sincos(poly, u[0], sa, ca);
             tilt_sincos(poly, u[1], sb, cb);
-            double xn[4], huu[2];
-            rm_rk4_lin(m, x, sa, sb, xn, SH.SC[sr], SH.SD[sr]);
-            rm_adjoint_curv(m, SH.SC[sr], SH.SD[sr], lamn, sa, sb, huu);
-            if (nod) {
-#pragma unroll
-                for (int i = 0; i < 6; ++i) SH.DL[k][i] = lamn[i];
-                SH.DL[k][6] = huu[0]; SH.DL[k][7] = huu[1]; SH.DL[k][8] = m.gz * ca; SH.DL[k][9] = m.gz * cb;
-            }
-            __syncthreads();
+            // the RK4 stage data stay in registers through the adjoint and the three directions of
+            // this lane (lanes k and k + 32 hold the same node: each has them without an LDS pass)
+            double xn[4], huu[2], scr[4][4], sdr[4][2];
+            rm_rk4_lin(m, x, sa, sb, xn, scr, sdr);
+            rm_adjoint_curv(m, scr, sdr, lamn, sa, sb, huu);
             STAMP(11);
             // lanes k and k + 32 own directions 0..2 and 3..5 of node k
-            if (uon) rm_directions(m, SH.SC[k], SH.SD[k], SH.DL[k], mir ? 3 : 0, &S->M[k][0][0], S->H[k], SH.JL[k]);
+            if (uon) rm_directions(m, scr, sdr, lamn, huu, m.gz * ca, m.gz * cb, mir ? 3 : 0, Mk, Hk, SH.JL[k]);
             __syncthreads();
             STAMP(12);
 #pragma unroll
