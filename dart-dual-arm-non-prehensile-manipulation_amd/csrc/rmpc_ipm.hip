@@ -379,8 +379,8 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     // incoming defect g_k of node k (6 rows: physical 4 + up copy 2) for a trial point
     auto defects = [&](const double* xx, const double* pp, const double* uu, double* g) {
         double sa, ca, sb, cb, xn[4];
-        tilt_sincos(poly, uu[0], sa, ca);
-        tilt_sincos(poly, uu[1], sb, cb);
+        tilt_sincos_econ(poly, uu[0], sa, ca);
+        tilt_sincos_econ(poly, uu[1], sb, cb);
         rm_rk4(m, xx, sa, sb, xn);
         double f[6];
 #pragma unroll
@@ -434,8 +434,8 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         double jl[6];            // J^T lambda_{k+1} (x columns 0..3, tilt 4..5)
         {
             double sa, ca, sb, cb;
-            tilt_sincos(poly, u[0], sa, ca);
-            tilt_sincos(poly, u[1], sb, cb);
+            tilt_sincos_econ(poly, u[0], sa, ca);
+            tilt_sincos_econ(poly, u[1], sb, cb);
             // the RK4 stage data stay in registers through the adjoint and the three directions of
             // this lane (lanes k and k + 32 hold the same node: each has them without an LDS pass)
             double xn[4], huu[2], scr[4][4], sdr[4][2];
