@@ -38,6 +38,7 @@ namespace dartmpc {
 constexpr int RM_NMAXS = 32;      // max shooting nodes (N <= 31)
 constexpr int RM_NIQ = 6;         // inequality rows per node: du_x, du_y, vx-vmax, -vx-vmax, vy-vmax, -vy-vmax
 constexpr int RM_NQ = 3;          // of them per lane: rows 0..2 on lane k, rows 3..5 on its mirror lane k + 32
+static_assert(2 * RM_NQ == RM_NIQ, "the node and mirror lanes split the rows evenly");
 using RmLds = OcpLds<6, RM_NMAXS>;
 
 #ifdef DART_STAMPS
@@ -54,9 +55,6 @@ struct RmShared {
     double theta[14];
     double rls_Pphi[2][7], rls_phiP[2][7];
     RmModel model;                            // uniform, read at the use sites (keeps VGPRs free)
-    // [Sigma, psi, r] of the slack rows (node lane: rows 0..2, mirror lane: 3..5), parked from the QP
-    // build to the slack steps (the kernel runs at the register limit)
-    NodeArr<double[3][RM_NIQ], RM_NMAXS + 1> SR;
     NodeArr<double[8], RM_NMAXS + 1> JL;      // J^T lambda staging, primal residual maxima
 };
 
@@ -241,7 +239,6 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     const int lane = threadIdx.x;
     const int k = lane & 31;
     const bool mir = lane >= 32, nod = !mir;
-    const int q0 = mir ? RM_NQ : 0;           // first slack row of this lane
     const int N = a.N;
     const bool xon = k <= N, uon = k < N;
     const double* pr = a.prm + 10 * b;
@@ -574,10 +571,6 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) Hk[hp(8, j)] = gq[j];
             }
-#pragma unroll
-            for (int i = 0; i < RM_NQ; ++i) {
-                SH.SR[sr][0][q0 + i] = sig[i]; SH.SR[sr][1][q0 + i] = psi[i]; SH.SR[sr][2][q0 + i] = rq[i];
-            }
             if (k == N && nod) {   // terminal surrogate G_N: value function [[Q_N, q_N], [q_N^T, 0]], Quu = I
                 double* GN = S->G[N];
                 for (int e = 0; e < tri(9); ++e) GN[e] = 0.0;
@@ -640,8 +633,8 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             rm_iq3(dzv, 0.0, mir, cdz);
 #pragma unroll
             for (int i = 0; i < RM_NQ; ++i) {
-                dS[i] = uon ? cdz[i] + SH.SR[sr][2][q0 + i] : 0.0;
-                dY[i] = uon ? SH.SR[sr][0][q0 + i] * dS[i] + SH.SR[sr][1][q0 + i] - yq[i] : 0.0;
+                dS[i] = uon ? cdz[i] + rq[i] : 0.0;
+                dY[i] = uon ? sig[i] * dS[i] + psi[i] - yq[i] : 0.0;
                 const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
                 const double idl = tw[i] ? frcp(dl) : 0.0, idu = frcp(du_);
                 dvl[i] = uon && tw[i] ? fma(mu, idl, -vl[i]) - vl[i] * idl * dS[i] : 0.0;
@@ -668,16 +661,6 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
                 if (dS[i] > 0) amax = fmin(amax, tau * (sU[i] - s[i]) * frcp(dS[i]));
                 if (tw[i] && dvl[i] < 0) az = fmin(az, -tau * vl[i] * frcp(dvl[i]));
                 if (dvu[i] < 0) az = fmin(az, -tau * vu[i] * frcp(dvu[i]));
-            }
-        }
-        // [dY, dvl, dvu] parked until the accept in the node's closed-loop rows (dead after the
-        // forward sweep until the next iteration)
-        double* SY = &S->F[uon ? k : 0][0][0];
-        if (uon) {
-#pragma unroll
-            for (int i = 0; i < RM_NQ; ++i) {
-                SY[q0 + i] = dY[i]; SY[8 + q0 + i] = dvu[i];
-                if (tw[i]) SY[6 + i] = dvl[i];
             }
         }
         float amax_f = (float)amax, az_f = (float)az;
@@ -710,7 +693,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             if (uon) {
                 if (nod) gtdl += (gq[6] - mu * isl0 + mu * isu0) * dU[0] + (gq[7] - mu * isl1 + mu * isu1) * dU[1];
 #pragma unroll
-                for (int i = 0; i < RM_NQ; ++i) gtdl += SH.SR[sr][1][q0 + i] * dS[i];
+                for (int i = 0; i < RM_NQ; ++i) gtdl += psi[i] * dS[i];
             }
         }
         const double phi = wsum_rl(phil), gTd = wsum_rl(gtdl);
@@ -795,11 +778,11 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 #pragma unroll
             for (int i = 0; i < RM_NQ; ++i) {
                 s[i] = fma(alpha, dS[i], s[i]);
-                yq[i] = fma(alpha, SY[q0 + i], yq[i]);
+                yq[i] = fma(alpha, dY[i], yq[i]);
                 const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
                 const double idl = tw[i] ? frcp(dl) : 0.0, idu = frcp(du_);
-                if (tw[i]) vl[i] = fmax(fmin(fma(az, SY[6 + i], vl[i]), 1e10 * mu * idl), 1e-10 * mu * idl);
-                vu[i] = fmax(fmin(fma(az, SY[8 + q0 + i], vu[i]), 1e10 * mu * idu), 1e-10 * mu * idu);
+                if (tw[i]) vl[i] = fmax(fmin(fma(az, dvl[i], vl[i]), 1e10 * mu * idl), 1e-10 * mu * idl);
+                vu[i] = fmax(fmin(fma(az, dvu[i], vu[i]), 1e10 * mu * idu), 1e-10 * mu * idu);
             }
         }
         theta = th_t;
