@@ -66,7 +66,6 @@ struct LmSub {
 
 struct LmShared {
     LmLds ocp;
-    NodeArr<double[7], 2 * LM_NMAXS> JL;     // J^T lambda_{k+1} (x 4, u 1), primal residual maxima
     NodeArr<double[5], 2 * LM_NMAXS> CS;     // second-order correction: c_soc rows of node k (incoming defect)
     NodeArr<double[11], 2 * LM_NMAXS> SV;    // second-order correction: the plain step (dx~, lambda+, du)
     LmSub sub[2];                   // uniform problem data of the two halves
@@ -487,6 +486,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
 #pragma unroll
         for (int i = 0; i < 5; ++i) { const double t = from_next(lam[i]); lamn[i] = uon ? t : 0.0; }
         double jl[5];       // J^T lambda_{k+1} (x columns 0..3, tilt 4)
+        double pinf, pinf_u;  // primal residual maxima
         {
             double xn[4];
             if (it == 0) {      // the setup's derivative pass (lambda = 0: J^T lambda = 0)
@@ -510,10 +510,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     const double cu = sc * 2.0 * (Ru + Rdu) + zl * isl + zu * isu;
 #pragma unroll
                     for (int d = 0; d < 5; ++d)
-                        SH.JL[sl][d] = sub_direction(mr, scr, cvr, huu, LM_G * ca, d, lamn, Mk, Hk,
-                                                     d < 4 ? sc * 2.0 * Wq[d] : cu);
-#pragma unroll
-                    for (int d = 0; d < 5; ++d) jl[d] = SH.JL[sl][d];
+                        jl[d] = sub_direction(mr, scr, cvr, huu, LM_G * ca, d, lamn, Mk, Hk, d < 4 ? sc * 2.0 * Wq[d] : cu);
                     Hk[hp(4, 4)] = sc * 2.0 * Rdu;
                     Hk[hp(5, 4)] = -sc * 2.0 * Rdu;
                 } else {
@@ -545,10 +542,9 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 if (k == 0) S->dx0[hf][i] = -gi;
                 SH.CS[sl][i] = gi;       // c(x) for a second-order correction
             }
-            SH.JL[sl][5] = pl; SH.JL[sl][6] = plu;      // primal residual maxima (LDS: frees registers)
+            pinf = pl; pinf_u = plu;
         }
         double dinf = 0.0, c0 = 0.0, cmin = 1e300, suml = 0.0, sumz = 0.0;
-        double pinf = SH.JL[sl][5], pinf_u = SH.JL[sl][6];
         {
             double gl[6];
             cost_grad(x, u, up, gl);
