@@ -495,30 +495,30 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
 #pragma unroll
                 for (int i = 0; i < 5; ++i) jl[i] = 0.0;
             } else {
-            double sa, ca;
-            tilt_sincos_econ(poly, u, sa, ca);
-            // stage data of the RK4 pass stay in registers through the adjoint and the five directions
-            double scr[4][LM_NSC], cvr[4][4];
-            sub_rk4_lin(m, x, sa, xn, scr, cvr);
-            {
-                const double huu = sub_adjoint_curv(m, scr, cvr, lamn, sa);
-                STAMP(13);
-                // exact dynamics Hessian (x, u blocks) and the Jacobian columns of node k
-                if (uon) {
-                    const LmSub mr = m;     // model to registers once for the five directions
-                    // with the cost / barrier terms of z = [x(4), up, u, 1] on the diagonal (gradient row later)
-                    const double cu = sc * 2.0 * (Ru + Rdu) + zl * isl + zu * isu;
+                double sa, ca;
+                tilt_sincos_econ(poly, u, sa, ca);
+                // stage data of the RK4 pass stay in registers through the adjoint and the five directions
+                double scr[4][LM_NSC], cvr[4][4];
+                sub_rk4_lin(m, x, sa, xn, scr, cvr);
+                {
+                    const double huu = sub_adjoint_curv(m, scr, cvr, lamn, sa);
+                    STAMP(13);
+                    // exact dynamics Hessian (x, u blocks) and the Jacobian columns of node k
+                    if (uon) {
+                        const LmSub mr = m;     // model to registers once for the five directions
+                        // with the cost / barrier terms of z = [x(4), up, u, 1] on the diagonal (gradient row later)
+                        const double cu = sc * 2.0 * (Ru + Rdu) + zl * isl + zu * isu;
 #pragma unroll
-                    for (int d = 0; d < 5; ++d)
-                        jl[d] = sub_direction(mr, scr, cvr, huu, LM_G * ca, d, lamn, Mk, Hk, d < 4 ? sc * 2.0 * Wq[d] : cu);
-                    Hk[hp(4, 4)] = sc * 2.0 * Rdu;
-                    Hk[hp(5, 4)] = -sc * 2.0 * Rdu;
-                } else {
+                        for (int d = 0; d < 5; ++d)
+                            jl[d] = sub_direction(mr, scr, cvr, huu, LM_G * ca, d, lamn, Mk, Hk, d < 4 ? sc * 2.0 * Wq[d] : cu);
+                        Hk[hp(4, 4)] = sc * 2.0 * Rdu;
+                        Hk[hp(5, 4)] = -sc * 2.0 * Rdu;
+                    } else {
 #pragma unroll
-                    for (int i = 0; i < 5; ++i) jl[i] = 0.0;
+                        for (int i = 0; i < 5; ++i) jl[i] = 0.0;
+                    }
+                    STAMP(14);
                 }
-                STAMP(14);
-            }
             }
             // outgoing augmented defect c_k = [F(z_k); u_k] - x~_{k+1} -> defect column of M~
             double cdef[5];
