@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=18, help="instances per step per GPU (18 = the metric's config)")
     ap.add_argument("--N", type=int, default=20)
     ap.add_argument("--tol", type=float, default=1e-8)
+    ap.add_argument("--pmpc-path", default="ipopt", choices=("ipopt", "reduced"),
+                    help="PMPC path: IPOPT's iterates on the full NLP (default, the drop-in) or the reduced opt-in")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-calls", type=int, default=200, help="calls of the host-pointer (PCIe-inclusive) path")
@@ -151,7 +153,7 @@ def bench_pmpc_driver_horizon(args, torch, dev, stream, dart_mpc, N=15):
     FV = torch.empty((K + 5, B), dtype=torch.float64, device=dev)
     ST = torch.empty((K + 5, B), dtype=torch.int32, device=dev)
     IT = torch.empty((K + 5, B), dtype=torch.int32, device=dev)
-    s = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=B, device=dev.index)
+    s = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=B, device=dev.index, path=args.pmpc_path)
     sp = stream.cuda_stream
 
     def launch(i):
@@ -222,7 +224,7 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False):
     IT = torch.empty(n, dtype=torch.int32, device=dev)
     block = torch.zeros((per, RESULT_COLS), dtype=dt64, device=dev)
     full = torch.zeros((world * per, RESULT_COLS), dtype=dt64, device=dev)
-    solver = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=max(1, n), device=dev.index)
+    solver = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=max(1, n), device=dev.index, path=args.pmpc_path)
     sp = stream.cuda_stream
 
     def step(gather=True):
@@ -539,7 +541,7 @@ def main():
     ST = torch.empty((W + K, B), dtype=torch.int32, device=dev)
     IT = torch.empty((W + K, B), dtype=torch.int32, device=dev)
 
-    solver = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=B, device=local)
+    solver = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=B, device=local, path=args.pmpc_path)
     stream = torch.cuda.Stream(device=dev)
     sp = stream.cuda_stream
 
@@ -625,7 +627,7 @@ def main():
         sx = torch.tensor(S[:Bs], device=dev); st_ = torch.tensor(T[:Bs], device=dev); spr = torch.tensor(P[:Bs], device=dev)
         su = torch.empty((Bs, 2), dtype=torch.float64, device=dev); sf = torch.empty(Bs, dtype=torch.float64, device=dev)
         ss = torch.empty(Bs, dtype=torch.int32, device=dev); si = torch.empty(Bs, dtype=torch.int32, device=dev)
-        big = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=Bs, device=local)
+        big = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=Bs, device=local, path=args.pmpc_path)
         for rep in range(3):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -645,7 +647,7 @@ def main():
     # supplementary host-pointer path (dart_mpc_solve_batch): H2D copies + solve + D2H + sync per call
     host_path = None
     if rank == 0 and args.host_calls > 0:
-        hs = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=B, device=local)
+        hs = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=B, device=local, path=args.pmpc_path)
         S, T, P = steps_in[W]
         for _ in range(5):
             hs.solve_batch(S, T, P)

@@ -159,9 +159,13 @@ struct dart_mpc_handle {
     hipStream_t stream = nullptr;
     HostStage st;                  // staging of the host-pointer entries
     std::string err;
-    int32_t seq = 0;               // completion-word sequence of the host-pointer PMPC entry
-    int32_t* hdone = nullptr;      // PMPC: B_max completion words, mapped host memory (only ever
-    int32_t* ddone = nullptr;      //   hold sequence numbers of earlier calls) and their device address
+    uint32_t seq = 0;              // completion-word sequence of the host-pointer PMPC entry (wraps, skips 0)
+    uint32_t* hdone = nullptr;     // PMPC: B_max completion words, mapped host memory (only ever
+    uint32_t* ddone = nullptr;     //   hold 0 or sequence numbers of earlier calls) and their device address
+    // the host PMPC entry returns once every completion word is visible, possibly before the stream
+    // has retired the kernel's last instructions: the next entry on the handle settles that stream
+    // first, so a late stream error is reported as the previous call's, not blamed on the new one
+    hipStream_t pending = nullptr;
     // Serialises the entries on this handle: the host-pointer entries share the pinned staging
     // buffers and the handle's stream, and every entry may write err.  Concurrent callers (the
     // reference runs controllers on background threads, RMPC/dev_dual/controller/convimp.py:435)
@@ -194,13 +198,27 @@ int check_cfg(const dart_mpc_config* c) {
     if (!(c->Ts > 0.0) || !(c->tol > 0.0) || !(c->gravity == c->gravity) || c->max_iter < 1 || c->B_max < 1) return 0;
     if (c->acceptable_iter < 0 || (c->acceptable_iter > 0 && !(c->acceptable_tol > 0.0))) return 0;
     if (c->max_soc < 0 || c->max_soc > 8) return 0;
+    if (c->pmpc_path != 0 && c->pmpc_path != 1) return 0;
     return 1;
+}
+
+// settle the stream of an earlier host PMPC call that returned on its completion words (see
+// dart_mpc_handle::pending)
+int settle_pending(dart_mpc_handle* h) {
+    if (!h->pending) return DART_MPC_OK;
+    hipStream_t s = h->pending;
+    h->pending = nullptr;
+    hipError_t e = hipStreamQuery(s);
+    if (e == hipErrorNotReady) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail(h, DART_MPC_EHIP, "previous PMPC call's stream", e);
+    return DART_MPC_OK;
 }
 
 int launch(dart_mpc_handle* h, int B, const double* x0, const double* ref, const double* prm, const double* w_warm,
            double* u0, double* f, double* w_out, int32_t* status, int32_t* iters, hipStream_t s) {
     dartmpc::PmpcArgs a;
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter; a.g = h->cfg.gravity;
+    a.max_soc = h->cfg.max_soc; a.reduced = h->cfg.pmpc_path;
     a.x0 = x0; a.ref = ref; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     a.done = nullptr; a.seq = 0;
@@ -212,7 +230,7 @@ int launch(dart_mpc_handle* h, int B, const double* x0, const double* ref, const
 // every instance with a system-scope release).  Spinning on them returns as soon as the last store
 // lands, without the stream-completion round trip; the stream is queried now and then, and if it is
 // done (or failed) without every word set, the stream's own status decides.
-int wait_done(dart_mpc_handle* h, hipStream_t s, const volatile int32_t* done, int B, int32_t seq) {
+int wait_done(dart_mpc_handle* h, hipStream_t s, const volatile uint32_t* done, int B, uint32_t seq) {
     for (unsigned n = 1;; ++n) {
         int b = 0;
         while (b < B && __atomic_load_n(done + b, __ATOMIC_ACQUIRE) == seq) ++b;
@@ -242,6 +260,7 @@ void dart_mpc_config_default(dart_mpc_config* c) {
     c->acceptable_tol = 1e-6;      // IPOPT defaults
     c->acceptable_iter = 15;
     c->max_soc = 4;
+    c->pmpc_path = 0;
 }
 
 int dart_mpc_nw(int N) { return 6 * (N + 1) + 2 * N; }
@@ -283,9 +302,9 @@ int dart_mpc_create(const dart_mpc_config* cfg, int device, dart_mpc_handle** ou
     if (e == hipSuccess)
         e = h->st.reserve(zc ? A : nin * sizeof(double) + A, nout * sizeof(double) + A, zc ? nin * sizeof(double) + A : 0);
     if (e == hipSuccess && zc) {
-        e = hipHostMalloc((void**)&h->hdone, sizeof(int32_t) * B, hipHostMallocMapped | hipHostMallocCoherent);
+        e = hipHostMalloc((void**)&h->hdone, sizeof(uint32_t) * B, hipHostMallocMapped | hipHostMallocCoherent);
         if (e == hipSuccess) {
-            std::memset(h->hdone, 0, sizeof(int32_t) * B);
+            std::memset(h->hdone, 0, sizeof(uint32_t) * B);
             e = hipHostGetDevicePointer((void**)&h->ddone, h->hdone, 0);
         }
     }
@@ -307,6 +326,7 @@ int dart_mpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* x0, const 
         return fail(h, DART_MPC_EINVAL, "null pointer or negative batch");
     if (B == 0) return DART_MPC_OK;
     HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    if (int rc = settle_pending(h)) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     return launch(h, B, x0, ref, prm, w_warm, u0, f, w_out, status, iters, s);
 }
@@ -322,6 +342,7 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     if (B > h->cfg.B_max) return fail(h, DART_MPC_EINVAL, "batch larger than B_max");
     if (B == 0) return DART_MPC_OK;
     HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    if (int rc = settle_pending(h)) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     const size_t nw = (size_t)dart_mpc_nw(h->cfg.N);
     HostStage& S = h->st;
@@ -337,16 +358,22 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     double* d_wo = w_out ? S.out<double>(nw * B) : nullptr;
     int32_t* d_st = S.out<int32_t>(B);
     int32_t* d_it = S.out<int32_t>(B);
-    int32_t* d_done = h->ddone;
+    uint32_t* d_done = h->ddone;
     HIPCHK(h, S.upload(s), "copy inputs");
     dartmpc::PmpcArgs a;
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter; a.g = h->cfg.gravity;
+    a.max_soc = h->cfg.max_soc; a.reduced = h->cfg.pmpc_path;
     a.x0 = d_x0; a.ref = d_ref; a.prm = d_prm; a.w_warm = d_ww;
     a.u0 = d_u0; a.f = d_f; a.w_out = d_wo; a.status = d_st; a.iters = d_it;
-    a.done = d_done; a.seq = ++h->seq;
+    if (++h->seq == 0) {            // wrapped: clear the words so that no stale one can match
+        std::memset(h->hdone, 0, sizeof(uint32_t) * h->cfg.B_max);
+        h->seq = 1;
+    }
+    a.done = d_done; a.seq = h->seq;
     HIPCHK(h, dartmpc_launch_pmpc(&a, s), "kernel launch");
     const int rc = wait_done(h, s, h->hdone, B, a.seq);
     if (rc) return rc;
+    h->pending = s;
     S.take(u0, d_u0, 2 * B); S.take(f, d_f, B); S.take(w_out, d_wo, nw * B);
     S.take(status, d_st, B); S.take(iters, d_it, B);
     return DART_MPC_OK;
@@ -670,16 +697,17 @@ int dart_rls_update_batch(int B, double* theta, double* P, const double* phi, co
 int dart_mpc_sync(dart_mpc_handle* h) {
     if (!h) return DART_MPC_EINVAL;
     std::unique_lock<std::recursive_mutex> lock_(h->mu);
+    if (int rc = settle_pending(h)) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
     return DART_MPC_OK;
 }
 
-// internal self-test of the wave primitives (not in include/dart_mpc.h): host_out[201]
+// internal self-test of the wave primitives (not in include/dart_mpc.h): host_out[265]
 int dartmpc_selftest(double* host_out) {
     double* d = nullptr;
-    if (hipMalloc(&d, 201 * sizeof(double)) != hipSuccess) return DART_MPC_EHIP;
+    if (hipMalloc(&d, 265 * sizeof(double)) != hipSuccess) return DART_MPC_EHIP;
     hipError_t e = dartmpc_wave_selftest(d, nullptr);
-    if (e == hipSuccess) e = hipMemcpy(host_out, d, 201 * sizeof(double), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(host_out, d, 265 * sizeof(double), hipMemcpyDeviceToHost);
     (void)hipFree(d);
     return e == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
 }

@@ -9,6 +9,8 @@ struct PmpcArgs {
     int B, N;
     double Ts, tol, g;      // g = model.opt.gravity[2]
     int max_iter;
+    int max_soc;            // IPOPT max_soc: second-order corrections after a rejected first trial (default 4)
+    int reduced;            // 1: the reduced (x, y) path (dart_mpc_config.pmpc_path), 0: IPOPT's path
     int pack;               // blocks per instance slot: 8 packs a small batch onto one XCD (launcher)
     const double* x0;       // [B][6]   device
     const double* ref;      // [B][6]
@@ -22,8 +24,8 @@ struct PmpcArgs {
     // host-pointer entry only: completion word per instance in mapped host memory, set to `seq`
     // after every other output of the instance is visible system-wide (the host polls it instead of
     // waiting for the stream); nullptr on the device entry
-    int32_t* done;          // [B] or nullptr
-    int32_t seq;
+    uint32_t* done;         // [B] or nullptr
+    uint32_t seq;           // wraps modulo 2^32 (defined unsigned arithmetic); never 0 (0 = cleared word)
 };
 
 }  // namespace dartmpc

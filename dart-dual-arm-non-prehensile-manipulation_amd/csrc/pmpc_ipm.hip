@@ -4,23 +4,26 @@
 // PMPC.solve (PMPC/src/controller/mpc_3d.py:115-138) for a whole batch of
 // independent tray-tilt NMPC instances.
 //
-// Structure exploited: the reference NLP (mpc_3d.py:28-85)
-// splits into two independent scalar-input optimal-control problems -- the x
-// axis (px, vx; theta_x) and the y axis (py, vy; theta_y) -- plus the cost-free
-// z sub-state (pz, vz), which only follows the controls (its multipliers are
-// zero at every KKT point).  Each axis is linear in its state with input
-// sin(theta):  x+ = Phi x + Gamma sin(theta), Phi/Gamma being exactly the RK4
-// map of mpc_3d.py:99-104 applied to :91-92.  The kernel runs IPOPT's
-// primal-dual barrier method on the (x, y) problem in lock-step (one mu, one
-// step length, one filter, as IPOPT does on the full NLP) and rebuilds the z
-// trajectory by the reference's own RK4 once the controls are final.
+// Structure exploited: the Newton system of the reference NLP
+// (mpc_3d.py:28-85) splits into two independent scalar-input optimal-control
+// problems -- the x axis (px, vx; theta_x) and the y axis (py, vy; theta_y) --
+// plus the cost-free z sub-state (pz, vz).  Each axis is linear in its state
+// with input sin(theta):  x+ = Phi x + Gamma sin(theta), Phi/Gamma being exactly
+// the RK4 map of mpc_3d.py:99-104 applied to :91-92.  z is affine in its state
+// and in vz_new = -g (theta_x^2 + theta_y^2) (:93-97): it carries no cost, so
+// its multipliers stay 0 and it never enters the (x, y) Riccati solve, but its
+// defect rows (:37, :48) are part of IPOPT's constraint violation.  The kernel
+// therefore runs IPOPT's primal-dual barrier method on the FULL 6-state NLP:
+// one mu, one step length, one filter; theta, the primal infeasibility, the
+// tiny-step test and the second-order correction see the z rows, and z moves
+// with its own Newton step (an affine scan driven by the tilt steps).
 //
 // Mapping: one wave64 per instance, lane k <-> shooting node k (0..N, N <= 63).
 // Everything per node lives in VGPRs.  Stage-coupled recursions (Riccati
-// backward sweep, forward state sweep, z rollout) hand 2x2 blocks to the
-// neighbouring lane with DPP wave shifts (wave_shl:1 / wave_shr:1, no LDS);
-// norms and inner products are DPP row reductions + 4 readlanes.  No LDS and
-// no global traffic inside the iteration loop.
+// backward sweep, forward state sweep, z sweep) are DPP scans or hand 2x2
+// blocks to the neighbouring lane with DPP wave shifts (no LDS); norms and
+// inner products are DPP row reductions.  No LDS and no global traffic inside
+// the iteration loop.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -120,6 +123,17 @@ __device__ __forceinline__ void affine_scan_const(double f11, double f12, double
     c1 = fma(f11, q1, fma(f12, q2, c1));
     c2 = fma(f21, q1, fma(f22, q2, c2));
 }
+// the same two levels for scalar affine maps z -> m z + c (the z sub-state's Newton sweep)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void affine1_scan_level(double& m, double& c) {
+    const double pm = dpp_fill<CTRL, ROWMASK, 1>(m), pc = dpp_fill<CTRL, ROWMASK, 0>(c);
+    c = fma(m, pc, c);
+    m = m * pm;
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void affine1_scan_const(double m, double& c) {
+    c = fma(m, dpp_fill<CTRL, ROWMASK, 0>(c), c);
+}
 
 // One level of a suffix scan of 4x4 matrices (T <- T * F, F fetched from lane k + d by DPP
 // row_shl:d, identity where out of range)
@@ -166,7 +180,10 @@ __device__ __forceinline__ void mat4_scan_level(double* T) {
 //   Occupancy: the sequential NAX == 1 build is the throughput variant and must fit two waves per
 //   SIMD (<= 256 registers); the ILP-oriented scheduler of this file (Makefile) would otherwise spend
 //   the whole register file on one wave
-template <int NAX, bool QSCAN, bool ONEROW = false, bool SHORT2 = false>
+//   RED: the reduced (x, y) path (opt-in, dart_mpc_config.pmpc_path = 1): theta, the filter and the
+//   error measures leave the z rows out and there is no second-order correction, z is rolled out from
+//   the final controls.  Same KKT point, fewer iterations, but not IPOPT's iterates.
+template <int NAX, bool QSCAN, bool ONEROW = false, bool SHORT2 = false, bool RED = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu((QSCAN || NAX == 2) ? 1 : 2)))
 void pmpc_ipm_kernel(PmpcArgs a) {
     STAMP_DECL
@@ -183,20 +200,22 @@ void pmpc_ipm_kernel(PmpcArgs a) {
     constexpr bool short2 = SHORT2 && !ONEROW;
     const double h = a.Ts;
 
+    // every input is read here, at the start (the host entry hands them over in mapped host memory,
+    // dart_mpc_abi.hip)
     const double* st = a.x0 + 6 * b;
     const double* rf = a.ref + 6 * b;
     const double* pr = a.prm + 6 * b;
     const double mu_f = pr[0], Qp = pr[1], Qv = pr[2], R = pr[3], ulo = pr[4], uhi = pr[5];
-    // every input is read here, at the start (the host entry hands them over in mapped host memory,
-    // dart_mpc_abi.hip); pz / vz are only needed by the final z rollout, so they wait in LDS rather
-    // than in registers through the iteration loop
-    __shared__ double z0[2];
-    if (a.w_out && lane < 2) z0[lane] = st[4 + lane];
 
     // RK4 map of the linear axis model applied to the basis: exact Phi = [[1,a12],[0,a22]], Gamma = [b1,b2]
     double a12, a22, b1, b2;
     axis_rk4(h, a.g, mu_f, 0.0, 0.0, 1.0, a12, a22);
     axis_rk4(h, a.g, mu_f, 1.0, 0.0, 0.0, b1, b2);
+    // the same for the z sub-state, z+ = zA z + zC w with w = vz_new (mpc_3d.py:93-97, RK4 :99-104):
+    // pz+ = pz + cp w, vz+ = av vz + cv w
+    double zp1, zav, zcp, zcv;
+    z_rk4(h, 0.0, 1.0, 1.0, zp1, zav);
+    z_rk4(h, 1.0, 0.0, 0.0, zcp, zcv);
     const double lo = ulo - 1e-8 * fmax(1.0, fabs(ulo));       // IPOPT bound_relax_factor = 1e-8
     const double hi = uhi + 1e-8 * fmax(1.0, fabs(uhi));
     const bool poly = fmax(fabs(lo), fabs(hi)) <= 1.0;
@@ -208,9 +227,11 @@ void pmpc_ipm_kernel(PmpcArgs a) {
     const double uonf = uon ? 1.0 : 0.0, ai12k = uon ? ai12 : 0.0, ai22k = uon ? ai22 : 1.0, a22i = uon ? a22 : 1.0;
     const double A11k = a12k * a12k, A12k = 2.0 * a12k * a22k, A22k = a22k * a22k;
 
-    // per-lane axis slots
+    // per-lane axis slots; z slots: NAX == 1 keeps pz on the x half and vz on the y half, NAX == 2
+    // keeps pz in slot 0 and vz in slot 1 of every lane
     double sp[NAX], sv[NAX], rp[NAX], rv[NAX];
     double p[NAX], v[NAX], th[NAX], lp[NAX], lv[NAX], zl[NAX], zu[NAX];
+    double zA[NAX], zC[NAX], zs[NAX], zz[NAX];
     const int nw = 6 * (N + 1) + 2 * N;
     const double* ww = a.w_warm ? a.w_warm + (size_t)nw * b : nullptr;
     const double pushl = fmin(1e-2 * fmax(1.0, fabs(lo)), 1e-2 * (hi - lo));   // IPOPT bound_push / frac
@@ -230,6 +251,10 @@ void pmpc_ipm_kernel(PmpcArgs a) {
         zl[j] = uon ? 1.0 : 0.0; zu[j] = uon ? 1.0 : 0.0;      // bound_mult_init_val = 1
         if (xon) gmax = fmax(gmax, fmax(fabs(2 * Qp * (p[j] - rp[j])), fabs(2 * Qv * (v[j] - rv[j]))));
         if (uon) gmax = fmax(gmax, fabs(2 * R * th[j]));
+        // z slot (ax here is 0 = pz, 1 = vz)
+        zA[j] = ax ? zav : zp1; zC[j] = ax ? zcv : zcp;
+        zs[j] = st[4 + ax];
+        zz[j] = xon ? (ww ? ww[6 * k + 4 + ax] : zs[j]) : 0.0;
     }
     gmax = wmax(gmax);
     const double sc = gmax > 100.0 ? 100.0 / gmax : 1.0;     // nlp_scaling_max_gradient = 100
@@ -249,18 +274,42 @@ void pmpc_ipm_kernel(PmpcArgs a) {
         g1 = (k == 0) ? pj - spj : pj - ip;
         g2 = (k == 0) ? vj - svj : vj - iv;
     };
+    // the sum over both axes of a per-axis quantity of this lane's node (NAX == 1: the other half's
+    // lane k + 32 / k - 32 holds the other axis)
+    auto axes_sum = [&](const double (&q)[NAX]) -> double {
+        if constexpr (NAX == 1) return half_pair_sum(q[0]);
+        else return q[0] + q[1];
+    };
+    // z defects of this lane's node from the z slots zj and this lane's w = vz_new: the node k - 1
+    // prediction zA z + zC w comes from the previous lane
+    auto zdefect = [&](double zj, double wj, int j) -> double {
+        const double fz = fma(zA[j], zj, zC[j] * wj);
+        const double ip = from_prev(fz);
+        return (k == 0) ? zj - zs[j] : zj - ip;
+    };
+    // w = vz_new = -g (theta_x^2 + theta_y^2) at this lane's node (mpc_3d.py:93), 0 past the horizon
+    auto vz_new = [&](const double (&t)[NAX]) -> double {
+        double sq[NAX];
+#pragma unroll
+        for (int j = 0; j < NAX; ++j) sq[j] = uon ? t[j] * t[j] : 0.0;
+        return -a.g * axes_sum(sq);
+    };
 
     // sines and defects of the current point: computed here once, then carried over from the
     // accepted line-search trial (the update x + alpha d repeats the trial's arithmetic exactly)
-    double g1[NAX], g2[NAX], snc[NAX];
+    double g1[NAX], g2[NAX], gz[NAX], snc[NAX];
     double th0 = 0.0;
+    {
+        const double w0 = vz_new(th);
 #pragma unroll
-    for (int j = 0; j < NAX; ++j) {
-        double s0, c0_;
-        tilt_sincos(poly, th[j], s0, c0_);
-        snc[j] = uon ? s0 : 0.0;
-        defects(p[j], v[j], snc[j], sp[j], sv[j], g1[j], g2[j]);
-        if (xon) th0 += fabs(g1[j]) + fabs(g2[j]);
+        for (int j = 0; j < NAX; ++j) {
+            double s0, c0_;
+            tilt_sincos(poly, th[j], s0, c0_);
+            snc[j] = uon ? s0 : 0.0;
+            defects(p[j], v[j], snc[j], sp[j], sv[j], g1[j], g2[j]);
+            gz[j] = RED ? 0.0 : zdefect(zz[j], w0, j);
+            if (xon) th0 += fabs(g1[j]) + fabs(g2[j]) + fabs(gz[j]);
+        }
     }
     double theta = wsum(th0);                                  // filter's constraint violation
     const double th_max = 1e4 * fmax(1.0, theta), th_min = 1e-4 * fmax(1.0, theta);
@@ -295,7 +344,7 @@ void pmpc_ipm_kernel(PmpcArgs a) {
             const double ru = fma(r2, th[j], -cs[j] * fma(b1, lpn[j], b2 * lvn[j])) - zl[j] + zu[j];
             dinf = fmax(dinf, xon ? fmax(fabs(r1), fabs(r2x)) : 0.0);
             dinf = fmax(dinf, uon ? fabs(ru) : 0.0);
-            pinf = fmax(pinf, xon ? fmax(fabs(g1[j]), fabs(g2[j])) : 0.0);
+            pinf = fmax(pinf, xon ? fmax(fmax(fabs(g1[j]), fabs(g2[j])), fabs(gz[j])) : 0.0);
             suml += xon ? fabs(lp[j]) + fabs(lv[j]) : 0.0;
             c0 = fmax(c0, uon ? fmax(zl[j] * sl, zu[j] * su) : 0.0);
             cmin = fmin(cmin, uon ? fmin(zl[j] * sl, zu[j] * su) : 1e300);
@@ -325,7 +374,7 @@ void pmpc_ipm_kernel(PmpcArgs a) {
         STAMP(2);
 
         // -------- Newton step: Riccati recursion + inertia correction ---------------
-        double be1[NAX], be2[NAX], E11[NAX], E12[NAX], E22[NAX], Rt0[NAX], rt[NAX], q1[NAX], q2[NAX], gn1[NAX], gn2[NAX];
+        double be1[NAX], be2[NAX], E11[NAX], E12[NAX], E22[NAX], Rt0[NAX], rt[NAX], q1[NAX], q2[NAX];
 #pragma unroll
         for (int j = 0; j < NAX; ++j) {
             be1[j] = b1 * cs[j]; be2[j] = b2 * cs[j];           // B_k = Gamma cos(theta_k); 0 on idle lanes
@@ -334,9 +383,8 @@ void pmpc_ipm_kernel(PmpcArgs a) {
             Rt0[j] = uon ? fma(sn[j], fma(b1, lpn[j], b2 * lvn[j]), r2 + zl[j] * isl[j] + zu[j] * isu[j]) : 1.0;
             rt[j] = uon ? fma(r2, th[j], mu * (isu[j] - isl[j])) : 0.0;
             q1[j] = qp2 * (p[j] - rp[j]); q2[j] = qv2 * (v[j] - rv[j]);
-            gn1[j] = from_next(g1[j]); gn2[j] = from_next(g2[j]);
         }
-        double W1[NAX], W2[NAX], kff[NAX], P11[NAX], P12[NAX], P22[NAX], p1[NAX], p2[NAX], iQs[NAX];
+        double W1[NAX], W2[NAX], P11[NAX], P12[NAX], P22[NAX], iQs[NAX];
         double delta = 0.0;
         bool ok = false;
         int attempt = 0;
@@ -349,7 +397,6 @@ void pmpc_ipm_kernel(PmpcArgs a) {
 #pragma unroll
             for (int j = 0; j < NAX; ++j) {      // terminal value function in every lane
                 P11[j] = X11d; P12[j] = 0.0; P22[j] = X22d;
-                p1[j] = q1[j]; p2[j] = q2[j];
                 Rt[j] = Rt0[j] + delta;
             }
             // Quadratic part as a scan: with P = Y U^-1 the stage map P_k = X + A^T (P_{k+1}^-1 + G_k)^-1 A
@@ -446,11 +493,10 @@ void pmpc_ipm_kernel(PmpcArgs a) {
             // backward sweep: every lane maps its neighbour's value function through its own
             // stage; after step j lane N-1-j is final.  Terminal/idle lanes have Phi = 0, B = 0.
             for (int step = 0; step < N; ++step) {
-                double n11[NAX], n12[NAX], n22[NAX], n1[NAX], n2[NAX];
+                double n11[NAX], n12[NAX], n22[NAX];
 #pragma unroll
                 for (int j = 0; j < NAX; ++j) {
                     n11[j] = from_next(P11[j]); n12[j] = from_next(P12[j]); n22[j] = from_next(P22[j]);
-                    if constexpr (NAX == 2) { n1[j] = from_next(p1[j]); n2[j] = from_next(p2[j]); }
                 }
 #pragma unroll
                 for (int j = 0; j < NAX; ++j) {
@@ -465,15 +511,6 @@ void pmpc_ipm_kernel(PmpcArgs a) {
                     P11[j] = fma(-w1, U1, fma(f11, n11[j], X11d));
                     P12[j] = fma(-w1, U2, X12);
                     P22[j] = fma(-w2, U2, X22);
-                    if constexpr (NAX == 2) {   // NAX == 1 runs the linear part as a scan afterwards
-                        const double h1 = n1[j] - fma(n11[j], gn1[j], n12[j] * gn2[j]);
-                        const double h2 = n2[j] - fma(n12[j], gn1[j], n22[j] * gn2[j]);
-                        const double qu = fma(e1, h1, fma(e2, h2, rt[j]));
-                        const double kf = -iQ * qu;
-                        p1[j] = fma(U1, kf, fma(f11, h1, q1[j]));
-                        p2[j] = fma(U2, kf, q2[j] + fma(a12k, h1, a22k * h2));
-                        kff[j] = kf;
-                    }
                     W1[j] = w1; W2[j] = w2;
                     Quu[j] = Q; iQs[j] = iQ;
                 }
@@ -483,8 +520,23 @@ void pmpc_ipm_kernel(PmpcArgs a) {
             for (int j = 0; j < NAX; ++j) bad = bad || !(Quu[j] > 0.0) || !isfinite(Quu[j]);
             ok = !wany(bad);
         }
-        if constexpr (NAX == 1) {
-            if (ok) {
+        STAMP_ADD(9, attempt);
+        STAMP(3);
+        if (!ok) { status = -3; break; }
+        if (delta > 0.0) delta_last = delta;
+
+        // -------- the step for the constraint right-hand side (g1, g2, gz) ---------------
+        // One call site serves the Newton step and IPOPT's second-order correction passes
+        // (FilterLSAcceptor::TrySecondOrderCorrection, kappa_soc 0.99): a correction re-solves the
+        // factorised system with c_soc <- alpha_soc c_soc + c(x_trial) (from c(x), alpha_soc = alpha)
+        // in place of the defects, so while it runs g1 / g2 / gz hold c_soc.
+        double dp[NAX], dv[NAX], dth[NAX], dlp[NAX], dlv[NAX], dzl[NAX], dzu[NAX], dz[NAX];
+        double amax = 1.0, az = 1.0;
+        auto direction = [&]() {
+            double p1[NAX], p2[NAX], kff[NAX], gn1[NAX], gn2[NAX];
+#pragma unroll
+            for (int j = 0; j < NAX; ++j) { gn1[j] = from_next(g1[j]); gn2[j] = from_next(g2[j]); }
+            if constexpr (NAX == 1) {
                 // linear part of the value function, p_k = M_k p_{k+1} + m_k with M_k = A_k^T - w_k e_k^T
                 // and m_k = q_k - w_k rt_k - M_k P_{k+1} g_{k+1}: a suffix scan of affine maps (row_shl
                 // 1/2/4/8 inside the rows, then row 1 -> row 0 of each half by a lane shuffle); the
@@ -516,8 +568,8 @@ void pmpc_ipm_kernel(PmpcArgs a) {
                         c2 = fma(m21, s1, fma(m22, s2, c2));
                     }
                 } else {
-                affine_scan_level<0x108, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:8
-                if constexpr (!one_row) {   // rows 0 and 2 compose with the suffix held by the first lane of rows 1 and 3
+                    affine_scan_level<0x108, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:8
+                    // rows 0 and 2 compose with the suffix held by the first lane of rows 1 and 3
                     const bool lo_row = (lane & 16) == 0;
                     const double r1 = half_bcast_c<16>(c1), r2 = half_bcast_c<16>(c2);   // only the constant is needed now
                     if (lo_row) {
@@ -525,152 +577,254 @@ void pmpc_ipm_kernel(PmpcArgs a) {
                         c2 = fma(m21, r1, fma(m22, r2, c2));
                     }
                 }
-                }
                 p1[0] = c1; p2[0] = c2;
                 // feed-forward k_k = -(e^T h + rt) / Q with h = p_{k+1} - P_{k+1} g_{k+1}
                 const double np1 = from_next(c1), np2 = from_next(c2);
                 const double h1 = np1 - t1, h2 = np2 - t2;
                 kff[0] = -iQs[0] * fma(e1, h1, fma(e2, h2, rtk));
-            }
-        }
-        STAMP_ADD(9, attempt);
-        STAMP(3);
-        if (!ok) { status = -3; break; }
-        if (delta > 0.0) delta_last = delta;
 
-        // -------- forward sweep of the state step ----------------------------------
-        double dp[NAX], dv[NAX];
+                // forward sweep of the state step: dx_k = F_{k-1} dx_{k-1} + f_{k-1} - g_k as an
+                // inclusive scan of affine maps within each 32-lane axis half (DPP row_shr 1/2/4/8 inside
+                // the 16-lane rows, then row_bcast:15 into the second row of each half)
+                const double pw1 = from_prev(W1[0]), pw2 = from_prev(W2[0]), pkf = from_prev(kff[0]);
+                const double pb1 = from_prev(be1[0]), pb2 = from_prev(be2[0]);
+                double f11_ = 1.0 - pb1 * pw1, f12_ = fma(-pb1, pw2, a12), f21_ = -pb2 * pw1, f22_ = fma(-pb2, pw2, a22);
+                double d1 = fma(pb1, pkf, -g1[0]), d2 = fma(pb2, pkf, -g2[0]);
+                if (k == 0) { f11_ = 0.0; f12_ = 0.0; f21_ = 0.0; f22_ = 0.0; d1 = -g1[0]; d2 = -g2[0]; }
+                affine_scan_level<0x111, 0xf>(f11_, f12_, f21_, f22_, d1, d2);   // row_shr:1
+                affine_scan_level<0x112, 0xf>(f11_, f12_, f21_, f22_, d1, d2);   // row_shr:2
+                affine_scan_level<0x114, 0xf>(f11_, f12_, f21_, f22_, d1, d2);   // row_shr:4
+                // after 3 levels the windows of lanes 0-7 reach node 0 (map 0, a constant): with N <= 23
+                // the row_shr:8 level only moves constants (row 1's lanes 16-23 read nothing); lane 15 is
+                // a constant once row 0 is done, so the row_bcast:15 level into rows 1 / 3 is one too
+                if constexpr (one_row || short2) affine_scan_const<0x118, 0xf>(f11_, f12_, f21_, f22_, d1, d2);
+                else affine_scan_level<0x118, 0xf>(f11_, f12_, f21_, f22_, d1, d2);   // row_shr:8
+                if constexpr (!one_row) affine_scan_const<0x142, 0xa>(f11_, f12_, f21_, f22_, d1, d2);   // row_bcast:15 -> rows 1, 3
+                dp[0] = d1; dv[0] = d2;
+            } else {
+                // linear part of the value function (sequential): p_k = q_k + A_k^T h - w_k (e^T h + rt)
+                double nP11[NAX], nP12[NAX], nP22[NAX];
 #pragma unroll
-        for (int j = 0; j < NAX; ++j) { dp[j] = -g1[j]; dv[j] = -g2[j]; }
-        if constexpr (NAX == 1) {
-            // dx_k = F_{k-1} dx_{k-1} + f_{k-1} - g_k as an inclusive scan of affine maps within each
-            // 32-lane axis half (DPP row_shr 1/2/4/8 inside the 16-lane rows, then row_bcast:15 into
-            // the second row of each half): 5 composition levels instead of N dependent steps
-            const double pw1 = from_prev(W1[0]), pw2 = from_prev(W2[0]), pkf = from_prev(kff[0]);
-            const double pb1 = from_prev(be1[0]), pb2 = from_prev(be2[0]);
-            double f11 = 1.0 - pb1 * pw1, f12 = fma(-pb1, pw2, a12), f21 = -pb2 * pw1, f22 = fma(-pb2, pw2, a22);
-            double c1 = fma(pb1, pkf, -g1[0]), c2 = fma(pb2, pkf, -g2[0]);
-            if (k == 0) { f11 = 0.0; f12 = 0.0; f21 = 0.0; f22 = 0.0; c1 = -g1[0]; c2 = -g2[0]; }
-            affine_scan_level<0x111, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:1
-            affine_scan_level<0x112, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:2
-            affine_scan_level<0x114, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:4
-            // after 3 levels the windows of lanes 0-7 reach node 0 (map 0, a constant): with N <= 23
-            // the row_shr:8 level only moves constants (row 1's lanes 16-23 read nothing); lane 15 is
-            // a constant once row 0 is done, so the row_bcast:15 level into rows 1 / 3 is one too
-            if constexpr (one_row || short2) affine_scan_const<0x118, 0xf>(f11, f12, f21, f22, c1, c2);
-            else affine_scan_level<0x118, 0xf>(f11, f12, f21, f22, c1, c2);   // row_shr:8
-            if constexpr (!one_row) affine_scan_const<0x142, 0xa>(f11, f12, f21, f22, c1, c2);   // row_bcast:15 -> rows 1, 3
-            dp[0] = c1; dv[0] = c2;
-        } else
-        for (int step = 0; step < N; ++step) {
-            double op[NAX], ov[NAX];
+                for (int j = 0; j < NAX; ++j) {
+                    nP11[j] = from_next(P11[j]); nP12[j] = from_next(P12[j]); nP22[j] = from_next(P22[j]);
+                    p1[j] = q1[j]; p2[j] = q2[j]; kff[j] = 0.0;
+                }
+                for (int step = 0; step < N; ++step) {
+                    double n1[NAX], n2[NAX];
+#pragma unroll
+                    for (int j = 0; j < NAX; ++j) { n1[j] = from_next(p1[j]); n2[j] = from_next(p2[j]); }
+#pragma unroll
+                    for (int j = 0; j < NAX; ++j) {
+                        const double h1 = n1[j] - fma(nP11[j], gn1[j], nP12[j] * gn2[j]);
+                        const double h2 = n2[j] - fma(nP12[j], gn1[j], nP22[j] * gn2[j]);
+                        const double qu = fma(be1[j], h1, fma(be2[j], h2, rt[j]));
+                        kff[j] = -iQs[j] * qu;
+                        p1[j] = fma(-W1[j], qu, fma(f11, h1, q1[j]));
+                        p2[j] = fma(-W2[j], qu, q2[j] + fma(a12k, h1, a22k * h2));
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < NAX; ++j) { dp[j] = -g1[j]; dv[j] = -g2[j]; }
+                for (int step = 0; step < N; ++step) {
+                    double op[NAX], ov[NAX];
+#pragma unroll
+                    for (int j = 0; j < NAX; ++j) {
+                        const double dt_ = fma(-W1[j], dp[j], fma(-W2[j], dv[j], kff[j]));
+                        op[j] = fma(a12, dv[j], fma(be1[j], dt_, dp[j]));
+                        ov[j] = fma(a22, dv[j], be2[j] * dt_);
+                    }
+#pragma unroll
+                    for (int j = 0; j < NAX; ++j) {
+                        const double ip = from_prev(op[j]), iv = from_prev(ov[j]);
+                        dp[j] = k >= 1 ? ip - g1[j] : dp[j];
+                        dv[j] = k >= 1 ? iv - g2[j] : dv[j];
+                    }
+                }
+            }
+            double am = 1.0, az_ = 1.0, twd[NAX];
 #pragma unroll
             for (int j = 0; j < NAX; ++j) {
-                const double dth = fma(-W1[j], dp[j], fma(-W2[j], dv[j], kff[j]));
-                op[j] = fma(a12, dv[j], fma(be1[j], dth, dp[j]));
-                ov[j] = fma(a22, dv[j], be2[j] * dth);
+                dth[j] = uon ? fma(-W1[j], dp[j], fma(-W2[j], dv[j], kff[j])) : 0.0;
+                // new multipliers lam+ = -(P dx + p), step = lam+ - lam
+                dlp[j] = xon ? -fma(P11[j], dp[j], fma(P12[j], dv[j], p1[j])) - lp[j] : 0.0;
+                dlv[j] = xon ? -fma(P12[j], dp[j], fma(P22[j], dv[j], p2[j])) - lv[j] : 0.0;
+                const double sl = th[j] - lo, su = hi - th[j];
+                const double zlx = zl[j] * isl[j], zux = zu[j] * isu[j];
+                dzl[j] = uon ? fma(-zlx, dth[j], fma(mu, isl[j], -zl[j])) : 0.0;
+                dzu[j] = uon ? fma(zux, dth[j], fma(mu, isu[j], -zu[j])) : 0.0;
+                const double ith = frcp(dth[j]);
+                const double cand = dth[j] < 0 ? -tau * sl * ith : (dth[j] > 0 ? tau * su * ith : 1.0);
+                const double czl = dzl[j] < 0 ? -tau * zl[j] * frcp(dzl[j]) : 1.0;
+                const double czu = dzu[j] < 0 ? -tau * zu[j] * frcp(dzu[j]) : 1.0;
+                am = fmin(am, uon ? cand : 1.0);
+                az_ = fmin(az_, uon ? fmin(czl, czu) : 1.0);
+                twd[j] = 2.0 * th[j] * dth[j];
             }
+            // f32 minima rounded down: tau <= 0.99 leaves far more slack than the f32 rounding
+            float amax_f = (float)am, az_f = (float)az_;
+            wmin2f(amax_f, az_f);
+            amax = (double)amax_f * (1.0 - 1.0 / 1048576.0);
+            az = (double)az_f * (1.0 - 1.0 / 1048576.0);
+            // z step: dz_k = zA dz_{k-1} + zC dw_{k-1} - gz_k, dw = -g (2 theta_x dtheta_x + 2 theta_y dtheta_y)
+            const double wd = RED ? 0.0 : -a.g * axes_sum(twd);
+            if constexpr (RED) {
 #pragma unroll
-            for (int j = 0; j < NAX; ++j) {
-                const double ip = from_prev(op[j]), iv = from_prev(ov[j]);
-                dp[j] = k >= 1 ? ip - g1[j] : dp[j];
-                dv[j] = k >= 1 ? iv - g2[j] : dv[j];
+                for (int j = 0; j < NAX; ++j) dz[j] = 0.0;
+            } else if constexpr (NAX == 1) {
+                const double src = from_prev(zC[0] * wd);
+                double m = k == 0 ? 0.0 : zA[0], c = k == 0 ? -gz[0] : src - gz[0];
+                affine1_scan_level<0x111, 0xf>(m, c);   // row_shr:1
+                affine1_scan_level<0x112, 0xf>(m, c);   // row_shr:2
+                affine1_scan_level<0x114, 0xf>(m, c);   // row_shr:4
+                if constexpr (one_row || short2) affine1_scan_const<0x118, 0xf>(m, c);
+                else affine1_scan_level<0x118, 0xf>(m, c);   // row_shr:8
+                if constexpr (!one_row) affine1_scan_const<0x142, 0xa>(m, c);   // row_bcast:15 -> rows 1, 3
+                dz[0] = c;
+            } else {
+#pragma unroll
+                for (int j = 0; j < NAX; ++j) dz[j] = -gz[j];
+                for (int step = 0; step < N; ++step) {
+#pragma unroll
+                    for (int j = 0; j < NAX; ++j) {
+                        const double ip = from_prev(fma(zA[j], dz[j], zC[j] * wd));
+                        dz[j] = k >= 1 ? ip - gz[j] : dz[j];
+                    }
+                }
             }
-        }
-        double amax = 1.0, az = 1.0;
-        double dth[NAX], dlp[NAX], dlv[NAX], dzl[NAX], dzu[NAX];
-#pragma unroll
-        for (int j = 0; j < NAX; ++j) {
-            dth[j] = uon ? fma(-W1[j], dp[j], fma(-W2[j], dv[j], kff[j])) : 0.0;
-            // new multipliers lam+ = -(P dx + p), step = lam+ - lam
-            dlp[j] = xon ? -fma(P11[j], dp[j], fma(P12[j], dv[j], p1[j])) - lp[j] : 0.0;
-            dlv[j] = xon ? -fma(P12[j], dp[j], fma(P22[j], dv[j], p2[j])) - lv[j] : 0.0;
-            const double sl = th[j] - lo, su = hi - th[j];
-            const double zlx = zl[j] * isl[j], zux = zu[j] * isu[j];
-            dzl[j] = uon ? fma(-zlx, dth[j], fma(mu, isl[j], -zl[j])) : 0.0;
-            dzu[j] = uon ? fma(zux, dth[j], fma(mu, isu[j], -zu[j])) : 0.0;
-            const double ith = frcp(dth[j]);
-            const double cand = dth[j] < 0 ? -tau * sl * ith : (dth[j] > 0 ? tau * su * ith : 1.0);
-            const double czl = dzl[j] < 0 ? -tau * zl[j] * frcp(dzl[j]) : 1.0;
-            const double czu = dzu[j] < 0 ? -tau * zu[j] * frcp(dzu[j]) : 1.0;
-            amax = fmin(amax, uon ? cand : 1.0);
-            az = fmin(az, uon ? fmin(czl, czu) : 1.0);
-        }
-        // f32 minima rounded down: tau <= 0.99 leaves far more slack than the f32 rounding
-        float amax_f = (float)amax, az_f = (float)az;
-        wmin2f(amax_f, az_f);
-        amax = (double)amax_f * (1.0 - 1.0 / 1048576.0);
-        az = (double)az_f * (1.0 - 1.0 / 1048576.0);
-        STAMP(4);
+        };
 
-        // -------- filter line search (Waechter & Biegler 2006, Alg. A) -------------
-        double phil = 0.0, gtdl = 0.0;
-#pragma unroll
-        for (int j = 0; j < NAX; ++j) {
-            const double ep = p[j] - rp[j], ev = v[j] - rv[j];
-            const double sl = th[j] - lo, su = hi - th[j];
-            phil += xon ? fma(scQp * ep, ep, scQv * ev * ev) : 0.0;
-            gtdl += xon ? fma(qp2 * ep, dp[j], qv2 * ev * dv[j]) : 0.0;
-            phil += uon ? fma(scR * th[j], th[j], -mu * log_fast(sl * su)) : 0.0;
-            gtdl += uon ? rt[j] * dth[j] : 0.0;
-        }
-        wsum2(phil, gtdl);
-        const double phi = phil, gTd = gtdl;
-        // switching condition alpha (-gTd)^s_ph > delta theta^s_th, compared in log2 space
-        const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
-        const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
-        const float lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;    // log2(theta^s_th / (-gTd)^s_ph)
-        double amin = gam_th;
-        if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta * frcp(-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
-        amin *= gam_al;
-        double alpha = amax, th_t = 0.0, ph_t = 0.0;
-        bool accepted = false, ftype = false;
-        // IPOPT's tiny-step test: max |d|/(1+|x|) < 10 eps_mach accepts the full step unfiltered
-        float tnl = 0.0f;
-#pragma unroll
-        for (int j = 0; j < NAX; ++j) {
-            tnl = fmaxf(tnl, xon ? fabsf((float)dp[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)p[j])) : 0.0f);
-            tnl = fmaxf(tnl, xon ? fabsf((float)dv[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)v[j])) : 0.0f);
-            tnl = fmaxf(tnl, uon ? fabsf((float)dth[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)th[j])) : 0.0f);
-        }
-        const bool tiny = wmaxf(tnl) < 2.2e-15f;
-        STAMP(5);
-        int ls = 0;
-        double snt[NAX], g1t[NAX], g2t[NAX];     // the trial's sines and defects (carried on acceptance)
-        for (; ls < 80; ++ls) {
-            double thl = 0.0, phl = 0.0;
+        // -------- filter line search (Waechter & Biegler 2006, Alg. A) with second-order correction
+        double alpha = 1.0, amain = 1.0, th_t = 0.0, ph_t = 0.0, th_old = 0.0, phi = 0.0, gTd = 0.0, amin = 0.0;
+        float lg_sw = 0.0f;
+        bool accepted = false, ftype = false, tiny = false;
+        int ls = 0, soc = 0;        // soc: 0 Newton step, 1.. correction pass, -1 Newton step again after failed passes
+        double snt[NAX], g1t[NAX], g2t[NAX], gzt[NAX];     // the trial's sines and defects (carried on acceptance)
+        // trial point x + al d: defects, wave-summed theta and barrier objective
+        auto trial = [&](double al) {
+            double thl = 0.0, phl = 0.0, tt[NAX];
 #pragma unroll
             for (int j = 0; j < NAX; ++j) {
-                const double pt = fma(alpha, dp[j], p[j]), vt = fma(alpha, dv[j], v[j]), tt = fma(alpha, dth[j], th[j]);
+                const double pt = fma(al, dp[j], p[j]), vt = fma(al, dv[j], v[j]);
+                tt[j] = fma(al, dth[j], th[j]);
                 double s_, c_;
-                tilt_sincos(poly, tt, s_, c_);
+                tilt_sincos(poly, tt[j], s_, c_);
                 snt[j] = uon ? s_ : 0.0;
-                double& t1 = g1t[j];
-                double& t2 = g2t[j];
-                defects(pt, vt, snt[j], sp[j], sv[j], t1, t2);
+                defects(pt, vt, snt[j], sp[j], sv[j], g1t[j], g2t[j]);
                 const double ep = pt - rp[j], ev = vt - rv[j];
-                thl += xon ? fabs(t1) + fabs(t2) : 0.0;
+                thl += xon ? fabs(g1t[j]) + fabs(g2t[j]) : 0.0;
                 phl += xon ? fma(scQp * ep, ep, scQv * ev * ev) : 0.0;
-                phl += uon ? fma(scR * tt, tt, -mu * log_fast((tt - lo) * (hi - tt))) : 0.0;
+                phl += uon ? fma(scR * tt[j], tt[j], -mu * log_fast((tt[j] - lo) * (hi - tt[j]))) : 0.0;
+            }
+            if constexpr (RED) {
+#pragma unroll
+                for (int j = 0; j < NAX; ++j) gzt[j] = 0.0;
+            } else {
+                const double wt = vz_new(tt);
+#pragma unroll
+                for (int j = 0; j < NAX; ++j) {
+                    gzt[j] = zdefect(fma(al, dz[j], zz[j]), wt, j);
+                    thl += xon ? fabs(gzt[j]) : 0.0;
+                }
             }
             wsum2(thl, phl);
             th_t = thl; ph_t = phl;
-            if (tiny) { accepted = true; ftype = true; break; }
+        };
+        // filter acceptance of (th_t, ph_t) for the step size al_test (IPOPT alpha_primal_test)
+        auto acceptable = [&](double al_test, bool& ft) {
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
             in_filter = in_filter || wany(lane < nfilt && th_t >= fth && ph_t >= fph);
-            if (!in_filter) {
-                const bool sw = gTd < 0.0 && lg2(alpha) > lg_sw;
-                if (theta <= th_min && sw) {
-                    if (cmp_le(ph_t, phi + eta_ph * alpha * gTd, phi)) { accepted = true; ftype = true; }
-                } else if (cmp_le(th_t, (1 - gam_th) * theta, theta) || cmp_le(ph_t - phi, -gam_ph * theta, phi)) {
-                    accepted = true;
-                }
+            if (in_filter) return false;
+            const bool sw = gTd < 0.0 && lg2(al_test) > lg_sw;
+            if (theta <= th_min && sw) {
+                if (cmp_le(ph_t, phi + eta_ph * al_test * gTd, phi)) { ft = true; return true; }
+                return false;
             }
-            if (accepted) break;
-            alpha *= 0.5;
-            if (alpha < amin) break;
+            return cmp_le(th_t, (1 - gam_th) * theta, theta) || cmp_le(ph_t - phi, -gam_ph * theta, phi);
+        };
+        for (;;) {
+            direction();
+            STAMP(4);
+            if (soc == 0) {
+                double phil = 0.0, gtdl = 0.0;
+#pragma unroll
+                for (int j = 0; j < NAX; ++j) {
+                    const double ep = p[j] - rp[j], ev = v[j] - rv[j];
+                    const double sl = th[j] - lo, su = hi - th[j];
+                    phil += xon ? fma(scQp * ep, ep, scQv * ev * ev) : 0.0;
+                    gtdl += xon ? fma(qp2 * ep, dp[j], qv2 * ev * dv[j]) : 0.0;
+                    phil += uon ? fma(scR * th[j], th[j], -mu * log_fast(sl * su)) : 0.0;
+                    gtdl += uon ? rt[j] * dth[j] : 0.0;
+                }
+                wsum2(phil, gtdl);
+                phi = phil; gTd = gtdl;
+                // switching condition alpha (-gTd)^s_ph > delta theta^s_th, compared in log2 space
+                const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
+                const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
+                lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;    // log2(theta^s_th / (-gTd)^s_ph)
+                amin = gam_th;
+                if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta * frcp(-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
+                amin *= gam_al;
+                // IPOPT's tiny-step test: max |d|/(1+|x|) < 10 eps_mach accepts the full step unfiltered
+                float tnl = 0.0f;
+#pragma unroll
+                for (int j = 0; j < NAX; ++j) {
+                    tnl = fmaxf(tnl, xon ? fabsf((float)dp[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)p[j])) : 0.0f);
+                    tnl = fmaxf(tnl, xon ? fabsf((float)dv[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)v[j])) : 0.0f);
+                    tnl = fmaxf(tnl, xon ? fabsf((float)dz[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)zz[j])) : 0.0f);
+                    tnl = fmaxf(tnl, uon ? fabsf((float)dth[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)th[j])) : 0.0f);
+                }
+                tiny = wmaxf(tnl) < 2.2e-15f;
+                alpha = amax; amain = amax;
+            } else if (soc > 0) {
+                alpha = amax;                 // alpha_soc: fraction to the boundary of the corrected step
+            }
+            STAMP(5);
+            bool again = false;
+            for (;;) {
+                trial(alpha);
+                bool ft = false;
+                if (soc == 0 && tiny) { accepted = true; ftype = true; break; }
+                if (acceptable(soc > 0 ? amain : alpha, ft)) { accepted = true; ftype = ft; break; }
+                if (!RED && soc == 0 && ls == 0 && a.max_soc > 0 && !(th_t < theta)) {
+                    // first correction: c_soc = alpha c(x) + c(x_trial)
+#pragma unroll
+                    for (int j = 0; j < NAX; ++j) {
+                        g1[j] = fma(alpha, g1[j], g1t[j]); g2[j] = fma(alpha, g2[j], g2t[j]);
+                        gz[j] = fma(alpha, gz[j], gzt[j]);
+                    }
+                    th_old = th_t; soc = 1; again = true;
+                    break;
+                }
+                if (soc > 0) {
+                    if (soc < a.max_soc && th_t <= 0.99 * th_old) {      // next pass: c_soc <- alpha_soc c_soc + c(trial)
+#pragma unroll
+                        for (int j = 0; j < NAX; ++j) {
+                            g1[j] = fma(alpha, g1[j], g1t[j]); g2[j] = fma(alpha, g2[j], g2t[j]);
+                            gz[j] = fma(alpha, gz[j], gzt[j]);
+                        }
+                        th_old = th_t; ++soc; again = true;
+                        break;
+                    }
+                    // the corrections failed: the defects of the current point back (the same
+                    // arithmetic as their first evaluation), the Newton step again, backtrack from alpha/2
+                    const double w0 = RED ? 0.0 : vz_new(th);
+#pragma unroll
+                    for (int j = 0; j < NAX; ++j) {
+                        defects(p[j], v[j], snc[j], sp[j], sv[j], g1[j], g2[j]);
+                        gz[j] = RED ? 0.0 : zdefect(zz[j], w0, j);
+                    }
+                    soc = -1; ls = 1; alpha = 0.5 * amain;
+                    again = !(alpha < amin);
+                    break;
+                }
+                ++ls;
+                alpha *= 0.5;
+                if (alpha < amin || ls >= 80) break;
+            }
+            if (!again) break;
         }
         STAMP_ADD(10, ls + 1);
+        STAMP_ADD(15, soc > 0 ? 1 : 0);
         STAMP(6);
         if (!accepted) { status = -2; break; }   // IPOPT would enter its restoration phase here
         if (!ftype && nfilt < kWave) {
@@ -680,8 +834,9 @@ void pmpc_ipm_kernel(PmpcArgs a) {
         // -------- accept the step ----------------------------------------------------
 #pragma unroll
         for (int j = 0; j < NAX; ++j) {
-            snc[j] = snt[j]; g1[j] = g1t[j]; g2[j] = g2t[j];
+            snc[j] = snt[j]; g1[j] = g1t[j]; g2[j] = g2t[j]; gz[j] = gzt[j];
             p[j] = fma(alpha, dp[j], p[j]); v[j] = fma(alpha, dv[j], v[j]);
+            zz[j] = fma(alpha, dz[j], zz[j]);
             lp[j] = fma(alpha, dlp[j], lp[j]); lv[j] = fma(alpha, dlv[j], lv[j]);
             th[j] = fma(alpha, dth[j], th[j]);
             const double il = frcp(th[j] - lo), iu = frcp(hi - th[j]);
@@ -720,24 +875,26 @@ void pmpc_ipm_kernel(PmpcArgs a) {
         a.iters[b] = it;
     }
     if (a.w_out) {
-        // z sub-state follows the final controls through the reference RK4 (mpc_3d.py:93-97, :99-104)
-        const double w = uon ? -a.g * (tx * tx + ty * ty) : 0.0;
-        __syncthreads();
-        double pz = z0[0], vz = z0[1];
-        for (int step = 0; step < N; ++step) {
-            double pzn, vzn;
-            z_rk4(h, w, pz, vz, pzn, vzn);
-            const double ip = from_prev(pzn), iv = from_prev(vzn);
-            pz = k >= 1 ? ip : pz; vz = k >= 1 ? iv : vz;
-        }
         double* wo = a.w_out + (size_t)nw * b;
+        if constexpr (RED) {
+            // the z sub-state follows the final controls through the reference RK4 (mpc_3d.py:93-97, :99-104)
+            const double w = uon ? -a.g * (tx * tx + ty * ty) : 0.0;
+            double pz = st[4], vz = st[5];
+            for (int step = 0; step < N; ++step) {
+                double pzn, vzn;
+                z_rk4(h, w, pz, vz, pzn, vzn);
+                const double ip = from_prev(pzn), iv = from_prev(vzn);
+                pz = k >= 1 ? ip : pz; vz = k >= 1 ? iv : vz;
+            }
+#pragma unroll
+            for (int j = 0; j < NAX; ++j) zz[j] = (NAX == 1 ? ax0 : j) ? vz : pz;
+        }
 #pragma unroll
         for (int j = 0; j < NAX; ++j) {
             const int ax = NAX == 1 ? ax0 : j;
-            if (xon) { wo[6 * k + 2 * ax] = p[j]; wo[6 * k + 2 * ax + 1] = v[j]; }
+            if (xon) { wo[6 * k + 2 * ax] = p[j]; wo[6 * k + 2 * ax + 1] = v[j]; wo[6 * k + 4 + ax] = zz[j]; }
             if (uon) wo[6 * (N + 1) + 2 * k + ax] = th[j];
         }
-        if (xon && (NAX == 2 || ax0 == 0)) { wo[6 * k + 4] = pz; wo[6 * k + 5] = vz; }
     }
     if (a.done) {
         // release at system scope: the wave's output stores (any lane) are visible before the word
@@ -753,7 +910,8 @@ void pmpc_ipm_kernel(PmpcArgs a) {
 // out[128] = wsum(lane), out[129] = wmax(lane), out[130] = wmin(lane + 1),
 // out[131..194] = relative error of the raw v_rcp_f64 on x_i = 1.37^(i-32)*pi (diagnostic),
 // out[195] = wsumf(lane), out[196] = wmaxf(v), out[197] = wminf(v + 0.5) with v = (37 lane) mod 64,
-// out[198] = wmaxf(0 except lane 40: inf), out[199] / out[200] = half_bcast<3>(lane) at lanes 0 / 40
+// out[198] = wmaxf(0 except lane 40: inf), out[199] / out[200] = half_bcast<3>(lane) at lanes 0 / 40,
+// out[201..264] = half_pair_sum(lane^2)
 __global__ __launch_bounds__(kWave) void wave_selftest_kernel(double* out) {
     const double x = (double)threadIdx.x;
     const double n = from_next(x), p = from_prev(x);
@@ -769,6 +927,7 @@ __global__ __launch_bounds__(kWave) void wave_selftest_kernel(double* out) {
     const double hb = half_bcast_c<3>(x);
     if (threadIdx.x == 0) { out[195] = sf; out[196] = mxf; out[197] = mnf; out[198] = inf1; out[199] = hb; }
     if (threadIdx.x == 40) out[200] = hb;
+    out[201 + threadIdx.x] = half_pair_sum(x * x);
 }
 
 #endif  // PMPC_SEQ
@@ -778,14 +937,22 @@ __global__ __launch_bounds__(kWave) void wave_selftest_kernel(double* out) {
 #ifdef PMPC_SEQ
 // one-row scan build (onerow != 0, N <= 15), else the sequential (throughput) builds: two waves per
 // SIMD, used once B exceeds the scan limit or N > 31
+template <bool RED>
+static void launch_seq(const dartmpc::PmpcArgs* a, unsigned grid, hipStream_t stream, int onerow) {
+    if (onerow)
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, true, false, RED>), dim3(grid), dim3(dartmpc::kWave), 0,
+                           stream, *a);
+    else if (a->N <= 31)
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, false, false, false, RED>), dim3(grid), dim3(dartmpc::kWave), 0,
+                           stream, *a);
+    else
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<2, false, false, false, RED>), dim3(grid), dim3(dartmpc::kWave), 0,
+                           stream, *a);
+}
 extern "C" hipError_t dartmpc_launch_pmpc_seq(const dartmpc::PmpcArgs* a, unsigned grid, hipStream_t stream,
                                               int onerow) {
-    if (onerow)
-        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, true>), dim3(grid), dim3(dartmpc::kWave), 0, stream, *a);
-    else if (a->N <= 31)
-        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, false>), dim3(grid), dim3(dartmpc::kWave), 0, stream, *a);
-    else
-        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<2, false>), dim3(grid), dim3(dartmpc::kWave), 0, stream, *a);
+    if (a->reduced) launch_seq<true>(a, grid, stream, onerow);
+    else launch_seq<false>(a, grid, stream, onerow);
     return hipGetLastError();
 }
 #else
@@ -807,11 +974,17 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
     }();
     if (a.N <= 15 && a.B <= qscan_max_b)
         return dartmpc_launch_pmpc_seq(&a, grid.x, stream, 1);
-    else if (a.N <= 23 && a.B <= qscan_max_b)
-        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
-    else if (a.N <= 31 && a.B <= qscan_max_b)
-        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
-    else
+    else if (a.N <= 23 && a.B <= qscan_max_b) {
+        if (a.reduced)
+            hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+        else
+            hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+    } else if (a.N <= 31 && a.B <= qscan_max_b) {
+        if (a.reduced)
+            hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+        else
+            hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+    } else
         return dartmpc_launch_pmpc_seq(&a, grid.x, stream, 0);
     return hipGetLastError();
 }

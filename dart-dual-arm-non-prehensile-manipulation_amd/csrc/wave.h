@@ -92,6 +92,19 @@ __device__ __forceinline__ double half_bcast(double x, int i) {
         default: return half_bcast_c<15>(x);
     }
 }
+// x[i] + x[i + 32] in lane i and lane i + 32 (the two 32-lane halves summed pairwise): two
+// v_permlane32_swap_b32 (gfx950 VALU, no LDS crossbar) exchange lanes 32-63 of one copy with lanes
+// 0-31 of the other, after which the two copies hold the low and the high half in every lane; the
+// sum needs no select and is the same value (low + high) in both lanes of a pair
+__device__ __forceinline__ double half_pair_sum(double x) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+    const unsigned lo = (unsigned)(b & 0xffffffffu), hi = (unsigned)(b >> 32);
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const double a = __builtin_bit_cast(double, ((unsigned long long)rh[0] << 32) | rl[0]);
+    const double c = __builtin_bit_cast(double, ((unsigned long long)rh[1] << 32) | rl[1]);
+    return a + c;
+}
 constexpr int kWaveShl1 = 0x130;   // lane k <- lane k+1 (lane 63 <- 0)
 constexpr int kWaveShr1 = 0x138;   // lane k <- lane k-1 (lane 0 <- 0)
 __device__ __forceinline__ double from_next(double x) { return dpp<kWaveShl1>(x); }

@@ -34,7 +34,7 @@ EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch",
            "dart_arm_config_default", "dart_arm_snapshot_len", "dart_arm_param_len", "dart_arm_solve_batch",
            "dart_arm_solve_batch_dev")
 VARIANT_PMPC, VARIANT_RMPC, VARIANT_LMPC = 0, 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class DartMPCError(RuntimeError):
@@ -46,7 +46,7 @@ class Config(ctypes.Structure):
     _fields_ = [("variant", ctypes.c_int32), ("N", ctypes.c_int32), ("Ts", ctypes.c_double),
                 ("tol", ctypes.c_double), ("max_iter", ctypes.c_int32), ("B_max", ctypes.c_int32),
                 ("gravity", ctypes.c_double), ("acceptable_tol", ctypes.c_double),
-                ("acceptable_iter", ctypes.c_int32), ("max_soc", ctypes.c_int32)]
+                ("acceptable_iter", ctypes.c_int32), ("max_soc", ctypes.c_int32), ("pmpc_path", ctypes.c_int32)]
 
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -150,7 +150,7 @@ def wave_selftest():
     L = lib()
     L.dartmpc_selftest.argtypes = [ctypes.c_void_p]
     L.dartmpc_selftest.restype = ctypes.c_int
-    out = np.zeros(201)
+    out = np.zeros(265)
     rc = L.dartmpc_selftest(ctypes.c_void_p(out.ctypes.data))
     if rc != 0:
         raise DartMPCError(f"dartmpc_selftest failed ({rc})")
@@ -170,12 +170,20 @@ def _ptr(a):
 
 
 class Solver:
-    """Owns one ``dart_mpc_handle`` (device workspace + stream) for a fixed N/Ts/tol."""
+    """Owns one ``dart_mpc_handle`` (device workspace + stream) for a fixed N/Ts/tol.  ``max_soc`` is
+    IPOPT's second-order-correction count (default 4, as ``mpc_3d.py:82`` leaves it; 0 = off).
+    ``path``: "ipopt" (default) follows IPOPT's iterates on the full 6-state NLP; "reduced" is the
+    faster opt-in that solves the (x, y) problem and rolls z out afterwards (same KKT point)."""
 
-    def __init__(self, N=20, Ts=0.002, tol=1e-8, max_iter=3000, B_max=1024, device=0, gravity=-9.81):
+    PATHS = {"ipopt": 0, "reduced": 1}
+
+    def __init__(self, N=20, Ts=0.002, tol=1e-8, max_iter=3000, B_max=1024, device=0, gravity=-9.81, max_soc=4,
+                 path="ipopt"):
         self._h = ctypes.c_void_p()
+        if path not in self.PATHS:
+            raise DartMPCError(f"unknown PMPC path {path!r} (expected one of {sorted(self.PATHS)})")
         self.cfg = default_config(N=int(N), Ts=float(Ts), tol=float(tol), max_iter=int(max_iter), B_max=int(B_max),
-                                  gravity=float(gravity))
+                                  gravity=float(gravity), max_soc=int(max_soc), pmpc_path=self.PATHS[path])
         rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
         if rc != 0:
             raise DartMPCError(f"dart_mpc_create failed with code {rc} (no gfx950 device or bad config)")

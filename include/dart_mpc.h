@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define DART_MPC_ABI_VERSION 4
+#define DART_MPC_ABI_VERSION 5
 
 enum dart_mpc_variant {
     DART_MPC_PMPC = 0,      /* PMPC/src/controller/mpc_3d.py, N <= 63 */
@@ -101,7 +101,12 @@ typedef struct dart_mpc_config {
     double acceptable_tol;   /* IPOPT acceptable_tol; used by LMPC (rlmpc2.py:487: 1e-3) */
     int32_t acceptable_iter; /* IPOPT acceptable_iter, 0 = off; used by LMPC (rlmpc2.py:488: 5) */
     int32_t max_soc;    /* IPOPT max_soc (second-order corrections per line search), default 4, 0 = off,
-                           <= 8; used by LMPC (the reference leaves IPOPT's default, rlmpc2.py:480-489) */
+                           <= 8; used by PMPC and LMPC (the reference leaves IPOPT's default,
+                           mpc_3d.py:82, rlmpc2.py:480-489) */
+    int32_t pmpc_path;  /* PMPC only (ABI 5): 0 = IPOPT's path on the full 6-state NLP (default; the z
+                           defect rows of mpc_3d.py:37, :48 in theta, the filter, the error measures and
+                           the second-order correction); 1 = the reduced (x, y) path, opt-in: same KKT
+                           point to the tolerance, fewer iterations, but not IPOPT's iterates */
 } dart_mpc_config;
 
 typedef struct dart_mpc_handle dart_mpc_handle;
@@ -111,7 +116,11 @@ void dart_mpc_config_default(dart_mpc_config *cfg);
 int dart_mpc_create(const dart_mpc_config *cfg, int device, dart_mpc_handle **out);
 
 /* Host-pointer entry: stages inputs to HBM, solves, copies results back and
- * blocks until they are in host memory.  w_warm (nullable) is an initial
+ * blocks until they are in host memory.  It returns as soon as every
+ * instance's results are visible in host memory, which can be a moment before
+ * the stream retires the kernel; the next entry on the handle (or
+ * dart_mpc_sync) settles that stream first and reports a late stream error as
+ * the previous call's.  w_warm (nullable) is an initial
  * guess in the w layout; NULL = the reference's cold start (mpc_3d.py:123).
  * w_out is nullable. */
 int dart_mpc_solve_batch(dart_mpc_handle *h, int B,

@@ -83,27 +83,23 @@ def test_full_w_layout_and_kkt_certificate(dm, goldens):
             prob = PMPCProblem(N=N, Ts=Ts, Qp=qp, Qv=qv, R=r, mu=mu, u_bounds=(lo, hi))
             p = np.concatenate([G["state"][i], G["target"][i]])
             c = kkt_certificate(prob, out["w"][j], p, act_tol=U_TOL)
-            assert c["primal"] <= 1e-9, (i, c["primal"])
+            assert c["primal"] <= 1e-8, (i, c["primal"])      # IPOPT's stopping test: primal <= tol
             assert c["bound"] == 0.0, i
             assert c["stat_free"] <= 1e-5 * max(1.0, c["grad_scale"]), (i, c["stat_free"])
             assert c["stat_sign"] <= 1e-5 * max(1.0, c["grad_scale"]), (i, c["stat_sign"])
-            # the z sub-state follows the reference RK4 exactly
+            # the z sub-state is an iterate of the full NLP: its defects are within the tolerance
             X, U = prob.unpack(out["w"][j])
-            assert np.max(np.abs(X[1:, 4:] - prob.step(X[:-1], U)[:, 4:])) <= 1e-12
+            assert np.max(np.abs(X[1:, 4:] - prob.step(X[:-1], U)[:, 4:])) <= 1e-8
 
 
 def test_c2_and_c4_batches_match_oracle(dm):
-    """C2 (18 configs) and C4 (18 x 64 seeds) against the C oracle on the full 6-state NLP.
-
-    At the reference tolerance (tol 1e-8) an interior-point answer sits up to
-    mu_final/z inside a weakly active bound; with z -> 0 (degenerate bound, seen
-    in C4) two such answers differ by up to ~1e-4 in u0 while their objectives
-    agree to 1e-7 relative.  At tol 1e-11 both are at the exact KKT point."""
+    """C2 (18 configs) and C4 (18 x 64 seeds) against the C oracle on the full 6-state NLP, at the
+    reference tolerance (tol 1e-8) and at tol 1e-11: u0 within 1e-6 rad, objectives 1e-7 relative."""
     import oracle_lib
     from dart_mpc.workload import pmpc_batch
     for n_seeds in (1, 64):
         S, T, P = pmpc_batch(n_seeds)
-        for tol, utol in ((1e-8, 1e-4), (1e-11, 1e-6)):
+        for tol, utol in ((1e-8, 1e-6), (1e-11, 1e-6)):
             s = dm.Solver(N=20, Ts=0.002, tol=tol, B_max=S.shape[0])
             out = s.solve_batch(S, T, P)
             s.close()
@@ -111,6 +107,51 @@ def test_c2_and_c4_batches_match_oracle(dm):
             assert np.all(out["status"] == 0) and np.all(ref["status"] == 0)
             assert np.max(np.abs(out["u0"] - ref["u0"])) <= utol, (n_seeds, tol)
             np.testing.assert_allclose(out["f"], ref["f"], rtol=1e-7, atol=1e-9)
+
+
+@pytest.mark.parametrize("max_soc", [4, 0])
+def test_same_path_as_oracle(dm, max_soc):
+    """IPOPT's path on the full 6-state NLP (mpc_3d.py:28-85): the z defect rows enter theta, the filter,
+    the primal infeasibility and the second-order correction.  Against the C oracle with the same max_soc,
+    on C2 and C4's 1152 instances at the reference's tol 1e-8 (mpc_3d.py:82 leaves IPOPT's defaults),
+    every instance ends with the same status, >= 99 % take the same iterations, u0 within 1e-6."""
+    import oracle_lib
+    from dart_mpc.workload import pmpc_batch
+    for n_seeds in (1, 64):
+        S, T, P = pmpc_batch(n_seeds)
+        s = dm.Solver(N=20, Ts=0.002, tol=1e-8, B_max=S.shape[0], max_soc=max_soc)
+        g = s.solve_batch(S, T, P)
+        s.close()
+        o = oracle_lib.solve_batch(S, T, P, N=20, Ts=0.002, tol=1e-8, max_iter=3000, nthreads=8, want_w=False,
+                                   soc=max_soc)
+        assert np.array_equal(g["status"], o["status"]), (n_seeds, g["status"], o["status"])
+        assert np.mean(g["iters"] == o["iters"]) >= 0.99, (n_seeds, g["iters"], o["iters"])
+        ok = o["status"] == 0       # (with the correction off IPOPT's line search fails on ~7 % of C4)
+        assert np.mean(ok) >= (0.99 if max_soc else 0.5)
+        assert np.max(np.abs(g["u0"] - o["u0"])[ok]) <= 1e-6, (n_seeds, np.max(np.abs(g["u0"] - o["u0"])[ok]))
+
+
+def test_reduced_path_opt_in(dm):
+    """pmpc_path = 1 (opt-in): the (x, y) problem without the z rows in theta / the filter and without the
+    second-order correction.  Not IPOPT's iterates, but the same KKT point: at tol 1e-11 u0 within 1e-6 of
+    the full-NLP oracle, every instance solved, z rolled out from the final controls exactly."""
+    import oracle_lib
+    from dart_mpc.workload import pmpc_batch
+    from pmpc_nlp import PMPCProblem
+    S, T, P = pmpc_batch(8)
+    s = dm.Solver(N=20, Ts=0.002, tol=1e-11, B_max=S.shape[0], path="reduced")
+    g = s.solve_batch(S, T, P, want_w=True)
+    s.close()
+    o = oracle_lib.solve_batch(S, T, P, N=20, Ts=0.002, tol=1e-11, nthreads=8, want_w=False)
+    assert np.all(g["status"] == 0)
+    assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6
+    for i in range(0, S.shape[0], 17):
+        mu, qp, qv, r, lo, hi = P[i]
+        prob = PMPCProblem(N=20, Ts=0.002, Qp=qp, Qv=qv, R=r, mu=mu, u_bounds=(lo, hi))
+        X, U = prob.unpack(g["w"][i])
+        assert np.max(np.abs(X[1:, 4:] - prob.step(X[:-1], U)[:, 4:])) <= 1e-12
+    with pytest.raises(dm.DartMPCError):
+        dm.Solver(N=20, path="fast")
 
 
 def test_wide_tilt_box_library_trig_path(dm):
@@ -136,9 +177,10 @@ def test_wide_tilt_box_library_trig_path(dm):
 def test_scan_and_sequential_riccati_agree(dm, N):
     """The launcher runs the quadratic Riccati part as a DPP scan for B <= 1664 and as the sequential
     sweep beyond (throughput regime).  The same 1152 instances solved as one launch of 2304 (sequential;
-    every instance twice) and as 64 launches of 18 (scan) take the same iterations and agree to 1e-9.
-    N covers every scan instantiation: one-row (N <= 15, the DART driver's horizon), SHORT2
-    (16 <= N <= 23, both ends) and the full scan (N = 24, 31)."""
+    every instance twice) and as 64 launches of 18 (scan) end with the same status, take the same
+    iterations and agree to 1e-9.  N covers every scan instantiation: one-row (N <= 15, the DART driver's
+    horizon), SHORT2 (16 <= N <= 23, both ends) and the full scan (N = 24, 31).  (At N = 31 IPOPT's filter
+    line search fails on 3 of the 1152 instances, oracle and kernel alike: status -2, restoration.)"""
     from dart_mpc.workload import pmpc_batch
     S, T, P = pmpc_batch(64)
     s = dm.Solver(N=N, Ts=0.002, tol=1e-8, B_max=2 * S.shape[0])
@@ -148,10 +190,14 @@ def test_scan_and_sequential_riccati_agree(dm, N):
     u_small = np.concatenate([o["u0"] for o in small])
     it_small = np.concatenate([o["iters"] for o in small])
     B = S.shape[0]
-    np.testing.assert_array_equal(big["status"], 0)
+    st_small = np.concatenate([o["status"] for o in small])
+    np.testing.assert_array_equal(big["status"][:B], big["status"][B:])
+    np.testing.assert_array_equal(big["status"][:B], st_small)
+    assert np.mean(st_small == 0) >= 0.99
     np.testing.assert_array_equal(big["iters"][:B], big["iters"][B:])
     assert np.mean(big["iters"][:B] == it_small) >= 0.99
-    assert np.max(np.abs(big["u0"][:B] - u_small)) <= 1e-9
+    ok = st_small == 0
+    assert np.max(np.abs(big["u0"][:B] - u_small)[ok]) <= 1e-9
 
 
 def test_symmetry_and_rest_properties(dm):
@@ -258,6 +304,8 @@ def test_wave_primitives_selftest(dm):
     # f32 reductions (row_bcast chaining; max / min on the unsigned order of non-negative floats)
     assert out[195] == lanes.sum() and out[196] == 63.0 and out[197] == 0.5 and np.isinf(out[198])
     assert out[199] == 3.0 and out[200] == 35.0               # ds_swizzle broadcast within each half
+    pair = lanes[:32] ** 2 + lanes[32:] ** 2                  # v_permlane32_swap pairwise half sum
+    np.testing.assert_array_equal(out[201:265], np.concatenate([pair, pair]))
     print("raw v_rcp_f64 max relative error:", np.max(np.abs(out[131:195])))
 
 

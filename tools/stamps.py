@@ -18,9 +18,9 @@ from dart_mpc.workload import pmpc_batch  # noqa: E402
 _lib.LIB_PATH = os.path.join(_lib.PKG_DIR, os.environ.get("DART_STAMPS_LIB", "libdartmpc_stamps.so"))
 L = _lib.lib()
 L.dartmpc_read_stamps.argtypes = [ctypes.c_void_p]
-PHASES = ["setup", "eval+errors", "mu update", "riccati", "forward+dz", "ls prep", "ls trials", "update", "outputs"]
+PHASES = ["setup", "eval+errors", "mu update", "riccati", "direction", "ls prep", "ls trials", "update", "outputs"]
 S, T, P = pmpc_batch(1)
-s = _lib.Solver(N=20, B_max=64)
+s = _lib.Solver(N=20, B_max=64, path=os.environ.get("DART_PMPC_PATH", "ipopt"))
 for rep in range(3):
     out = s.solve_batch(S, T, P)
 st = np.zeros(16, dtype=np.uint64)
@@ -32,5 +32,5 @@ for i, n in enumerate(PHASES):
 print(f"  scan-path Riccati passes {int(st[11])}")
 it0 = int(st[0:9].sum() - st[0] - st[8])
 print(f"  first iteration {int(st[12])} cycles, mean iteration {it0 / max(1, out['iters'][0]):.0f} cycles")
-print(f"  riccati passes {int(st[9])}, line-search trials {int(st[10])}")
+print(f"  riccati passes {int(st[9])}, line-search trials {int(st[10])}, iterations with a correction {int(st[15])}")
 print("batch iters:", out["iters"].tolist())
