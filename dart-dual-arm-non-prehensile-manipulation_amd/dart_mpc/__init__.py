@@ -20,7 +20,8 @@ from .rmpc import AdaptiveNPMPCSmooth, RLS, RMPCStep  # noqa: F401
 from .lmpc import RLMPC, LmpcPolicy, init_policy_weights, policy_solve_batch  # noqa: F401
 from .lmpc_shm import RLMPCAsync, lmpc_policy_worker, lmpc_solver_worker  # noqa: F401
 from .arm import ArmControl, ArmSolver  # noqa: F401
+from .mjdata import BodyData  # noqa: F401
 from . import harness, workload  # noqa: F401
 
 __all__ = ["PMPC", "mpc_worker", "Solver", "RmpcSolver", "LmpcSolver", "RLMPC", "LmpcPolicy", "init_policy_weights", "policy_solve_batch", "RLMPCAsync", "lmpc_solver_worker", "lmpc_policy_worker", "ArmControl", "ArmSolver", "AdaptiveNPMPCSmooth", "RLS", "RMPCStep", "DartMPCError",
-           "build", "lib", "rls_update_batch", "tilt_to_quat", "workload", "harness"]
+           "build", "lib", "rls_update_batch", "tilt_to_quat", "workload", "harness", "BodyData"]

@@ -24,12 +24,13 @@ _SOLVERS = {}
 _SOLVERS_LOCK = threading.Lock()
 
 
-def _solver(N, Ts, tol, max_iter, device, gravity, B_max):
-    key = (int(N), float(Ts), float(tol), int(max_iter), int(device), float(gravity))
+def _solver(N, Ts, tol, max_iter, device, gravity, B_max, path="ipopt"):
+    key = (int(N), float(Ts), float(tol), int(max_iter), int(device), float(gravity), path)
     with _SOLVERS_LOCK:
         s = _SOLVERS.get(key)
         if s is None or s.cfg.B_max < B_max:
-            s = Solver(N=N, Ts=Ts, tol=tol, max_iter=max_iter, B_max=max(B_max, 1024), device=device, gravity=gravity)
+            s = Solver(N=N, Ts=Ts, tol=tol, max_iter=max_iter, B_max=max(B_max, 1024), device=device, gravity=gravity,
+                       path=path)
             _SOLVERS[key] = s
         return s
 
@@ -38,7 +39,7 @@ class PMPC:
     """Tray-tilt NMPC, reference constructor signature (mpc_3d.py:12)."""
 
     def __init__(self, model=None, data=None, Ts=0.002, nx=6, nu=2, N=20, Qp=100, Qv=0, R=0.1, mu=0.4,
-                 u_bounds=(-0.5, 0.5), *, device=0, tol=1e-8, max_iter=3000):
+                 u_bounds=(-0.5, 0.5), *, device=0, tol=1e-8, max_iter=3000, path="ipopt"):
         if nx != 6 or nu != 2:
             # the reference dynamics (mpc_3d.py:87-97) are hard-wired to 6 states / 2 tilts
             raise ValueError("PMPC dynamics are defined for nx=6, nu=2 only (mpc_3d.py:87-97)")
@@ -56,6 +57,9 @@ class PMPC:
         self.u_bounds = (float(u_bounds[0]), float(u_bounds[1]))
         self.target_body = "cube"                                                # mpc_3d.py:26
         self.tol, self.max_iter, self.device = float(tol), int(max_iter), int(device)
+        if path not in Solver.PATHS:
+            raise ValueError(f"path must be one of {sorted(Solver.PATHS)}")
+        self.path = path          # "ipopt": IPOPT's iterates (default); "reduced": the faster opt-in
         self.nw = self.nx * (self.N + 1) + self.nu * self.N
         self.w0 = np.zeros(self.nw)                                              # mpc_3d.py:85
         self.lbx = [-np.inf] * (self.nx * (self.N + 1)) + [self.u_bounds[0]] * (self.nu * self.N)
@@ -72,7 +76,7 @@ class PMPC:
         return np.array([self.mu, self.Qp, self.Qv, self.R, self.u_bounds[0], self.u_bounds[1]])
 
     def _engine(self, B):
-        return _solver(self.N, self.Ts, self.tol, self.max_iter, self.device, self.g, B)
+        return _solver(self.N, self.Ts, self.tol, self.max_iter, self.device, self.g, B, self.path)
 
     # -- reference API --------------------------------------------------------
     def get_state(self):

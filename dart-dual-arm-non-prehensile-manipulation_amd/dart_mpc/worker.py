@@ -7,8 +7,12 @@ from ``state_queue`` (FIFO, blocking, one reply per request) and writes
 ``spawn`` method (main_parallel_enhanced.py:106): the GPU context is created
 inside the worker.
 
-``model_path`` is accepted for signature compatibility; when MuJoCo is
-importable the model's gravity is used (mpc_3d.py:23), otherwise it is ignored.
+The loop is the reference's: the received state is written into
+``data.body(ctrl.target_body).xpos / .cvel`` and ``ctrl.solve(target)`` reads
+it back through ``get_state`` (main_parallel_enhanced.py:47-52).  When MuJoCo
+is importable the model (its gravity, mpc_3d.py:23) and ``MjData`` come from
+``model_path``; otherwise ``data`` is a ``dart_mpc.mjdata.BodyData`` and
+``model_path`` is ignored.
 """
 from __future__ import annotations
 
@@ -17,37 +21,35 @@ import time
 import numpy as np
 
 
-def _gravity_from_model(model_path):
+def _mujoco_model(model_path):
+    """(model, MjData) from the xml when MuJoCo is importable, else (None, None)."""
     if not model_path:
-        return None
+        return None, None
     try:
-        import mujoco  # noqa: F401  (absent in this image)
+        import mujoco  # absent in this image
+        model = mujoco.MjModel.from_xml_path(model_path)
+        return model, mujoco.MjData(model)
     except Exception:
-        return None
-    try:
-        return float(mujoco.MjModel.from_xml_path(model_path).opt.gravity[2])
-    except Exception:
-        return None
+        return None, None
 
 
 def mpc_worker(model_path, target_body, params, state_queue, control_queue):
+    from .mjdata import BodyData
     from .pmpc import PMPC
 
-    params = dict(params)
-    g = _gravity_from_model(model_path)
-
-    class _Opt:                     # minimal stand-in exposing opt.gravity for the shim
-        def __init__(self, gz):
-            self.opt = type("opt", (), {"gravity": np.array([0.0, 0.0, gz])})()
-
-    ctrl = PMPC(_Opt(g) if g is not None else None, None, **params)
-    ctrl.target_body = target_body
+    model, data = _mujoco_model(model_path)
+    if data is None:
+        data = BodyData(target_body)
+    ctrl = PMPC(model, data, **dict(params))
+    ctrl.target_body = target_body                                      # main_parallel_enhanced.py:41
     while True:
         item = state_queue.get()
         if isinstance(item, str) and item == "STOP":
             break
         state, target = item
+        data.body(ctrl.target_body).xpos[:] = [state[0], state[2], state[4]]      # :48
+        data.body(ctrl.target_body).cvel[3:6] = [state[1], state[3], state[5]]    # :49
         t0 = time.time()
-        u_cmd, loss = ctrl.solve(target, state=np.asarray(state, float))
+        u_cmd, loss = ctrl.solve(np.asarray(target, float))
         solve_time = time.time() - t0
         control_queue.put((u_cmd, loss, solve_time))

@@ -33,7 +33,8 @@ def test_policy_kernel_matches_oracle_over_steps():
 
 def test_rlmpc_front_end_step():
     """RLMPC.solve (rlmpc2.py:986-1021) on an explicit state: policy step -> pvec -> warm-started solve,
-    against the oracle chain (restated policy + C solver without SOC, the kernel's line search)."""
+    against the oracle chain (restated policy + C solver, IPOPT's default second-order correction on,
+    as in the kernel)."""
     import dart_mpc
     ctl = dart_mpc.RLMPC(None, None, dict(N=20), seed=4)
     st = lp.PolicyState(ctl.policy.current_k[0])
@@ -49,7 +50,7 @@ def test_rlmpc_front_end_step():
         ctl.w0 = out["w"][0]; ctl.last_control = out["u0"][0]
         lp.policy_step(st, ctl.policy.weights, state, target, uprev, eps)
         o = oracle_lib.lmpc_solve_batch(state[None], uprev[None], st.model_params[None], target[None], N=20,
-                                        w_init=w0[None], soc=False)
+                                        w_init=w0[None], soc=True)
         w0 = o["w"][0]; uprev = o["u0"][0]
         assert np.allclose(ctl.policy.model_params[0], st.model_params, atol=1e-6)
         assert np.max(np.abs(out["u0"][0] - o["u0"][0])) <= 1e-6, k
@@ -97,7 +98,7 @@ def test_rlmpc_fused_front_end_matches_oracle_chain():
         u, loss = ctl.solve(target, state=state)
         lp.policy_step(st, ctl.policy.weights, state, target, uprev, eps)
         o = oracle_lib.lmpc_solve_batch(state[None], uprev[None], st.model_params[None], target[None], N=20,
-                                        w_init=w0[None], soc=False)
+                                        w_init=w0[None], soc=True)
         w0 = o["w"][0]; uprev = o["u0"][0]
         assert np.allclose(ctl.policy.model_params[0], st.model_params, atol=1e-6)
         assert np.max(np.abs(u - o["u0"][0])) <= 1e-6, k
@@ -131,3 +132,37 @@ def test_rlmpc_fused_and_two_launch_front_ends_agree():
         assert np.array_equal(ctl[0].w0, ctl[1].w0), k
         for a in ("model_params", "obs_mean", "obs_M2", "history", "timestep", "obs_count"):
             assert np.array_equal(getattr(ctl[0].policy, a), getattr(ctl[1].policy, a)), (k, a)
+
+
+def test_c5_as_configured_fused_launch_matches_oracle_chain():
+    """BASELINE.json C5 as configured: the policy step fused into the LMPC solve launch
+    (dart_lmpc_policy_solve_batch), N = 30, B = 18, over 10 control steps (the logit update fires at
+    steps 0 and 8), each solve warm-started from the previous plan (rlmpc2.py:510-520) with u_prev =
+    the previous control, against the oracle chain: the restated policy step per instance
+    (oracle/lmpc_policy.py) and the C oracle solve with the reference's IPOPT options (tol 1e-4,
+    max_iter 50, acceptable 1e-3 x 5, max_soc 4).  The plant advances by the oracle's model RK4 under
+    the oracle's control.  Every step: model_params within 1e-6, statuses equal, u0 within 1e-6."""
+    import dart_mpc
+    from dart_mpc.workload import lmpc_batch
+    B, N, T = 18, 30, 10
+    D = lmpc_batch(1, seed0=5)
+    rng = np.random.default_rng(77)
+    pol = dart_mpc.LmpcPolicy(B, seed=13)
+    orc = [lp.PolicyState(pol.current_k[b]) for b in range(B)]
+    s = dart_mpc.LmpcSolver(N=N, B_max=B)
+    state, target = D["state"].copy(), D["target"]
+    up_k, up_o = D["u_prev"].copy(), D["u_prev"].copy()
+    wk = wo = None
+    for t in range(T):
+        eps = rng.standard_normal((B, 34)).astype(np.float32)
+        out = dart_mpc.policy_solve_batch(s, pol, state, up_k, target, w_warm=wk, want_w=True, noise=eps)
+        for b in range(B):
+            lp.policy_step(orc[b], pol.weights, state[b], target[b], up_o[b], eps[b])
+        mp_o = np.stack([o.model_params for o in orc])
+        o = oracle_lib.lmpc_solve_batch(state, up_o, mp_o, target, N=N, w_init=wo, nthreads=8)
+        assert np.max(np.abs(pol.model_params - mp_o)) <= 1e-6, t
+        assert np.array_equal(out["status"], o["status"]), (t, out["status"], o["status"])
+        assert np.max(np.abs(out["u0"] - o["u0"])) <= 1e-6, (t, np.max(np.abs(out["u0"] - o["u0"])))
+        wk, wo, up_k, up_o = out["w"], o["w"], out["u0"], o["u0"]
+        state = oracle_lib.lmpc_rk4(state, o["u0"], mp_o)
+    s.close()

@@ -1,6 +1,6 @@
 """Launch duration of the C2 PMPC batch against the iteration cap: t(max_iter) = t0 + n t_iter.
 The intercept t0 holds the launch's fixed costs (setup, cold instruction fetch, outputs).
-Usage (GPU box): python tools/iter_cost.py"""
+Usage (GPU box): [DART_PMPC_PATH=reduced] python tools/iter_cost.py"""
 import os
 import sys
 
@@ -22,7 +22,7 @@ IT = torch.empty(18, dtype=torch.int32, device=dev)
 stream = torch.cuda.Stream(device=dev)
 rows = []
 for mi in (1, 2, 3, 4, 6, 8, 30):
-    s = dart_mpc.Solver(N=20, tol=1e-8, max_iter=mi, B_max=18)
+    s = dart_mpc.Solver(N=20, tol=1e-8, max_iter=mi, B_max=18, path=os.environ.get("DART_PMPC_PATH", "ipopt"))
     launch = lambda: s.solve_batch_dev(18, X0.data_ptr(), RF.data_ptr(), PR.data_ptr(), U0.data_ptr(), FV.data_ptr(),
                                        ST.data_ptr(), IT.data_ptr(), stream=stream.cuda_stream)
     for _ in range(20):
