@@ -672,6 +672,12 @@ int dart_rls_update_batch_dev(int B, double* theta, double* P, const double* phi
     return dartmpc_launch_rls(B, theta, P, phi, y, lambda, (hipStream_t)stream) == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
 }
 
+int dart_set_device(int device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return DART_MPC_ENODEV;
+    return hipSetDevice(device) == hipSuccess ? DART_MPC_OK : DART_MPC_EHIP;
+}
+
 int dart_rls_update_batch(int B, double* theta, double* P, const double* phi, const double* y, double lambda) {
     if (B < 0 || (B > 0 && (!theta || !P || !phi || !y)) || !(lambda > 0.0)) return DART_MPC_EINVAL;
     if (B == 0) return DART_MPC_OK;

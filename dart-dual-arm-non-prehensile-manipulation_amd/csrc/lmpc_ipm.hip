@@ -877,7 +877,9 @@ extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStre
     }
     dartmpc::LmpcArgs a = *args;
     a.pack = (a.B <= 32) ? 8 : 1;            // one XCD (and its L2) for the code of a small batch
-    hipLaunchKernelGGL(dartmpc::lmpc_ipm_kernel, dim3(a.B * a.pack), dim3(dartmpc::kWave), lds, stream, a);
+    // the policy prologue's LDS only when the launch runs it (the opt-in above covers the maximum)
+    const size_t lds_launch = a.fuse_policy ? lds : sizeof(dartmpc::LmShared);
+    hipLaunchKernelGGL(dartmpc::lmpc_ipm_kernel, dim3(a.B * a.pack), dim3(dartmpc::kWave), lds_launch, stream, a);
     return hipGetLastError();
 }
 

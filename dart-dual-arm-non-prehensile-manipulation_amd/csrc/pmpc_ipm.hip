@@ -955,6 +955,13 @@ extern "C" hipError_t dartmpc_launch_pmpc_seq(const dartmpc::PmpcArgs* a, unsign
     else launch_seq<false>(a, grid, stream, onerow);
     return hipGetLastError();
 }
+#ifdef DART_STAMPS
+// diagnostic build only: the stamps of the one-row (N <= 15) and sequential builds of this object
+extern "C" hipError_t dartmpc_read_stamps_seq(unsigned long long* host_out) {
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp_seq), sizeof(unsigned long long) * 16, 0,
+                               hipMemcpyDeviceToHost);
+}
+#endif
 #else
 extern "C" hipError_t dartmpc_launch_pmpc_seq(const dartmpc::PmpcArgs* a, unsigned grid, hipStream_t stream,
                                               int onerow);

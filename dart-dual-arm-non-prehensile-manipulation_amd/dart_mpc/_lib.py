@@ -32,7 +32,7 @@ EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch",
            "dart_lmpc_policy_config_default", "dart_lmpc_policy_step", "dart_lmpc_policy_step_dev",
            "dart_lmpc_policy_solve_batch", "dart_lmpc_policy_solve_batch_dev",
            "dart_arm_config_default", "dart_arm_snapshot_len", "dart_arm_param_len", "dart_arm_solve_batch",
-           "dart_arm_solve_batch_dev")
+           "dart_arm_solve_batch_dev", "dart_set_device")
 VARIANT_PMPC, VARIANT_RMPC, VARIANT_LMPC = 0, 1, 2
 ABI_VERSION = 5
 
@@ -139,10 +139,19 @@ def lib():
     L.dart_arm_solve_batch_dev.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6
     L.dart_arm_solve_batch_dev.restype = ctypes.c_int
+    L.dart_set_device.argtypes = [ctypes.c_int]
+    L.dart_set_device.restype = ctypes.c_int
     if L.dart_mpc_abi_version() != ABI_VERSION:
         raise DartMPCError("libdartmpc.so ABI version mismatch")
     _lib = L
     return L
+
+
+def set_device(device: int):
+    """Select the device of the stateless entries (RLS, policy step, arm QP) for this thread."""
+    rc = lib().dart_set_device(int(device))
+    if rc != 0:
+        raise DartMPCError(f"dart_set_device({device}) failed ({rc})")
 
 
 def wave_selftest():

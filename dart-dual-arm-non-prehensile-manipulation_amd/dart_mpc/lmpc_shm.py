@@ -98,8 +98,8 @@ def lmpc_policy_worker(shm_names, events, packet, shapes):
     """Replaces the inference / parameter-write half of RLMPC._rl_worker (:537-769)."""
     shms, views = _attach(shm_names, shapes)
     try:
-        import torch     # the stateless policy entry runs on the current device
-        torch.cuda.set_device(int(packet.get("device", 0)))
+        from ._lib import set_device
+        set_device(int(packet.get("device", 0)))    # the stateless policy entry runs on the current device
         from .lmpc import LmpcPolicy
         k_max = float(packet.get("max_param_abs", DEFAULTS["max_param_abs"]))
         margin = float(packet.get("k_ceiling_margin", max(1e-3, 0.05 * k_max)))             # :589
@@ -175,8 +175,18 @@ class RLMPCAsync:
         th = Rot.from_matrix(np.asarray(b.xmat).reshape(3, 3)).as_euler("xyz", degrees=False)[:2]
         return np.array([b.xpos[0], b.cvel[3], b.xpos[1], b.cvel[4], th[0], b.cvel[0], th[1], b.cvel[1]])
 
+    def _check_workers(self):
+        """A worker that died (an exception in its loop, a failed device selection) would leave solve()
+        shifting or holding the last plan forever: raise instead."""
+        for pr in self.procs:
+            if not pr.is_alive():
+                from ._lib import DartMPCError
+                raise DartMPCError(f"LMPC worker process {pr.name} exited (code {pr.exitcode})")
+
     def solve(self, target, state=None):
-        """Non-blocking control step (:986-1021); returns (control[2], loss)."""
+        """Non-blocking control step (:986-1021); returns (control[2], loss).  Raises DartMPCError when a
+        worker process has died."""
+        self._check_workers()
         state = self.get_state() if state is None else np.asarray(state, float)
         self.views["state"][:] = state
         self.views["target"][:] = target
@@ -204,8 +214,17 @@ class RLMPCAsync:
         self.views["in_contact"][:] = contact
 
     def wait_solution(self, timeout=5.0) -> bool:
-        """Test / driver helper (not in the reference): block until the solver has published."""
-        return self.events["ctrl_ready"].wait(timeout)
+        """Test / driver helper (not in the reference): block until the solver has published (raises
+        DartMPCError if a worker died meanwhile)."""
+        import time
+        t_end = time.monotonic() + timeout
+        while True:
+            self._check_workers()
+            left = t_end - time.monotonic()
+            if self.events["ctrl_ready"].wait(min(0.05, max(0.0, left))):
+                return True
+            if left <= 0.0:
+                return False
 
     def close(self):
         if not self.shms:

@@ -269,6 +269,11 @@ int dart_lmpc_policy_solve_batch(dart_mpc_handle *h, const dart_lmpc_policy_conf
  * theta [B][7] and P [B][7][7] updated in place with regressors phi [B][7], targets y [B],
  * forgetting factor lambda.  The host entry stages through device memory and blocks. */
 int dart_rls_update_batch(int B, double *theta, double *P, const double *phi, const double *y, double lambda);
+
+/* Device of the stateless entries (dart_rls_update_batch*, dart_lmpc_policy_step*, dart_arm_solve_batch*)
+ * for the calling thread: they run on the HIP current device.  Returns DART_MPC_ENODEV for a device
+ * that does not exist.  (Handles carry their own device.) */
+int dart_set_device(int device);
 int dart_rls_update_batch_dev(int B, double *theta, double *P, const double *phi, const double *y, double lambda,
                               void *hip_stream);
 

@@ -17,14 +17,20 @@ from dart_mpc.workload import pmpc_batch  # noqa: E402
 
 _lib.LIB_PATH = os.path.join(_lib.PKG_DIR, os.environ.get("DART_STAMPS_LIB", "libdartmpc_stamps.so"))
 L = _lib.lib()
-L.dartmpc_read_stamps.argtypes = [ctypes.c_void_p]
+N = int(os.environ.get("DART_STAMPS_N", "20"))
+B = int(os.environ.get("DART_STAMPS_B", "18"))
+# the one-row (N <= 15) and the sequential (B above the scan limit, or N > 31) builds live in the
+# PMPC_SEQ object, which has its own stamp array
+read = L.dartmpc_read_stamps_seq if (N <= 15 or N > 31 or B > 1664) else L.dartmpc_read_stamps
+read.argtypes = [ctypes.c_void_p]
 PHASES = ["setup", "eval+errors", "mu update", "riccati", "direction", "ls prep", "ls trials", "update", "outputs"]
-S, T, P = pmpc_batch(1)
-s = _lib.Solver(N=20, B_max=64, path=os.environ.get("DART_PMPC_PATH", "ipopt"))
+S, T, P = pmpc_batch(-(-B // 18))
+S, T, P = S[:B], T[:B], P[:B]
+s = _lib.Solver(N=N, B_max=B, path=os.environ.get("DART_PMPC_PATH", "ipopt"))
 for rep in range(3):
     out = s.solve_batch(S, T, P)
 st = np.zeros(16, dtype=np.uint64)
-L.dartmpc_read_stamps(ctypes.c_void_p(st.ctypes.data))
+read(ctypes.c_void_p(st.ctypes.data))
 tot = float(st[:9].sum())
 print(f"block0 iters={out['iters'][0]} total cycles={tot:.0f}")
 for i, n in enumerate(PHASES):
