@@ -971,13 +971,15 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
     dartmpc::PmpcArgs a = *args;
     a.pack = (a.B <= 32) ? 8 : 1;          // <= 32 waves fit one XCD's CUs
     // The quadratic scan shortens the dependent chain but needs more registers (one wave per SIMD
-    // instead of two): worth it while every wave has a SIMD of its own (B <= 4 x 256) and, measured
-    // (tools/c4_ab.sh), up to ~1.7 k instances, where its second round of waves still finishes before
-    // one round of sequential waves at two per SIMD (B = 1152: 80 against 89 us; 1792: 100 against 97).
+    // instead of two).  On IPOPT's path (z rows, second-order correction) the sequential build no
+    // longer fits two waves per SIMD without scratch spills, and the scan build is faster at every
+    // batch size measured (B = 4096: 15.9 against 14.7 M solves/s; 18432: 18.1 against 17.4 M), so
+    // it serves every N <= 31 batch; the sequential builds remain for N > 31 and for the
+    // DART_PMPC_QSCAN_MAX_B experiment knob (the round-2 crossover was ~1.7 k instances).
     const dim3 grid(a.B * a.pack);
-    static const int qscan_max_b = [] {     // experiment knob: DART_PMPC_QSCAN_MAX_B (default 1664)
+    static const int qscan_max_b = [] {
         const char* e = getenv("DART_PMPC_QSCAN_MAX_B");
-        return e ? atoi(e) : 1664;
+        return e ? atoi(e) : (1 << 30);
     }();
     if (a.N <= 15 && a.B <= qscan_max_b)
         return dartmpc_launch_pmpc_seq(&a, grid.x, stream, 1);

@@ -175,10 +175,10 @@ def test_wide_tilt_box_library_trig_path(dm):
 
 @pytest.mark.parametrize("N", [15, 16, 20, 23, 24, 31])
 def test_scan_and_sequential_riccati_agree(dm, N):
-    """The launcher runs the quadratic Riccati part as a DPP scan for B <= 1664 and as the sequential
-    sweep beyond (throughput regime).  The same 1152 instances solved as one launch of 2304 (sequential;
-    every instance twice) and as 64 launches of 18 (scan) end with the same status, take the same
-    iterations and agree to 1e-9.  N covers every scan instantiation: one-row (N <= 15, the DART driver's
+    """The same 1152 instances solved as one launch of 2304 (every instance twice; one block per
+    instance) and as 64 launches of 18 (eight blocks per instance slot, one XCD) end with the same
+    status, take the same iterations and agree to 1e-9; with DART_PMPC_QSCAN_MAX_B the big launch
+    would run the sequential Riccati sweep (tools/c4_ab.sh).  N covers every scan instantiation: one-row (N <= 15, the DART driver's
     horizon), SHORT2 (16 <= N <= 23, both ends) and the full scan (N = 24, 31).  (At N = 31 IPOPT's filter
     line search fails on 3 of the 1152 instances, oracle and kernel alike: status -2, restoration.)"""
     from dart_mpc.workload import pmpc_batch

@@ -14,6 +14,8 @@ for r in $(seq 1 $REPS); do
 import json, sys
 d = json.load(open("gpurun_out/ab.json"))
 out = [sys.argv[1], "C2", round(d["value"]), round(d["roofline"]["kernel_ms"] * 1e3, 2), "us"]
+if d.get("saturation"):
+    out += ["sat", round(d["saturation"]["solves_per_s"] / 1e6, 2), "M"]
 for k in ("rmpc_c3", "lmpc_c5", "arm_qp", "pmpc_n15"):
     if d.get(k):
         out += [k, round(d[k]["solves_per_s"]), round(d[k].get("kernel_ms", d[k]["ms_per_step"]) * 1e3, 1), "us"]
