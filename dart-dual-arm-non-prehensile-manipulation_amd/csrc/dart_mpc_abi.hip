@@ -199,6 +199,7 @@ int check_cfg(const dart_mpc_config* c) {
     if (c->acceptable_iter < 0 || (c->acceptable_iter > 0 && !(c->acceptable_tol > 0.0))) return 0;
     if (c->max_soc < 0 || c->max_soc > 8) return 0;
     if (c->pmpc_path != 0 && c->pmpc_path != 1) return 0;
+    if (!(c->constr_mult_init_max >= 0.0)) return 0;
     return 1;
 }
 
@@ -219,6 +220,7 @@ int launch(dart_mpc_handle* h, int B, const double* x0, const double* ref, const
     dartmpc::PmpcArgs a;
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter; a.g = h->cfg.gravity;
     a.max_soc = h->cfg.max_soc; a.reduced = h->cfg.pmpc_path;
+    a.mult_init_max = h->cfg.constr_mult_init_max;
     a.x0 = x0; a.ref = ref; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     a.done = nullptr; a.seq = 0;
@@ -261,6 +263,7 @@ void dart_mpc_config_default(dart_mpc_config* c) {
     c->acceptable_iter = 15;
     c->max_soc = 4;
     c->pmpc_path = 0;
+    c->constr_mult_init_max = 1000.0;
 }
 
 int dart_mpc_nw(int N) { return 6 * (N + 1) + 2 * N; }
@@ -363,6 +366,7 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     dartmpc::PmpcArgs a;
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter; a.g = h->cfg.gravity;
     a.max_soc = h->cfg.max_soc; a.reduced = h->cfg.pmpc_path;
+    a.mult_init_max = h->cfg.constr_mult_init_max;
     a.x0 = d_x0; a.ref = d_ref; a.prm = d_prm; a.w_warm = d_ww;
     a.u0 = d_u0; a.f = d_f; a.w_out = d_wo; a.status = d_st; a.iters = d_it;
     if (++h->seq == 0) {            // wrapped: clear the words so that no stale one can match

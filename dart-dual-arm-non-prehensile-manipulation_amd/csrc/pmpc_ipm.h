@@ -11,6 +11,7 @@ struct PmpcArgs {
     int max_iter;
     int max_soc;            // IPOPT max_soc: second-order corrections after a rejected first trial (default 4)
     int reduced;            // 1: the reduced (x, y) path (dart_mpc_config.pmpc_path), 0: IPOPT's path
+    double mult_init_max;   // IPOPT constr_mult_init_max: > 0 least-square starting multipliers (default 1000)
     int pack;               // blocks per instance slot: 8 packs a small batch onto one XCD (launcher)
     const double* x0;       // [B][6]   device
     const double* ref;      // [B][6]

@@ -323,7 +323,14 @@ void pmpc_ipm_kernel(PmpcArgs a) {
 #ifdef DART_STAMPS
     const unsigned long long t_loop0 = __builtin_amdgcn_s_memtime();
 #endif
-    for (it = 0; it < a.max_iter; ++it) {
+    // it = -1 (a.mult_init_max > 0): IPOPT's least-square estimate of the starting equality
+    // multipliers (DefaultIterateInitializer::least_square_mults, constr_mult_init_max = 1000): the
+    // step solve of the loop body with unit weights (X = I, R = 1), the gradient r = grad f - z_L + z_U
+    // and a zero constraint right-hand side gives y = argmin ||r + J^T y|| as its new multipliers
+    // (LeastSquareMultipliers: [I J^T; J 0] [d; y] = [-r; 0]).  Cold start: the z rows' input columns
+    // vanish (theta = 0), so the estimate separates per axis and y_z = 0.
+    for (it = a.mult_init_max > 0.0 ? -1 : 0; it < a.max_iter; ++it) {
+        const bool lsm = it < 0;
 #ifdef DART_STAMPS
         if (it == 1) t_acc_[12] = __builtin_amdgcn_s_memtime() - t_loop0;      // the first iteration (cold code)
 #endif
@@ -361,10 +368,10 @@ void pmpc_ipm_kernel(PmpcArgs a) {
         const double is_c = 100.0 * frcp(fmax(100.0, (double)sz_w * inv_nb));
         dinf = dinf_w; pinf = pinf_w; c0 = c0_w;
         STAMP(1);
-        if (fmax(dinf * is_d, fmax(pinf, c0 * is_c)) <= tol) { status = 0; break; }
+        if (!lsm && fmax(dinf * is_d, fmax(pinf, c0 * is_c)) <= tol) { status = 0; break; }
         // -------- monotone barrier update (Fiacco-McCormick, may fire repeatedly) --
         // max_i |z_i s_i - mu| = max(max z s - mu, mu - min z s): one reduction pair, scalar loop
-        for (;;) {
+        for (; !lsm;) {
             const double cmu = fmax(c0 - mu, mu - cmin_w);
             if (fmax(dinf * is_d, fmax(pinf, cmu * is_c)) > 10.0 * mu || mu <= mu_min) break;
             mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
@@ -381,7 +388,8 @@ void pmpc_ipm_kernel(PmpcArgs a) {
             E11[j] = be1[j] * be1[j]; E12[j] = 2.0 * be1[j] * be2[j]; E22[j] = be2[j] * be2[j];
             // Hessian of the Lagrangian in theta: 2R + lam_{k+1}^T Gamma sin(theta) + Sigma
             Rt0[j] = uon ? fma(sn[j], fma(b1, lpn[j], b2 * lvn[j]), r2 + zl[j] * isl[j] + zu[j] * isu[j]) : 1.0;
-            rt[j] = uon ? fma(r2, th[j], mu * (isu[j] - isl[j])) : 0.0;
+            // the barrier gradient in theta (least-square estimate: r_u = grad f - z_L + z_U)
+            rt[j] = uon ? (lsm ? r2 * th[j] - zl[j] + zu[j] : fma(r2, th[j], mu * (isu[j] - isl[j]))) : 0.0;
             q1[j] = qp2 * (p[j] - rp[j]); q2[j] = qv2 * (v[j] - rv[j]);
         }
         double W1[NAX], W2[NAX], P11[NAX], P12[NAX], P22[NAX], iQs[NAX];
@@ -392,12 +400,12 @@ void pmpc_ipm_kernel(PmpcArgs a) {
             if (attempt > 0)
                 delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))   // IPOPT perturb_dec_fact 1/3
                                        : delta * (delta_last == 0.0 ? 100.0 : 8.0);
-            const double X11d = qp2 + delta, X22d = qv2 + delta;
+            const double X11d = lsm ? 1.0 : qp2 + delta, X22d = lsm ? 1.0 : qv2 + delta;
             double Quu[NAX], Rt[NAX];
 #pragma unroll
             for (int j = 0; j < NAX; ++j) {      // terminal value function in every lane
                 P11[j] = X11d; P12[j] = 0.0; P22[j] = X22d;
-                Rt[j] = Rt0[j] + delta;
+                Rt[j] = (lsm ? 1.0 : Rt0[j]) + delta;
             }
             // Quadratic part as a scan: with P = Y U^-1 the stage map P_k = X + A^T (P_{k+1}^-1 + G_k)^-1 A
             // (G_k = B_k B_k^T / R_k) is linear on [U; Y]: [U; Y]_k = S_k [U; Y]_{k+1},
@@ -532,8 +540,13 @@ void pmpc_ipm_kernel(PmpcArgs a) {
         // in place of the defects, so while it runs g1 / g2 / gz hold c_soc.
         double dp[NAX], dv[NAX], dth[NAX], dlp[NAX], dlv[NAX], dzl[NAX], dzu[NAX], dz[NAX];
         double amax = 1.0, az = 1.0;
+        const double (&g1o)[NAX] = g1, (&g2o)[NAX] = g2, (&gzo)[NAX] = gz;
         auto direction = [&]() {
-            double p1[NAX], p2[NAX], kff[NAX], gn1[NAX], gn2[NAX];
+            double p1[NAX], p2[NAX], kff[NAX], gn1[NAX], gn2[NAX], g1[NAX], g2[NAX], gz[NAX];
+#pragma unroll
+            for (int j = 0; j < NAX; ++j) {      // right-hand side: the defects (0 for the multiplier estimate)
+                g1[j] = lsm ? 0.0 : g1o[j]; g2[j] = lsm ? 0.0 : g2o[j]; gz[j] = lsm ? 0.0 : gzo[j];
+            }
 #pragma unroll
             for (int j = 0; j < NAX; ++j) { gn1[j] = from_next(g1[j]); gn2[j] = from_next(g2[j]); }
             if constexpr (NAX == 1) {
@@ -741,6 +754,18 @@ void pmpc_ipm_kernel(PmpcArgs a) {
             }
             return cmp_le(th_t, (1 - gam_th) * theta, theta) || cmp_le(ph_t - phi, -gam_ph * theta, phi);
         };
+        if (lsm) {
+            direction();
+            // constr_mult_init_max: an estimate larger than it (max norm) is discarded (multipliers 0)
+            double ym = 0.0;
+#pragma unroll
+            for (int j = 0; j < NAX; ++j) ym = fmax(ym, xon ? fmax(fabs(dlp[j]), fabs(dlv[j])) : 0.0);
+            if (wmax(ym) <= a.mult_init_max) {
+#pragma unroll
+                for (int j = 0; j < NAX; ++j) { lp[j] += dlp[j]; lv[j] += dlv[j]; }
+            }
+            continue;
+        }
         for (;;) {
             direction();
             STAMP(4);

@@ -46,7 +46,8 @@ class Config(ctypes.Structure):
     _fields_ = [("variant", ctypes.c_int32), ("N", ctypes.c_int32), ("Ts", ctypes.c_double),
                 ("tol", ctypes.c_double), ("max_iter", ctypes.c_int32), ("B_max", ctypes.c_int32),
                 ("gravity", ctypes.c_double), ("acceptable_tol", ctypes.c_double),
-                ("acceptable_iter", ctypes.c_int32), ("max_soc", ctypes.c_int32), ("pmpc_path", ctypes.c_int32)]
+                ("acceptable_iter", ctypes.c_int32), ("max_soc", ctypes.c_int32), ("pmpc_path", ctypes.c_int32),
+                ("constr_mult_init_max", ctypes.c_double)]
 
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -187,12 +188,13 @@ class Solver:
     PATHS = {"ipopt": 0, "reduced": 1}
 
     def __init__(self, N=20, Ts=0.002, tol=1e-8, max_iter=3000, B_max=1024, device=0, gravity=-9.81, max_soc=4,
-                 path="ipopt"):
+                 path="ipopt", constr_mult_init_max=1000.0):
         self._h = ctypes.c_void_p()
         if path not in self.PATHS:
             raise DartMPCError(f"unknown PMPC path {path!r} (expected one of {sorted(self.PATHS)})")
         self.cfg = default_config(N=int(N), Ts=float(Ts), tol=float(tol), max_iter=int(max_iter), B_max=int(B_max),
-                                  gravity=float(gravity), max_soc=int(max_soc), pmpc_path=self.PATHS[path])
+                                  gravity=float(gravity), max_soc=int(max_soc), pmpc_path=self.PATHS[path],
+                                  constr_mult_init_max=float(constr_mult_init_max))
         rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
         if rc != 0:
             raise DartMPCError(f"dart_mpc_create failed with code {rc} (no gfx950 device or bad config)")

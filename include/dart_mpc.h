@@ -107,6 +107,9 @@ typedef struct dart_mpc_config {
                            defect rows of mpc_3d.py:37, :48 in theta, the filter, the error measures and
                            the second-order correction); 1 = the reduced (x, y) path, opt-in: same KKT
                            point to the tolerance, fewer iterations, but not IPOPT's iterates */
+    double constr_mult_init_max;  /* IPOPT constr_mult_init_max (default 1000): the starting equality
+                           multipliers are IPOPT's least-square estimate unless its max norm exceeds this
+                           (then 0); 0 = always start from 0.  Used by PMPC */
 } dart_mpc_config;
 
 typedef struct dart_mpc_handle dart_mpc_handle;

@@ -52,7 +52,8 @@ def _p(a, t=_dp):
     return a.ctypes.data_as(t)
 
 
-def solve_batch(states, targets, params, N=20, Ts=0.002, max_iter=200, tol=1e-9, nthreads=1, want_w=True, soc=True):
+def solve_batch(states, targets, params, N=20, Ts=0.002, max_iter=200, tol=1e-9, nthreads=1, want_w=True, soc=True,
+                mult_init_max=1000.0):
     states = np.ascontiguousarray(states, np.float64)
     targets = np.ascontiguousarray(targets, np.float64)
     params = np.ascontiguousarray(params, np.float64)
@@ -64,6 +65,7 @@ def solve_batch(states, targets, params, N=20, Ts=0.002, max_iter=200, tol=1e-9,
     st = np.zeros(B, np.int32)
     it = np.zeros(B, np.int32)
     lib().oracle_pmpc_set_soc(_max_soc(soc))
+    lib().oracle_pmpc_set_mult_init_max(ctypes.c_double(float(mult_init_max)))
     lib().oracle_pmpc_solve_batch(B, N, Ts, _p(states), _p(targets), _p(params), max_iter, tol, nthreads,
                                   _p(u0), _p(f), _p(w) if want_w else None, _p(st, _ip), _p(it, _ip))
     return dict(u0=u0, f=f, w=w, status=st, iters=it)

@@ -14,15 +14,16 @@
  *   - IPOPT's primal-dual barrier method as configured by mpc_3d.py:82
  *     (all options at IPOPT defaults): monotone mu (mu_init 0.1, kappa_mu 0.2,
  *     theta_mu 1.5, kappa_eps 10), fraction-to-boundary tau = max(0.99, 1-mu),
- *     bound_relax_factor 1e-8, bound multipliers initialised to 1,
- *     gradient-based objective scaling (nlp_scaling_max_gradient 100),
- *     exact Lagrangian Hessian, inertia correction (delta_w first 1e-4,
- *     x100 first time / x8 afterwards, reuse last/3).
+ *     bound_relax_factor 1e-8, bound multipliers initialised to 1, equality
+ *     multipliers initialised to IPOPT's least-square estimate
+ *     (constr_mult_init_max 1000), gradient-based objective scaling
+ *     (nlp_scaling_max_gradient 100), exact Lagrangian Hessian, inertia
+ *     correction (delta_w first 1e-4, x100 first time / x8 afterwards, reuse
+ *     last/3), the filter line search of Waechter & Biegler 2006 (Alg. A,
+ *     IPOPT's constants) with the second-order correction (max_soc 4).
  *   Deviations (documented in DESIGN.md): the KKT system is solved by an
  *   exact stage-wise Riccati recursion instead of MUMPS (same Newton step up
- *   to rounding), and the globalisation is an l1-merit Armijo backtracking
- *   line search instead of IPOPT's filter; both change only the iteration
- *   path, not the KKT point the method converges to.
+ *   to rounding); no restoration phase (status -2 where IPOPT would enter it).
  *
  * Exact first/second derivatives of the RK4 map are taken with second-order
  * forward "jets" (value, gradient, Hessian in the 8 stage variables x,u).
@@ -335,6 +336,73 @@ static double bound_dual_step(const ctx_t *C, work_t *W, int nU, double tau) {
     return az;
 }
 
+/* IPOPT's least-square estimate of the equality multipliers at the starting point
+ * (DefaultIterateInitializer::least_square_mults -> LeastSquareMultipliers::CalculateMultipliers, on by
+ * default with constr_mult_init_max = 1000): the augmented system [I J^T; J 0] [d; y] = [-r; 0] with
+ * r = grad f (scaled) - z_L + z_U, i.e. y minimises ||r + J^T y||.  With the stage structure of the
+ * shooting defects (J d = 0: d_x0 = 0, d_x(k+1) = A_k d_xk + B_k d_uk) it is an LQR with unit weights:
+ * y_k = -(P_k dx_k + p_k).  Uses W->A, W->Bm of the starting point; returns max |y|. */
+static double ls_multipliers(const ctx_t *C, work_t *W, double *y) {
+    const prob_t *P = C->P; const int N = C->N; const double sc = C->sc;
+    double Pm[NX][NX], pv[NX], gx[NX];
+    static __thread double Ks[NMAX][NU][NX], ks[NMAX][NU], Ps[NMAX + 1][NX][NX], ps[NMAX + 1][NX];
+    cost_grad_x(P, W->X + NX * N, C->ref, gx);
+    for (int i = 0; i < NX; ++i) { for (int j = 0; j < NX; ++j) Pm[i][j] = (i == j); pv[i] = sc * gx[i]; }
+    memcpy(Ps[N], Pm, sizeof Pm); memcpy(ps[N], pv, sizeof pv);
+    for (int k = N - 1; k >= 0; --k) {
+        double (*A)[NX] = W->A[k], (*Bm)[NU] = W->Bm[k];
+        double PA[NX][NX], PB[NX][NU], Qxx[NX][NX], Qux[NU][NX], Quu[NU][NU], qx[NX], qu[NU], L[3];
+        for (int i = 0; i < NX; ++i) {
+            for (int j = 0; j < NX; ++j) { double t = 0; for (int m = 0; m < NX; ++m) t += Ps[k + 1][i][m] * A[m][j]; PA[i][j] = t; }
+            for (int j = 0; j < NU; ++j) { double t = 0; for (int m = 0; m < NX; ++m) t += Ps[k + 1][i][m] * Bm[m][j]; PB[i][j] = t; }
+        }
+        cost_grad_x(P, W->X + NX * k, C->ref, gx);
+        for (int i = 0; i < NX; ++i) {
+            for (int j = 0; j < NX; ++j) { double t = (i == j); for (int m = 0; m < NX; ++m) t += A[m][i] * PA[m][j]; Qxx[i][j] = t; }
+            double t = sc * gx[i]; for (int m = 0; m < NX; ++m) t += A[m][i] * ps[k + 1][m]; qx[i] = t;
+        }
+        for (int a = 0; a < NU; ++a) {
+            const int j = NU * k + a;
+            for (int i = 0; i < NX; ++i) { double t = 0; for (int m = 0; m < NX; ++m) t += Bm[m][a] * PA[m][i]; Qux[a][i] = t; }
+            for (int c = 0; c < NU; ++c) { double t = (a == c); for (int m = 0; m < NX; ++m) t += Bm[m][a] * PB[m][c]; Quu[a][c] = t; }
+            double t = sc * 2 * P->R * W->U[j] - W->zL[j] + W->zU[j];
+            for (int m = 0; m < NX; ++m) t += Bm[m][a] * ps[k + 1][m];
+            qu[a] = t;
+        }
+        chol2(Quu[0][0], 0.5 * (Quu[0][1] + Quu[1][0]), Quu[1][1], L);      /* Quu >= I: positive definite */
+        double x2[2];
+        chol2_solve(L, qu, x2); ks[k][0] = -x2[0]; ks[k][1] = -x2[1];
+        for (int i = 0; i < NX; ++i) {
+            double b2[2] = {Qux[0][i], Qux[1][i]};
+            chol2_solve(L, b2, x2); Ks[k][0][i] = -x2[0]; Ks[k][1][i] = -x2[1];
+        }
+        for (int i = 0; i < NX; ++i) {
+            for (int j = 0; j < NX; ++j) Ps[k][i][j] = Qxx[i][j] + Qux[0][i] * Ks[k][0][j] + Qux[1][i] * Ks[k][1][j];
+            ps[k][i] = qx[i] + Qux[0][i] * ks[k][0] + Qux[1][i] * ks[k][1];
+        }
+    }
+    double dx[NX] = {0}, ymax = 0.0;
+    for (int k = 0; k <= N; ++k) {
+        for (int i = 0; i < NX; ++i) {
+            double t = ps[k][i]; for (int m = 0; m < NX; ++m) t += Ps[k][i][m] * dx[m];
+            y[NX * k + i] = -t; ymax = fmax(ymax, fabs(t));
+        }
+        if (k == N) break;
+        double du[NU], dn[NX];
+        for (int a = 0; a < NU; ++a) { double t = ks[k][a]; for (int i = 0; i < NX; ++i) t += Ks[k][a][i] * dx[i]; du[a] = t; }
+        for (int i = 0; i < NX; ++i) {
+            double t = 0; for (int m = 0; m < NX; ++m) t += W->A[k][i][m] * dx[m];
+            for (int a = 0; a < NU; ++a) t += W->Bm[k][i][a] * du[a];
+            dn[i] = t;
+        }
+        memcpy(dx, dn, sizeof dx);
+    }
+    return ymax;
+}
+
+static double g_mult_init_max = 1e3;   /* IPOPT constr_mult_init_max (default 1000; 0 = zero multipliers) */
+void oracle_pmpc_set_mult_init_max(double m) { g_mult_init_max = m; }
+
 int oracle_pmpc_solve(int N, double Ts, const double *state, const double *target, const double *prm,
                       const double *w_init, int max_iter, double tol,
                       double *u0, double *fval, double *w_out, int32_t *iters_out) {
@@ -368,6 +436,14 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
     ctx_t C = {&P, state, target, gmax > 100.0 ? 100.0 / gmax : 1.0, 0.1, lo, hi, N};
     double (*g)[NX] = (double (*)[NX])calloc(N + 1, sizeof(double[NX]));
 
+    if (g_mult_init_max > 0.0) {
+        for (int k = 0; k < N; ++k) {
+            double xn[NX], nl[NX] = {0};
+            rk4_derivs(&P, W->X + NX * k, W->U + NU * k, nl, xn, W->A[k], W->Bm[k], W->H[k]);
+        }
+        const double ymax = ls_multipliers(&C, W, W->lam);
+        if (!(ymax <= g_mult_init_max)) memset(W->lam, 0, sizeof(double) * ng);     /* constr_mult_init_max */
+    }
     double th = constraints(&C, W->X, W->U, g);
     const double th_max = 1e4 * fmax(1.0, th), th_min = 1e-4 * fmax(1.0, th);
     int nfilt = 0, status = ST_MAXITER, it;
