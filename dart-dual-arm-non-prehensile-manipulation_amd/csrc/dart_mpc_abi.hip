@@ -460,7 +460,7 @@ int dart_lmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* state, co
     HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
     dartmpc::LmpcArgs a;
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter;
-    a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc;
+    a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc; a.mult_init_max = h->cfg.constr_mult_init_max;
     a.state = state; a.u_prev = u_prev; a.pvec = pvec; a.target = target; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     a.fuse_policy = 0;
@@ -605,7 +605,7 @@ int dart_lmpc_policy_solve_batch_dev(dart_mpc_handle* h, const dart_lmpc_policy_
     a.pol.timestep = timestep; a.pol.noise = noise; a.pol.model_params = model_params; a.pol.action_out = action_out;
     a.fuse_policy = 1;
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter;
-    a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc;
+    a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc; a.mult_init_max = h->cfg.constr_mult_init_max;
     a.state = state; a.u_prev = u_prev; a.pvec = nullptr; a.target = target; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     HIPCHK(h, dartmpc_launch_lmpc(&a, stream ? (hipStream_t)stream : h->stream), "kernel launch");

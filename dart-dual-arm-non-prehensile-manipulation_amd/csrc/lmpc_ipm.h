@@ -15,6 +15,7 @@ struct LmpcArgs {
     double Ts, tol, acc_tol;
     int max_iter, acc_iter;
     int max_soc;             // IPOPT max_soc: second-order corrections after a rejected first trial
+    double mult_init_max;    // IPOPT constr_mult_init_max: > 0 least-square starting multipliers (default 1000)
     int pack;                // blocks per instance slot (set by the launcher; 8 = one XCD for small B)
     const double* state;     // [B][8]  [px, vx, py, vy, theta_x, omega_x, theta_y, omega_y]
     const double* u_prev;    // [B][2]

@@ -479,7 +479,15 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     int status = -1, it = 0;
 
     STAMP(0);
-    for (it = 0;; ++it) {
+    // it = -1 (a.mult_init_max > 0): IPOPT's least-square estimate of the starting multipliers
+    // (DefaultIterateInitializer::least_square_mults, constr_mult_init_max 1000) by the loop's own
+    // Riccati machinery: [W J^T; J 0] [d; y] = [-r; 0] with unit weights on x and u, weight 0 on the
+    // u_{k-1} copies (their columns then absorb the Delta-u gradient exactly and the defect multipliers
+    // are those of the reference NLP, which has no copy rows), r = scaled grad f - z_L + z_U, and a zero
+    // defect column; y = the step's new multipliers.  Mirrors ls_multipliers in oracle/lmpc_ipm.c.
+    const bool lsinit = a.mult_init_max > 0.0;
+    for (it = lsinit ? -1 : 0;; ++it) {
+        const bool lsm = it < 0;
         // ---------------- derivatives, residuals, optimality error ---------------------------
         const double isl = uon ? frcp(u - lo) : 0.0, isu = uon ? frcp(hi - u) : 0.0;
         double lamn[5];
@@ -489,7 +497,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         double pinf, pinf_u;  // primal residual maxima
         {
             double xn[4];
-            if (it == 0) {      // the setup's derivative pass (lambda = 0: J^T lambda = 0)
+            if (it <= 0 && (lsm || !lsinit)) {      // the setup's derivative pass (lambda = 0: J^T lambda = 0)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) xn[i] = SH.CS[sl][i];
 #pragma unroll
@@ -575,14 +583,15 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         const double is_c = 100.0 * frcp(fmax(100.0, sumz * (1.0 / nb)));
         const double err = fmax(dinf * is_d, fmax(pinf, c0 * is_c));
         // IPOPT OptimalityErrorConvergenceCheck: optimal, then acceptable, then the iteration cap
-        if (err <= tol && dinf <= sc && pinf_u <= 1e-4 && c0 <= 1e-4 * sc) { status = 0; break; }
-        if (a.acc_iter > 0 && err <= a.acc_tol && pinf_u <= 1e-2 && c0 <= 1e-2 * sc) {
+        if (!lsm && err <= tol && dinf <= sc && pinf_u <= 1e-4 && c0 <= 1e-4 * sc) { status = 0; break; }
+        if (lsm) {
+        } else if (a.acc_iter > 0 && err <= a.acc_tol && pinf_u <= 1e-2 && c0 <= 1e-2 * sc) {
             if (++acc_count >= a.acc_iter) { status = 1; break; }
         } else {
             acc_count = 0;
         }
         if (it >= a.max_iter) { status = -1; break; }
-        for (;;) {
+        for (; !lsm;) {
             const double cmu = fmax(c0 - mu, mu - cminw);
             if (fmax(dinf * is_d, fmax(pinf, cmu * is_c)) > 10.0 * mu || mu <= mu_min) break;
             mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
@@ -592,7 +601,36 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         STAMP(1);
 
         // ---------------- gradient rows (they depend on mu) ------------------------------------
-        {
+        if (lsm) {      // the least-square system: unit weights on x and u, 0 on the copy, zero defects
+            double gq[6];
+            cost_grad(x, u, up, gq);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) gq[j] *= sc;
+            if (uon) {
+                gq[5] += zu - zl;
+                for (int e = 0; e < LmLds::NTP; ++e) Hk[e] = 0.0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) Hk[hp(i, i)] = 1.0;
+                Hk[hp(5, 5)] = 1.0;
+#pragma unroll
+                for (int j = 0; j < 6; ++j) Hk[hp(6, j)] = gq[j];
+#pragma unroll
+                for (int r = 0; r < 5; ++r) Mk[6 * NC + r] = 0.0;
+            }
+            if (k == 0) {
+#pragma unroll
+                for (int r = 0; r < 5; ++r) S->dx0[hf][r] = 0.0;
+            }
+            if (k == N) {
+                double* GN = S->G[sl];
+                for (int e = 0; e < LmLds::NTP; ++e) GN[e] = 0.0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) GN[gszz<5>(i, i)] = 1.0;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) GN[gszz<5>(5, j)] = gq[j];
+                GN[hp(5, 5)] = 1.0;
+            }
+        } else {
             double gq[6];
             cost_grad(x, u, up, gq);
 #pragma unroll
@@ -614,6 +652,26 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         }
         __syncthreads();
         STAMP(2);
+        if (lsm) {
+            (void)riccati_s_sweep(S, N, RR);      // unit weights: every Quu >= 1
+            closed_loop_s(S, N);
+            double dxl[5], lmp[5];
+            forward_sweep_s(S, N, k, dxl);
+            const double* K = S->KK[uon ? sl : hf * LM_NMAXS];
+            double d0 = K[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) d0 = fma(K[j], dxl[j], d0);
+            node_multiplier_s(S, xon ? sl : hf * LM_NMAXS, dxl, uon ? d0 : 0.0, lmp);
+            // constr_mult_init_max on IPOPT's (row-scaled) multipliers of the reference's rows
+            double ym = 0.0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ym = fmax(ym, xon ? fabs(lmp[i]) * frcp(dsc[i]) : 0.0);
+            if (wmax(ym) <= a.mult_init_max) {
+#pragma unroll
+                for (int i = 0; i < 5; ++i) lam[i] = xon ? lmp[i] : 0.0;
+            }
+            continue;
+        }
 
         // ---------------- Newton step and filter line search ----------------------------------
         // One copy of the Riccati solve serves the plain Newton step (with inertia correction) and

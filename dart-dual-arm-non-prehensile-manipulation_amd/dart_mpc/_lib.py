@@ -356,14 +356,16 @@ LMPC_PRM_DEFAULT = np.array([200.0, 2.0, 200.0, 2.0, 0.0, 0.0, 0.0, 0.0,     # Q
 class LmpcSolver(Solver):
     """``dart_mpc_handle`` of variant LMPC, N <= 31.  Defaults are the reference's IPOPT options
     (LMPC/src/controller/rlmpc2.py:480-489): max_iter 50, tol 1e-4, acceptable_tol 1e-3,
-    acceptable_iter 5, and IPOPT's default max_soc 4 (second-order correction; 0 = off)."""
+    acceptable_iter 5, and IPOPT's defaults max_soc 4 (second-order correction; 0 = off) and
+    constr_mult_init_max 1000 (least-square starting multipliers; 0 = start from 0)."""
 
     def __init__(self, N=20, Ts=0.002, tol=1e-4, max_iter=50, acceptable_tol=1e-3, acceptable_iter=5,
-                 B_max=1024, device=0, max_soc=4):
+                 B_max=1024, device=0, max_soc=4, constr_mult_init_max=1000.0):
         self._h = ctypes.c_void_p()
         self.cfg = default_config(variant=VARIANT_LMPC, N=int(N), Ts=float(Ts), tol=float(tol), max_iter=int(max_iter),
                                   B_max=int(B_max), acceptable_tol=float(acceptable_tol),
-                                  acceptable_iter=int(acceptable_iter), max_soc=int(max_soc))
+                                  acceptable_iter=int(acceptable_iter), max_soc=int(max_soc),
+                                  constr_mult_init_max=float(constr_mult_init_max))
         rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
         if rc != 0:
             raise DartMPCError(f"dart_mpc_create(LMPC) failed with code {rc} (no gfx950 device or bad config)")

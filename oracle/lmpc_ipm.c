@@ -409,6 +409,78 @@ static void linearise(const prob_t *P, work_t *W) {
     }
 }
 
+/* IPOPT's least-square estimate of the starting equality multipliers (DefaultIterateInitializer::
+ * least_square_mults -> LeastSquareMultipliers, constr_mult_init_max 1000): y = argmin ||r + J^T y||
+ * over the columns of the reference NLP (x_k, u_k), r = scaled grad f - z_L + z_U.  In the augmented
+ * formulation [x_k; u_{k-1}] the copy rows x~_{k+1} = u_k are not rows of the reference NLP; giving the
+ * copy variables weight 0 in [W J^T; J 0] [d; y] = [-r; 0] makes their columns absorb the Delta-u
+ * gradient exactly (y_copy = -r_copy) and leaves the defect multipliers IPOPT's.  An LQR with unit
+ * weights on x and u, weight 0 on the copies, zero constraint right-hand side: y_k = -(P_k dx_k + p_k).
+ * Uses W->A / W->Bm of the starting point; fills lam (unscaled rows), returns max |lam / dsc|
+ * (IPOPT compares the scaled multipliers). */
+static double ls_multipliers(const ctx_t *C, work_t *W) {
+    const prob_t *P = C->P; const int N = P->N; const double sc = C->sc;
+    static __thread double Ks[NMAX][NU][NA], ks[NMAX][NU], Ps[NMAX + 1][NA][NA], ps[NMAX + 1][NA];
+    double zN[NZ], gN[NZ];
+    for (int i = 0; i < NA; ++i) zN[i] = W->X[NA * N + i];
+    zN[10] = zN[11] = 0.0;
+    cost_grad(P, zN, C->tgt, 1, gN);
+    for (int i = 0; i < NA; ++i) { for (int j = 0; j < NA; ++j) Ps[N][i][j] = (i == j && i < 8); ps[N][i] = sc * gN[i]; }
+    for (int k = N - 1; k >= 0; --k) {
+        double z[NZ], gq[NZ];
+        stage_z(W->X, W->U, k, z);
+        cost_grad(P, z, C->tgt, 0, gq);
+        for (int j = 0; j < NZ; ++j) gq[j] *= sc;
+        for (int a = 0; a < NU; ++a) gq[10 + a] += -W->zL[NU * k + a] + W->zU[NU * k + a];
+        double (*A)[NA] = W->A[k], (*Bm)[NU] = W->Bm[k], (*Pp)[NA] = Ps[k + 1];
+        double PA[NA][NA], PB[NA][NU], Qxx[NA][NA], Qux[NU][NA], Quu[NU][NU], qx[NA], qu[NU], L[3] = {1, 0, 1}, x2[2];
+        for (int i = 0; i < NA; ++i) {
+            for (int j = 0; j < NA; ++j) { double t = 0; for (int m = 0; m < NA; ++m) t += Pp[i][m] * A[m][j]; PA[i][j] = t; }
+            for (int j = 0; j < NU; ++j) { double t = 0; for (int m = 0; m < NA; ++m) t += Pp[i][m] * Bm[m][j]; PB[i][j] = t; }
+        }
+        for (int i = 0; i < NA; ++i) {
+            for (int j = 0; j < NA; ++j) { double t = (i == j && i < 8); for (int m = 0; m < NA; ++m) t += A[m][i] * PA[m][j]; Qxx[i][j] = t; }
+            double t = gq[i]; for (int m = 0; m < NA; ++m) t += A[m][i] * ps[k + 1][m]; qx[i] = t;
+        }
+        for (int a = 0; a < NU; ++a) {
+            for (int i = 0; i < NA; ++i) { double t = 0; for (int m = 0; m < NA; ++m) t += Bm[m][a] * PA[m][i]; Qux[a][i] = t; }
+            for (int c = 0; c < NU; ++c) { double t = (a == c); for (int m = 0; m < NA; ++m) t += Bm[m][a] * PB[m][c]; Quu[a][c] = t; }
+            double t = gq[NA + a]; for (int m = 0; m < NA; ++m) t += Bm[m][a] * ps[k + 1][m]; qu[a] = t;
+        }
+        chol2(Quu[0][0], 0.5 * (Quu[0][1] + Quu[1][0]), Quu[1][1], L);      /* Quu >= I */
+        chol2_solve(L, qu, x2); ks[k][0] = -x2[0]; ks[k][1] = -x2[1];
+        for (int i = 0; i < NA; ++i) {
+            double b2[2] = {Qux[0][i], Qux[1][i]};
+            chol2_solve(L, b2, x2); Ks[k][0][i] = -x2[0]; Ks[k][1][i] = -x2[1];
+        }
+        for (int i = 0; i < NA; ++i) {
+            for (int j = 0; j < NA; ++j) Ps[k][i][j] = Qxx[i][j] + Qux[0][i] * Ks[k][0][j] + Qux[1][i] * Ks[k][1][j];
+            ps[k][i] = qx[i] + Qux[0][i] * ks[k][0] + Qux[1][i] * ks[k][1];
+        }
+    }
+    double dx[NA] = {0}, ymax = 0.0;
+    for (int k = 0; k <= N; ++k) {
+        for (int i = 0; i < NA; ++i) {
+            double t = ps[k][i]; for (int m = 0; m < NA; ++m) t += Ps[k][i][m] * dx[m];
+            W->lam[NA * k + i] = -t;
+            if (i < 8) ymax = fmax(ymax, fabs(t) / W->dsc[NA * k + i]);   /* the copy rows are not IPOPT's */
+        }
+        if (k == N) break;
+        double du[NU], dn[NA];
+        for (int a = 0; a < NU; ++a) { double t = ks[k][a]; for (int i = 0; i < NA; ++i) t += Ks[k][a][i] * dx[i]; du[a] = t; }
+        for (int i = 0; i < NA; ++i) {
+            double t = 0; for (int m = 0; m < NA; ++m) t += W->A[k][i][m] * dx[m];
+            for (int a = 0; a < NU; ++a) t += W->Bm[k][i][a] * du[a];
+            dn[i] = t;
+        }
+        memcpy(dx, dn, sizeof dx);
+    }
+    return ymax;
+}
+
+static double g_mult_init_max = 1e3;   /* IPOPT constr_mult_init_max (default 1000; 0 = zero multipliers) */
+void oracle_lmpc_set_mult_init_max(double m) { g_mult_init_max = m; }
+
 /* prm = [Q(8), Qt(8), R(4), u_lo, u_hi];  acc_tol / acc_iter: IPOPT acceptable_tol / acceptable_iter (0 = off) */
 /* filter line-search acceptance of a trial (th_t, ph_t) for the step size alpha (IPOPT
    FilterLSAcceptor::CheckAcceptabilityOfTrialPoint with alpha_primal_test = alpha); *ftype is set
@@ -490,6 +562,10 @@ int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_pre
         W->dsc[NA * (k + 1) + i] = m > 100.0 ? 100.0 / m : 1.0;
     }
 
+    if (g_mult_init_max > 0.0) {
+        if (!(ls_multipliers(&C, W) <= g_mult_init_max)) memset(W->lam, 0, sizeof(double) * nA);
+        linearise(&P, W);      /* the Lagrangian Hessian of iteration 0 with these multipliers */
+    }
     double (*g)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
     double (*gt)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
     double (*csg)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));

@@ -133,3 +133,24 @@ def test_reference_options_same_path_as_oracle(dm, max_soc):
     assert np.array_equal(g["status"], o["status"])
     assert np.array_equal(g["iters"], o["iters"])
     assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6
+
+
+@pytest.mark.parametrize("mult_init", [1000.0, 0.0])
+def test_least_square_starting_multipliers_same_path(dm, mult_init):
+    """IPOPT starts the equality multipliers from its least-square estimate (constr_mult_init_max 1000,
+    the reference's nlpsol leaves it, rlmpc2.py:480-489); at the reference's loose tolerance the start
+    changes the answer (up to 0.64 rad on a 720-instance N = 20 oracle batch).  With the estimate and
+    with zero multipliers (constr_mult_init_max 0) the kernel takes the oracle's path on 360 C5
+    instances: same statuses and iterations, |du0| <= 1e-6."""
+    from dart_mpc.workload import lmpc_batch
+    D = lmpc_batch(20, seed0=9100)
+    s = dm.LmpcSolver(N=30, B_max=512, constr_mult_init_max=mult_init)
+    g = s.solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"])
+    s.close()
+    args = (D["state"], D["u_prev"], D["pvec"], D["target"])
+    o = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=8, mult_init_max=mult_init)
+    other = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=8, mult_init_max=1000.0 - mult_init)
+    assert np.mean(o["iters"] != other["iters"]) > 0.01      # the starting multipliers change the path
+    assert np.array_equal(g["status"], o["status"])
+    assert np.array_equal(g["iters"], o["iters"])
+    assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6
