@@ -396,7 +396,7 @@ int dart_rmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* x0, const
     if (B == 0) return DART_MPC_OK;
     HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
     dartmpc::RmpcArgs a;
-    a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.g = h->cfg.gravity; a.max_iter = h->cfg.max_iter;
+    a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.g = h->cfg.gravity; a.max_iter = h->cfg.max_iter; a.mult_init_max = h->cfg.constr_mult_init_max;
     a.x0 = x0; a.u_prev = u_prev; a.theta = theta; a.rls_P = rls_P; a.rls_phi = rls_phi; a.rls_y = rls_y;
     a.rls_lambda = rls_lambda; a.Rref = Rref; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;

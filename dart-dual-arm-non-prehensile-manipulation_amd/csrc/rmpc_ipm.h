@@ -9,6 +9,7 @@ struct RmpcArgs {
     int B, N;
     double Ts, tol, g;
     int max_iter;
+    double mult_init_max;   // IPOPT constr_mult_init_max: > 0 least-square starting multipliers (default 1000)
     int pack;                // blocks per instance slot (set by the launcher; 8 = one XCD for small B)
     const double* x0;        // [B][4]
     const double* u_prev;    // [B][2]

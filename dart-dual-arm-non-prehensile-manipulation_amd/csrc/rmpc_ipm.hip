@@ -421,7 +421,14 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     int status = -1, it = 0;
 
     STAMP(0);
-    for (it = 0; it < a.max_iter; ++it) {
+    // it = -1 (a.mult_init_max > 0): IPOPT's least-square estimate of the starting multipliers
+    // (DefaultIterateInitializer::least_square_mults, constr_mult_init_max 1000) through the loop's own
+    // stage QPs and Riccati sweep: unit weights on x and u (0 on the u_{k-1} copies, which are not
+    // variables of the reference NLP), the slack columns eliminated with weight 1 (Hessian C^T C,
+    // gradient C^T r_s, r_s = -v_L + v_U), r = scaled grad f - z_L + z_U, zero defects; the equality
+    // multipliers are the step's new multipliers, y_d = C dz + r_s.  Mirrors oracle/rmpc_ipm.c.
+    for (it = a.mult_init_max > 0.0 ? -1 : 0; it < a.max_iter; ++it) {
+        const bool lsm = it < 0;
         // ---------------- derivatives, residuals, optimality error ---------------------------
         // stage data go to LDS as soon as they exist (Jacobian columns, dynamics Hessian, defect
         // column, dx~_0) to keep the register working set small
@@ -451,7 +458,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             { const double t0 = from_next(up[0]), t1 = from_next(up[1]); cdef[4] = u[0] - t0; cdef[5] = u[1] - t1; }
             if (uon) {
 #pragma unroll
-                for (int r = 0; r < 6; ++r) Mk[8 * RmLds::NC + r] = cdef[r];
+                for (int r = 0; r < 6; ++r) Mk[8 * RmLds::NC + r] = lsm ? 0.0 : cdef[r];
             }
             double pl = 0.0;     // incoming defect g_k: primal residual, -g_0 = dx~_0
 #pragma unroll
@@ -460,7 +467,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
                 double gi = -t;
                 if (k == 0) gi = i < 4 ? x[i] - x0[i] : up[i - 4] - upv[i - 4];
                 pl = fmax(pl, xon ? fabs(gi) : 0.0);
-                if (k == 0) S->dx0[i] = -gi;
+                if (k == 0) S->dx0[i] = lsm ? 0.0 : -gi;
             }
             SH.JL[sr][6] = pl;
         }
@@ -472,8 +479,9 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             rq[i] = uon ? cz[i] - s[i] : 0.0;
             const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
             const double idl = tw[i] ? frcp(dl) : 0.0, idu = frcp(du_);
-            sig[i] = uon ? fma(vl[i], idl, vu[i] * idu) : 0.0;
-            psi[i] = uon ? mu * (idu - idl) : 0.0;
+            sig[i] = uon ? (lsm ? 1.0 : fma(vl[i], idl, vu[i] * idu)) : 0.0;
+            psi[i] = uon ? (lsm ? vu[i] - vl[i] : mu * (idu - idl)) : 0.0;     // (least squares: r_s)
+            rq[i] = lsm ? 0.0 : rq[i];
         }
         double dinf = 0.0, pinf = SH.JL[sr][6], c0 = 0.0, cmin = 1e300, suml = 0.0, sumz = 0.0;
         {
@@ -524,8 +532,8 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         // IPOPT's scalings s_d, s_c (>= 1) as reciprocals
         const double is_d = 100.0 * frcp(fmax(100.0, (suml + sumz) * (1.0 / (nA + nI + nb))));
         const double is_c = 100.0 * frcp(fmax(100.0, sumz * (1.0 / nb)));
-        if (fmax(dinf * is_d, fmax(pinf, c0 * is_c)) <= tol) { status = 0; break; }
-        for (;;) {
+        if (!lsm && fmax(dinf * is_d, fmax(pinf, c0 * is_c)) <= tol) { status = 0; break; }
+        for (; !lsm;) {
             const double cmu = fmax(c0 - mu, mu - cminw);
             if (fmax(dinf * is_d, fmax(pinf, cmu * is_c)) > 10.0 * mu || mu <= mu_min) break;
             mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
@@ -557,25 +565,32 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 #pragma unroll
             for (int i = 0; i < RM_NQ; ++i) { so[i] = __shfl_xor(sig[i], 32); to[i] = __shfl_xor(tq[i], 32); }
             if (uon && nod) {
-                gq[6] += -mu * isl0 + mu * isu0; gq[7] += -mu * isl1 + mu * isu1;
+                if (lsm) {      // least squares: the box gradient -z_L + z_U, unit weights (0 on the copies)
+                    gq[6] += zu[0] - zl[0]; gq[7] += zu[1] - zl[1];
+                } else {
+                    gq[6] += -mu * isl0 + mu * isu0; gq[7] += -mu * isl1 + mu * isu1;
+                }
                 gq[6] += tq[0]; gq[4] -= tq[0]; gq[7] += tq[1]; gq[5] -= tq[1];
                 gq[1] += tq[2] - to[0];
                 gq[3] += to[1] - to[2];
-                Hk[hp(0, 0)] += sc * 2 * Qp; Hk[hp(2, 2)] += sc * 2 * Qp;
-                Hk[hp(1, 1)] += sc * 2 * Qv + sig[2] + so[0];
-                Hk[hp(3, 3)] += sc * 2 * Qv + so[1] + so[2];
-                Hk[hp(6, 6)] += sc * 2 * (Ru + Rdu) + zl[0] * isl0 + zu[0] * isu0 + sig[0];
-                Hk[hp(7, 7)] += sc * 2 * (Ru + Rdu) + zl[1] * isl1 + zu[1] * isu1 + sig[1];
-                Hk[hp(4, 4)] = sc * 2 * Rdu + sig[0]; Hk[hp(5, 5)] = sc * 2 * Rdu + sig[1];
-                Hk[hp(6, 4)] = -sc * 2 * Rdu - sig[0]; Hk[hp(7, 5)] = -sc * 2 * Rdu - sig[1];
+                const double wp = lsm ? 1.0 : sc * 2 * Qp, wv = lsm ? 1.0 : sc * 2 * Qv, wd = lsm ? 0.0 : sc * 2 * Rdu;
+                const double wu0 = lsm ? 1.0 : sc * 2 * (Ru + Rdu) + zl[0] * isl0 + zu[0] * isu0;
+                const double wu1 = lsm ? 1.0 : sc * 2 * (Ru + Rdu) + zl[1] * isl1 + zu[1] * isu1;
+                Hk[hp(0, 0)] += wp; Hk[hp(2, 2)] += wp;
+                Hk[hp(1, 1)] += wv + sig[2] + so[0];
+                Hk[hp(3, 3)] += wv + so[1] + so[2];
+                Hk[hp(6, 6)] += wu0 + sig[0];
+                Hk[hp(7, 7)] += wu1 + sig[1];
+                Hk[hp(4, 4)] = wd + sig[0]; Hk[hp(5, 5)] = wd + sig[1];
+                Hk[hp(6, 4)] = -wd - sig[0]; Hk[hp(7, 5)] = -wd - sig[1];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) Hk[hp(8, j)] = gq[j];
             }
             if (k == N && nod) {   // terminal surrogate G_N: value function [[Q_N, q_N], [q_N^T, 0]], Quu = I
                 double* GN = S->G[N];
                 for (int e = 0; e < tri(9); ++e) GN[e] = 0.0;
-                GN[hp(0, 0)] = sc * 2 * Qp; GN[hp(2, 2)] = sc * 2 * Qp;
-                GN[hp(1, 1)] = sc * 2 * Qv; GN[hp(3, 3)] = sc * 2 * Qv;
+                GN[hp(0, 0)] = lsm ? 1.0 : sc * 2 * Qp; GN[hp(2, 2)] = lsm ? 1.0 : sc * 2 * Qp;
+                GN[hp(1, 1)] = lsm ? 1.0 : sc * 2 * Qv; GN[hp(3, 3)] = lsm ? 1.0 : sc * 2 * Qv;
                 GN[hp(6, 6)] = 1.0; GN[hp(7, 7)] = 1.0;
 #pragma unroll
                 for (int j = 0; j < 6; ++j) GN[hp(8, j)] = gq[j];
@@ -583,6 +598,33 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         }
         __syncthreads();
         STAMP(2);
+        if (lsm) {
+            (void)riccati_sweep_aug(S, N);      // unit weights: positive definite
+            closed_loop(S, N);
+            double dxl[6], dUl[2], lmp[6];
+            forward_sweep(S, N, k, dxl);
+            const double* K0 = S->KK[uon ? k : 0][0];
+            const double* K1 = S->KK[uon ? k : 0][1];
+            double d0 = K0[6], d1 = K1[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) { d0 = fma(K0[j], dxl[j], d0); d1 = fma(K1[j], dxl[j], d1); }
+            dUl[0] = uon ? d0 : 0.0; dUl[1] = uon ? d1 : 0.0;
+            node_multiplier(S, xon ? k : 0, dxl, dUl, lmp);
+            const double dzv[8] = {dxl[0], dxl[1], dxl[2], dxl[3], dxl[4], dxl[5], dUl[0], dUl[1]};
+            double cdz[RM_NQ], yd[RM_NQ], ym = 0.0;
+            rm_iq3(dzv, 0.0, mir, cdz);
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) { yd[i] = uon ? cdz[i] + psi[i] : 0.0; ym = fmax(ym, fabs(yd[i])); }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ym = fmax(ym, nod && xon ? fabs(lmp[i]) : 0.0);   // (copy rows are not IPOPT's)
+            if (wmax(ym) <= a.mult_init_max) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) lam[i] = xon ? lmp[i] : 0.0;
+#pragma unroll
+                for (int i = 0; i < RM_NQ; ++i) yq[i] = yd[i];
+            }
+            continue;
+        }
 
         // ---------------- Newton step: Riccati with inertia correction -----------------------
         double delta = 0.0, dapplied = 0.0;

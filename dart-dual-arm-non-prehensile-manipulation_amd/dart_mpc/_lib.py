@@ -140,8 +140,9 @@ def lib():
     L.dart_arm_solve_batch_dev.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6
     L.dart_arm_solve_batch_dev.restype = ctypes.c_int
-    L.dart_set_device.argtypes = [ctypes.c_int]
-    L.dart_set_device.restype = ctypes.c_int
+    if hasattr(L, "dart_set_device"):       # (absent only in older in-tree builds used for A/B timing)
+        L.dart_set_device.argtypes = [ctypes.c_int]
+        L.dart_set_device.restype = ctypes.c_int
     if L.dart_mpc_abi_version() != ABI_VERSION:
         raise DartMPCError("libdartmpc.so ABI version mismatch")
     _lib = L
@@ -305,10 +306,12 @@ class Solver:
 class RmpcSolver(Solver):
     """``dart_mpc_handle`` of variant RMPC (regressor NMPC + fused RLS), N <= 31."""
 
-    def __init__(self, N=20, Ts=0.002, tol=1e-8, max_iter=200, B_max=1024, device=0, gravity=-9.81):
+    def __init__(self, N=20, Ts=0.002, tol=1e-8, max_iter=200, B_max=1024, device=0, gravity=-9.81,
+                 constr_mult_init_max=1000.0):
         self._h = ctypes.c_void_p()
         self.cfg = default_config(variant=VARIANT_RMPC, N=int(N), Ts=float(Ts), tol=float(tol),
-                                  max_iter=int(max_iter), B_max=int(B_max), gravity=float(gravity))
+                                  max_iter=int(max_iter), B_max=int(B_max), gravity=float(gravity),
+                                  constr_mult_init_max=float(constr_mult_init_max))
         rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
         if rc != 0:
             raise DartMPCError(f"dart_mpc_create(RMPC) failed with code {rc} (no gfx950 device or bad config)")

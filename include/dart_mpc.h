@@ -109,7 +109,7 @@ typedef struct dart_mpc_config {
                            point to the tolerance, fewer iterations, but not IPOPT's iterates */
     double constr_mult_init_max;  /* IPOPT constr_mult_init_max (default 1000): the starting equality
                            multipliers are IPOPT's least-square estimate unless its max norm exceeds this
-                           (then 0); 0 = always start from 0.  Used by PMPC and LMPC */
+                           (then 0); 0 = always start from 0.  Used by PMPC, RMPC and LMPC */
 } dart_mpc_config;
 
 typedef struct dart_mpc_handle dart_mpc_handle;

@@ -10,9 +10,10 @@
  *   (defects :109-112, du rows :114-121, velocity caps :123-127, cost :129-140,
  *   U box :146-154); solve with warm start :212-222; IPOPT options
  *   print_level 0, sb yes, max_iter 200 (:158-162), everything else default.
- * IPOPT's algorithm as in pmpc_ipm.c (monotone mu, filter line search with
- * second-order correction, inertia correction, bound_relax 1e-8, gradient
- * scaling), with IPOPT's slack formulation for the inequality rows
+ * IPOPT's algorithm as in pmpc_ipm.c (monotone mu, least-square starting
+ * multipliers, filter line search with second-order correction, inertia
+ * correction, bound_relax 1e-8, gradient scaling), with IPOPT's slack
+ * formulation for the inequality rows
  * g(w) - s = 0, g_L <= s <= g_U.  The KKT system is solved by a Riccati
  * recursion on the augmented state [x_k; u_{k-1}] (the Delta-u rows couple
  * consecutive controls); slacks and their multipliers are eliminated per stage.
@@ -427,6 +428,95 @@ static double dual_steps(const ctx_t *C, work_t *W, int nU, double tau) {
     return az;
 }
 
+/* IPOPT's least-square estimate of the starting multipliers (DefaultIterateInitializer::least_square_mults
+ * -> LeastSquareMultipliers, constr_mult_init_max 1000): [I J^T; J 0] [d; y] = [-r; 0] over the columns of
+ * x, u and the slacks s of the inequality rows d(x) - s = 0, with r_x = scaled grad f - z_L + z_U and
+ * r_s = -v_L + v_U.  Eliminating d_s = J_d d_x gives per stage the Hessian I + C^T C (the u_{k-1} copies of
+ * the augmented state weighted 0: they are not variables of the reference NLP, see lmpc_ipm.c) and the
+ * gradient r + C^T r_s; y_c = -(P_k dx_k + p_k), y_d = C dz + r_s.  Fills W->lam and W->y at the starting
+ * point (W->A / W->Bm set); returns max(|y_c|, |y_d|) over the rows of the reference NLP. */
+static double ls_multipliers(const ctx_t *C, work_t *W) {
+    const prob_t *P = C->P; const int N = P->N; const double sc = C->sc;
+    static __thread double Ks[NMAX][NU][NA], ks[NMAX][NU], Ps[NMAX + 1][NA][NA], ps[NMAX + 1][NA];
+    static __thread double Hs[NMAX][NZ][NZ], gs[NMAX][NZ];
+    double zN[NZ], gN[NZ];
+    stage_z(W->X, W->U, N, zN);
+    cost_grad(P, zN, C->R + 4 * N, 1, gN);
+    for (int i = 0; i < NA; ++i) { for (int j = 0; j < NA; ++j) Ps[N][i][j] = (i == j && i < 4); ps[N][i] = sc * gN[i]; }
+    for (int k = N - 1; k >= 0; --k) {
+        double z[NZ], (*Hq)[NZ] = Hs[k], *gq = gs[k];
+        stage_z(W->X, W->U, k, z);
+        cost_grad(P, z, C->R + 4 * k, 0, gq);
+        for (int a = 0; a < NZ; ++a) { gq[a] *= sc; for (int b2 = 0; b2 < NZ; ++b2) Hq[a][b2] = (a == b2 && (a < 4 || a >= NA)); }
+        for (int a = 0; a < NU; ++a) gq[NA + a] += -W->zL[NU * k + a] + W->zU[NU * k + a];
+        for (int i = 0; i < NIQ; ++i) {
+            double cr[NZ];
+            iq_row(i, cr);
+            const double rs = -W->vL[k][i] + W->vU[k][i];
+            for (int a = 0; a < NZ; ++a) {
+                if (cr[a] == 0.0) continue;
+                for (int b2 = 0; b2 < NZ; ++b2) Hq[a][b2] += cr[a] * cr[b2];
+                gq[a] += cr[a] * rs;
+            }
+        }
+        double (*A)[NA] = W->A[k], (*Bm)[NU] = W->Bm[k], (*Pp)[NA] = Ps[k + 1];
+        double PA[NA][NA], PB[NA][NU], Qxx[NA][NA], Qux[NU][NA], Quu[NU][NU], qx[NA], qu[NU], L[3] = {1, 0, 1}, x2[2];
+        for (int i = 0; i < NA; ++i) {
+            for (int j = 0; j < NA; ++j) { double t = 0; for (int m = 0; m < NA; ++m) t += Pp[i][m] * A[m][j]; PA[i][j] = t; }
+            for (int j = 0; j < NU; ++j) { double t = 0; for (int m = 0; m < NA; ++m) t += Pp[i][m] * Bm[m][j]; PB[i][j] = t; }
+        }
+        for (int i = 0; i < NA; ++i) {
+            for (int j = 0; j < NA; ++j) { double t = Hq[i][j]; for (int m = 0; m < NA; ++m) t += A[m][i] * PA[m][j]; Qxx[i][j] = t; }
+            double t = gq[i]; for (int m = 0; m < NA; ++m) t += A[m][i] * ps[k + 1][m]; qx[i] = t;
+        }
+        for (int a = 0; a < NU; ++a) {
+            for (int i = 0; i < NA; ++i) { double t = Hq[NA + a][i]; for (int m = 0; m < NA; ++m) t += Bm[m][a] * PA[m][i]; Qux[a][i] = t; }
+            for (int c = 0; c < NU; ++c) { double t = Hq[NA + a][NA + c]; for (int m = 0; m < NA; ++m) t += Bm[m][a] * PB[m][c]; Quu[a][c] = t; }
+            double t = gq[NA + a]; for (int m = 0; m < NA; ++m) t += Bm[m][a] * ps[k + 1][m]; qu[a] = t;
+        }
+        chol2(Quu[0][0], 0.5 * (Quu[0][1] + Quu[1][0]), Quu[1][1], L);      /* Quu >= I */
+        chol2_solve(L, qu, x2); ks[k][0] = -x2[0]; ks[k][1] = -x2[1];
+        for (int i = 0; i < NA; ++i) {
+            double b2[2] = {Qux[0][i], Qux[1][i]};
+            chol2_solve(L, b2, x2); Ks[k][0][i] = -x2[0]; Ks[k][1][i] = -x2[1];
+        }
+        for (int i = 0; i < NA; ++i) {
+            for (int j = 0; j < NA; ++j) Ps[k][i][j] = Qxx[i][j] + Qux[0][i] * Ks[k][0][j] + Qux[1][i] * Ks[k][1][j];
+            ps[k][i] = qx[i] + Qux[0][i] * ks[k][0] + Qux[1][i] * ks[k][1];
+        }
+    }
+    double dx[NA] = {0}, ymax = 0.0;
+    for (int k = 0; k <= N; ++k) {
+        for (int i = 0; i < NA; ++i) {
+            double t = ps[k][i]; for (int m = 0; m < NA; ++m) t += Ps[k][i][m] * dx[m];
+            W->lam[NA * k + i] = -t;
+            if (i < 4) ymax = fmax(ymax, fabs(t));      /* the copy rows are not IPOPT's */
+        }
+        if (k == N) break;
+        double du[NU], dn[NA], dz[NZ];
+        for (int a = 0; a < NU; ++a) { double t = ks[k][a]; for (int i = 0; i < NA; ++i) t += Ks[k][a][i] * dx[i]; du[a] = t; }
+        for (int i = 0; i < NA; ++i) dz[i] = dx[i];
+        dz[NA] = du[0]; dz[NA + 1] = du[1];
+        for (int i = 0; i < NIQ; ++i) {
+            double cr[NZ], cdz = 0.0;
+            iq_row(i, cr);
+            for (int a = 0; a < NZ; ++a) cdz += cr[a] * dz[a];
+            W->y[k][i] = cdz - W->vL[k][i] + W->vU[k][i];
+            ymax = fmax(ymax, fabs(W->y[k][i]));
+        }
+        for (int i = 0; i < NA; ++i) {
+            double t = 0; for (int m = 0; m < NA; ++m) t += W->A[k][i][m] * dx[m];
+            for (int a = 0; a < NU; ++a) t += W->Bm[k][i][a] * du[a];
+            dn[i] = t;
+        }
+        memcpy(dx, dn, sizeof dx);
+    }
+    return ymax;
+}
+
+static double g_mult_init_max = 1e3;   /* IPOPT constr_mult_init_max (default 1000; 0 = zero multipliers) */
+void oracle_rmpc_set_mult_init_max(double m) { g_mult_init_max = m; }
+
 int oracle_rmpc_solve(int N, double Ts, const double *x0, const double *u_prev, const double *theta,
                       const double *Rref, const double *prm, const double *w_init, int max_iter, double tol,
                       double *u0, double *fval, double *w_out, int32_t *iters_out) {
@@ -486,6 +576,19 @@ int oracle_rmpc_solve(int N, double Ts, const double *x0, const double *u_prev, 
     }
     C.sc = gmax > 100.0 ? 100.0 / gmax : 1.0;
 
+    if (g_mult_init_max > 0.0) {
+        for (int k = 0; k < N; ++k) {        /* the Jacobian at the starting point */
+            double xn[4], nl[4] = {0, 0, 0, 0}, J[4][NZ];
+            rk4_derivs(&P, W->X + NA * k, W->U + NU * k, nl, xn, J, W->Hs[k]);
+            for (int i = 0; i < NA; ++i) { for (int j = 0; j < NA; ++j) W->A[k][i][j] = 0.0; W->Bm[k][i][0] = W->Bm[k][i][1] = 0.0; }
+            for (int i = 0; i < 4; ++i) { for (int j = 0; j < 4; ++j) W->A[k][i][j] = J[i][j]; W->Bm[k][i][0] = J[i][6]; W->Bm[k][i][1] = J[i][7]; }
+            W->Bm[k][4][0] = 1.0; W->Bm[k][5][1] = 1.0;
+        }
+        if (!(ls_multipliers(&C, W) <= g_mult_init_max)) {
+            memset(W->lam, 0, sizeof W->lam);
+            for (int k = 0; k < N; ++k) for (int i = 0; i < NIQ; ++i) W->y[k][i] = 0.0;
+        }
+    }
     double (*g)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
     double (*r)[NIQ] = (double (*)[NIQ])calloc(N, sizeof(double[NIQ]));
     double (*gt)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));

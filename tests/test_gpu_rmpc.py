@@ -170,6 +170,26 @@ def test_closed_loop_driver_matches_oracle_loop(dm):
         up = u
 
 
+@pytest.mark.parametrize("mult_init", [1000.0, 0.0])
+def test_least_square_starting_multipliers_same_path(dm, mult_init):
+    """IPOPT starts y_c and y_d (the slack rows) from its least-square estimate (constr_mult_init_max 1000;
+    np_mpc...:158-162 leaves it): on C3 it changes a third of the iteration counts.  With the estimate and
+    with zero multipliers the kernel follows the oracle: same statuses, >= 99 % same iterations,
+    |du0| <= 1e-6 at the reference's tol 1e-8."""
+    from dart_mpc.workload import rmpc_batch
+    D = rmpc_batch(8, seed0=60)
+    s = dm.RmpcSolver(N=20, tol=1e-8, B_max=256, constr_mult_init_max=mult_init)
+    g = s.solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
+    s.close()
+    args = (D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
+    o = oracle_lib.rmpc_solve_batch(*args, N=20, tol=1e-8, nthreads=8, mult_init_max=mult_init)
+    other = oracle_lib.rmpc_solve_batch(*args, N=20, tol=1e-8, nthreads=8, mult_init_max=1000.0 - mult_init)
+    assert np.mean(o["iters"] != other["iters"]) > 0.05
+    assert np.array_equal(g["status"], o["status"])
+    assert np.mean(g["iters"] == o["iters"]) >= 0.99, (g["iters"], o["iters"])
+    assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6
+
+
 @pytest.mark.parametrize("soc", [False, True])
 def test_same_path_as_oracle(dm, soc):
     """Exact derivatives in the kernel: against the C oracle with its second-order correction off
