@@ -166,6 +166,24 @@ struct dart_mpc_handle {
     // has retired the kernel's last instructions: the next entry on the handle settles that stream
     // first, so a late stream error is reported as the previous call's, not blamed on the new one
     hipStream_t pending = nullptr;
+    // resident PMPC server (dart_mpc_serve_start): its own stream, a mailbox, inputs and outputs at
+    // fixed mapped addresses for B_serve slots
+    struct Server {
+        bool wanted = false;               // serve_start called, serve_stop not yet
+        bool running = false;
+        int B = 0;
+        hipStream_t stream = nullptr;
+        uint32_t* mbox = nullptr;          // mapped: the 64-bit request word (pmpc_ipm.h PmpcServe)
+        uint32_t* dmbox = nullptr;
+        unsigned long long idle_ticks = 0;
+    } srv;
+    // PMPC in-place I/O area (dart_mpc_bind; the resident server's inputs and outputs): mapped,
+    // coherent pinned memory for B_max instances at fixed addresses
+    struct Io {
+        char* hin = nullptr;  char* din = nullptr;      // x0 | ref | prm | w_warm
+        char* hout = nullptr; char* dout = nullptr;     // u0 | f | w_out | status | iters
+        size_t off_ref = 0, off_prm = 0, off_ww = 0, off_f = 0, off_wo = 0, off_st = 0, off_it = 0;
+    } io;
     // Serialises the entries on this handle: the host-pointer entries share the pinned staging
     // buffers and the handle's stream, and every entry may write err.  Concurrent callers (the
     // reference runs controllers on background threads, RMPC/dev_dual/controller/convimp.py:435)
@@ -201,6 +219,78 @@ int check_cfg(const dart_mpc_config* c) {
     if (c->pmpc_path != 0 && c->pmpc_path != 1) return 0;
     if (!(c->constr_mult_init_max >= 0.0)) return 0;
     return 1;
+}
+
+void server_release(dart_mpc_handle* h) {
+    auto& v = h->srv;
+    if (v.mbox) (void)hipHostFree(v.mbox);
+    if (v.stream) (void)hipStreamDestroy(v.stream);
+    v = dart_mpc_handle::Server{};
+}
+
+void io_release(dart_mpc_handle* h) {
+    auto& o = h->io;
+    if (o.hin) (void)hipHostFree(o.hin);
+    if (o.hout) (void)hipHostFree(o.hout);
+    o = dart_mpc_handle::Io{};
+}
+
+// the in-place I/O area for B_max instances (allocated once)
+hipError_t ensure_io(dart_mpc_handle* h) {
+    auto& o = h->io;
+    if (o.hin) return hipSuccess;
+    const size_t nw = (size_t)dart_mpc_nw(h->cfg.N), Bm = (size_t)h->cfg.B_max;
+    auto al = [](size_t n) { return (n + 255) & ~size_t(255); };
+    o.off_ref = al(sizeof(double) * 6 * Bm); o.off_prm = 2 * o.off_ref; o.off_ww = 3 * o.off_ref;
+    const size_t in_bytes = o.off_ww + al(sizeof(double) * nw * Bm);
+    o.off_f = al(sizeof(double) * 2 * Bm); o.off_wo = o.off_f + al(sizeof(double) * Bm);
+    o.off_st = o.off_wo + al(sizeof(double) * nw * Bm); o.off_it = o.off_st + al(sizeof(int32_t) * Bm);
+    const size_t out_bytes = o.off_it + al(sizeof(int32_t) * Bm);
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    hipError_t e = hipHostMalloc((void**)&o.hin, in_bytes, fl);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&o.din, o.hin, 0);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&o.hout, out_bytes, fl);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&o.dout, o.hout, 0);
+    if (e != hipSuccess) { io_release(h); return e; }
+    std::memset(o.hin, 0, in_bytes);
+    std::memset(o.hout, 0, out_bytes);
+    return hipSuccess;
+}
+
+// kernel arguments reading / writing the I/O area
+dartmpc::PmpcArgs io_args(dart_mpc_handle* h, int B, bool ww, bool wo) {
+    const auto& o = h->io;
+    dartmpc::PmpcArgs a;
+    a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter; a.g = h->cfg.gravity;
+    a.max_soc = h->cfg.max_soc; a.reduced = h->cfg.pmpc_path; a.mult_init_max = h->cfg.constr_mult_init_max;
+    a.x0 = (const double*)o.din; a.ref = (const double*)(o.din + o.off_ref); a.prm = (const double*)(o.din + o.off_prm);
+    a.w_warm = ww ? (const double*)(o.din + o.off_ww) : nullptr;
+    a.u0 = (double*)o.dout; a.f = (double*)(o.dout + o.off_f); a.w_out = wo ? (double*)(o.dout + o.off_wo) : nullptr;
+    a.status = (int32_t*)(o.dout + o.off_st); a.iters = (int32_t*)(o.dout + o.off_it);
+    a.done = h->ddone; a.seq = h->seq;
+    return a;
+}
+
+// (re)launch the resident grid; it takes every request with a sequence other than `seen`
+hipError_t server_launch(dart_mpc_handle* h, uint32_t seen) {
+    auto& v = h->srv;
+    dartmpc::PmpcArgs a = io_args(h, v.B, true, true);     // the flags of each request select w_warm / w_out
+    a.seq = seen;
+    dartmpc::PmpcServe sv{v.dmbox, v.idle_ticks};
+    const hipError_t e = dartmpc_launch_pmpc_serve(&a, &sv, v.stream);
+    v.running = e == hipSuccess;
+    return e;
+}
+
+// stop the resident server (if any) and wait until its grid has drained
+int server_stop(dart_mpc_handle* h) {
+    auto& v = h->srv;
+    if (!v.stream) return DART_MPC_OK;
+    __atomic_store_n((unsigned long long*)v.mbox, (unsigned long long)v.mbox[0] | (1ull << 56), __ATOMIC_RELEASE);
+    const hipError_t e = hipStreamSynchronize(v.stream);
+    v.running = false;
+    server_release(h);
+    return e == hipSuccess ? DART_MPC_OK : fail(h, DART_MPC_EHIP, "resident server", e);
 }
 
 // settle the stream of an earlier host PMPC call that returned on its completion words (see
@@ -244,6 +334,49 @@ int wait_done(dart_mpc_handle* h, hipStream_t s, const volatile uint32_t* done, 
     for (int b = 0; b < B; ++b)
         if (__atomic_load_n(done + b, __ATOMIC_ACQUIRE) != seq) return fail(h, DART_MPC_EHIP, "kernel did not complete");
     return DART_MPC_OK;
+}
+
+// post a request to the resident server (inputs already in the I/O area) and wait for its B
+// completion words; a grid that drained meanwhile (idle timeout) is relaunched and takes the request
+int served_request(dart_mpc_handle* h, int B, bool ww, bool wo) {
+    auto& v = h->srv;
+    if (!v.running || hipStreamQuery(v.stream) != hipErrorNotReady) {     // drained (idle timeout)
+        HIPCHK(h, hipStreamSynchronize(v.stream), "resident server");
+        HIPCHK(h, server_launch(h, v.mbox[0]), "resident server relaunch");
+    }
+    if (++h->seq == 0) h->seq = 1;      // (done words are only compared for equality)
+    const uint32_t sq = h->seq;
+    const unsigned long long fl = (ww ? 1ull : 0ull) | (wo ? 2ull : 0ull);
+    __atomic_store_n((unsigned long long*)v.mbox, (unsigned long long)sq | ((unsigned long long)B << 32) | (fl << 48),
+                     __ATOMIC_RELEASE);
+    for (unsigned n = 1;; ++n) {
+        int bb = 0;
+        while (bb < B && __atomic_load_n(h->hdone + bb, __ATOMIC_ACQUIRE) == sq) ++bb;
+        if (bb == B) return DART_MPC_OK;
+        if ((n & 1023) == 0 && hipStreamQuery(v.stream) != hipErrorNotReady) {
+            bb = 0;
+            while (bb < B && __atomic_load_n(h->hdone + bb, __ATOMIC_ACQUIRE) == sq) ++bb;
+            if (bb == B) return DART_MPC_OK;
+            v.running = false;
+            HIPCHK(h, hipStreamSynchronize(v.stream), "resident server");
+            // the grid drained before it saw the request: relaunch with the request already posted
+            HIPCHK(h, server_launch(h, sq - 1), "resident server relaunch");
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+// one launch over the I/O area (no resident server), completion words as the host entry
+int bound_launch(dart_mpc_handle* h, int B, bool ww, bool wo) {
+    if (++h->seq == 0) {
+        std::memset(h->hdone, 0, sizeof(uint32_t) * h->cfg.B_max);
+        h->seq = 1;
+    }
+    dartmpc::PmpcArgs a = io_args(h, B, ww, wo);
+    HIPCHK(h, dartmpc_launch_pmpc(&a, h->stream), "kernel launch");
+    const int rc = wait_done(h, h->stream, h->hdone, B, a.seq);
+    if (rc == DART_MPC_OK) h->pending = h->stream;
+    return rc;
 }
 
 }  // namespace
@@ -346,8 +479,24 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     if (B == 0) return DART_MPC_OK;
     HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
     if (int rc = settle_pending(h)) return rc;
-    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     const size_t nw = (size_t)dart_mpc_nw(h->cfg.N);
+    if (h->srv.wanted && B <= h->srv.B && !stream) {
+        // resident server: inputs into the I/O area, the request posted by the request word
+        const auto& o = h->io;
+        std::memcpy(o.hin, x0, sizeof(double) * 6 * B);
+        std::memcpy(o.hin + o.off_ref, ref, sizeof(double) * 6 * B);
+        std::memcpy(o.hin + o.off_prm, prm, sizeof(double) * 6 * B);
+        if (w_warm) std::memcpy(o.hin + o.off_ww, w_warm, sizeof(double) * nw * B);
+        if (int rc = served_request(h, B, w_warm != nullptr, w_out != nullptr)) return rc;
+        std::memcpy(u0, o.hout, sizeof(double) * 2 * B);
+        std::memcpy(f, o.hout + o.off_f, sizeof(double) * B);
+        if (w_out) std::memcpy(w_out, o.hout + o.off_wo, sizeof(double) * nw * B);
+        std::memcpy(status, o.hout + o.off_st, sizeof(int32_t) * B);
+        std::memcpy(iters, o.hout + o.off_it, sizeof(int32_t) * B);
+        return DART_MPC_OK;
+    }
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+
     HostStage& S = h->st;
     S.begin();
     // the PMPC kernel reads x0 / ref / prm / w_warm once, at its start: zero-copy from mapped host
@@ -704,6 +853,82 @@ int dart_rls_update_batch(int B, double* theta, double* P, const double* phi, co
     return DART_MPC_OK;
 }
 
+int dart_mpc_serve_start(dart_mpc_handle* h, int B_serve, double idle_timeout_s) {
+    if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
+    if (h->cfg.variant != DART_MPC_PMPC) return fail(h, DART_MPC_EINVAL, "handle is not a PMPC handle");
+    if (h->cfg.N > 31 || h->cfg.pmpc_path != 0)
+        return fail(h, DART_MPC_EINVAL, "the resident server serves IPOPT's path with N <= 31");
+    if (B_serve < 1 || B_serve > h->cfg.B_max || B_serve > 65535 || !(idle_timeout_s > 0.0) || idle_timeout_s > 3600.0)
+        return fail(h, DART_MPC_EINVAL, "B_serve must be in [1, min(B_max, 65535)], idle timeout in (0, 3600] s");
+    HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    if (int rc = settle_pending(h)) return rc;
+    if (int rc = server_stop(h)) return rc;
+    HIPCHK(h, ensure_io(h), "I/O area");
+    auto& v = h->srv;
+    hipError_t e = hipHostMalloc((void**)&v.mbox, 256, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&v.dmbox, v.mbox, 0);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { server_release(h); return fail(h, DART_MPC_EHIP, "resident server buffers", e); }
+    std::memset(v.mbox, 0, 256);
+    v.B = B_serve;
+    v.idle_ticks = (unsigned long long)(idle_timeout_s * 1.0e8);      // s_memrealtime: 100 MHz
+    v.mbox[0] = h->seq;
+    e = server_launch(h, h->seq);
+    if (e != hipSuccess) { server_release(h); return fail(h, DART_MPC_EHIP, "resident server launch", e); }
+    v.wanted = true;
+    return DART_MPC_OK;
+}
+
+int dart_mpc_bind(dart_mpc_handle* h, double** x0, double** ref, double** prm, double** w_warm, double** u0, double** f,
+                  double** w_out, int32_t** status, int32_t** iters) {
+    if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
+    if (h->cfg.variant != DART_MPC_PMPC) return fail(h, DART_MPC_EINVAL, "handle is not a PMPC handle");
+    HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    HIPCHK(h, ensure_io(h), "I/O area");
+    const auto& o = h->io;
+    if (x0) *x0 = (double*)o.hin;
+    if (ref) *ref = (double*)(o.hin + o.off_ref);
+    if (prm) *prm = (double*)(o.hin + o.off_prm);
+    if (w_warm) *w_warm = (double*)(o.hin + o.off_ww);
+    if (u0) *u0 = (double*)o.hout;
+    if (f) *f = (double*)(o.hout + o.off_f);
+    if (w_out) *w_out = (double*)(o.hout + o.off_wo);
+    if (status) *status = (int32_t*)(o.hout + o.off_st);
+    if (iters) *iters = (int32_t*)(o.hout + o.off_it);
+    return DART_MPC_OK;
+}
+
+int dart_mpc_solve_bound(dart_mpc_handle* h, int B, int flags) {
+    if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
+    if (h->cfg.variant != DART_MPC_PMPC) return fail(h, DART_MPC_EINVAL, "handle is not a PMPC handle");
+    if (!h->io.hin) return fail(h, DART_MPC_EINVAL, "dart_mpc_bind first");
+    if (B < 0 || B > h->cfg.B_max || (flags & ~3)) return fail(h, DART_MPC_EINVAL, "bad batch or flags");
+    if (B == 0) return DART_MPC_OK;
+    HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    if (int rc = settle_pending(h)) return rc;
+    const bool ww = flags & DART_MPC_BOUND_W_WARM, wo = flags & DART_MPC_BOUND_W_OUT;
+    if (h->srv.wanted && B <= h->srv.B) return served_request(h, B, ww, wo);
+    return bound_launch(h, B, ww, wo);
+}
+
+int dart_mpc_serve_stop(dart_mpc_handle* h) {
+    if (!h) return DART_MPC_EINVAL;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
+    HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
+    return server_stop(h);
+}
+
+int dart_mpc_serve_running(dart_mpc_handle* h) {
+    if (!h) return 0;
+    std::unique_lock<std::recursive_mutex> lock_(h->mu);
+    if (!h->srv.running) return 0;
+    if (hipStreamQuery(h->srv.stream) != hipErrorNotReady) h->srv.running = false;     // idle timeout: drained
+    return h->srv.running ? 1 : 0;
+}
+
 int dart_mpc_sync(dart_mpc_handle* h) {
     if (!h) return DART_MPC_EINVAL;
     std::unique_lock<std::recursive_mutex> lock_(h->mu);
@@ -726,8 +951,10 @@ const char* dart_mpc_last_error(const dart_mpc_handle* h) { return h ? h->err.c_
 
 void dart_mpc_destroy(dart_mpc_handle* h) {
     if (!h) return;
+    (void)server_stop(h);                                     // the resident grid drains first
     if (h->stream) (void)hipStreamSynchronize(h->stream);    // no launch may still use the buffers below
     h->st.release();
+    io_release(h);
     if (h->hdone) (void)hipHostFree(h->hdone);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;

@@ -29,7 +29,16 @@ struct PmpcArgs {
     uint32_t seq;           // wraps modulo 2^32 (defined unsigned arithmetic); never 0 (0 = cleared word)
 };
 
+// resident-server mailbox (mapped host memory): one 64-bit request word,
+// sequence | batch << 32 | flags << 48 | stop << 56
+struct PmpcServe {
+    const uint32_t* mailbox;
+    unsigned long long idle_ticks;   // s_memrealtime ticks (100 MHz) without a request before the waves exit
+};
+
 }  // namespace dartmpc
 
 extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStream_t stream);
+extern "C" hipError_t dartmpc_launch_pmpc_serve(const dartmpc::PmpcArgs* args, const dartmpc::PmpcServe* sv,
+                                               hipStream_t stream);
 extern "C" hipError_t dartmpc_wave_selftest(double* d_out, hipStream_t stream);

@@ -183,14 +183,11 @@ __device__ __forceinline__ void mat4_scan_level(double* T) {
 //   RED: the reduced (x, y) path (opt-in, dart_mpc_config.pmpc_path = 1): theta, the filter and the
 //   error measures leave the z rows out and there is no second-order correction, z is rolled out from
 //   the final controls.  Same KKT point, fewer iterations, but not IPOPT's iterates.
-template <int NAX, bool QSCAN, bool ONEROW = false, bool SHORT2 = false, bool RED = false>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu((QSCAN || NAX == 2) ? 1 : 2)))
-void pmpc_ipm_kernel(PmpcArgs a) {
+// the solve of instance b by the calling wave (the body of pmpc_ipm_kernel and of the resident
+// server pmpc_serve_kernel)
+template <int NAX, bool QSCAN, bool ONEROW, bool SHORT2, bool RED>
+__device__ __forceinline__ void pmpc_solve(const PmpcArgs& a, const int b) {
     STAMP_DECL
-    // small batches: the launcher deals 8 blocks per instance and only every 8th works, so all
-    // instances land on one XCD (blocks go round-robin over the 8 XCDs) and share its L2 for the code
-    if (blockIdx.x % a.pack) return;
-    const int b = blockIdx.x / a.pack;
     const int lane = threadIdx.x;
     const int k = NAX == 1 ? (lane & 31) : lane;            // shooting node of this lane
     const int ax0 = NAX == 1 ? (lane >> 5) : 0;               // axis of slot 0 (NAX == 1)
@@ -930,6 +927,56 @@ void pmpc_ipm_kernel(PmpcArgs a) {
     STAMP_FLUSH(b);
 }
 
+template <int NAX, bool QSCAN, bool ONEROW = false, bool SHORT2 = false, bool RED = false>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu((QSCAN || NAX == 2) ? 1 : 2)))
+void pmpc_ipm_kernel(PmpcArgs a) {
+    // small batches: the launcher deals 8 blocks per instance and only every 8th works, so all
+    // instances land on one XCD (blocks go round-robin over the 8 XCDs) and share its L2 for the code
+    if (blockIdx.x % a.pack) return;
+    pmpc_solve<NAX, QSCAN, ONEROW, SHORT2, RED>(a, blockIdx.x / a.pack);
+}
+
+// Resident solver (dart_mpc_serve_start): the waves of one launch stay on the GPU and take request
+// after request from a mailbox in mapped host memory, so a host call costs no kernel launch, no
+// dispatch and no cold instruction cache.  Mailbox: one 64-bit request word written by the host in
+// one release store, sequence | batch B << 32 | flags << 48 (bit 0: w_warm given, bit 1: w_out
+// wanted) | stop << 56.  Inputs and outputs live at fixed mapped addresses (the PmpcArgs pointers).  Every
+// wave leaves the loop on stop or after sv.idle_ticks of s_memrealtime (100 MHz) without a request,
+// so the grid always drains.
+template <int NAX, bool ONEROW, bool SHORT2>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1)))
+void pmpc_serve_kernel(PmpcArgs a, PmpcServe sv) {
+    if (blockIdx.x % a.pack) return;
+    const int b = blockIdx.x / a.pack;
+    uint32_t seen = a.seq;
+    unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        // one uncached 8-byte read over the link: the request word (sequence | batch << 32 | flags << 48 |
+        // stop << 56), written by the host in one store
+        const unsigned long long w =
+            __hip_atomic_load((const unsigned long long*)sv.mailbox, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(w & 0xffffffffu));
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(w >> 32));
+        const uint32_t sq = lo;
+        if (hi >> 24) break;                                            // stop
+        if (sq == seen) {
+            if (__builtin_amdgcn_s_memrealtime() - t_last > sv.idle_ticks) break;
+            __builtin_amdgcn_s_sleep(4);
+            continue;
+        }
+        seen = sq;
+        const uint32_t B = hi & 0xffffu, fl = (hi >> 16) & 0xffu;
+        if ((uint32_t)b < B) {
+            PmpcArgs r = a;
+            r.B = (int)B; r.seq = sq;
+            r.w_warm = (fl & 1u) ? a.w_warm : nullptr;
+            r.w_out = (fl & 2u) ? a.w_out : nullptr;
+            pmpc_solve<NAX, true, ONEROW, SHORT2, false>(r, b);
+        }
+        t_last = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 #ifndef PMPC_SEQ
 // self-test of the wave primitives: out[0..63] = from_next(lane), out[64..127] = from_prev(lane),
 // out[128] = wsum(lane), out[129] = wmax(lane), out[130] = wmin(lane + 1),
@@ -980,6 +1027,12 @@ extern "C" hipError_t dartmpc_launch_pmpc_seq(const dartmpc::PmpcArgs* a, unsign
     else launch_seq<false>(a, grid, stream, onerow);
     return hipGetLastError();
 }
+extern "C" hipError_t dartmpc_launch_pmpc_serve_onerow(const dartmpc::PmpcArgs* a, const dartmpc::PmpcServe* sv,
+                                                      unsigned grid, hipStream_t stream) {
+    hipLaunchKernelGGL((dartmpc::pmpc_serve_kernel<1, true, false>), dim3(grid), dim3(dartmpc::kWave), 0, stream, *a,
+                       *sv);
+    return hipGetLastError();
+}
 #ifdef DART_STAMPS
 // diagnostic build only: the stamps of the one-row (N <= 15) and sequential builds of this object
 extern "C" hipError_t dartmpc_read_stamps_seq(unsigned long long* host_out) {
@@ -990,6 +1043,25 @@ extern "C" hipError_t dartmpc_read_stamps_seq(unsigned long long* host_out) {
 #else
 extern "C" hipError_t dartmpc_launch_pmpc_seq(const dartmpc::PmpcArgs* a, unsigned grid, hipStream_t stream,
                                               int onerow);
+extern "C" hipError_t dartmpc_launch_pmpc_serve_onerow(const dartmpc::PmpcArgs* a, const dartmpc::PmpcServe* sv,
+                                                      unsigned grid, hipStream_t stream);
+
+// the resident server for B_serve slots (IPOPT's path, N <= 31): one wave per slot, one XCD when it fits
+extern "C" hipError_t dartmpc_launch_pmpc_serve(const dartmpc::PmpcArgs* args, const dartmpc::PmpcServe* sv,
+                                               hipStream_t stream) {
+    if (args->B <= 0 || args->N > 31) return hipErrorInvalidValue;
+    dartmpc::PmpcArgs a = *args;
+    a.pack = (a.B <= 32) ? 8 : 1;
+    const unsigned grid = (unsigned)(a.B * a.pack);
+    if (a.N <= 15) return dartmpc_launch_pmpc_serve_onerow(&a, sv, grid, stream);
+    if (a.N <= 23)
+        hipLaunchKernelGGL((dartmpc::pmpc_serve_kernel<1, false, true>), dim3(grid), dim3(dartmpc::kWave), 0, stream, a,
+                           *sv);
+    else
+        hipLaunchKernelGGL((dartmpc::pmpc_serve_kernel<1, false, false>), dim3(grid), dim3(dartmpc::kWave), 0, stream, a,
+                           *sv);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStream_t stream) {
     if (args->B <= 0) return hipSuccess;

@@ -32,7 +32,8 @@ EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch",
            "dart_lmpc_policy_config_default", "dart_lmpc_policy_step", "dart_lmpc_policy_step_dev",
            "dart_lmpc_policy_solve_batch", "dart_lmpc_policy_solve_batch_dev",
            "dart_arm_config_default", "dart_arm_snapshot_len", "dart_arm_param_len", "dart_arm_solve_batch",
-           "dart_arm_solve_batch_dev", "dart_set_device")
+           "dart_arm_solve_batch_dev", "dart_set_device", "dart_mpc_serve_start", "dart_mpc_serve_stop",
+           "dart_mpc_serve_running", "dart_mpc_bind", "dart_mpc_solve_bound")
 VARIANT_PMPC, VARIANT_RMPC, VARIANT_LMPC = 0, 1, 2
 ABI_VERSION = 5
 
@@ -140,6 +141,18 @@ def lib():
     L.dart_arm_solve_batch_dev.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6
     L.dart_arm_solve_batch_dev.restype = ctypes.c_int
+    if hasattr(L, "dart_mpc_bind"):         # (absent only in older in-tree builds used for A/B timing)
+        L.dart_mpc_bind.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 9
+        L.dart_mpc_bind.restype = ctypes.c_int
+        L.dart_mpc_solve_bound.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.dart_mpc_solve_bound.restype = ctypes.c_int
+    if hasattr(L, "dart_mpc_serve_start"):  # (absent only in older in-tree builds used for A/B timing)
+        L.dart_mpc_serve_start.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
+        L.dart_mpc_serve_start.restype = ctypes.c_int
+        L.dart_mpc_serve_stop.argtypes = [ctypes.c_void_p]
+        L.dart_mpc_serve_stop.restype = ctypes.c_int
+        L.dart_mpc_serve_running.argtypes = [ctypes.c_void_p]
+        L.dart_mpc_serve_running.restype = ctypes.c_int
     if hasattr(L, "dart_set_device"):       # (absent only in older in-tree builds used for A/B timing)
         L.dart_set_device.argtypes = [ctypes.c_int]
         L.dart_set_device.restype = ctypes.c_int
@@ -291,9 +304,41 @@ class Solver:
         if rc != 0:
             self._err(rc, "dart_mpc_sync")
 
+    # -- resident solver (PMPC, IPOPT's path, N <= 31): dart_mpc_serve_start / _stop / _running ----
+    def serve_start(self, B_serve=18, idle_timeout=1.0):
+        """Keep a grid of ``B_serve`` waves resident; later ``solve_batch`` / ``solve_one`` calls with
+        B <= B_serve are served without a kernel launch (bit-identical results)."""
+        rc = lib().dart_mpc_serve_start(self._h, int(B_serve), float(idle_timeout))
+        if rc != 0:
+            self._err(rc, "dart_mpc_serve_start")
+        return self
+
+    def serve_stop(self):
+        rc = lib().dart_mpc_serve_stop(self._h)
+        if rc != 0:
+            self._err(rc, "dart_mpc_serve_stop")
+
+    def serving(self):
+        return bool(lib().dart_mpc_serve_running(self._h))
+
+    def bind(self):
+        """In-place I/O (dart_mpc_bind): a ``Bound`` whose numpy views live in the handle's mapped, pinned
+        I/O area.  Write the inputs of the first B rows, call ``bound.solve(B)``, read the outputs: no
+        copies and a two-argument ctypes call per solve."""
+        b = getattr(self, "_bound", None)
+        if b is None:
+            b = self._bound = Bound(self)
+        return b
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
     def close(self):
         if self._h:
-            lib().dart_mpc_destroy(self._h)
+            lib().dart_mpc_destroy(self._h)      # stops a resident grid first
             self._h = ctypes.c_void_p()
 
     def __del__(self):
@@ -301,6 +346,35 @@ class Solver:
             self.close()
         except Exception:
             pass
+
+
+class Bound:
+    """Views of a PMPC handle's in-place I/O area for B_max instances (Solver.bind)."""
+
+    def __init__(self, solver):
+        ptrs = [ctypes.c_void_p() for _ in range(9)]
+        rc = lib().dart_mpc_bind(solver._h, *[ctypes.byref(p) for p in ptrs])
+        if rc != 0:
+            solver._err(rc, "dart_mpc_bind")
+        Bm, nw = int(solver.cfg.B_max), solver.nw
+
+        def view(p, shape, ct):
+            n = int(np.prod(shape))
+            return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ct)), shape=(n,)).reshape(shape)
+
+        d = ctypes.c_double
+        self.x0, self.ref, self.prm = view(ptrs[0], (Bm, 6), d), view(ptrs[1], (Bm, 6), d), view(ptrs[2], (Bm, 6), d)
+        self.w_warm = view(ptrs[3], (Bm, nw), d)
+        self.u0, self.f, self.w_out = view(ptrs[4], (Bm, 2), d), view(ptrs[5], (Bm,), d), view(ptrs[6], (Bm, nw), d)
+        self.status, self.iters = view(ptrs[7], (Bm,), ctypes.c_int32), view(ptrs[8], (Bm,), ctypes.c_int32)
+        self._solver = solver
+        self._fn = lib().dart_mpc_solve_bound
+        self._h = solver._h
+
+    def solve(self, B, w_warm=False, want_w=False):
+        rc = self._fn(self._h, B, (1 if w_warm else 0) | (2 if want_w else 0))
+        if rc != 0:
+            self._solver._err(rc, "dart_mpc_solve_bound")
 
 
 class RmpcSolver(Solver):

@@ -132,6 +132,33 @@ int dart_mpc_solve_batch(dart_mpc_handle *h, int B,
                          double *u0, double *f, double *w_out,
                          int32_t *status, int32_t *iters, void *hip_stream);
 
+/* Resident solver (ABI 5, PMPC with pmpc_path 0 and N <= 31): dart_mpc_serve_start launches one
+ * long-lived grid of B_serve waves on a stream of its own; every later dart_mpc_solve_batch on the
+ * handle with B <= B_serve and a NULL stream is then served by it through a mailbox in mapped host
+ * memory (inputs and outputs at fixed mapped addresses, completion words as before): no kernel
+ * launch, no dispatch and a warm instruction cache per call; the results are bit-identical to a
+ * launch.  Replaces nothing in the reference; it is the low-latency form of PMPC.solve's per-step
+ * call (mpc_3d.py:115-138, main_parallel_enhanced.py:22-55).  The waves leave when
+ * dart_mpc_serve_stop (or dart_mpc_destroy) is called, or after idle_timeout_s seconds without a
+ * request (the next call then restarts the grid transparently).  dart_mpc_serve_running reports
+ * whether the grid is resident.  Larger batches, caller streams and the _dev entry still launch. */
+int dart_mpc_serve_start(dart_mpc_handle *h, int B_serve, double idle_timeout_s);
+
+/* In-place I/O (ABI 5, PMPC): dart_mpc_bind returns host pointers into the handle's mapped, pinned
+ * I/O area for B_max instances (any argument may be NULL): inputs x0 / ref / prm [B_max][6] and
+ * w_warm [B_max][nw], outputs u0 [B_max][2], f, w_out [B_max][nw], status, iters.  A caller writes
+ * the first B rows of the inputs in place and calls dart_mpc_solve_bound(h, B, flags); the results
+ * are in the output views when it returns (blocking, like dart_mpc_solve_batch, served by the resident
+ * solver when it runs).  No copy on either side of the call.  flags: DART_MPC_BOUND_W_WARM (use w_warm),
+ * DART_MPC_BOUND_W_OUT (fill w_out).  The pointers stay valid until dart_mpc_destroy. */
+#define DART_MPC_BOUND_W_WARM 1
+#define DART_MPC_BOUND_W_OUT 2
+int dart_mpc_bind(dart_mpc_handle *h, double **x0, double **ref, double **prm, double **w_warm,
+                  double **u0, double **f, double **w_out, int32_t **status, int32_t **iters);
+int dart_mpc_solve_bound(dart_mpc_handle *h, int B, int flags);
+int dart_mpc_serve_stop(dart_mpc_handle *h);
+int dart_mpc_serve_running(dart_mpc_handle *h);
+
 /* Device-pointer entry: all pointers are device memory; asynchronous on
  * hip_stream (NULL = the handle's own stream).  Call dart_mpc_sync or
  * synchronise the stream before reading results. */
