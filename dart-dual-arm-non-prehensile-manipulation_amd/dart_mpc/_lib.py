@@ -75,10 +75,12 @@ def lib():
     # the one torch bundles, and the first one loaded serves both.  torch only works on its own, so
     # load torch first when it is installed (it is the device-memory / stream plumbing of the
     # package); our library then binds to the same runtime.
-    try:
-        import torch  # noqa: F401
-    except ImportError:     # pragma: no cover - the C ABI works without torch
-        pass
+    # (DART_MPC_NO_TORCH=1: a process that never uses torch -- a controller worker -- skips it)
+    if os.environ.get("DART_MPC_NO_TORCH", "0") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:     # pragma: no cover - the C ABI works without torch
+            pass
     L = ctypes.CDLL(LIB_PATH)
     L.dart_mpc_config_default.argtypes = [ctypes.POINTER(Config)]
     L.dart_mpc_config_default.restype = None

@@ -1,7 +1,7 @@
 # Round-end measurement set (GPU box): tests, bench line, rocprofv3 trace + HBM passes, SQ counters,
 # phase stamps.  Usage: bash tools/gpu_round.sh <tag>
 set -o pipefail
-TAG=${1:-r02}
+TAG=${1:-r03}
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/gpu_tests.log; exit 1; }
 tail -2 gpurun_out/gpu_tests.log
