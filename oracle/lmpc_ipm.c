@@ -212,9 +212,105 @@ typedef struct {
     double filt_th[256], filt_ph[256];
 } work_t;
 
+struct resto_s;
 typedef struct {
     const prob_t *P; const double *x0, *up0, *tgt; double sc, mu, lo, hi;
+    struct resto_s *R;      /* restoration phase data (NULL: the original problem) */
+    int mode;               /* 0 original problem, 1 restoration Newton step, 2 restoration least-square multipliers */
 } ctx_t;
+
+/* IPOPT's restoration phase (MinC_1NrmRestorationPhase, RestoIpoptNLP): the feasibility problem
+ *   min rho sum(p + n) + eta/2 ||D_R (x - x_R)||^2   s.t.  d c(x) + n - p = 0,  p, n >= 0,  lo <= u <= hi
+ * over the reference NLP's variables x = [X; U] and a pair (p, n) per physical defect row (scaled by
+ * the row scaling d; the Delta-u copy rows of the augmented formulation are not rows of the reference
+ * NLP and stay hard).  Eliminating p, n from the Newton system leaves each physical row soft:
+ * J dx - D dlam = rhs with D = (1/(Sigma_p + delta) + 1/(Sigma_n + delta)) / d^2, which the Riccati
+ * recursion absorbs per node as P~ = P (I + D P)^-1, p~ = (I + P D)^-1 p (value function seen through
+ * the soft rows) and dx+ = (I + D P)^-1 (A dx + B du - rg - D p). */
+typedef struct resto_s {
+    double pc[NA * (NMAX + 1)], nc[NA * (NMAX + 1)], zp[NA * (NMAX + 1)], zn[NA * (NMAX + 1)];
+    double dpc[NA * (NMAX + 1)], dnc[NA * (NMAX + 1)], dzp[NA * (NMAX + 1)], dzn[NA * (NMAX + 1)];
+    double rp[NA * (NMAX + 1)], rn[NA * (NMAX + 1)];   /* p / n rows of the barrier Lagrangian gradient */
+    double D[NA * (NMAX + 1)], Spd[NA * (NMAX + 1)], Snd[NA * (NMAX + 1)];   /* of the current factorisation */
+    double XR[NA * (NMAX + 1)], UR[NU * NMAX], DRx[NA * (NMAX + 1)], DRu[NU * NMAX];
+    double M[NMAX + 1][NA][NA], Pt[NMAX + 1][NA][NA];
+    double filt_th[256], filt_ph[256];
+    double pt_[NA * (NMAX + 1)], nt_[NA * (NMAX + 1)];    /* trial p, n */
+    double rho, eta;
+    const double *dsc;
+} resto_t;
+
+/* solve A X = B (n x n, nrhs columns of B stored row-major with stride NA + 1 ... ) by Gaussian
+   elimination with partial pivoting; A and B are overwritten */
+static void gauss_solve(int n, double A[NA][NA], double B[NA][NA], int nrhs) {
+    for (int c = 0; c < n; ++c) {
+        int piv = c;
+        for (int r = c + 1; r < n; ++r) if (fabs(A[r][c]) > fabs(A[piv][c])) piv = r;
+        if (piv != c) {
+            for (int j = 0; j < n; ++j) { double t = A[c][j]; A[c][j] = A[piv][j]; A[piv][j] = t; }
+            for (int j = 0; j < nrhs; ++j) { double t = B[c][j]; B[c][j] = B[piv][j]; B[piv][j] = t; }
+        }
+        for (int r = c + 1; r < n; ++r) {
+            const double f = A[r][c] / A[c][c];
+            if (f == 0.0) continue;
+            for (int j = c; j < n; ++j) A[r][j] -= f * A[c][j];
+            for (int j = 0; j < nrhs; ++j) B[r][j] -= f * B[c][j];
+        }
+    }
+    for (int c = n - 1; c >= 0; --c)
+        for (int j = 0; j < nrhs; ++j) {
+            double t = B[c][j];
+            for (int m = c + 1; m < n; ++m) t -= A[c][m] * B[m][j];
+            B[c][j] = t / A[c][c];
+        }
+}
+/* x <- M^-1 x  (M = R->M[k]) */
+static void soft_apply_minv(const resto_t *R, int k, double *x) {
+    double A[NA][NA], Bv[NA][NA];
+    memcpy(A, R->M[k], sizeof A);
+    for (int i = 0; i < NA; ++i) Bv[i][0] = x[i];
+    gauss_solve(NA, A, Bv, 1);
+    for (int i = 0; i < NA; ++i) x[i] = Bv[i][0];
+}
+/* x <- M^-T x */
+static void soft_apply_mtinv(const resto_t *R, int k, double *x) {
+    double A[NA][NA], Bv[NA][NA];
+    for (int i = 0; i < NA; ++i) for (int j = 0; j < NA; ++j) A[i][j] = R->M[k][j][i];
+    for (int i = 0; i < NA; ++i) Bv[i][0] = x[i];
+    gauss_solve(NA, A, Bv, 1);
+    for (int i = 0; i < NA; ++i) x[i] = Bv[i][0];
+}
+/* soft rows of node k with the Hessian shift delta: D, M = I + D P_k, P~_k = solve(M^T, P_k).  Returns
+   0 if S = P_k(phys, phys) + D^-1 is not positive definite: eliminating the row slack w = D lam of the
+   soft rows is then not a minimisation and the KKT matrix has the wrong inertia (the Riccati form of
+   IPOPT's inertia test, next to Quu > 0) */
+static int soft_node(const ctx_t *C, const double Pk[NA][NA], int k, double delta) {
+    resto_t *R = C->R;
+    for (int i = 0; i < NA; ++i) {
+        const int r = NA * k + i;
+        double D = 0.0;
+        if (i < 8) {
+            const double d = R->dsc[r];
+            if (C->mode == 2) { R->Spd[r] = 1.0; R->Snd[r] = 1.0; }
+            else { R->Spd[r] = R->zp[r] / R->pc[r] + delta; R->Snd[r] = R->zn[r] / R->nc[r] + delta; }
+            D = (1.0 / R->Spd[r] + 1.0 / R->Snd[r]) / (d * d);
+        }
+        R->D[r] = D;
+        for (int j = 0; j < NA; ++j) R->M[k][i][j] = (i == j) + D * Pk[i][j];
+    }
+    double A[NA][NA], Bm[NA][NA];
+    for (int i = 0; i < NA; ++i) for (int j = 0; j < NA; ++j) { A[i][j] = R->M[k][j][i]; Bm[i][j] = Pk[i][j]; }
+    gauss_solve(NA, A, Bm, NA);
+    for (int i = 0; i < NA; ++i) for (int j = 0; j < NA; ++j) R->Pt[k][i][j] = 0.5 * (Bm[i][j] + Bm[j][i]);
+    double L[8][8];     /* Cholesky of S */
+    for (int i = 0; i < 8; ++i) for (int j = 0; j <= i; ++j) {
+        double t = Pk[i][j] + (i == j ? 1.0 / R->D[NA * k + i] : 0.0);
+        for (int m = 0; m < j; ++m) t -= L[i][m] * L[j][m];
+        if (i == j) { if (!(t > 0.0)) return 0; L[i][i] = sqrt(t); }
+        else L[i][j] = t / L[j][j];
+    }
+    return 1;
+}
 
 enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_MAXITER = -1, ST_LS_FAIL = -2, ST_INERTIA_FAIL = -3, ST_BAD_INPUT = -10 };
 
@@ -296,6 +392,35 @@ static void stage_qp(const ctx_t *C, const work_t *W, int k, double delta, doubl
     const prob_t *P = C->P; const double sc = C->sc;
     double z[NZ];
     stage_z(W->X, W->U, k, z);
+    if (C->mode) {
+        /* restoration: the proximity term eta/2 ||D_R (x - x_R)||^2 on the reference NLP's variables
+           (states and inputs, not the Delta-u copies), plus the lambda-weighted dynamics Hessian
+           (mode 1); mode 2 (least-square multipliers): unit weights, gradient - z_L + z_U on u */
+        const resto_t *R = C->R;
+        for (int a = 0; a < NZ; ++a) for (int b = 0; b < NZ; ++b) Hq[a][b] = C->mode == 1 ? W->Hs[k][a][b] : 0.0;
+        for (int j = 0; j < NZ; ++j) gq[j] = 0.0;
+        for (int i = 0; i < 8; ++i) {
+            const int r = NA * k + i;
+            const double w = R->eta * R->DRx[r] * R->DRx[r];
+            Hq[i][i] += C->mode == 1 ? w : 1.0;
+            gq[i] = w * (z[i] - R->XR[r]);
+        }
+        for (int a = 0; a < NU; ++a) {
+            const int j = NU * k + a;
+            const double w = R->eta * R->DRu[j] * R->DRu[j];
+            double sl = W->U[j] - C->lo, su = C->hi - W->U[j];
+            gq[10 + a] = w * (z[10 + a] - R->UR[j]);
+            if (C->mode == 1) {
+                Hq[10 + a][10 + a] += w + W->zL[j] / sl + W->zU[j] / su;
+                gq[10 + a] += -C->mu / sl + C->mu / su;
+            } else {
+                Hq[10 + a][10 + a] += 1.0;
+                gq[10 + a] += -W->zL[j] + W->zU[j];
+            }
+        }
+        if (C->mode == 1) for (int a = 0; a < NZ; ++a) Hq[a][a] += delta;
+        return;
+    }
     for (int a = 0; a < NZ; ++a) for (int b = 0; b < NZ; ++b) Hq[a][b] = W->Hs[k][a][b];
     for (int i = 0; i < 8; ++i) Hq[i][i] += sc * 2 * P->Q[i];
     for (int a = 0; a < 2; ++a) {
@@ -313,16 +438,43 @@ static void stage_qp(const ctx_t *C, const work_t *W, int k, double delta, doubl
     for (int a = 0; a < NZ; ++a) Hq[a][a] += delta;
 }
 
-static int riccati_factor(const ctx_t *C, work_t *W, double delta) {
-    const prob_t *P = C->P; const int N = P->N; const double sc = C->sc;
-    double (*Pn)[NA] = W->Pm[N];
+/* terminal value function (Hessian into Pn, gradient into pn) */
+static void terminal_qp(const ctx_t *C, const work_t *W, double delta, double Pn[NA][NA], double *pn) {
+    const prob_t *P = C->P; const int N = P->N;
     for (int i = 0; i < NA; ++i) for (int j = 0; j < NA; ++j) Pn[i][j] = 0.0;
-    for (int i = 0; i < 8; ++i) Pn[i][i] = sc * 2 * P->Qt[i];
+    if (C->mode) {
+        const resto_t *R = C->R;
+        for (int i = 0; i < NA; ++i) pn[i] = 0.0;
+        for (int i = 0; i < 8; ++i) {
+            const int r = NA * N + i;
+            const double w = R->eta * R->DRx[r] * R->DRx[r];
+            Pn[i][i] = C->mode == 1 ? w + delta : 1.0;
+            pn[i] = w * (W->X[r] - R->XR[r]);
+        }
+        if (C->mode == 1) { Pn[8][8] = delta; Pn[9][9] = delta; }
+        return;
+    }
+    double zN[NZ], gN[NZ];
+    for (int i = 0; i < NA; ++i) zN[i] = W->X[NA * N + i];
+    zN[10] = zN[11] = 0.0;
+    cost_grad(P, zN, C->tgt, 1, gN);
+    for (int i = 0; i < NA; ++i) pn[i] = C->sc * gN[i];
+    for (int i = 0; i < 8; ++i) Pn[i][i] = C->sc * 2 * P->Qt[i];
     for (int i = 0; i < NA; ++i) Pn[i][i] += delta;
+}
+
+static int riccati_factor(const ctx_t *C, work_t *W, double delta) {
+    const prob_t *P = C->P; const int N = P->N;
+    double pn[NA];
+    terminal_qp(C, W, delta, W->Pm[N], pn);
     for (int k = N - 1; k >= 0; --k) {
         double Hq[NZ][NZ], gq[NZ];
         stage_qp(C, W, k, delta, Hq, gq);
         double (*A)[NA] = W->A[k], (*Bm)[NU] = W->Bm[k], (*Pp)[NA] = W->Pm[k + 1];
+        if (C->R) {
+            if (!soft_node(C, (const double (*)[NA])W->Pm[k + 1], k + 1, delta)) return 0;
+            Pp = C->R->Pt[k + 1];
+        }
         double PA[NA][NA], PB[NA][NU], Quu[NU][NU];
         for (int i = 0; i < NA; ++i) {
             for (int j = 0; j < NA; ++j) { double s = 0; for (int m = 0; m < NA; ++m) s += Pp[i][m] * A[m][j]; PA[i][j] = s; }
@@ -345,21 +497,22 @@ static int riccati_factor(const ctx_t *C, work_t *W, double delta) {
             W->Pm[k][i][j] = Qxx[i][j] + W->Qux[k][0][i] * W->K[k][0][j] + W->Qux[k][1][i] * W->K[k][1][j];
         for (int i = 0; i < NA; ++i) for (int j = 0; j < i; ++j) { double s = 0.5 * (W->Pm[k][i][j] + W->Pm[k][j][i]); W->Pm[k][i][j] = W->Pm[k][j][i] = s; }
     }
+    if (C->R) return soft_node(C, (const double (*)[NA])W->Pm[0], 0, delta);     /* the soft initial-state rows */
     return 1;
 }
 
-/* vector pass + forward sweep for defect RHS rg (J d = -rg) */
+/* vector pass + forward sweep for defect RHS rg (J d = -rg; soft rows: J d - D lam+ = -rg) */
 static void riccati_solve(const ctx_t *C, work_t *W, double rg[][NA]) {
     const prob_t *P = C->P; const int N = P->N;
-    double zN[NZ], gN[NZ];
-    for (int i = 0; i < NA; ++i) zN[i] = W->X[NA * N + i];
-    zN[10] = zN[11] = 0.0;
-    cost_grad(P, zN, C->tgt, 1, gN);
-    for (int i = 0; i < NA; ++i) W->pv[N][i] = C->sc * gN[i];
+    const resto_t *R = C->R;
+    double Pdum[NA][NA];
+    terminal_qp(C, W, 0.0, Pdum, W->pv[N]);
     for (int k = N - 1; k >= 0; --k) {
         double Hq[NZ][NZ], gq[NZ];
         stage_qp(C, W, k, 0.0, Hq, gq);   /* only the gradient is used */
-        double (*A)[NA] = W->A[k], (*Bm)[NU] = W->Bm[k], (*Pp)[NA] = W->Pm[k + 1], *pp = W->pv[k + 1];
+        double (*A)[NA] = W->A[k], (*Bm)[NU] = W->Bm[k], (*Pp)[NA] = W->Pm[k + 1], pp[NA];
+        memcpy(pp, W->pv[k + 1], sizeof pp);
+        if (R) { Pp = (double (*)[NA])R->Pt[k + 1]; soft_apply_mtinv(R, k + 1, pp); }
         double hh[NA], qx[NA], qu[NU], kf[2];
         for (int i = 0; i < NA; ++i) { double s = pp[i]; for (int m = 0; m < NA; ++m) s -= Pp[i][m] * rg[k + 1][m]; hh[i] = s; }
         for (int i = 0; i < NA; ++i) { double s = gq[i]; for (int m = 0; m < NA; ++m) s += A[m][i] * hh[m]; qx[i] = s; }
@@ -368,16 +521,19 @@ static void riccati_solve(const ctx_t *C, work_t *W, double rg[][NA]) {
         W->kff[k][0] = -kf[0]; W->kff[k][1] = -kf[1];
         for (int i = 0; i < NA; ++i) W->pv[k][i] = qx[i] + W->Qux[k][0][i] * W->kff[k][0] + W->Qux[k][1][i] * W->kff[k][1];
     }
-    for (int i = 0; i < NA; ++i) W->dX[i] = -rg[0][i];
+    for (int i = 0; i < NA; ++i) W->dX[i] = -rg[0][i] - (R ? R->D[i] * W->pv[0][i] : 0.0);
+    if (R) soft_apply_minv(R, 0, W->dX);
     for (int k = 0; k < N; ++k) {
-        double *dx = W->dX + NA * k, *du = W->dU + NU * k;
+        double *dx = W->dX + NA * k, *du = W->dU + NU * k, *dn = W->dX + NA * (k + 1);
         for (int a = 0; a < NU; ++a) { double s = W->kff[k][a]; for (int i = 0; i < NA; ++i) s += W->K[k][a][i] * dx[i]; du[a] = s; }
         for (int i = 0; i < NA; ++i) {
             double s = -rg[k + 1][i];
             for (int m = 0; m < NA; ++m) s += W->A[k][i][m] * dx[m];
             for (int a = 0; a < NU; ++a) s += W->Bm[k][i][a] * du[a];
-            W->dX[NA * (k + 1) + i] = s;
+            if (R) s -= R->D[NA * (k + 1) + i] * W->pv[k + 1][i];
+            dn[i] = s;
         }
+        if (R) soft_apply_minv(R, k + 1, dn);
     }
     for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) {
         double s = W->pv[k][i]; for (int m = 0; m < NA; ++m) s += W->Pm[k][i][m] * W->dX[NA * k + m];
@@ -464,6 +620,7 @@ static double ls_multipliers(const ctx_t *C, work_t *W) {
             double t = ps[k][i]; for (int m = 0; m < NA; ++m) t += Ps[k][i][m] * dx[m];
             W->lam[NA * k + i] = -t;
             if (i < 8) ymax = fmax(ymax, fabs(t) / W->dsc[NA * k + i]);   /* the copy rows are not IPOPT's */
+            if (!isfinite(t)) ymax = INFINITY;     /* the recursion overflowed: far above constr_mult_init_max */
         }
         if (k == N) break;
         double du[NU], dn[NA];
@@ -478,8 +635,505 @@ static double ls_multipliers(const ctx_t *C, work_t *W) {
     return ymax;
 }
 
+/* KKT residual measures at the iterate held in W (A, Bm linearised there) with defects g: max norms
+   of IPOPT's eq. 5 (dinf, scaled pinf, unscaled pinf_u, complementarity c0 with mu = 0), the sums of
+   |y~| and |z| for s_d / s_c and, when pd != NULL, IPOPT's primal-dual system error at C->mu
+   (IpoptCalculatedQuantities::curr_primal_dual_system_error: the l1 norms of the primal
+   infeasibility, the dual infeasibility and the complementarity z s - mu, added) */
+static void kkt_errors(const ctx_t *C, const work_t *W, double g[][NA], double *sum_l_, double *sum_z_,
+                       double *dinf_, double *pinf_, double *pinf_u_, double *c0_, double *pd) {
+    const prob_t *P = C->P; const int N = P->N, nA = NA * (N + 1);
+    double sum_l = 0, sum_z = 0, dinf = 0, pinf = 0, pinf_u = 0, c0 = 0, l1p = 0, l1d = 0, l1c = 0;
+    for (int i = 0; i < nA; ++i) sum_l += fabs(W->lam[i]) / W->dsc[i];
+    for (int k = 0; k <= N; ++k) {
+        double z[NZ], gc[NZ], gl[NZ];
+        for (int i = 0; i < NA; ++i) z[i] = W->X[NA * k + i];
+        z[10] = k < N ? W->U[NU * k] : 0.0; z[11] = k < N ? W->U[NU * k + 1] : 0.0;
+        cost_grad(P, z, C->tgt, k == N, gc);
+        for (int j = 0; j < NZ; ++j) gl[j] = C->sc * gc[j];
+        for (int i = 0; i < NA; ++i) gl[i] += W->lam[NA * k + i];
+        if (k < N) {
+            for (int m = 0; m < NA; ++m) {
+                double l = W->lam[NA * (k + 1) + m];
+                for (int i = 0; i < NA; ++i) gl[i] -= W->A[k][m][i] * l;
+                gl[10] -= W->Bm[k][m][0] * l; gl[11] -= W->Bm[k][m][1] * l;
+            }
+            gl[10] += -W->zL[NU * k] + W->zU[NU * k]; gl[11] += -W->zL[NU * k + 1] + W->zU[NU * k + 1];
+            for (int j = 0; j < NZ; ++j) { dinf = fmax(dinf, fabs(gl[j])); l1d += fabs(gl[j]); }
+            for (int a = 0; a < NU; ++a) {
+                const int j = NU * k + a;
+                const double cl = W->zL[j] * (W->U[j] - C->lo), cu = W->zU[j] * (C->hi - W->U[j]);
+                c0 = fmax(c0, fmax(fabs(cl), fabs(cu)));
+                l1c += fabs(cl - C->mu) + fabs(cu - C->mu);
+                sum_z += W->zL[j] + W->zU[j];
+            }
+        } else {
+            for (int i = 0; i < NA; ++i) { dinf = fmax(dinf, fabs(gl[i])); l1d += fabs(gl[i]); }
+        }
+        for (int i = 0; i < NA; ++i) {
+            pinf = fmax(pinf, W->dsc[NA * k + i] * fabs(g[k][i]));
+            pinf_u = fmax(pinf_u, fabs(g[k][i]));
+            l1p += W->dsc[NA * k + i] * fabs(g[k][i]);
+        }
+    }
+    *sum_l_ = sum_l; *sum_z_ = sum_z; *dinf_ = dinf; *pinf_ = pinf; *pinf_u_ = pinf_u; *c0_ = c0;
+    if (pd) *pd = l1p + l1d + l1c;
+}
+
 static double g_mult_init_max = 1e3;   /* IPOPT constr_mult_init_max (default 1000; 0 = zero multipliers) */
 void oracle_lmpc_set_mult_init_max(double m) { g_mult_init_max = m; }
+
+/* IPOPT's soft restoration phase (BacktrackingLineSearch::TrySoftRestoStep, soft_resto_pderror_reduction_factor
+ * 0.9999): the primal-dual step of the current direction, damped only by the fraction to the boundary
+ * (one step length min(alpha_primal_max, alpha_dual_max) for x, y and z), is taken if the original filter
+ * accepts it with alpha_primal_test = 0 (*orig = 1: the phase ends) or if it reduces the primal-dual system
+ * error at the current mu by the factor.  Returns the step length (0: rejected); W is left unchanged. */
+static double bound_dual_step(const ctx_t *C, work_t *W, int nU, double tau);
+static int g_soft_resto = 1;
+void oracle_lmpc_set_soft_resto(int on) { g_soft_resto = on; }
+
+static double soft_resto_step(const ctx_t *C, work_t *W, int nfilt, double th, double phi, double th_max,
+                              double tau, double curr_pd, double gt[][NA], double *th_t, double *ph_t, int *orig) {
+    const prob_t *P = C->P; const int N = P->N, nU = NU * N, nA = NA * (N + 1);
+    const double gam_th = 1e-5, gam_ph = 1e-8;
+    const double a = fmin(frac_to_boundary(C, W, W->dU, tau), bound_dual_step(C, W, nU, tau));
+    for (int i = 0; i < nA; ++i) W->Xt[i] = W->X[i] + a * W->dX[i];
+    for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + a * W->dU[j];
+    *th_t = residuals(C, W, W->Xt, W->Ut, gt);
+    *ph_t = barrier_obj(C, W->Xt, W->Ut);
+    *orig = 0;
+    /* FilterLSAcceptor::CheckAcceptabilityOfTrialPoint(0): sufficient decrease against the current
+       iterate (no Armijo branch at alpha 0), then the filter (which holds the current point) */
+    int in_filter = !(*th_t < th_max) || !isfinite(*ph_t);
+    for (int q = 0; q < nfilt && !in_filter; ++q) in_filter = *th_t >= W->filt_th[q] && *ph_t >= W->filt_ph[q];
+    if (!in_filter && (LE(*th_t, (1 - gam_th) * th, th) || LE(*ph_t - phi, -gam_ph * th, phi))) { *orig = 1; return a; }
+    if (!isfinite(*ph_t)) return 0.0;
+    /* the primal-dual system error at the trial point (x, y, z all moved by a) */
+    work_t *S = (work_t *)malloc(sizeof(work_t));
+    memcpy(S, W, sizeof(work_t));
+    memcpy(W->X, S->Xt, sizeof(double) * nA); memcpy(W->U, S->Ut, sizeof(double) * nU);
+    for (int i = 0; i < nA; ++i) W->lam[i] = S->lam[i] + a * (S->lamp[i] - S->lam[i]);
+    for (int j = 0; j < nU; ++j) { W->zL[j] = S->zL[j] + a * S->dzL[j]; W->zU[j] = S->zU[j] + a * S->dzU[j]; }
+    linearise(P, W);
+    double sl, sz, di, pi, pu, c0, pd;
+    kkt_errors(C, W, gt, &sl, &sz, &di, &pi, &pu, &c0, &pd);
+    memcpy(W, S, sizeof(work_t));
+    free(S);
+    return pd <= 0.9999 * curr_pd ? a : 0.0;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * IPOPT's restoration phase (MinC_1NrmRestorationPhase::PerformRestoration with RestoIpoptNLP,
+ * RestoIterateInitializer and RestoFilterConvergenceCheck; IPOPT 3.14 defaults, restated -- no IPOPT
+ * source is in the image):
+ *   - rho = resto_penalty_parameter 1000, eta(mu) = resto_proximity_weight 1 * sqrt(mu) of the
+ *     restoration's current mu, D_R = diag(min(1, 1/|x_R|)), x_R = the current point;
+ *   - start: mu_R = max(mu, ||d c||_inf); x = x_R; per row n = a + sqrt(a^2 + b), p = d c + n with
+ *     a = mu_R/(2 rho) - d c/2, b = d c mu_R/(2 rho); z_p = mu_R/p, z_n = mu_R/n; the u-bound
+ *     multipliers min(rho, z); equality multipliers by least squares (dropped above 1000);
+ *   - the restoration problem is solved by the same algorithm (monotone mu, filter line search with
+ *     second-order correction, inertia correction) with its own filter; its iterations count in the
+ *     iteration counter and max_iter caps the total;
+ *   - at every iteration after the first the original problem's progress is tested at the current
+ *     point: theta_orig <= 0.9 theta_orig(start) (required_infeasibility_reduction) and acceptable
+ *     to the original filter (which holds the start point) and to the start point; then the phase
+ *     returns: the u-bound multipliers take the step (mu - z s_trial)/s that pretends the whole
+ *     progress was one primal-dual Newton step, cut by the fraction to the boundary and reset to 1
+ *     if any exceeds bound_mult_reset_threshold 1000; the equality multipliers restart at 0
+ *     (constr_mult_reset_threshold 0);
+ *   - the restoration problem converging (optimal or acceptable) means local infeasibility; a failed
+ *     line search inside it is a restoration failure: both end the solve with status -2.
+ * Returns 1 with the new iterate in W (multipliers included) and *it set to the last restoration
+ * iteration, 0 with *status set.
+ * --------------------------------------------------------------------------------------------- */
+static int g_resto = 1;
+void oracle_lmpc_set_resto(int on) { g_resto = on; }
+
+/* restoration residuals: p, n rows (rp, rn of the barrier Lagrangian gradient), soft-row right-hand
+   sides rg = cres/d - (rn/Sn - rp/Sp)/d + D lam (physical rows) or g (copy rows) for constraint values
+   cres (d g + n - p, or a second-order correction's c_soc) */
+static void resto_rhs(const ctx_t *C, const work_t *W, double cres[][NA], double rg[][NA]) {
+    const resto_t *R = C->R; const int N = C->P->N;
+    for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) {
+        const int r = NA * k + i;
+        if (i < 8) {
+            const double d = R->dsc[r];
+            rg[k][i] = cres[k][i] / d - (R->rn[r] / R->Snd[r] - R->rp[r] / R->Spd[r]) / d + R->D[r] * W->lam[r];
+        } else {
+            rg[k][i] = cres[k][i];
+        }
+    }
+}
+/* constraint values of the restoration problem at (X, U, p, n): d g + n - p on the physical rows, g
+   on the copy rows; returns its l1 norm (theta of the restoration problem) */
+static double resto_cons(const ctx_t *C, work_t *W, const double *X, const double *U, const double *pc,
+                         const double *nc, double g[][NA], double cres[][NA]) {
+    const resto_t *R = C->R; const int N = C->P->N;
+    residuals(C, W, X, U, g);
+    double th = 0.0;
+    for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) {
+        const int r = NA * k + i;
+        cres[k][i] = i < 8 ? R->dsc[r] * g[k][i] + nc[r] - pc[r] : g[k][i];
+        th += fabs(cres[k][i]);
+    }
+    return th;
+}
+static double resto_barrier(const ctx_t *C, const double *X, const double *U, const double *pc, const double *nc) {
+    const resto_t *R = C->R; const int N = C->P->N;
+    double f = 0.0, lb = 0.0;
+    for (int k = 0; k <= N; ++k) for (int i = 0; i < 8; ++i) {
+        const int r = NA * k + i;
+        const double e = R->DRx[r] * (X[r] - R->XR[r]);
+        f += R->rho * (pc[r] + nc[r]) + 0.5 * R->eta * e * e;
+        if (!(pc[r] > 0) || !(nc[r] > 0)) return INFINITY;
+        lb += log(pc[r]) + log(nc[r]);
+    }
+    for (int j = 0; j < NU * N; ++j) {
+        const double e = R->DRu[j] * (U[j] - R->UR[j]);
+        f += 0.5 * R->eta * e * e;
+        double sl = U[j] - C->lo, su = C->hi - U[j];
+        if (!(sl > 0) || !(su > 0)) return INFINITY;
+        lb += log(sl) + log(su);
+    }
+    return f - C->mu * lb;
+}
+/* optimality-error measures of the restoration problem at the iterate in W (A, Bm there) */
+static void resto_errors(const ctx_t *C, const work_t *W, double cres[][NA], double *dinf_, double *pinf_,
+                         double *c0_, double *cmin_, double *sum_l_, double *sum_z_) {
+    const resto_t *R = C->R; const int N = C->P->N;
+    double dinf = 0, pinf = 0, c0 = 0, cmin = INFINITY, sum_l = 0, sum_z = 0;
+    for (int k = 0; k <= N; ++k) {
+        double gl[NZ];
+        for (int j = 0; j < NZ; ++j) gl[j] = 0.0;
+        for (int i = 0; i < 8; ++i) {
+            const int r = NA * k + i;
+            gl[i] = R->eta * R->DRx[r] * R->DRx[r] * (W->X[r] - R->XR[r]);
+        }
+        for (int i = 0; i < NA; ++i) gl[i] += W->lam[NA * k + i];
+        if (k < N) {
+            for (int a = 0; a < NU; ++a) {
+                const int j = NU * k + a;
+                gl[10 + a] = R->eta * R->DRu[j] * R->DRu[j] * (W->U[j] - R->UR[j]) - W->zL[j] + W->zU[j];
+            }
+            for (int m = 0; m < NA; ++m) {
+                double l = W->lam[NA * (k + 1) + m];
+                for (int i = 0; i < NA; ++i) gl[i] -= W->A[k][m][i] * l;
+                gl[10] -= W->Bm[k][m][0] * l; gl[11] -= W->Bm[k][m][1] * l;
+            }
+            for (int j = 0; j < NZ; ++j) dinf = fmax(dinf, fabs(gl[j]));
+            for (int a = 0; a < NU; ++a) {
+                const int j = NU * k + a;
+                const double cl = W->zL[j] * (W->U[j] - C->lo), cu = W->zU[j] * (C->hi - W->U[j]);
+                c0 = fmax(c0, fmax(cl, cu)); cmin = fmin(cmin, fmin(cl, cu));
+                sum_z += W->zL[j] + W->zU[j];
+            }
+        } else {
+            for (int i = 0; i < NA; ++i) dinf = fmax(dinf, fabs(gl[i]));
+        }
+        for (int i = 0; i < NA; ++i) {
+            const int r = NA * k + i;
+            pinf = fmax(pinf, fabs(cres[k][i]));
+            if (i < 8) {
+                const double y = W->lam[r] / R->dsc[r];
+                dinf = fmax(dinf, fmax(fabs(R->rho - R->zp[r] - y), fabs(R->rho - R->zn[r] + y)));
+                const double cp = R->zp[r] * R->pc[r], cn = R->zn[r] * R->nc[r];
+                c0 = fmax(c0, fmax(cp, cn)); cmin = fmin(cmin, fmin(cp, cn));
+                sum_z += R->zp[r] + R->zn[r];
+                sum_l += fabs(y);
+            } else {
+                sum_l += fabs(W->lam[r]);
+            }
+        }
+    }
+    *dinf_ = dinf; *pinf_ = pinf; *c0_ = c0; *cmin_ = cmin; *sum_l_ = sum_l; *sum_z_ = sum_z;
+}
+
+static int restoration(const ctx_t *C0, work_t *W, int *it_io, int max_iter, double tol, double acc_tol, int acc_iter,
+                       double th0, double phi0, int nfilt0, double tau0, double g0[][NA], int *status) {
+    const prob_t *P = C0->P; const int N = P->N, nU = NU * N, nA = NA * (N + 1), nrow = 8 * (N + 1);
+    const double gam_th = 1e-5, gam_ph = 1e-8, s_th = 1.1, s_ph = 2.3, gam_al = 0.05, kap_soc = 0.99;
+    const double mu_min = tol / 10, s_max = 100.0;
+    resto_t *R = (resto_t *)calloc(1, sizeof(resto_t));
+    work_t *V = (work_t *)malloc(sizeof(work_t));
+    memcpy(V, W, sizeof(work_t));
+    double (*g)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
+    double (*gt)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
+    double (*cres)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
+    double (*ct)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
+    double (*csg)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
+    double (*rg)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
+    double *sv = (double *)malloc(sizeof(double) * (2 * nA + nU + 2 * nA));
+    ctx_t C = *C0;
+    C.R = R; C.mode = 1;
+    R->rho = 1000.0; R->dsc = W->dsc;
+    int ok_out = 0;
+    /* RestoIpoptNLP: reference point and D_R */
+    for (int r = 0; r < nA; ++r) { R->XR[r] = W->X[r]; R->DRx[r] = 1.0 / fmax(1.0, fabs(W->X[r])); }
+    for (int j = 0; j < nU; ++j) { R->UR[j] = W->U[j]; R->DRu[j] = 1.0 / fmax(1.0, fabs(W->U[j])); }
+    /* RestoIterateInitializer */
+    double cmax = 0.0;
+    for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) cmax = fmax(cmax, W->dsc[NA * k + i] * fabs(g0[k][i]));
+    C.mu = fmax(C0->mu, cmax);
+    R->eta = sqrt(C.mu);
+    for (int k = 0; k <= N; ++k) for (int i = 0; i < 8; ++i) {
+        const int r = NA * k + i;
+        const double c = W->dsc[r] * g0[k][i];
+        const double a = C.mu / (2.0 * R->rho) - 0.5 * c, b = c * C.mu / (2.0 * R->rho);
+        R->nc[r] = a + sqrt(a * a + b);
+        R->pc[r] = c + R->nc[r];
+        R->zp[r] = C.mu / R->pc[r]; R->zn[r] = C.mu / R->nc[r];
+    }
+    for (int j = 0; j < nU; ++j) { V->zL[j] = fmin(R->rho, W->zL[j]); V->zU[j] = fmin(R->rho, W->zU[j]); }
+    /* least-square equality multipliers (LeastSquareMultipliers on the restoration problem: unit
+       weights on x, u, p, n; the p / n columns make every physical row soft with D = 2/d^2) */
+    linearise(P, V);
+    {
+        C.mode = 2;
+        for (int r = 0; r < nA; ++r) { R->rp[r] = (r % NA) < 8 ? R->rho - R->zp[r] : 0.0; R->rn[r] = (r % NA) < 8 ? R->rho - R->zn[r] : 0.0; }
+        riccati_factor(&C, V, 0.0);      /* unit weights: every Quu >= I */
+        memset(V->lam, 0, sizeof(double) * nA);
+        for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) cres[k][i] = 0.0;
+        resto_rhs(&C, V, cres, rg);       /* rg = -(rn - rp)/d: D lam = 0, Sp = Sn = 1 */
+        riccati_solve(&C, V, rg);
+        double ym = 0.0;
+        for (int r = 0; r < nA; ++r) if ((r % NA) < 8) ym = fmax(ym, fabs(V->lamp[r]) / W->dsc[r]);
+        if (ym <= 1e3) memcpy(V->lam, V->lamp, sizeof(double) * nA);
+        else memset(V->lam, 0, sizeof(double) * nA);
+        C.mode = 1;
+    }
+    double th = resto_cons(&C, V, V->X, V->U, R->pc, R->nc, g, cres);
+    const double th_max = 1e4 * fmax(1.0, th), th_min = 1e-4 * fmax(1.0, th);
+    int nfilt = 0, rit = *it_io + 1, first = 1, acc_count = 0;
+    double delta_last = 0.0;
+    for (;; ++rit) {
+        linearise(P, V);
+        if (!first) {
+            /* RestoConvergenceCheck: progress of the original problem at the current point */
+            const double tho = residuals(C0, V, V->X, V->U, gt);
+            if (tho <= 0.9 * th0) {
+                const double pho = barrier_obj(C0, V->X, V->U);
+                int acc = isfinite(pho);
+                for (int q = 0; q < nfilt0 && acc; ++q) acc = !(tho >= W->filt_th[q] && pho >= W->filt_ph[q]);
+                acc = acc && (LE(tho, (1 - gam_th) * th0, th0) || LE(pho - phi0, -gam_ph * th0, phi0));
+                if (acc) { ok_out = 1; break; }
+            }
+        }
+        first = 0;
+        double dinf, pinf, c0, cmin, sum_l, sum_z;
+        resto_errors(&C, V, cres, &dinf, &pinf, &c0, &cmin, &sum_l, &sum_z);
+        const double nb = 2.0 * nU + 2.0 * nrow;
+        const double s_d = fmax(s_max, (sum_l + sum_z) / (nA + 2.0 * nrow + nb)) / s_max;
+        const double s_c = fmax(s_max, sum_z / nb) / s_max;
+        const double err = fmax(dinf / s_d, fmax(pinf, c0 / s_c));
+        if (rit >= max_iter) { *status = ST_MAXITER; break; }
+        if (err <= tol && dinf <= 1.0 && pinf <= 1e-4 && c0 <= 1e-4) { *status = ST_LS_FAIL; break; }   /* local infeasibility */
+        if (acc_iter > 0 && err <= acc_tol && pinf <= 1e-2 && c0 <= 1e-2) {
+            if (++acc_count >= acc_iter) { *status = ST_LS_FAIL; break; }
+        } else {
+            acc_count = 0;
+        }
+        for (;;) {
+            const double cmu = fmax(c0 - C.mu, C.mu - cmin);
+            if (fmax(dinf / s_d, fmax(pinf, cmu / s_c)) > 10.0 * C.mu || C.mu <= mu_min) break;
+            C.mu = fmax(mu_min, fmin(0.2 * C.mu, pow(C.mu, 1.5)));
+            R->eta = sqrt(C.mu);
+            nfilt = 0;
+        }
+        const double tau = fmax(0.99, 1.0 - C.mu);
+        for (int r = 0; r < nA; ++r) if ((r % NA) < 8) {
+            const double y = V->lam[r] / W->dsc[r];
+            R->rp[r] = R->rho - C.mu / R->pc[r] - y;
+            R->rn[r] = R->rho - C.mu / R->nc[r] + y;
+        }
+        double delta = 0.0;
+        int ok = riccati_factor(&C, V, 0.0);
+        for (int attempt = 0; !ok && attempt < 60; ++attempt) {
+            delta = (attempt == 0) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))
+                                   : delta * (delta_last == 0.0 ? 100.0 : 8.0);
+            ok = riccati_factor(&C, V, delta);
+        }
+        if (!ok) { *status = ST_INERTIA_FAIL; break; }
+        if (delta > 0) delta_last = delta;
+        /* the step: Riccati for the soft rows, then p, n and every bound multiplier */
+        double amax = 0, az = 0;
+        #define RESTO_STEP(CV) do {                                                                   \
+            resto_rhs(&C, V, CV, rg);                                                                 \
+            riccati_solve(&C, V, rg);                                                                 \
+            amax = frac_to_boundary(&C, V, V->dU, tau); az = 1.0;                                     \
+            for (int r = 0; r < nA; ++r) if ((r % NA) < 8) {                                         \
+                const double dy = (V->lamp[r] - V->lam[r]) / W->dsc[r];                               \
+                R->dpc[r] = (dy - R->rp[r]) / R->Spd[r];                                              \
+                R->dnc[r] = (-dy - R->rn[r]) / R->Snd[r];                                             \
+                R->dzp[r] = C.mu / R->pc[r] - R->zp[r] - R->zp[r] / R->pc[r] * R->dpc[r];             \
+                R->dzn[r] = C.mu / R->nc[r] - R->zn[r] - R->zn[r] / R->nc[r] * R->dnc[r];             \
+                if (R->dpc[r] < 0) amax = fmin(amax, -tau * R->pc[r] / R->dpc[r]);                    \
+                if (R->dnc[r] < 0) amax = fmin(amax, -tau * R->nc[r] / R->dnc[r]);                    \
+                if (R->dzp[r] < 0) az = fmin(az, -tau * R->zp[r] / R->dzp[r]);                        \
+                if (R->dzn[r] < 0) az = fmin(az, -tau * R->zn[r] / R->dzn[r]);                        \
+            }                                                                                         \
+            az = fmin(az, bound_dual_step(&C, V, nU, tau));                                           \
+        } while (0)
+        RESTO_STEP(cres);
+#ifdef ORACLE_DEBUG
+        {   /* linearised restoration constraints: d J dx + dn - dp = -cres (physical rows), J dx = -g (copies);
+               p-row stationarity: Sp dp - dy = -rp */
+            double e1 = 0.0, e2 = 0.0;
+            for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) {
+                const int r = NA * k + i;
+                double jd = V->dX[r];
+                if (k > 0) {
+                    for (int m = 0; m < NA; ++m) jd -= V->A[k - 1][i][m] * V->dX[NA * (k - 1) + m];
+                    for (int a = 0; a < NU; ++a) jd -= V->Bm[k - 1][i][a] * V->dU[NU * (k - 1) + a];
+                }
+                if (i < 8) {
+                    e1 = fmax(e1, fabs(W->dsc[r] * jd + R->dnc[r] - R->dpc[r] + cres[k][i]));
+                    const double dy = (V->lamp[r] - V->lam[r]) / W->dsc[r];
+                    e2 = fmax(e2, fabs(R->Spd[r] * R->dpc[r] - dy + R->rp[r]) + fabs(R->Snd[r] * R->dnc[r] + dy + R->rn[r]));
+                } else e1 = fmax(e1, fabs(jd + cres[k][i]));
+            }
+            fprintf(stderr, "  resto step check: constraint %.2e  p/n rows %.2e\n", e1, e2);
+        }
+#endif
+        const double phi = resto_barrier(&C, V->X, V->U, R->pc, R->nc);
+        double gTd = 0.0;
+        for (int k = 0; k <= N; ++k) for (int i = 0; i < 8; ++i) {
+            const int r = NA * k + i;
+            gTd += R->eta * R->DRx[r] * R->DRx[r] * (V->X[r] - R->XR[r]) * V->dX[r];
+            gTd += (R->rho - C.mu / R->pc[r]) * R->dpc[r] + (R->rho - C.mu / R->nc[r]) * R->dnc[r];
+        }
+        for (int j = 0; j < nU; ++j)
+            gTd += (R->eta * R->DRu[j] * R->DRu[j] * (V->U[j] - R->UR[j]) - C.mu / (V->U[j] - C.lo) + C.mu / (C.hi - V->U[j])) * V->dU[j];
+        double amin = gam_th;
+        if (gTd < 0) amin = fmin(gam_th, fmin(gam_ph * th / (-gTd), pow(th, s_th) / pow(-gTd, s_ph)));
+        amin *= gam_al;
+        double alpha = amax, th_t = 0, ph_t = 0;
+        int accepted = 0, ftype = 0;
+        #define RESTO_TRIAL(AL) do {                                                                  \
+            for (int i = 0; i < nA; ++i) V->Xt[i] = V->X[i] + (AL) * V->dX[i];                       \
+            for (int j = 0; j < nU; ++j) V->Ut[j] = V->U[j] + (AL) * V->dU[j];                       \
+            for (int r = 0; r < nA; ++r) if ((r % NA) < 8) {                                         \
+                R->pt_[r] = R->pc[r] + (AL) * R->dpc[r]; R->nt_[r] = R->nc[r] + (AL) * R->dnc[r];    \
+            }                                                                                         \
+            th_t = resto_cons(&C, V, V->Xt, V->Ut, R->pt_, R->nt_, gt, ct);                          \
+            ph_t = resto_barrier(&C, V->Xt, V->Ut, R->pt_, R->nt_);                                  \
+        } while (0)
+        for (int ls = 0; ls < 80 && !accepted; ++ls) {
+            if (alpha < amin && ls > 0) break;
+            RESTO_TRIAL(alpha);
+            /* the restoration problem's own filter (filter_accept reads W->filt_*: swap in R's) */
+            {
+                int in_f = !(th_t < th_max) || !isfinite(ph_t);
+                for (int q = 0; q < nfilt && !in_f; ++q) in_f = th_t >= R->filt_th[q] && ph_t >= R->filt_ph[q];
+                if (!in_f) {
+                    const int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > pow(th, s_th);
+                    if (th <= th_min && sw) { if (LE(ph_t, phi + 1e-8 * alpha * gTd, phi)) { accepted = 1; ftype = 1; } }
+                    else accepted = LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi);
+                }
+            }
+            if (!accepted && ls == 0 && !(th_t < th)) {
+                /* second-order correction on the restoration problem's constraints */
+                memcpy(sv, V->dX, sizeof(double) * nA); memcpy(sv + nA, V->lamp, sizeof(double) * nA);
+                memcpy(sv + 2 * nA, V->dU, sizeof(double) * nU);
+                memcpy(sv + 2 * nA + nU, R->dpc, sizeof(double) * nA); memcpy(sv + 3 * nA + nU, R->dnc, sizeof(double) * nA);
+                double asoc = alpha, th_old = 0.0;
+                for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] = cres[k][i];
+                for (int c = 0; c < 4; ++c) {
+                    if (c > 0 && !(th_t <= kap_soc * th_old)) break;
+                    th_old = th_t;
+                    for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] = asoc * csg[k][i] + ct[k][i];
+                    RESTO_STEP(csg);
+                    asoc = amax;
+                    RESTO_TRIAL(asoc);
+                    int in_f = !(th_t < th_max) || !isfinite(ph_t);
+                    for (int q = 0; q < nfilt && !in_f; ++q) in_f = th_t >= R->filt_th[q] && ph_t >= R->filt_ph[q];
+                    int acc = 0;
+                    if (!in_f) {
+                        const int sw = gTd < 0 && alpha * pow(-gTd, s_ph) > pow(th, s_th);
+                        if (th <= th_min && sw) { if (LE(ph_t, phi + 1e-8 * alpha * gTd, phi)) { acc = 1; ftype = 1; } }
+                        else acc = LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi);
+                    }
+                    if (acc) { accepted = 1; alpha = asoc; break; }
+                }
+                if (!accepted) {
+                    memcpy(V->dX, sv, sizeof(double) * nA); memcpy(V->lamp, sv + nA, sizeof(double) * nA);
+                    memcpy(V->dU, sv + 2 * nA, sizeof(double) * nU);
+                    memcpy(R->dpc, sv + 2 * nA + nU, sizeof(double) * nA); memcpy(R->dnc, sv + 3 * nA + nU, sizeof(double) * nA);
+                    /* the bound-multiplier steps of the plain direction back */
+                    for (int r = 0; r < nA; ++r) if ((r % NA) < 8) {
+                        R->dzp[r] = C.mu / R->pc[r] - R->zp[r] - R->zp[r] / R->pc[r] * R->dpc[r];
+                        R->dzn[r] = C.mu / R->nc[r] - R->zn[r] - R->zn[r] / R->nc[r] * R->dnc[r];
+                    }
+                    az = 1.0;
+                    for (int r = 0; r < nA; ++r) if ((r % NA) < 8) {
+                        if (R->dzp[r] < 0) az = fmin(az, -tau * R->zp[r] / R->dzp[r]);
+                        if (R->dzn[r] < 0) az = fmin(az, -tau * R->zn[r] / R->dzn[r]);
+                    }
+                    az = fmin(az, bound_dual_step(&C, V, nU, tau));
+                }
+            }
+            if (!accepted) alpha *= 0.5;
+        }
+#ifdef ORACLE_DEBUG
+        fprintf(stderr, "  resto it %3d mu %.2e err %.2e dinf %.2e pinf %.2e c0 %.2e delta %.1e amax %.3e alpha %.3e th %.3e th_t %.3e phi %.6e ph_t %.6e gTd %.3e acc %d\n",
+                rit, C.mu, err, dinf / s_d, pinf, c0 / s_c, delta, amax, alpha, th, th_t, phi, ph_t, gTd, accepted);
+#endif
+        if (!accepted) { *status = ST_LS_FAIL; break; }     /* restoration failure */
+        if (!ftype && nfilt < 256) { R->filt_th[nfilt] = (1 - gam_th) * th; R->filt_ph[nfilt] = phi - gam_ph * th; ++nfilt; }
+        memcpy(V->X, V->Xt, sizeof(double) * nA);
+        memcpy(V->U, V->Ut, sizeof(double) * nU);
+        for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) cres[k][i] = ct[k][i];
+        th = th_t;
+        for (int i = 0; i < nA; ++i) V->lam[i] += alpha * (V->lamp[i] - V->lam[i]);
+        for (int r = 0; r < nA; ++r) if ((r % NA) < 8) {
+            R->pc[r] = R->pt_[r]; R->nc[r] = R->nt_[r];
+            const double zp = R->zp[r] + az * R->dzp[r], zn = R->zn[r] + az * R->dzn[r];
+            R->zp[r] = fmax(fmin(zp, 1e10 * C.mu / R->pc[r]), C.mu / (1e10 * R->pc[r]));
+            R->zn[r] = fmax(fmin(zn, 1e10 * C.mu / R->nc[r]), C.mu / (1e10 * R->nc[r]));
+        }
+        for (int j = 0; j < nU; ++j) {
+            double sl = V->U[j] - C.lo, su = C.hi - V->U[j];
+            double zl = V->zL[j] + az * V->dzL[j], zu = V->zU[j] + az * V->dzU[j];
+            V->zL[j] = fmax(fmin(zl, 1e10 * C.mu / sl), C.mu / (1e10 * sl));
+            V->zU[j] = fmax(fmin(zu, 1e10 * C.mu / su), C.mu / (1e10 * su));
+        }
+        #undef RESTO_TRIAL
+        #undef RESTO_STEP
+    }
+    if (ok_out) {
+        /* back to the original problem: x from the restoration phase, u-bound multipliers by the
+           pretended Newton step (mu - z s_trial)/s cut by the fraction to the boundary, reset to 1
+           above 1000; equality multipliers 0 */
+        const double mu0 = C0->mu;
+        double az = 1.0, zmax = 0.0;
+        for (int j = 0; j < nU; ++j) {
+            const double sl = W->U[j] - C0->lo, su = C0->hi - W->U[j];
+            const double slt = V->U[j] - C0->lo, sut = C0->hi - V->U[j];
+            W->dzL[j] = (mu0 - W->zL[j] * slt) / sl;
+            W->dzU[j] = (mu0 - W->zU[j] * sut) / su;
+            if (W->dzL[j] < 0) az = fmin(az, -tau0 * W->zL[j] / W->dzL[j]);
+            if (W->dzU[j] < 0) az = fmin(az, -tau0 * W->zU[j] / W->dzU[j]);
+        }
+        for (int j = 0; j < nU; ++j) {
+            W->zL[j] += az * W->dzL[j]; W->zU[j] += az * W->dzU[j];
+            zmax = fmax(zmax, fmax(W->zL[j], W->zU[j]));
+        }
+        if (zmax > 1e3) for (int j = 0; j < nU; ++j) { W->zL[j] = 1.0; W->zU[j] = 1.0; }
+        memcpy(W->X, V->X, sizeof(double) * nA);
+        memcpy(W->U, V->U, sizeof(double) * nU);
+        memset(W->lam, 0, sizeof(double) * nA);
+        for (int j = 0; j < nU; ++j) {      /* AcceptTrialPoint: kappa_sigma correction */
+            const double sl = W->U[j] - C0->lo, su = C0->hi - W->U[j];
+            W->zL[j] = fmax(fmin(W->zL[j], 1e10 * mu0 / sl), mu0 / (1e10 * sl));
+            W->zU[j] = fmax(fmin(W->zU[j], 1e10 * mu0 / su), mu0 / (1e10 * su));
+        }
+        *it_io = rit - 1;
+    } else {
+        *it_io = rit;
+    }
+    free(g); free(gt); free(cres); free(ct); free(csg); free(rg); free(sv);
+    free(V); free(R);
+    return ok_out;
+}
 
 /* prm = [Q(8), Qt(8), R(4), u_lo, u_hi];  acc_tol / acc_iter: IPOPT acceptable_tol / acceptable_iter (0 = off) */
 /* filter line-search acceptance of a trial (th_t, ph_t) for the step size alpha (IPOPT
@@ -530,7 +1184,7 @@ int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_pre
     const int nU = NU * N, nA = NA * (N + 1);
     ctx_t C;
     memset(&C, 0, sizeof C);
-    C.P = &P; C.x0 = state; C.up0 = u_prev; C.tgt = target; C.mu = 0.1; C.lo = lo; C.hi = hi;
+    C.P = &P; C.x0 = state; C.up0 = u_prev; C.tgt = target; C.mu = 0.1; C.lo = lo; C.hi = hi; C.R = NULL; C.mode = 0;
     /* initial point: w_init (the worker's warm start, zeros on the first solve :492) */
     for (int k = 0; k <= N; ++k)
         for (int i = 0; i < 8; ++i) W->X[NA * k + i] = w_init ? w_init[8 * k + i] : 0.0;
@@ -571,41 +1225,13 @@ int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_pre
     double (*csg)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));
     double th = residuals(&C, W, W->X, W->U, g);
     const double th_max = 1e4 * fmax(1.0, th), th_min = 1e-4 * fmax(1.0, th);
-    int nfilt = 0, status = ST_MAXITER, it, acc_count = 0;
+    int nfilt = 0, status = ST_MAXITER, it, acc_count = 0, in_soft = 0, soft_count = 0;
     double delta_last = 0.0;
     for (it = 0;; ++it) {
         if (it > 0) linearise(&P, W);
         /* optimality error (IPOPT eq. 5) with scaled rows: y~ = lam / d */
-        double sum_l = 0, sum_z = 0, dinf = 0, pinf = 0, pinf_u = 0, c0 = 0;
-        for (int i = 0; i < nA; ++i) sum_l += fabs(W->lam[i]) / W->dsc[i];
-        for (int k = 0; k <= N; ++k) {
-            double z[NZ], gc[NZ], gl[NZ];
-            for (int i = 0; i < NA; ++i) z[i] = W->X[NA * k + i];
-            z[10] = k < N ? W->U[NU * k] : 0.0; z[11] = k < N ? W->U[NU * k + 1] : 0.0;
-            cost_grad(&P, z, target, k == N, gc);
-            for (int j = 0; j < NZ; ++j) gl[j] = C.sc * gc[j];
-            for (int i = 0; i < NA; ++i) gl[i] += W->lam[NA * k + i];
-            if (k < N) {
-                for (int m = 0; m < NA; ++m) {
-                    double l = W->lam[NA * (k + 1) + m];
-                    for (int i = 0; i < NA; ++i) gl[i] -= W->A[k][m][i] * l;
-                    gl[10] -= W->Bm[k][m][0] * l; gl[11] -= W->Bm[k][m][1] * l;
-                }
-                gl[10] += -W->zL[NU * k] + W->zU[NU * k]; gl[11] += -W->zL[NU * k + 1] + W->zU[NU * k + 1];
-                for (int j = 0; j < NZ; ++j) dinf = fmax(dinf, fabs(gl[j]));
-                for (int a = 0; a < NU; ++a) {
-                    const int j = NU * k + a;
-                    c0 = fmax(c0, fmax(fabs(W->zL[j] * (W->U[j] - lo)), fabs(W->zU[j] * (hi - W->U[j]))));
-                    sum_z += W->zL[j] + W->zU[j];
-                }
-            } else {
-                for (int i = 0; i < NA; ++i) dinf = fmax(dinf, fabs(gl[i]));
-            }
-            for (int i = 0; i < NA; ++i) {
-                pinf = fmax(pinf, W->dsc[NA * k + i] * fabs(g[k][i]));
-                pinf_u = fmax(pinf_u, fabs(g[k][i]));
-            }
-        }
+        double sum_l, sum_z, dinf, pinf, pinf_u, c0;
+        kkt_errors(&C, W, g, &sum_l, &sum_z, &dinf, &pinf, &pinf_u, &c0, NULL);
         const int nb = 2 * nU;
         const double s_d = fmax(s_max, (sum_l + sum_z) / (nA + nb)) / s_max;
         const double s_c = fmax(s_max, sum_z / nb) / s_max;
@@ -624,7 +1250,7 @@ int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_pre
                 cmu = fmax(cmu, fmax(fabs(W->zL[j] * (W->U[j] - lo) - C.mu), fabs(W->zU[j] * (hi - W->U[j]) - C.mu)));
             if (fmax(dinf / s_d, fmax(pinf, cmu / s_c)) > kappa_eps * C.mu || C.mu <= mu_min) break;
             C.mu = fmax(mu_min, fmin(kappa_mu * C.mu, pow(C.mu, theta_mu)));
-            nfilt = 0;
+            nfilt = 0; in_soft = 0;      /* BacktrackingLineSearch::Reset: the filter and the soft phase */
         }
         const double tau = fmax(0.99, 1.0 - C.mu);
         double delta = 0.0;
@@ -663,7 +1289,7 @@ int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_pre
         for (int i = 0; i < nA; ++i) tn = fmax(tn, fabs(W->dX[i]) / (1.0 + fabs(W->X[i])));
         for (int j = 0; j < nU; ++j) tn = fmax(tn, fabs(W->dU[j]) / (1.0 + fabs(W->U[j])));
         const int tiny = tn < 10.0 * 2.220446049250313e-16;
-        for (int ls = 0; ls < 80 && !accepted; ++ls) {
+        for (int ls = 0; ls < 80 && !accepted && !in_soft; ++ls) {
             if (alpha < amin && ls > 0) break;
             for (int i = 0; i < nA; ++i) W->Xt[i] = W->X[i] + alpha * W->dX[i];
             for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + alpha * W->dU[j];
@@ -705,12 +1331,46 @@ int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_pre
             }
             if (!accepted) alpha *= 0.5;
         }
+        int soft = 0;
+        if (!accepted && g_soft_resto) {
+            /* the line search failed (or the soft restoration phase is on): IPOPT's soft restoration
+               phase, at most max_soft_resto_iters = 10 steps; on entry PrepareRestoPhaseStart puts the
+               current point into the filter */
+            if (!in_soft) {
+                if (nfilt < 256) { W->filt_th[nfilt] = (1 - gam_th) * th; W->filt_ph[nfilt] = phi - gam_ph * th; ++nfilt; }
+                soft_count = 0;
+            }
+            if (!(in_soft && ++soft_count > 10)) {
+                double sl_, sz_, di_, pi_, pu_, c0_, pd;
+                kkt_errors(&C, W, g, &sl_, &sz_, &di_, &pi_, &pu_, &c0_, &pd);
+                int orig = 0;
+                const double a = soft_resto_step(&C, W, nfilt, th, phi, th_max, tau, pd, gt, &th_t, &ph_t, &orig);
+                if (a > 0.0) {
+                    accepted = 1; soft = 1; alpha = a; az = a;
+                    in_soft = !orig;
+                    if (orig) soft_count = 0;
+                }
+            }
+        }
 #ifdef ORACLE_DEBUG
-        fprintf(stderr, "it %3d mu %.2e err %.2e dinf %.2e pinf %.2e c0 %.2e delta %.1e amax %.3e alpha %.3e th %.3e th_t %.3e phi %.6e ph_t %.6e gTd %.3e acc %d\n",
-                it, C.mu, err, dinf / s_d, pinf, c0 / s_c, delta, amax, alpha, th, th_t, phi, ph_t, gTd, accepted);
+        fprintf(stderr, "it %3d soft %d mu %.2e err %.2e dinf %.2e pinf %.2e c0 %.2e delta %.1e amax %.3e alpha %.3e th %.3e th_t %.3e phi %.6e ph_t %.6e gTd %.3e acc %d\n",
+                it, in_soft, C.mu, err, dinf / s_d, pinf, c0 / s_c, delta, amax, alpha, th, th_t, phi, ph_t, gTd, accepted);
 #endif
+        if (!accepted && g_resto) {
+            /* IPOPT's restoration phase (the start point entered the filter with the soft phase above,
+               or enters it here when that phase is off) */
+            if (!g_soft_resto && nfilt < 256) { W->filt_th[nfilt] = (1 - gam_th) * th; W->filt_ph[nfilt] = phi - gam_ph * th; ++nfilt; }
+            int rst = ST_LS_FAIL;
+            if (!restoration(&C, W, &it, max_iter, tol, acc_tol, acc_iter, th, phi, nfilt, tau, g, &rst)) {
+                status = rst;
+                break;
+            }
+            th = residuals(&C, W, W->X, W->U, g);
+            in_soft = 0; soft_count = 0;
+            continue;
+        }
         if (!accepted) { status = ST_LS_FAIL; break; }
-        if (!ftype && nfilt < 256) { W->filt_th[nfilt] = (1 - gam_th) * th; W->filt_ph[nfilt] = phi - gam_ph * th; ++nfilt; }
+        if (!soft && !ftype && nfilt < 256) { W->filt_th[nfilt] = (1 - gam_th) * th; W->filt_ph[nfilt] = phi - gam_ph * th; ++nfilt; }
         memcpy(W->X, W->Xt, sizeof(double) * nA);
         memcpy(W->U, W->Ut, sizeof(double) * nU);
         memcpy(g, gt, sizeof(double) * NA * (N + 1));

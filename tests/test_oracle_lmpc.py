@@ -103,3 +103,24 @@ def test_soc_switch_changes_path_not_solution(lmpc_goldens):
     b = _solve(G, idx, 30, tol=1e-11, acc_iter=0, max_iter=500, soc=False)
     assert np.all(a["status"] == 0) and np.all(b["status"] == 0)
     assert np.max(np.abs(a["u0"] - b["u0"])) <= 1e-7
+
+
+def test_restoration_phase_recovers_failed_line_searches():
+    """IPOPT's soft restoration and restoration phases (MinC_1NrmRestorationPhase, restated in
+    oracle/lmpc_ipm.c): on the cold-started C5 batch of 720 instances (reference options) the filter line
+    search fails on five instances; IPOPT leaves through the restoration phase there, and every one of
+    them then converges (no status -2 left), while the other 715 instances never touch it."""
+    from dart_mpc.workload import lmpc_batch
+    D = lmpc_batch(40, seed0=0)
+    args = (D["state"], D["u_prev"], D["pvec"], D["target"])
+    off = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=8, want_w=False, resto=False)
+    on = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=8, want_w=False)
+    failed = off["status"] == -2
+    assert failed.sum() == 5
+    assert not np.any(on["status"] == -2)
+    assert np.all(on["status"][failed] >= -1)
+    assert np.mean(on["status"][failed] == 0) >= 0.6
+    same = ~failed
+    assert np.array_equal(on["status"][same], off["status"][same])
+    assert np.array_equal(on["iters"][same], off["iters"][same])
+    assert np.array_equal(on["u0"][same], off["u0"][same])
