@@ -189,6 +189,10 @@ struct dart_mpc_handle {
     // reference runs controllers on background threads, RMPC/dev_dual/controller/convimp.py:435)
     // are safe but take turns; one handle per thread runs them side by side.
     std::recursive_mutex mu;     // recursive: the host entries call their _dev twins
+    // LMPC: hand-off area of the instances that enter IPOPT's restoration phases (lmpc_ipm.hip,
+    // [B][64][16] doubles), grown on demand
+    double* resto_buf = nullptr;
+    size_t resto_cap = 0;
 };
 
 namespace {
@@ -295,6 +299,22 @@ int server_stop(dart_mpc_handle* h) {
 
 // settle the stream of an earlier host PMPC call that returned on its completion words (see
 // dart_mpc_handle::pending)
+// the LMPC restoration hand-off area for B instances (device memory; a larger batch than before waits
+// for the device before the old area is freed)
+int lmpc_resto_area(dart_mpc_handle* h, int B) {
+    if (!h->cfg.restoration) return DART_MPC_OK;
+    const size_t need = (size_t)B * 64 * 16;
+    if (need <= h->resto_cap) return DART_MPC_OK;
+    if (h->resto_buf) {
+        HIPCHK(h, hipDeviceSynchronize(), "hipDeviceSynchronize");
+        (void)hipFree(h->resto_buf);
+        h->resto_buf = nullptr; h->resto_cap = 0;
+    }
+    HIPCHK(h, hipMalloc((void**)&h->resto_buf, need * sizeof(double)), "hipMalloc (restoration hand-off)");
+    h->resto_cap = need;
+    return DART_MPC_OK;
+}
+
 int settle_pending(dart_mpc_handle* h) {
     if (!h->pending) return DART_MPC_OK;
     hipStream_t s = h->pending;
@@ -397,6 +417,7 @@ void dart_mpc_config_default(dart_mpc_config* c) {
     c->max_soc = 4;
     c->pmpc_path = 0;
     c->constr_mult_init_max = 1000.0;
+    c->restoration = 1;
 }
 
 int dart_mpc_nw(int N) { return 6 * (N + 1) + 2 * N; }
@@ -610,6 +631,9 @@ int dart_lmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* state, co
     dartmpc::LmpcArgs a;
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter;
     a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc; a.mult_init_max = h->cfg.constr_mult_init_max;
+    a.resto = h->cfg.restoration;
+    if (int rc = lmpc_resto_area(h, B)) return rc;
+    a.resto_buf = h->resto_buf;
     a.state = state; a.u_prev = u_prev; a.pvec = pvec; a.target = target; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     a.fuse_policy = 0;
@@ -755,6 +779,9 @@ int dart_lmpc_policy_solve_batch_dev(dart_mpc_handle* h, const dart_lmpc_policy_
     a.fuse_policy = 1;
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter;
     a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc; a.mult_init_max = h->cfg.constr_mult_init_max;
+    a.resto = h->cfg.restoration;
+    if (int rc = lmpc_resto_area(h, B)) return rc;
+    a.resto_buf = h->resto_buf;
     a.state = state; a.u_prev = u_prev; a.pvec = nullptr; a.target = target; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     HIPCHK(h, dartmpc_launch_lmpc(&a, stream ? (hipStream_t)stream : h->stream), "kernel launch");
@@ -956,6 +983,7 @@ void dart_mpc_destroy(dart_mpc_handle* h) {
     h->st.release();
     io_release(h);
     if (h->hdone) (void)hipHostFree(h->hdone);
+    if (h->resto_buf) (void)hipFree(h->resto_buf);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }

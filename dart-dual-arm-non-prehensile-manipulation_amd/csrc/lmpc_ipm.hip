@@ -72,9 +72,143 @@ struct LmShared {
     double W[2][2][4], tg[2][4], st0[2][4];   // [half][stage, terminal] weights, target, x_0 (local order)
 };
 
-// dynamic LDS: LmShared, then (fused launches) the policy step's PolicyLds
+// ---------------------------------------------------------------------------------------------
+// IPOPT's restoration phase (MinC_1NrmRestorationPhase; oracle/lmpc_ipm.c `restoration`).  Every
+// physical defect row of the feasibility problem carries a slack pair (p, n); eliminating it leaves
+// the row soft, J dx - D dlam = rhs with D = (1/Sigma_p' + 1/Sigma_n') / d^2.  In the Riccati recursion
+// the value function of node k+1 is then seen through its soft rows: eliminating the row slack w
+// (Hessian D^-1 on the four physical rows) from V(x~ + w) is a second Schur complement over the value
+// indices [x~ (5); 1],
+//   Pt' = Pt - Pt(:, ph) S^-1 Pt(ph, :),   S = Pt(ph, ph) + D^-1,
+// with Pt from G_{k+1} by the Schur complement on u, so the node step runs unchanged on the surrogate
+// [[Pt', 0], [0, 1]]; the incoming rows of node k+1 map x~+ <- x~+ - E T [x~+; 1] with
+// T = S^-1 Pt(ph, :) (4 x 6), and S positive definite is part of the inertia test.
+// ---------------------------------------------------------------------------------------------
+struct LmResto {
+    NodeArr<double[24], 2 * LM_NMAXS> T;      // T of node k's soft rows (row-major 4 x 6, value indices)
+    NodeArr<double[4], 2 * LM_NMAXS> Dinv;    // 1 / D of node k's four physical incoming rows
+    NodeArr<double[20], 2 * LM_NMAXS> SV;     // a second-order correction: the plain step
+    double Gs[2][LmLds::NTP];                 // the surrogate of G_{k+1} (one per half)
+};
+
+// Pt(a, q) rows a < 4 of the value function in G slot Gn, S = Pt(ph, ph) + diag(dinv) = L diag(dd) L^T
+// and T = S^-1 Pt(ph, :); returns S > 0.  gu / iq: Gzu and 1 / Quu of Gn.
+__device__ __forceinline__ bool soft_T(const double* Gn, const double* dinv, double (&T)[4][6], double (&gu)[6],
+                                       double& iq) {
+    constexpr int NXA = 5;
+#pragma unroll
+    for (int p = 0; p < 6; ++p) gu[p] = Gn[gszu<NXA>(p)];
+    iq = frcp(Gn[hp(NXA, NXA)]);
+    double Pp[4][6];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) Pp[a][q] = fma(-gu[a] * iq, gu[q], Gn[gszz<NXA>(a, q)]);
+    double L[4][4], dd[4], id[4];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        double t = Pp[j][j] + dinv[j];
+#pragma unroll
+        for (int m = 0; m < j; ++m) t -= L[j][m] * L[j][m] * dd[m];
+        dd[j] = t;
+        ok = ok && t > 0.0 && isfinite(t);
+        id[j] = frcp(t);
+#pragma unroll
+        for (int i = j + 1; i < 4; ++i) {
+            double u = Pp[i][j];
+#pragma unroll
+            for (int m = 0; m < j; ++m) u -= L[i][m] * L[j][m] * dd[m];
+            L[i][j] = u * id[j];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        double y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            double t = Pp[i][q];
+#pragma unroll
+            for (int m = 0; m < i; ++m) t -= L[i][m] * y[m];
+            y[i] = t;
+        }
+#pragma unroll
+        for (int i = 3; i >= 0; --i) {
+            double t = y[i] * id[i];
+#pragma unroll
+            for (int m = i + 1; m < 4; ++m) t -= L[m][i] * T[m][q];
+            T[i][q] = t;
+        }
+    }
+    return ok;
+}
+
+// Backward sweep of both halves with soft physical rows (restoration phase): before the step of node
+// k, each half forms the surrogate of G_{k+1} seen through node k+1's soft rows (RL->Gs) and keeps
+// T_{k+1} for the forward map; T_0 of the soft initial rows comes last.  G[slot N] must hold the
+// terminal surrogate, RL->Dinv every node's 1 / D.  Returns false (wave-uniform) if some S or Quu is
+// not positive definite.
+__device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const RiccatiSRoles& R) {
+    constexpr int NXA = LmLds::NXA, NP = LmLds::NP;
+    const int h = threadIdx.x >> 5, base = h * LM_NMAXS, e0 = threadIdx.x & 31;
+    int zi = 0;
+    while (tri(zi + 1) <= R.e) ++zi;
+    const int zj = R.e - tri(zi);
+    const bool uent = zi == NXA || zj == NXA;                              // z index 5 = u
+    const int pv = zi == NXA + 1 ? NXA : (zi < NXA ? zi : 0), qv = zj == NXA + 1 ? NXA : (zj < NXA ? zj : 0);
+    auto soften = [&](int j, bool surrogate) {
+        const double* Gn = S->G[j];
+        double T[4][6], gu[6], iq;
+        const double qj = Gn[hp(NXA, NXA)];
+        const bool okj = soft_T(Gn, RL->Dinv[j], T, gu, iq) && qj > 0.0 && isfinite(qj);
+        if (surrogate) {
+            double v = fma(-gu[pv] * iq, gu[qv], Gn[gszz<NXA>(pv, qv)]);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) v -= fma(-gu[pv] * iq, gu[a], Gn[gszz<NXA>(pv, a)]) * T[a][qv];
+            RL->Gs[h][R.e] = uent ? ((zi == NXA && zj == NXA) ? 1.0 : 0.0) : v;
+        }
+        if (e0 < 24) RL->T[j][e0] = T[e0 / 6][e0 % 6];
+        return okj;
+    };
+    bool ok = true;
+    for (int k = N - 1; k >= 0; --k) {
+        ok = soften(base + k + 1, true) && ok;
+        __syncthreads();
+        const double hk = S->H[base + k][R.e];
+        const double* Mk = &S->M[base + k][0][0];
+        double vi[NP], vj[NP];
+#pragma unroll
+        for (int m = 0; m < NP; ++m) { vi[m] = Mk[R.ci + m]; vj[m] = Mk[R.cj + m]; }
+        const double* Gn = RL->Gs[h];
+        double t[NP];
+#pragma unroll
+        for (int m = 0; m < NP; ++m) t[m] = 0.0;
+#pragma unroll
+        for (int n = 0; n < NP; ++n)
+#pragma unroll
+            for (int m = 0; m < NP; ++m) t[m] = fma(Gn[gszz<NXA>(m, n)], vj[n], t[m]);
+        double ga = hk;
+#pragma unroll
+        for (int m = 0; m < NP; ++m) ga = fma(vi[m], t[m], ga);
+        S->G[base + k][R.e] = ga;
+        __syncthreads();
+    }
+    ok = soften(base, false) && ok;
+    __syncthreads();
+    const double q0 = S->G[base][hp(NXA, NXA)];
+    ok = ok && q0 > 0.0 && isfinite(q0);
+    return !wany(!ok);
+}
+
+// dynamic LDS: LmShared, then the policy step's PolicyLds (fused launches of lmpc_ipm_kernel<false>) or
+// LmResto (lmpc_ipm_kernel<true>) at the same offset
 constexpr size_t kLmPolicyLdsOff = (sizeof(LmShared) + 15) & ~size_t(15);
-constexpr size_t kLmLdsBytes = kLmPolicyLdsOff + sizeof(PolicyLds);
+constexpr size_t kLmRestoOff = kLmPolicyLdsOff;
+constexpr size_t kLmLdsBytes = kLmPolicyLdsOff + (sizeof(PolicyLds) > sizeof(LmResto) ? sizeof(PolicyLds) : sizeof(LmResto));
+// hand-off of an instance whose filter line search failed: its iteration-start state goes to HBM
+// (LmpcArgs::resto_buf, kLmNst doubles per lane) and lmpc_ipm_kernel<true> resumes it
+constexpr int kLmNeedResto = -100;
+constexpr int kLmNst = 16;
 
 __device__ __forceinline__ double sq(double p) { return fabs(p) + 1e-6; }   // squash_param :296-298
 
@@ -282,14 +416,24 @@ __device__ __forceinline__ double sub_direction(const LmSub& m, const double (*s
     return dot;
 }
 
+// RESTO = false: the fast kernel of every solve; an instance whose filter line search fails parks the
+// state of that iteration's start in a.resto_buf and ends with status kLmNeedResto.  RESTO = true: the
+// same solve with IPOPT's soft restoration and restoration phases inline (their registers would spill
+// the fast kernel's loop); launched right after it, only flagged instances run: they redo the setup,
+// reload the parked state and continue from the failed iteration.
+template <bool RESTO>
 __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     LmShared& SH = *reinterpret_cast<LmShared*>(smem);
     LmLds* S = &SH.ocp;
+    LmResto* RL = reinterpret_cast<LmResto*>(smem + kLmRestoOff);
     const RiccatiSRoles RR = riccati_s_roles<LmLds>();
     STAMP_DECL
     if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
     const int b = blockIdx.x / a.pack;
+    if constexpr (RESTO) {
+        if (a.status[b] != kLmNeedResto) return;     // wave-uniform: the instance was solved by <false>
+    }
     const int lane = threadIdx.x;
     const int hf = lane >> 5;                  // subsystem: 0 = x [px, vx, th_y, om_y; a], 1 = y [py, vy, th_x, om_x; b]
     const int k = lane & 31;                   // shooting node
@@ -297,8 +441,8 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     const int N = a.N;
     // fused policy step (C5: the learned parameter net in the same launch as the shooting defects it
     // parameterises): its LDS sits after LmShared, its output vector is this solve's pvec
-    const double* pvec = a.fuse_policy ? nullptr : a.pvec + LM_NPV * b;
-    if (a.fuse_policy) {
+    const double* pvec = a.fuse_policy ? (RESTO ? a.pol.model_params + LM_NPV * b : nullptr) : a.pvec + LM_NPV * b;
+    if (!RESTO && a.fuse_policy) {
         PolicyLds& PL = *reinterpret_cast<PolicyLds*>(smem + kLmPolicyLdsOff);
         policy_step_wave(a.pol, b, PL);
         pvec = PL.pv;
@@ -486,8 +630,85 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
     // are those of the reference NLP, which has no copy rows), r = scaled grad f - z_L + z_U, and a zero
     // defect column; y = the step's new multipliers.  Mirrors ls_multipliers in oracle/lmpc_ipm.c.
     const bool lsinit = a.mult_init_max > 0.0;
-    for (it = lsinit ? -1 : 0;; ++it) {
+    int in_soft = 0, soft_count = 0;       // IPOPT's soft restoration phase (BacktrackingLineSearch)
+    int it_start = lsinit ? -1 : 0;
+    if constexpr (RESTO) {      // resume a handed-off instance at the start of its failed iteration
+        const double* st = a.resto_buf + ((size_t)b * kWave + lane) * kLmNst;
+        const double* sc0 = a.resto_buf + (size_t)b * kWave * kLmNst + kLmNst - 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = st[i];
+        up = st[4]; u = st[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) lam[i] = st[6 + i];
+        zl = st[11]; zu = st[12]; fth = st[13]; fph = st[14];
+        mu = sc0[0]; theta = sc0[kLmNst]; delta_last = sc0[2 * kLmNst];
+        it_start = (int)sc0[3 * kLmNst]; nfilt = (int)sc0[4 * kLmNst]; acc_count = (int)sc0[5 * kLmNst];
+    }
+
+    // ---- helpers of the restoration phases (cold path) -----------------------------------------
+    // derivative pass at (xx, uu) with the next node's multipliers lmn: Jacobian columns into M~, the
+    // exact dynamics Hessian into H~ (diagonal + cadd), jl = J^T lmn, xn = x+ of node k
+    auto deriv_pass = [&](const double* xx, double uu, const double* lmn, const double* cadd4, double cadd_u,
+                          double* jl_, double* xn_) {
+        double sa, ca;
+        tilt_sincos_econ(poly, uu, sa, ca);
+        double scr[4][LM_NSC], cvr[4][4];
+        sub_rk4_lin(m, xx, sa, xn_, scr, cvr);
+        const double huu = sub_adjoint_curv(m, scr, cvr, lmn, sa);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) jl_[i] = 0.0;
+        if (uon) {
+            const LmSub mr = m;
+#pragma unroll 1
+            for (int d = 0; d < 5; ++d)
+                jl_[d] = sub_direction(mr, scr, cvr, huu, LM_G * ca, d, lmn, Mk, Hk, d < 4 ? cadd4[d] : cadd_u);
+        }
+    };
+    // incoming augmented defects g_k of node k from x+ of every node (as at the top of the loop)
+    auto incoming = [&](const double* xx, double ppv, double uu, const double* xn_, double* g) {
+        double cdef[5];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { const double t = from_next(xx[i]); cdef[i] = xn_[i] - t; }
+        { const double t0 = from_next(ppv); cdef[4] = uu - t0; }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const double t = from_prev(cdef[i]);
+            g[i] = k == 0 ? (i < 4 ? xx[i] - st0[i] : ppv - upv) : -t;
+        }
+    };
+    // IPOPT's primal-dual system error at mu (l1 norms of the scaled primal infeasibility, the dual
+    // infeasibility and z s - mu, added; IpoptCalculatedQuantities::curr_primal_dual_system_error) at
+    // (xx, ppv, uu) with multipliers lm, zlv, zuv.  Overwrites M~ / H~.
+    auto pd_l1 = [&](const double* xx, double ppv, double uu, const double* lm, double zlv, double zuv) {
+        double lmn[5], jl_[5], xn_[4], g[5], gl[6];
+        const double c0z[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < 5; ++i) { const double t = from_next(lm[i]); lmn[i] = uon ? t : 0.0; }
+        deriv_pass(xx, uu, lmn, c0z, 0.0, jl_, xn_);
+        incoming(xx, ppv, uu, xn_, g);
+        double tot = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tot += xon ? dsc[i] * fabs(g[i]) : 0.0;
+        tot += xon ? fabs(g[4]) : 0.0;
+        cost_grad(xx, uu, ppv, gl);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) gl[j] *= sc;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) gl[i] += lm[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gl[j] -= jl_[j];
+        gl[5] -= jl_[4] + lmn[4] + zlv - zuv;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) tot += ((j < 5) ? xon : uon) ? fabs(gl[j]) : 0.0;
+        tot += uon ? fabs(zlv * (uu - lo) - mu) + fabs(zuv * (hi - uu) - mu) : 0.0;
+        return wsum(tot);
+    };
+
+    for (it = it_start;; ++it) {
         const bool lsm = it < 0;
+        // the iteration-start values a hand-off parks (the rest of the state changes only on acceptance)
+        const double mu_it = mu, dl_it = delta_last;
+        const int nfilt_it = nfilt, acc_it = acc_count;
         // ---------------- derivatives, residuals, optimality error ---------------------------
         const double isl = uon ? frcp(u - lo) : 0.0, isu = uon ? frcp(hi - u) : 0.0;
         double lamn[5];
@@ -595,7 +816,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             const double cmu = fmax(c0 - mu, mu - cminw);
             if (fmax(dinf * is_d, fmax(pinf, cmu * is_c)) > 10.0 * mu || mu <= mu_min) break;
             mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
-            nfilt = 0;
+            nfilt = 0; in_soft = 0;       // BacktrackingLineSearch::Reset: the filter and the soft phase
         }
         const double tau = fmax(0.99, 1.0 - mu);
         STAMP(1);
@@ -664,9 +885,12 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             node_multiplier_s(S, xon ? sl : hf * LM_NMAXS, dxl, uon ? d0 : 0.0, lmp);
             // constr_mult_init_max on IPOPT's (row-scaled) multipliers of the reference's rows
             double ym = 0.0;
+            bool fin = true;        // an overflowed recursion (stiff, unstable dynamics) counts as too large
 #pragma unroll
             for (int i = 0; i < 4; ++i) ym = fmax(ym, xon ? fabs(lmp[i]) * frcp(dsc[i]) : 0.0);
-            if (wmax(ym) <= a.mult_init_max) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) fin = fin && (!xon || isfinite(lmp[i]));
+            if (!wany(!fin) && wmax(ym) <= a.mult_init_max) {
 #pragma unroll
                 for (int i = 0; i < 5; ++i) lam[i] = xon ? lmp[i] : 0.0;
             }
@@ -824,7 +1048,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 al_try = primal_ftb();
             }
             bool resolve = false;
-            for (;;) {
+            for (; !in_soft;) {
                 trial(al_try);
                 if (soc < 0) {
                     if (tiny) { accepted = true; ftype = true; break; }
@@ -873,8 +1097,533 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         if (!ok) { status = -3; break; }
         STAMP_ADD(10, ls + 1);
         STAMP(7);
+        // ---------------- IPOPT's soft restoration phase (BacktrackingLineSearch::TrySoftRestoStep) ------
+        // the line search failed, or the soft phase is on: the primal-dual step damped only by the
+        // fractions to the boundary (one length for x, lambda and z) is taken if the original filter
+        // accepts it with alpha_primal_test = 0 (the phase ends) or if it cuts the primal-dual system
+        // error at mu by the factor 0.9999; at most max_soft_resto_iters = 10 steps
+        if constexpr (!RESTO) {
+            if (!accepted && a.resto) {
+                // hand-off to lmpc_ipm_kernel<true>: the state of this iteration's start to HBM
+                double* st = a.resto_buf + ((size_t)b * kWave + lane) * kLmNst;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) st[i] = x[i];
+                st[4] = up; st[5] = u;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) st[6 + i] = lam[i];
+                st[11] = zl; st[12] = zu; st[13] = fth; st[14] = fph;
+                st[15] = lane == 0 ? mu_it : lane == 1 ? theta : lane == 2 ? dl_it : lane == 3 ? (double)it
+                       : lane == 4 ? (double)nfilt_it : (double)acc_it;
+                status = kLmNeedResto;
+                break;
+            }
+        }
+        bool soft = false;
+        if (RESTO && !accepted) {
+            if (!in_soft) {         // PrepareRestoPhaseStart: the current point enters the filter
+                if (nfilt < kWave) {
+                    if (lane == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
+                    ++nfilt;
+                }
+                soft_count = 0;
+            }
+            if (!(in_soft && ++soft_count > 10)) {
+                const double as = fmin(amax, az);
+                trial(as);
+                bool ft = false;
+                const bool orig = acceptable(0.0, ft);
+                bool take = orig;
+                if (!take && isfinite(ph_t)) {
+                    double pd0 = 0.0, pd1 = 0.0;
+#pragma unroll 1
+                    for (int pass = 0; pass < 2; ++pass) {
+                        const double al = pass ? as : 0.0;
+                        double xx[4], lm[5];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) xx[i] = fma(al, dx[i], x[i]);
+#pragma unroll
+                        for (int i = 0; i < 5; ++i) lm[i] = fma(al, lamp[i] - lam[i], lam[i]);
+                        const double e = pd_l1(xx, fma(al, dx[4], up), uon ? fma(al, dU, u) : u, lm, fma(al, dzl, zl),
+                                               fma(al, dzu, zu));
+                        if (pass) pd1 = e; else pd0 = e;
+                    }
+                    take = pd1 <= 0.9999 * pd0;
+                }
+                if (take) {
+                    accepted = true; soft = true; alpha = as; az = as;
+                    in_soft = orig ? 0 : 1;
+                    if (orig) soft_count = 0;
+                }
+            }
+        }
+        // ---------------- IPOPT's restoration phase (MinC_1NrmRestorationPhase) -------------------------
+        // (oracle/lmpc_ipm.c `restoration`; the soft-row Riccati sweep above).  rho 1000, eta = sqrt(mu_R),
+        // D_R = 1 / max(1, |x_R|); start mu_R = max(mu, ||d c||_inf), closed-form p, n, z_p = mu_R / p,
+        // z_n = mu_R / n, u-bound multipliers min(rho, z), least-square equality multipliers; its own
+        // filter, mu, inertia correction and second-order correction; leaves when the original problem's
+        // theta falls to 0.9 of its start value and the original filter accepts the point.
+        if (RESTO && !accepted) {
+            const double mu0 = mu, th0 = theta, phi0 = phi, tau0 = tau, rho = 1000.0;
+            double xr[4], drx[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { xr[i] = x[i]; drx[i] = 1.0 / fmax(1.0, fabs(x[i])); }
+            const double ur = u, dru = 1.0 / fmax(1.0, fabs(u));
+            double g0[5];
+            defects(x, up, u, g0);
+            double cmx = 0.0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cmx = fmax(cmx, xon ? dsc[i] * fabs(g0[i]) : 0.0);
+            cmx = fmax(cmx, xon ? fabs(g0[4]) : 0.0);
+            double rmu = fmax(mu0, wmax(cmx));
+            double eta = sqrt(rmu);
+            double pc[4], nc[4], zp[4], zn[4], rp[4], rn[4], sp[4], sn[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const double c = dsc[i] * g0[i];
+                const double aa = rmu / (2.0 * rho) - 0.5 * c, bb = c * rmu / (2.0 * rho);
+                nc[i] = xon ? aa + sqrt(aa * aa + bb) : 1.0;
+                pc[i] = xon ? c + nc[i] : 1.0;
+                zp[i] = xon ? rmu / pc[i] : 0.0;
+                zn[i] = xon ? rmu / nc[i] : 0.0;
+            }
+            double rzl = uon ? fmin(rho, zl) : 0.0, rzu = uon ? fmin(rho, zu) : 0.0;
+            double rl[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+            double jl[5], xn[4], lmn[5];
+            // H~ of the restoration problem: the dynamics Hessian (derivative pass, cadd = 0), then eta D_R^2
+            // and Sigma_u on the diagonal; no Delta-u cost
+            auto stage = [&]() {
+#pragma unroll
+                for (int i = 0; i < 5; ++i) { const double t = from_next(rl[i]); lmn[i] = uon ? t : 0.0; }
+                const double c0z[4] = {0.0, 0.0, 0.0, 0.0};
+                deriv_pass(x, u, lmn, c0z, 0.0, jl, xn);
+                if (uon) { Hk[hp(4, 4)] = 0.0; Hk[hp(5, 4)] = 0.0; }
+            };
+            // gradient rows of the stage QPs and the terminal surrogate (lsq: unit weights)
+            auto grad_rows = [&](bool lsq) {
+                if (uon) {
+                    const double isl = frcp(u - lo), isu = frcp(hi - u);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) Hk[hp(6, i)] = eta * drx[i] * drx[i] * (x[i] - xr[i]);
+                    Hk[hp(6, 4)] = 0.0;
+                    Hk[hp(6, 5)] = lsq ? fma(eta * dru * dru, u - ur, rzu - rzl)
+                                       : fma(eta * dru * dru, u - ur, rmu * isu - rmu * isl);
+                }
+                if (k == N) {
+                    double* GN = S->G[sl];
+                    for (int e = 0; e < LmLds::NTP; ++e) GN[e] = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        GN[gszz<5>(i, i)] = lsq ? 1.0 : eta * drx[i] * drx[i];
+                        GN[gszz<5>(5, i)] = eta * drx[i] * drx[i] * (x[i] - xr[i]);
+                    }
+                    GN[hp(5, 5)] = 1.0;
+                }
+            };
+            // soft rows of node k's incoming physical rows (Sigma + delta, 1 / D) and the right-hand
+            // side from the constraint values cv: rg = cv / d - (rn / Sn - rp / Sp) / d + D lambda
+            // (copy row: cv), into the defect column of M~ and dx~_0
+            auto soft_rows = [&](double delta, bool lsq, const double* cv) {
+                double rg[5];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const double d = dsc[i];
+                    sp[i] = lsq ? 1.0 : zp[i] / pc[i] + delta;
+                    sn[i] = lsq ? 1.0 : zn[i] / nc[i] + delta;
+                    const double Dd = (1.0 / sp[i] + 1.0 / sn[i]) / (d * d);
+                    RL->Dinv[sl][i] = 1.0 / Dd;
+                    rg[i] = cv[i] / d - (rn[i] / sn[i] - rp[i] / sp[i]) / d + Dd * rl[i];
+                }
+                rg[4] = cv[4];
+#pragma unroll
+                for (int r = 0; r < 5; ++r) {
+                    const double t = from_next(rg[r]);
+                    if (uon) Mk[6 * NC + r] = -t;
+                    if (k == 0) S->dx0[hf][r] = -rg[r];
+                }
+            };
+            // the step from the factorised soft system: dx~_0 and the closed-loop rows through the soft
+            // rows, forward sweep, du, lambda+
+            auto post_soft = [&](int slt, int) {
+                const double* T = RL->T[slt + 1];
+                double F[5][6];
+#pragma unroll
+                for (int r = 0; r < 5; ++r)
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) F[r][j] = S->F[slt][r][j];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) {
+                        double t = F[r][j] - (j == 5 ? T[6 * r + 5] : 0.0);
+#pragma unroll
+                        for (int aa = 0; aa < 5; ++aa) t -= T[6 * r + aa] * F[aa][j];
+                        S->F[slt][r][j] = t;
+                    }
+            };
+            double dxr[5], dUr = 0.0, lpr[5];
+            auto resto_step = [&]() {
+                if (k == 0) {
+                    double d0[5];
+#pragma unroll
+                    for (int r = 0; r < 5; ++r) d0[r] = S->dx0[hf][r];
+                    const double* T0 = RL->T[hf * LM_NMAXS];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        double t = d0[r] - T0[6 * r + 5];
+#pragma unroll
+                        for (int aa = 0; aa < 5; ++aa) t -= T0[6 * r + aa] * d0[aa];
+                        S->dx0[hf][r] = t;
+                    }
+                }
+                __syncthreads();
+                closed_loop_s(S, N, post_soft);
+                forward_sweep_s(S, N, k, dxr);
+                const double* K = S->KK[uon ? sl : hf * LM_NMAXS];
+                double d0 = K[5];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) d0 = fma(K[j], dxr[j], d0);
+                dUr = uon ? d0 : 0.0;
+                node_multiplier_s(S, xon ? sl : hf * LM_NMAXS, dxr, dUr, lpr);
+            };
+            // least-square equality multipliers of the restoration problem (unit weights on x, u, p, n:
+            // D = 2 / d^2, right-hand side (rp - rn) / d with rp = rho - z_p, rn = rho - z_n)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { rp[i] = rho - zp[i]; rn[i] = rho - zn[i]; }
+            {
+                stage();
+                if (uon) {
+                    for (int e = 0; e < LmLds::NTP; ++e) Hk[e] = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) Hk[hp(i, i)] = 1.0;
+                    Hk[hp(5, 5)] = 1.0;
+                }
+                grad_rows(true);
+                const double cz[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+                soft_rows(0.0, true, cz);
+                __syncthreads();
+                (void)riccati_s_sweep_soft(S, RL, N, RR);
+                resto_step();
+                double ym = 0.0;
+                bool fin = true;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) ym = fmax(ym, xon ? fabs(lpr[i]) / dsc[i] : 0.0);
+#pragma unroll
+                for (int i = 0; i < 5; ++i) fin = fin && (!xon || isfinite(lpr[i]));
+                const bool use = !wany(!fin) && wmax(ym) <= 1e3;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) rl[i] = (use && xon) ? lpr[i] : 0.0;
+            }
+            int rit = it + 1, rnf = 0, racc_count = 0, rstat = -2;
+            bool rfirst = true, rok = false;
+            double rfth = 0.0, rfph = 0.0, rdelta_last = 0.0, thr = 0.0, rth_max = 0.0, rth_min = 0.0;
+            double cres[5];
+            for (;; ++rit) {
+                stage();
+                double g[5];
+                incoming(x, up, u, xn, g);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cres[i] = xon ? dsc[i] * g[i] + nc[i] - pc[i] : 0.0;
+                cres[4] = xon ? g[4] : 0.0;
+                if (rfirst) {
+                    double t = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) t += fabs(cres[i]);
+                    thr = wsum(t);
+                    rth_max = 1e4 * fmax(1.0, thr); rth_min = 1e-4 * fmax(1.0, thr);
+                } else {
+                    // RestoConvergenceCheck: the original problem's progress at the current point
+                    const double tho = wsum(theta_of(g));
+                    if (tho <= 0.9 * th0) {
+                        double pl = sc * cost_val(x, u, up);
+                        if (uon) pl -= mu0 * log_fast((u - lo) * (hi - u));
+                        const double pho = wsum(pl);
+                        bool accp = isfinite(pho) && !wany(lane < nfilt && tho >= fth && pho >= fph);
+                        accp = accp && (cmp_le(tho, (1 - gam_th) * th0, th0) || cmp_le(pho - phi0, -gam_ph * th0, phi0));
+                        if (accp) { rok = true; theta = tho; break; }
+                    }
+                }
+                rfirst = false;
+                // optimality error of the restoration problem
+                double dinf = 0.0, pinf = 0.0, c0r = 0.0, cminr = 1e300, suml = 0.0, sumz = 0.0;
+                {
+                    double gl[6];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) gl[i] = eta * drx[i] * drx[i] * (x[i] - xr[i]) + rl[i] - jl[i];
+                    gl[4] = rl[4];
+                    gl[5] = eta * dru * dru * (u - ur) - jl[4] - lmn[4] - rzl + rzu;
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) dinf = fmax(dinf, ((j < 5) ? xon : uon) ? fabs(gl[j]) : 0.0);
+                    if (xon) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const double y = rl[i] / dsc[i];
+                            dinf = fmax(dinf, fmax(fabs(rho - zp[i] - y), fabs(rho - zn[i] + y)));
+                            pinf = fmax(pinf, fabs(cres[i]));
+                            c0r = fmax(c0r, fmax(zp[i] * pc[i], zn[i] * nc[i]));
+                            cminr = fmin(cminr, fmin(zp[i] * pc[i], zn[i] * nc[i]));
+                            sumz += zp[i] + zn[i];
+                            suml += fabs(y);
+                        }
+                        pinf = fmax(pinf, fabs(cres[4]));
+                        suml += fabs(rl[4]);
+                    }
+                    if (uon) {
+                        const double cl = rzl * (u - lo), cu = rzu * (hi - u);
+                        c0r = fmax(c0r, fmax(cl, cu)); cminr = fmin(cminr, fmin(cl, cu));
+                        sumz += rzl + rzu;
+                    }
+                    dinf = wmax(dinf); pinf = wmax(pinf); c0r = wmax(c0r); cminr = wmin(cminr);
+                    suml = wsum(suml); sumz = wsum(sumz);
+                }
+                const double nbr = 4.0 * N + 16.0 * (N + 1);
+                const double s_d = fmax(100.0, (suml + sumz) / (nA + nbr)) / 100.0;
+                const double s_c = fmax(100.0, sumz / nbr) / 100.0;
+                const double errr = fmax(dinf / s_d, fmax(pinf, c0r / s_c));
+                if (rit >= a.max_iter) { rstat = -1; break; }
+                if (errr <= tol && dinf <= 1.0 && pinf <= 1e-4 && c0r <= 1e-4) { rstat = -2; break; }   // local infeasibility
+                if (a.acc_iter > 0 && errr <= a.acc_tol && pinf <= 1e-2 && c0r <= 1e-2) {
+                    if (++racc_count >= a.acc_iter) { rstat = -2; break; }
+                } else {
+                    racc_count = 0;
+                }
+                for (;;) {
+                    const double cmu = fmax(c0r - rmu, rmu - cminr);
+                    if (fmax(dinf / s_d, fmax(pinf, cmu / s_c)) > 10.0 * rmu || rmu <= mu_min) break;
+                    rmu = fmax(mu_min, fmin(0.2 * rmu, rmu * sqrt(rmu)));
+                    eta = sqrt(rmu);
+                    rnf = 0;
+                }
+                const double taur = fmax(0.99, 1.0 - rmu);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    rp[i] = rho - rmu / pc[i] - rl[i] / dsc[i];
+                    rn[i] = rho - rmu / nc[i] + rl[i] / dsc[i];
+                }
+                const double isl = uon ? frcp(u - lo) : 0.0, isu = uon ? frcp(hi - u) : 0.0;
+                if (uon) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) Hk[hp(i, i)] += eta * drx[i] * drx[i];
+                    Hk[hp(5, 5)] += eta * dru * dru + rzl * isl + rzu * isu;
+                }
+                grad_rows(false);
+                double delta = 0.0, dapplied = 0.0;
+                int attempt = 0;
+                bool okr = false;
+                for (;;) {
+                    soft_rows(delta, false, cres);
+                    __syncthreads();
+                    okr = riccati_s_sweep_soft(S, RL, N, RR);
+                    if (okr || ++attempt >= 60) break;
+                    delta = (attempt == 1) ? (rdelta_last == 0.0 ? 1e-4 : fmax(1e-20, rdelta_last * (1.0 / 3.0)))
+                                           : delta * (rdelta_last == 0.0 ? 100.0 : 8.0);
+                    const double dd = delta - dapplied;
+                    if (uon) {
+#pragma unroll
+                        for (int j = 0; j < 6; ++j) Hk[hp(j, j)] += dd;
+                    }
+                    if (k == N) {
+#pragma unroll
+                        for (int j = 0; j < 5; ++j) S->G[sl][gszz<5>(j, j)] += dd;
+                    }
+                    dapplied = delta;
+                }
+                if (!okr) { rstat = -3; break; }
+                if (delta > 0.0) rdelta_last = delta;
+                // the step of p, n and every bound multiplier, and the fractions to the boundary
+                double dpc[4], dnc[4], dzp[4], dzn[4], dzlr = 0.0, dzur = 0.0, amr = 1.0, azr = 1.0;
+                auto pn_steps = [&]() {
+                    double am = 1.0, a2 = 1.0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const double dy = (lpr[i] - rl[i]) / dsc[i];
+                        dpc[i] = xon ? (dy - rp[i]) / sp[i] : 0.0;
+                        dnc[i] = xon ? (-dy - rn[i]) / sn[i] : 0.0;
+                        dzp[i] = xon ? rmu / pc[i] - zp[i] - zp[i] / pc[i] * dpc[i] : 0.0;
+                        dzn[i] = xon ? rmu / nc[i] - zn[i] - zn[i] / nc[i] * dnc[i] : 0.0;
+                        if (dpc[i] < 0) am = fmin(am, -taur * pc[i] / dpc[i]);
+                        if (dnc[i] < 0) am = fmin(am, -taur * nc[i] / dnc[i]);
+                        if (dzp[i] < 0) a2 = fmin(a2, -taur * zp[i] / dzp[i]);
+                        if (dzn[i] < 0) a2 = fmin(a2, -taur * zn[i] / dzn[i]);
+                    }
+                    dzlr = uon ? rmu * isl - rzl - rzl * isl * dUr : 0.0;
+                    dzur = uon ? rmu * isu - rzu + rzu * isu * dUr : 0.0;
+                    if (uon) {
+                        if (dUr < 0) am = fmin(am, -taur * (u - lo) / dUr);
+                        if (dUr > 0) am = fmin(am, taur * (hi - u) / dUr);
+                        if (dzlr < 0) a2 = fmin(a2, -taur * rzl / dzlr);
+                        if (dzur < 0) a2 = fmin(a2, -taur * rzu / dzur);
+                    }
+                    amr = wmin(am); azr = wmin(a2);
+                };
+                resto_step();
+                pn_steps();
+                // barrier objective of the restoration problem and its directional derivative
+                double phir, gtdr;
+                {
+                    double pl = 0.0, gd = 0.0;
+                    if (xon) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const double e = drx[i] * (x[i] - xr[i]);
+                            pl += rho * (pc[i] + nc[i]) + 0.5 * eta * e * e - rmu * (log(pc[i]) + log(nc[i]));
+                            gd += eta * drx[i] * e * dxr[i] + (rho - rmu / pc[i]) * dpc[i] + (rho - rmu / nc[i]) * dnc[i];
+                        }
+                    }
+                    if (uon) {
+                        const double e = dru * (u - ur);
+                        pl += 0.5 * eta * e * e - rmu * (log(u - lo) + log(hi - u));
+                        gd += (eta * dru * e - rmu * isl + rmu * isu) * dUr;
+                    }
+                    phir = wsum(pl); gtdr = wsum(gd);
+                }
+                double aminr = gam_th;
+                if (gtdr < 0) aminr = fmin(gam_th, fmin(gam_ph * thr / (-gtdr), pow(thr, s_th) / pow(-gtdr, s_ph)));
+                aminr *= gam_al;
+                double ct[5], pct[4], nct[4];
+                double tht = 0.0, pht = 0.0;
+                auto trial_r = [&](double al) {
+                    double xt[4], gt_[5];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) xt[i] = fma(al, dxr[i], x[i]);
+                    const double pt = fma(al, dxr[4], up), ut = uon ? fma(al, dUr, u) : u;
+                    defects(xt, pt, ut, gt_);
+                    double thl = 0.0, phl = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        pct[i] = fma(al, dpc[i], pc[i]); nct[i] = fma(al, dnc[i], nc[i]);
+                        ct[i] = xon ? dsc[i] * gt_[i] + nct[i] - pct[i] : 0.0;
+                        const double e = drx[i] * (xt[i] - xr[i]);
+                        if (xon) {
+                            thl += fabs(ct[i]);
+                            phl += (pct[i] > 0.0 && nct[i] > 0.0)
+                                       ? rho * (pct[i] + nct[i]) + 0.5 * eta * e * e - rmu * (log(pct[i]) + log(nct[i]))
+                                       : __builtin_inf();
+                        }
+                    }
+                    ct[4] = xon ? gt_[4] : 0.0;
+                    thl += fabs(ct[4]);
+                    if (uon) {
+                        const double e = dru * (ut - ur);
+                        phl += (ut > lo && ut < hi) ? 0.5 * eta * e * e - rmu * (log(ut - lo) + log(hi - ut)) : __builtin_inf();
+                    }
+                    wsum2(thl, phl);
+                    tht = thl; pht = phl;
+                };
+                auto racc = [&](double al_test, bool& ft) {
+                    const bool in_f = !(tht < rth_max) || !isfinite(pht) || wany(lane < rnf && tht >= rfth && pht >= rfph);
+                    if (in_f) return false;
+                    const bool sw = gtdr < 0.0 && al_test * pow(-gtdr, s_ph) > pow(thr, s_th);
+                    if (thr <= rth_min && sw) {
+                        if (cmp_le(pht, phir + eta_ph * al_test * gtdr, phir)) { ft = true; return true; }
+                        return false;
+                    }
+                    return cmp_le(tht, (1 - gam_th) * thr, thr) || cmp_le(pht - phir, -gam_ph * thr, phir);
+                };
+                double alr = amr;
+                bool accr = false, ftr = false;
+                for (int ls = 0; ls < 80 && !accr; ++ls) {
+                    if (alr < aminr && ls > 0) break;
+                    trial_r(alr);
+                    accr = racc(alr, ftr);
+                    if (!accr && ls == 0 && !(tht < thr) && a.max_soc > 0) {
+                        // second-order correction on the restoration problem's constraints; the plain step
+                        // is parked in LDS
+                        if (xon) {
+                            double* sv = RL->SV[sl];
+#pragma unroll
+                            for (int i = 0; i < 5; ++i) { sv[i] = dxr[i]; sv[5 + i] = lpr[i]; }
+                            sv[10] = dUr;
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) { sv[11 + i] = dpc[i]; sv[15 + i] = dnc[i]; }
+                        }
+                        double csoc[5], asoc = alr, th_old = 0.0;
+#pragma unroll
+                        for (int i = 0; i < 5; ++i) csoc[i] = cres[i];
+                        for (int c = 0; c < a.max_soc; ++c) {
+                            if (c > 0 && !(tht <= 0.99 * th_old)) break;
+                            th_old = tht;
+#pragma unroll
+                            for (int i = 0; i < 5; ++i) csoc[i] = fma(asoc, csoc[i], ct[i]);
+                            soft_rows(delta, false, csoc);
+                            __syncthreads();
+                            (void)riccati_s_sweep_soft(S, RL, N, RR);
+                            resto_step();
+                            pn_steps();
+                            asoc = amr;
+                            trial_r(asoc);
+                            bool ft2 = false;
+                            if (racc(alr, ft2)) { accr = true; ftr = ft2; alr = asoc; break; }
+                        }
+                        if (!accr) {        // back to the plain step
+                            if (xon) {
+                                const double* sv = RL->SV[sl];
+#pragma unroll
+                                for (int i = 0; i < 5; ++i) { dxr[i] = sv[i]; lpr[i] = sv[5 + i]; }
+                                dUr = sv[10];
+                            }
+                            pn_steps();
+                        }
+                    }
+                    if (!accr) alr *= 0.5;
+                }
+                if (!accr) { rstat = -2; break; }      // a failed line search in the restoration phase
+                if (!ftr && rnf < kWave) {
+                    if (lane == rnf) { rfth = (1 - gam_th) * thr; rfph = phir - gam_ph * thr; }
+                    ++rnf;
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[i] = xon ? fma(alr, dxr[i], x[i]) : x[i];
+                up = xon ? fma(alr, dxr[4], up) : up;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) rl[i] = xon ? fma(alr, lpr[i] - rl[i], rl[i]) : 0.0;
+                if (xon) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        pc[i] = pct[i]; nc[i] = nct[i];
+                        zp[i] = fmax(fmin(fma(azr, dzp[i], zp[i]), 1e10 * rmu / pc[i]), rmu / (1e10 * pc[i]));
+                        zn[i] = fmax(fmin(fma(azr, dzn[i], zn[i]), 1e10 * rmu / nc[i]), rmu / (1e10 * nc[i]));
+                    }
+                }
+                if (uon) {
+                    u = fma(alr, dUr, u);
+                    const double sl_ = u - lo, su_ = hi - u;
+                    rzl = fmax(fmin(fma(azr, dzlr, rzl), 1e10 * rmu / sl_), rmu / (1e10 * sl_));
+                    rzu = fmax(fmin(fma(azr, dzur, rzu), 1e10 * rmu / su_), rmu / (1e10 * su_));
+                }
+                thr = tht;
+            }
+            if (!rok) { status = rstat; it = rit; break; }
+            // back to the original problem: the u-bound multipliers take the step (mu - z s_trial) / s that
+            // pretends the restoration's progress was one Newton step, cut by the fraction to the boundary
+            // (tau of the original iteration) and reset to 1 above 1000; the equality multipliers restart at 0
+            {
+                double dzlo = 0.0, dzuo = 0.0, a2 = 1.0;
+                if (uon) {
+                    const double slo = ur - lo, suo = hi - ur;
+                    dzlo = (mu0 - zl * (u - lo)) / slo;
+                    dzuo = (mu0 - zu * (hi - u)) / suo;
+                    if (dzlo < 0) a2 = fmin(a2, -tau0 * zl / dzlo);
+                    if (dzuo < 0) a2 = fmin(a2, -tau0 * zu / dzuo);
+                }
+                const double azo = wmin(a2);
+                if (uon) { zl = fma(azo, dzlo, zl); zu = fma(azo, dzuo, zu); }
+                const bool reset = wmax(uon ? fmax(zl, zu) : 0.0) > 1e3;
+                if (uon) {
+                    if (reset) { zl = 1.0; zu = 1.0; }
+                    const double il = frcp(u - lo), iu = frcp(hi - u);
+                    zl = fmax(fmin(zl, 1e10 * mu0 * il), 1e-10 * mu0 * il);
+                    zu = fmax(fmin(zu, 1e10 * mu0 * iu), 1e-10 * mu0 * iu);
+                }
+#pragma unroll
+                for (int i = 0; i < 5; ++i) lam[i] = 0.0;
+            }
+            in_soft = 0; soft_count = 0;
+            it = rit - 1;
+            STAMP(8);
+            continue;
+        }
         if (!accepted) { status = -2; break; }
-        if (!ftype && nfilt < kWave) {
+        if (!soft && !ftype && nfilt < kWave) {
             if (lane == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
             ++nfilt;
         }
@@ -916,6 +1665,7 @@ extern "C" size_t dartmpc_lmpc_lds_bytes(void) { return dartmpc::kLmLdsBytes; }
 extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStream_t stream) {
     if (args->B <= 0) return hipSuccess;
     if (args->N < 1 || args->N >= dartmpc::LM_NMAXS) return hipErrorInvalidValue;
+    if (args->resto && !args->resto_buf) return hipErrorInvalidValue;
     // the dynamic-LDS opt-in is per device: set once for every device a launch goes to (thread-safe)
     static std::mutex mu;
     static bool attr_set[64] = {};
@@ -927,8 +1677,11 @@ extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStre
     {
         std::lock_guard<std::mutex> g(mu);
         if (!attr_set[dev]) {
-            e = hipFuncSetAttribute((const void*)dartmpc::lmpc_ipm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds);
+            e = hipFuncSetAttribute((const void*)dartmpc::lmpc_ipm_kernel<false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)dartmpc::lmpc_ipm_kernel<true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
             attr_set[dev] = true;
         }
@@ -936,8 +1689,12 @@ extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStre
     dartmpc::LmpcArgs a = *args;
     a.pack = (a.B <= 32) ? 8 : 1;            // one XCD (and its L2) for the code of a small batch
     // the policy prologue's LDS only when the launch runs it (the opt-in above covers the maximum)
-    const size_t lds_launch = a.fuse_policy ? lds : sizeof(dartmpc::LmShared);
-    hipLaunchKernelGGL(dartmpc::lmpc_ipm_kernel, dim3(a.B * a.pack), dim3(dartmpc::kWave), lds_launch, stream, a);
+    const size_t lds_launch = a.fuse_policy ? dartmpc::kLmPolicyLdsOff + sizeof(dartmpc::PolicyLds) : sizeof(dartmpc::LmShared);
+    hipLaunchKernelGGL(dartmpc::lmpc_ipm_kernel<false>, dim3(a.B * a.pack), dim3(dartmpc::kWave), lds_launch, stream, a);
+    // IPOPT's restoration phases for the instances the first launch handed off (the others return at once)
+    if (a.resto)
+        hipLaunchKernelGGL(dartmpc::lmpc_ipm_kernel<true>, dim3(a.B * a.pack), dim3(dartmpc::kWave),
+                           dartmpc::kLmRestoOff + sizeof(dartmpc::LmResto), stream, a);
     return hipGetLastError();
 }
 

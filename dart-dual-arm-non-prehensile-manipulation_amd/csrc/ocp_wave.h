@@ -478,9 +478,14 @@ __device__ bool riccati_s_sweep(L* S, int N, const RiccatiSRoles& R) {
     return !wany(!ok);
 }
 
-// [K | k] = -Guz / Quu and [Phi | f] of every node, lane 32 h + k per node (k < N).  Ends with a barrier.
-template <class L>
-__device__ void closed_loop_s(L* S, int N) {
+struct NoPost {
+    __device__ void operator()(int, int) const {}
+};
+// [K | k] = -Guz / Quu and [Phi | f] of every node, lane 32 h + k per node (k < N); post(slot, k) then
+// runs on each node's lane before the pair maps are composed (the LMPC restoration phase maps the rows
+// through its soft defect rows there).  Ends with a barrier.
+template <class L, class Post = NoPost>
+__device__ void closed_loop_s(L* S, int N, Post post = Post()) {
     constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND;
     const int k = threadIdx.x & 31, sl = (threadIdx.x >> 5) * L::NMAXS + k;
     if (k < N) {
@@ -508,6 +513,7 @@ __device__ void closed_loop_s(L* S, int N) {
             for (int j = 0; j < NXA; ++j) S->F[sl][r][j] = fma(bq, K[j], mk[j][r]);
             S->F[sl][r][NXA] = fma(bq, K[NXA], mk[NXA + 1][r]);
         }
+        post(sl, k);
     }
     __syncthreads();
     compose_pairs<2, L::NMAXS, NXA, 3>(S->F, S->F2, N);   // 2 x 2 x N / 2 tasks: one round

@@ -35,7 +35,7 @@ EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch",
            "dart_arm_solve_batch_dev", "dart_set_device", "dart_mpc_serve_start", "dart_mpc_serve_stop",
            "dart_mpc_serve_running", "dart_mpc_bind", "dart_mpc_solve_bound")
 VARIANT_PMPC, VARIANT_RMPC, VARIANT_LMPC = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class DartMPCError(RuntimeError):
@@ -48,7 +48,7 @@ class Config(ctypes.Structure):
                 ("tol", ctypes.c_double), ("max_iter", ctypes.c_int32), ("B_max", ctypes.c_int32),
                 ("gravity", ctypes.c_double), ("acceptable_tol", ctypes.c_double),
                 ("acceptable_iter", ctypes.c_int32), ("max_soc", ctypes.c_int32), ("pmpc_path", ctypes.c_int32),
-                ("constr_mult_init_max", ctypes.c_double)]
+                ("restoration", ctypes.c_int32), ("constr_mult_init_max", ctypes.c_double)]
 
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -435,16 +435,18 @@ LMPC_PRM_DEFAULT = np.array([200.0, 2.0, 200.0, 2.0, 0.0, 0.0, 0.0, 0.0,     # Q
 class LmpcSolver(Solver):
     """``dart_mpc_handle`` of variant LMPC, N <= 31.  Defaults are the reference's IPOPT options
     (LMPC/src/controller/rlmpc2.py:480-489): max_iter 50, tol 1e-4, acceptable_tol 1e-3,
-    acceptable_iter 5, and IPOPT's defaults max_soc 4 (second-order correction; 0 = off) and
-    constr_mult_init_max 1000 (least-square starting multipliers; 0 = start from 0)."""
+    acceptable_iter 5, and IPOPT's defaults max_soc 4 (second-order correction; 0 = off),
+    constr_mult_init_max 1000 (least-square starting multipliers; 0 = start from 0) and its soft
+    restoration / restoration phases after a failed line search (restoration=False: status -2 there)."""
 
     def __init__(self, N=20, Ts=0.002, tol=1e-4, max_iter=50, acceptable_tol=1e-3, acceptable_iter=5,
-                 B_max=1024, device=0, max_soc=4, constr_mult_init_max=1000.0):
+                 B_max=1024, device=0, max_soc=4, constr_mult_init_max=1000.0, restoration=True):
         self._h = ctypes.c_void_p()
         self.cfg = default_config(variant=VARIANT_LMPC, N=int(N), Ts=float(Ts), tol=float(tol), max_iter=int(max_iter),
                                   B_max=int(B_max), acceptable_tol=float(acceptable_tol),
                                   acceptable_iter=int(acceptable_iter), max_soc=int(max_soc),
-                                  constr_mult_init_max=float(constr_mult_init_max))
+                                  constr_mult_init_max=float(constr_mult_init_max),
+                                  restoration=int(bool(restoration)))
         rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
         if rc != 0:
             raise DartMPCError(f"dart_mpc_create(LMPC) failed with code {rc} (no gfx950 device or bad config)")

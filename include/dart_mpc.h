@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define DART_MPC_ABI_VERSION 5
+#define DART_MPC_ABI_VERSION 6
 
 enum dart_mpc_variant {
     DART_MPC_PMPC = 0,      /* PMPC/src/controller/mpc_3d.py, N <= 63 */
@@ -107,6 +107,9 @@ typedef struct dart_mpc_config {
                            defect rows of mpc_3d.py:37, :48 in theta, the filter, the error measures and
                            the second-order correction); 1 = the reduced (x, y) path, opt-in: same KKT
                            point to the tolerance, fewer iterations, but not IPOPT's iterates */
+    int32_t restoration;  /* LMPC (ABI 6): 1 = IPOPT's soft restoration and restoration phases after a
+                           failed filter line search (default; MinC_1NrmRestorationPhase, the fallback of
+                           every nlpsol call, rlmpc2.py:480-489); 0 = stop with status -2 there */
     double constr_mult_init_max;  /* IPOPT constr_mult_init_max (default 1000): the starting equality
                            multipliers are IPOPT's least-square estimate unless its max norm exceeds this
                            (then 0); 0 = always start from 0.  Used by PMPC, RMPC and LMPC */

@@ -896,7 +896,10 @@ static int restoration(const ctx_t *C0, work_t *W, int *it_io, int max_iter, dou
         resto_rhs(&C, V, cres, rg);       /* rg = -(rn - rp)/d: D lam = 0, Sp = Sn = 1 */
         riccati_solve(&C, V, rg);
         double ym = 0.0;
-        for (int r = 0; r < nA; ++r) if ((r % NA) < 8) ym = fmax(ym, fabs(V->lamp[r]) / W->dsc[r]);
+        for (int r = 0; r < nA; ++r) {
+            if ((r % NA) < 8) ym = fmax(ym, fabs(V->lamp[r]) / W->dsc[r]);
+            if (!isfinite(V->lamp[r])) ym = INFINITY;
+        }
         if (ym <= 1e3) memcpy(V->lam, V->lamp, sizeof(double) * nA);
         else memset(V->lam, 0, sizeof(double) * nA);
         C.mode = 1;
@@ -922,7 +925,7 @@ static int restoration(const ctx_t *C0, work_t *W, int *it_io, int max_iter, dou
         double dinf, pinf, c0, cmin, sum_l, sum_z;
         resto_errors(&C, V, cres, &dinf, &pinf, &c0, &cmin, &sum_l, &sum_z);
         const double nb = 2.0 * nU + 2.0 * nrow;
-        const double s_d = fmax(s_max, (sum_l + sum_z) / (nA + 2.0 * nrow + nb)) / s_max;
+        const double s_d = fmax(s_max, (sum_l + sum_z) / (nA + nb)) / s_max;     /* rows + bound multipliers */
         const double s_c = fmax(s_max, sum_z / nb) / s_max;
         const double err = fmax(dinf / s_d, fmax(pinf, c0 / s_c));
         if (rit >= max_iter) { *status = ST_MAXITER; break; }
@@ -1128,6 +1131,9 @@ static int restoration(const ctx_t *C0, work_t *W, int *it_io, int max_iter, dou
         }
         *it_io = rit - 1;
     } else {
+        /* IPOPT copies the restoration phase's last iterate into the original problem's fields on failure */
+        memcpy(W->X, V->X, sizeof(double) * nA);
+        memcpy(W->U, V->U, sizeof(double) * nU);
         *it_io = rit;
     }
     free(g); free(gt); free(cres); free(ct); free(csg); free(rg); free(sv);

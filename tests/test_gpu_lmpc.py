@@ -94,12 +94,11 @@ def test_horizons(dm, N):
     s.close()
     ref = oracle_lib.lmpc_solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"], N=N, tol=1e-10, acc_iter=0,
                                       max_iter=500, nthreads=4)
-    # seed 3 holds an instance (#15) on which IPOPT's line search fails from the cold start (it would
-    # enter its restoration phase, which neither the oracle nor the kernel restates): the kernel must
-    # fail exactly where the oracle fails, at the same iteration, and agree everywhere else
+    # seed 3 holds an instance (#15) on which IPOPT's filter line search fails from the cold start: kernel
+    # and oracle both go through IPOPT's restoration phase there and must come out on the same path
     assert np.array_equal(out["status"], ref["status"]), (out["status"], ref["status"])
+    assert np.array_equal(out["iters"], ref["iters"]), (out["iters"], ref["iters"])
     ok = ref["status"] == 0
-    assert np.array_equal(out["iters"][~ok], ref["iters"][~ok])
     nX = 8 * (N + 1)
     assert np.max(np.abs(out["w"][ok][:, nX:] - ref["w"][ok][:, nX:])) <= 1e-6
 
@@ -119,8 +118,8 @@ def test_reference_options_same_path_as_oracle(dm, max_soc):
     loose iterate, so the comparison is path-level.  With IPOPT's default second-order correction
     (max_soc 4) the kernel follows the oracle with SOC on; with max_soc 0 the oracle with SOC off.
     Either way the kernel takes the same number of iterations, ends with the same status and returns
-    the same control (|du0| <= 1e-6) on 360 C5 instances, among them instances where the correction
-    changes IPOPT's answer by up to 0.27 rad."""
+    the same control (|du0| <= 1e-6) on 360 C5 instances, among them four on which the correction changes
+    IPOPT's path (without the restoration phase, one of them ends 0.27 rad away)."""
     from dart_mpc.workload import lmpc_batch
     D = lmpc_batch(20, seed0=7000)
     s = dm.LmpcSolver(N=30, B_max=512, max_soc=max_soc)
@@ -129,10 +128,14 @@ def test_reference_options_same_path_as_oracle(dm, max_soc):
     args = (D["state"], D["u_prev"], D["pvec"], D["target"])
     o = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=8, soc=max_soc > 0)
     other = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=8, soc=max_soc == 0)
-    assert np.max(np.abs(o["u0"] - other["u0"])) > 1e-3     # the batch exercises the correction
+    assert np.sum(o["iters"] != other["iters"]) >= 3        # the batch exercises the correction
     assert np.array_equal(g["status"], o["status"])
     assert np.array_equal(g["iters"], o["iters"])
-    assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6
+    # two instances run into max_iter after six restoration phases each (delta up to 1e3, steps of 1e-6):
+    # on such a path rounding decides where the 50th iterate lands, so u0 is compared where IPOPT converged
+    conv = o["status"] >= 0
+    assert conv.sum() >= 355
+    assert np.max(np.abs(g["u0"][conv] - o["u0"][conv])) <= 1e-6
 
 
 @pytest.mark.parametrize("mult_init", [1000.0, 0.0])
@@ -154,3 +157,27 @@ def test_least_square_starting_multipliers_same_path(dm, mult_init):
     assert np.array_equal(g["status"], o["status"])
     assert np.array_equal(g["iters"], o["iters"])
     assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6
+
+
+@pytest.mark.parametrize("resto", [True, False])
+def test_restoration_phase_same_path_as_oracle(dm, resto):
+    """The cold-started C5 batch of 720 instances (reference options, N = 30): IPOPT's filter line search
+    fails on five of them.  With IPOPT's soft restoration and restoration phases (the default) the kernel
+    (lmpc_ipm_kernel<false> hands those instances to lmpc_ipm_kernel<true>) follows the oracle through
+    them -- same statuses and iteration counts everywhere, |du0| <= 1e-6 -- and no instance ends with
+    status -2; with the phases off both stop with -2 on exactly those five."""
+    from dart_mpc.workload import lmpc_batch
+    D = lmpc_batch(40, seed0=0)
+    args = (D["state"], D["u_prev"], D["pvec"], D["target"])
+    s = dm.LmpcSolver(N=30, B_max=1024, restoration=resto)
+    g = s.solve_batch(*args)
+    s.close()
+    o = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=8, want_w=False, resto=resto)
+    assert np.array_equal(g["status"], o["status"]), (np.where(g["status"] != o["status"]), g["status"][g["status"] != o["status"]], o["status"][g["status"] != o["status"]])
+    assert np.array_equal(g["iters"], o["iters"]), (np.where(g["iters"] != o["iters"]), g["iters"][g["iters"] != o["iters"]], o["iters"][g["iters"] != o["iters"]])
+    conv = o["status"] >= 0          # (the two max_iter instances: see test_reference_options_same_path_as_oracle)
+    assert np.max(np.abs(g["u0"][conv] - o["u0"][conv])) <= 1e-6
+    if resto:
+        assert not np.any(g["status"] == -2)
+    else:
+        assert np.sum(g["status"] == -2) == 5
