@@ -89,65 +89,20 @@ struct LmResto {
     NodeArr<double[4], 2 * LM_NMAXS> Dinv;    // 1 / D of node k's four physical incoming rows
     NodeArr<double[20], 2 * LM_NMAXS> SV;     // a second-order correction: the plain step
     double Gs[2][LmLds::NTP];                 // the surrogate of G_{k+1} (one per half)
+    double Pw[2][24];                         // soft transform: Pt(a, q), a < 4, of the node at hand
+    // per-node state of the restoration problem (node k's four physical incoming rows), kept in LDS
+    // rather than registers: p, n, z_p, z_n, rp, rn, Sigma_p', Sigma_n', x_R, D_R
+    NodeArr<double[40], 2 * LM_NMAXS> PN;
 };
-
-// Pt(a, q) rows a < 4 of the value function in G slot Gn, S = Pt(ph, ph) + diag(dinv) = L diag(dd) L^T
-// and T = S^-1 Pt(ph, :); returns S > 0.  gu / iq: Gzu and 1 / Quu of Gn.
-__device__ __forceinline__ bool soft_T(const double* Gn, const double* dinv, double (&T)[4][6], double (&gu)[6],
-                                       double& iq) {
-    constexpr int NXA = 5;
-#pragma unroll
-    for (int p = 0; p < 6; ++p) gu[p] = Gn[gszu<NXA>(p)];
-    iq = frcp(Gn[hp(NXA, NXA)]);
-    double Pp[4][6];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int q = 0; q < 6; ++q) Pp[a][q] = fma(-gu[a] * iq, gu[q], Gn[gszz<NXA>(a, q)]);
-    double L[4][4], dd[4], id[4];
-    bool ok = true;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        double t = Pp[j][j] + dinv[j];
-#pragma unroll
-        for (int m = 0; m < j; ++m) t -= L[j][m] * L[j][m] * dd[m];
-        dd[j] = t;
-        ok = ok && t > 0.0 && isfinite(t);
-        id[j] = frcp(t);
-#pragma unroll
-        for (int i = j + 1; i < 4; ++i) {
-            double u = Pp[i][j];
-#pragma unroll
-            for (int m = 0; m < j; ++m) u -= L[i][m] * L[j][m] * dd[m];
-            L[i][j] = u * id[j];
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-        double y[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            double t = Pp[i][q];
-#pragma unroll
-            for (int m = 0; m < i; ++m) t -= L[i][m] * y[m];
-            y[i] = t;
-        }
-#pragma unroll
-        for (int i = 3; i >= 0; --i) {
-            double t = y[i] * id[i];
-#pragma unroll
-            for (int m = i + 1; m < 4; ++m) t -= L[m][i] * T[m][q];
-            T[i][q] = t;
-        }
-    }
-    return ok;
-}
 
 // Backward sweep of both halves with soft physical rows (restoration phase): before the step of node
 // k, each half forms the surrogate of G_{k+1} seen through node k+1's soft rows (RL->Gs) and keeps
-// T_{k+1} for the forward map; T_0 of the soft initial rows comes last.  G[slot N] must hold the
-// terminal surrogate, RL->Dinv every node's 1 / D.  Returns false (wave-uniform) if some S or Quu is
-// not positive definite.
+// T_{k+1} for the forward map; T_0 of the soft initial rows comes last.  The transform of one node runs
+// in three lane-parallel phases of the half-wave: (1) lane e < 24 forms Pt(a, q) = Gzz - Gzu Gzu^T / Quu
+// for a = e / 6 < 4, q = e % 6; (2) lanes q < 6 factor S = Pt(ph, ph) + D^-1 = L diag(dd) L^T (each its
+// own copy) and solve column q of T = S^-1 Pt(ph, :); (3) every lane forms its packed surrogate entry
+// Pt(p, q) - Pt(p, ph) T(:, q).  G[slot N] must hold the terminal surrogate, RL->Dinv every node's 1 / D.
+// Returns false (wave-uniform) if some S or Quu is not positive definite.
 __device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const RiccatiSRoles& R) {
     constexpr int NXA = LmLds::NXA, NP = LmLds::NP;
     const int h = threadIdx.x >> 5, base = h * LM_NMAXS, e0 = threadIdx.x & 31;
@@ -156,24 +111,82 @@ __device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const Riccati
     const int zj = R.e - tri(zi);
     const bool uent = zi == NXA || zj == NXA;                              // z index 5 = u
     const int pv = zi == NXA + 1 ? NXA : (zi < NXA ? zi : 0), qv = zj == NXA + 1 ? NXA : (zj < NXA ? zj : 0);
+    const int ea = e0 < 24 ? e0 / 6 : 0, eq = e0 < 24 ? e0 % 6 : 0;       // phase 1 entry of this lane
+    double* Pw = RL->Pw[h];
+    bool ok = true;
     auto soften = [&](int j, bool surrogate) {
         const double* Gn = S->G[j];
-        double T[4][6], gu[6], iq;
         const double qj = Gn[hp(NXA, NXA)];
-        const bool okj = soft_T(Gn, RL->Dinv[j], T, gu, iq) && qj > 0.0 && isfinite(qj);
-        if (surrogate) {
-            double v = fma(-gu[pv] * iq, gu[qv], Gn[gszz<NXA>(pv, qv)]);
-#pragma unroll
-            for (int a = 0; a < 4; ++a) v -= fma(-gu[pv] * iq, gu[a], Gn[gszz<NXA>(pv, a)]) * T[a][qv];
-            RL->Gs[h][R.e] = uent ? ((zi == NXA && zj == NXA) ? 1.0 : 0.0) : v;
+        ok = ok && qj > 0.0 && isfinite(qj);
+        const double iq = frcp(qj);
+        // phase 1: Pt(a, q), a < 4
+        {
+            const double ga = Gn[gszu<NXA>(ea)], gq = Gn[gszu<NXA>(eq)];
+            const double v = fma(-ga * iq, gq, Gn[gszz<NXA>(ea, eq)]);
+            if (e0 < 24) Pw[e0] = v;
         }
-        if (e0 < 24) RL->T[j][e0] = T[e0 / 6][e0 % 6];
-        return okj;
-    };
-    bool ok = true;
-    for (int k = N - 1; k >= 0; --k) {
-        ok = soften(base + k + 1, true) && ok;
+        double pvq = 0.0;
+        if (surrogate) {
+            const double gp = Gn[gszu<NXA>(pv)], gq = Gn[gszu<NXA>(qv)];
+            pvq = fma(-gp * iq, gq, Gn[gszz<NXA>(pv, qv)]);
+        }
         __syncthreads();
+        // phase 2: lanes q < 6 solve column q of T
+        if (e0 < 6) {
+            double P[4][6];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int q = 0; q < 6; ++q) P[a][q] = Pw[6 * a + q];
+            const double* dinv = RL->Dinv[j];
+            double L[4][4], id[4], dd[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                double t = P[c][c] + dinv[c];
+#pragma unroll
+                for (int m = 0; m < c; ++m) t -= L[c][m] * L[c][m] * dd[m];
+                dd[c] = t;
+                ok = ok && t > 0.0 && isfinite(t);
+                id[c] = frcp(t);
+#pragma unroll
+                for (int i = c + 1; i < 4; ++i) {
+                    double u = P[i][c];
+#pragma unroll
+                    for (int m = 0; m < c; ++m) u -= L[i][m] * L[c][m] * dd[m];
+                    L[i][c] = u * id[c];
+                }
+            }
+            double y[4], t4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double t = P[i][e0];
+#pragma unroll
+                for (int m = 0; m < i; ++m) t -= L[i][m] * y[m];
+                y[i] = t;
+            }
+#pragma unroll
+            for (int i = 3; i >= 0; --i) {
+                double t = y[i] * id[i];
+#pragma unroll
+                for (int m = i + 1; m < 4; ++m) t -= L[m][i] * t4[m];
+                t4[i] = t;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) RL->T[j][6 * i + e0] = t4[i];
+        }
+        __syncthreads();
+        // phase 3: the surrogate entry of this lane (Pt(p, a) = Pt(a, p) for the physical a)
+        if (surrogate) {
+            const double* T = RL->T[j];
+            double v = pvq;
+#pragma unroll
+            for (int a = 0; a < 4; ++a) v -= Pw[6 * a + pv] * T[6 * a + qv];
+            RL->Gs[h][R.e] = uent ? ((zi == NXA && zj == NXA) ? 1.0 : 0.0) : v;
+            __syncthreads();
+        }
+    };
+    for (int k = N - 1; k >= 0; --k) {
+        soften(base + k + 1, true);
         const double hk = S->H[base + k][R.e];
         const double* Mk = &S->M[base + k][0][0];
         double vi[NP], vj[NP];
@@ -193,10 +206,7 @@ __device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const Riccati
         S->G[base + k][R.e] = ga;
         __syncthreads();
     }
-    ok = soften(base, false) && ok;
-    __syncthreads();
-    const double q0 = S->G[base][hp(NXA, NXA)];
-    ok = ok && q0 > 0.0 && isfinite(q0);
+    soften(base, false);
     return !wany(!ok);
 }
 
@@ -205,6 +215,7 @@ __device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const Riccati
 constexpr size_t kLmPolicyLdsOff = (sizeof(LmShared) + 15) & ~size_t(15);
 constexpr size_t kLmRestoOff = kLmPolicyLdsOff;
 constexpr size_t kLmLdsBytes = kLmPolicyLdsOff + (sizeof(PolicyLds) > sizeof(LmResto) ? sizeof(PolicyLds) : sizeof(LmResto));
+static_assert(kLmLdsBytes <= 160 * 1024, "LDS of one CU");
 // hand-off of an instance whose filter line search failed: its iteration-start state goes to HBM
 // (LmpcArgs::resto_buf, kLmNst doubles per lane) and lmpc_ipm_kernel<true> resumes it
 constexpr int kLmNeedResto = -100;
@@ -1164,7 +1175,16 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         // theta falls to 0.9 of its start value and the original filter accepts the point.
         if (RESTO && !accepted) {
             const double mu0 = mu, th0 = theta, phi0 = phi, tau0 = tau, rho = 1000.0;
-            double xr[4], drx[4];
+            double* const pc = RL->PN[sl];
+            double* const nc = pc + 4;
+            double* const zp = pc + 8;
+            double* const zn = pc + 12;
+            double* const rp = pc + 16;
+            double* const rn = pc + 20;
+            double* const sp = pc + 24;
+            double* const sn = pc + 28;
+            double* const xr = pc + 32;
+            double* const drx = pc + 36;
 #pragma unroll
             for (int i = 0; i < 4; ++i) { xr[i] = x[i]; drx[i] = 1.0 / fmax(1.0, fabs(x[i])); }
             const double ur = u, dru = 1.0 / fmax(1.0, fabs(u));
@@ -1176,7 +1196,6 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             cmx = fmax(cmx, xon ? fabs(g0[4]) : 0.0);
             double rmu = fmax(mu0, wmax(cmx));
             double eta = sqrt(rmu);
-            double pc[4], nc[4], zp[4], zn[4], rp[4], rn[4], sp[4], sn[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const double c = dsc[i] * g0[i];
