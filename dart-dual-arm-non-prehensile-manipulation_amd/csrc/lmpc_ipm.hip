@@ -715,7 +715,13 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         return wsum(tot);
     };
 
-    for (it = it_start;; ++it) {
+    // RESTO: the iteration loop is left for each restoration phase, which runs after it (outside the loop,
+    // so that its registers do not burden the iterations) and re-enters it at the next iteration
+    bool go_resto = false;
+    double phi_rs = 0.0;
+    int it_next = it_start;
+    for (;;) {
+    for (it = it_next;; ++it) {
         const bool lsm = it < 0;
         // the iteration-start values a hand-off parks (the rest of the state changes only on acceptance)
         const double mu_it = mu, dl_it = delta_last;
@@ -1173,8 +1179,32 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         // z_n = mu_R / n, u-bound multipliers min(rho, z), least-square equality multipliers; its own
         // filter, mu, inertia correction and second-order correction; leaves when the original problem's
         // theta falls to 0.9 of its start value and the original filter accepts the point.
-        if (RESTO && !accepted) {
-            const double mu0 = mu, th0 = theta, phi0 = phi, tau0 = tau, rho = 1000.0;
+        if (RESTO && !accepted) { phi_rs = phi; go_resto = true; break; }
+        if (!accepted) { status = -2; break; }
+        if (!soft && !ftype && nfilt < kWave) {
+            if (lane == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
+            ++nfilt;
+        }
+        // ---------------- accept ------------------------------------------------------------
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = xon ? fma(alpha, dx[i], x[i]) : x[i];
+        up = xon ? fma(alpha, dx[4], up) : up;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) lam[i] = xon ? fma(alpha, lamp[i] - lam[i], lam[i]) : 0.0;
+        if (uon) {
+            u = fma(alpha, dU, u);
+            const double il = frcp(u - lo), iu = frcp(hi - u);
+            zl = fmax(fmin(fma(az, dzl, zl), 1e10 * mu * il), 1e-10 * mu * il);
+            zu = fmax(fmin(fma(az, dzu, zu), 1e10 * mu * iu), 1e-10 * mu * iu);
+        }
+        theta = th_t;
+        STAMP(8);
+    }
+    if (!RESTO || !go_resto) break;
+    go_resto = false;
+    {
+            const double tau = fmax(0.99, 1.0 - mu);
+            const double mu0 = mu, th0 = theta, phi0 = phi_rs, tau0 = tau, rho = 1000.0;
             double* const pc = RL->PN[sl];
             double* const nc = pc + 4;
             double* const zp = pc + 8;
@@ -1637,29 +1667,9 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 for (int i = 0; i < 5; ++i) lam[i] = 0.0;
             }
             in_soft = 0; soft_count = 0;
-            it = rit - 1;
-            STAMP(8);
+            it_next = rit;
             continue;
         }
-        if (!accepted) { status = -2; break; }
-        if (!soft && !ftype && nfilt < kWave) {
-            if (lane == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
-            ++nfilt;
-        }
-        // ---------------- accept ------------------------------------------------------------
-#pragma unroll
-        for (int i = 0; i < 4; ++i) x[i] = xon ? fma(alpha, dx[i], x[i]) : x[i];
-        up = xon ? fma(alpha, dx[4], up) : up;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) lam[i] = xon ? fma(alpha, lamp[i] - lam[i], lam[i]) : 0.0;
-        if (uon) {
-            u = fma(alpha, dU, u);
-            const double il = frcp(u - lo), iu = frcp(hi - u);
-            zl = fmax(fmin(fma(az, dzl, zl), 1e10 * mu * il), 1e-10 * mu * il);
-            zu = fmax(fmin(fma(az, dzu, zu), 1e10 * mu * iu), 1e-10 * mu * iu);
-        }
-        theta = th_t;
-        STAMP(8);
     }
 
     // ---------------- outputs -------------------------------------------------------------
