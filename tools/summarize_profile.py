@@ -30,7 +30,8 @@ ALGO_BYTES = {"pmpc_ipm_kernel": 18 * 176, "rmpc_ipm_kernel": 18 * (4 + 2 + 14 +
 # of the same kernel in the bench (C4, saturation runs) are left out of the per-launch figures
 GRID = {"pmpc_ipm_kernel": 18 * 8 * 64, "rmpc_ipm_kernel": 18 * 8 * 64, "lmpc_ipm_kernel": 18 * 8 * 64,
         "arm_qp_kernel": 36 * 64}
-STATS_NAME = {"pmpc_ipm_kernel": "pmpc_ipm_kernel<1, true, false, true, false>"}   # template instance the C2 launch uses
+STATS_NAME = {"pmpc_ipm_kernel": "pmpc_ipm_kernel<1, true, false, true, false>",   # template instance the C2 launch uses
+              "lmpc_ipm_kernel": "lmpc_ipm_kernel<false>"}     # (<true> resumes restoration hand-offs only)
 
 
 def short(name):
@@ -56,6 +57,8 @@ for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             for row in csv.DictReader(fh):
                 k = short(row.get("Kernel_Name", ""))
                 if k is None or row.get("Counter_Name") != ctr or int(row.get("Grid_Size", 0)) != GRID[k]:
+                    continue
+                if STATS_NAME.get(k, k) not in row.get("Kernel_Name", "") and k != "pmpc_ipm_kernel":
                     continue
                 per[k][ctr].append(float(row["Counter_Value"]))
                 meta[k] = {"grid_size": int(row.get("Grid_Size", 0)), "VGPR_Count": int(row.get("VGPR_Count", 0)),
