@@ -273,13 +273,19 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_lib   # checker only
     ref = oracle_lib.solve_batch(S[:36], T[:36], P[:36], N=N, Ts=0.002, tol=1e-11, nthreads=4, want_w=False)
+    # the same path at the same tolerance: every one of the 1152 gathered controls against the oracle at tol 1e-8
+    same = oracle_lib.solve_batch(S, T, P, N=N, Ts=0.002, tol=args.tol, nthreads=8, want_w=False)
     return {"workload": "C4: PMPC 18 configs x 64 seeds = 1152 instances, N=20, tol 1e-8, cold start, contiguous "
                         "blocks over the ranks + all_gather_into_tensor of [u0, f, status] (RCCL)",
             "global_batch": Bg, "per_rank": per, "n_gpus": world, "scaling": "strong", "steps": K,
             "solves_per_s": Bg * K / dt, "ms_per_step": dt / K * 1e3, "gather_in_timed_region": world > 1,
             "solves_per_s_without_gather": Bg * K / dt_solve, "ms_per_step_without_gather": dt_solve / K * 1e3,
             "status_ok_frac": float(np.mean(res[:, 3] == 0)), "rank_blocks_consistent": mine,
-            "max_abs_u0_err_vs_exact_optimum_first36": float(np.max(np.abs(res[:36, 0:2] - ref["u0"])))}
+            "max_abs_u0_err_vs_oracle_same_tol": float(np.max(np.abs(res[:, 0:2] - same["u0"]))),
+            "status_equal_to_oracle": bool(np.array_equal(res[:, 3].astype(np.int32), same["status"])),
+            "max_abs_u0_err_vs_exact_optimum_first36": float(np.max(np.abs(res[:36, 0:2] - ref["u0"]))),
+            "note_exact_optimum": "IPOPT's own stopping point at tol 1e-8 sits ~mu/z inside weakly active bounds: "
+                                  "the oracle at tol 1e-8 is as far from the tol-1e-11 optimum"}
 
 
 def bench_lmpc(args, torch, dev, stream, dart_mpc):
