@@ -335,12 +335,21 @@ __device__ __forceinline__ double cos_econ(double x) {       // the cosine half 
     const double y = x * x;
     return fma(y, cos_poly_(y), 1.0);
 }
-__device__ __forceinline__ double tilt_cos(bool poly, double x) { return poly ? cos_small(x) : cos(x); }
+// poly: |bounds| <= 1 rad (every configuration of the reference); the library branch is laid out off
+// the hot path (PMPC: C2 +2.1 %, N = 15 +5.9 %, A/B tools/ab_lib.sh)
+__device__ __forceinline__ double tilt_cos(bool poly, double x) {
+    if (__builtin_expect(poly, 1)) return cos_small(x);
+    return cos(x);
+}
 __device__ __forceinline__ void tilt_sincos(bool poly, double x, double& s, double& c) {
-    if (poly) sincos_small(x, s, c);
+    if (__builtin_expect(poly, 1)) sincos_small(x, s, c);
     else sincos(x, &s, &c);
 }
-__device__ __forceinline__ double tilt_cos_econ(bool poly, double x) { return poly ? cos_econ(x) : cos(x); }
+__device__ __forceinline__ double tilt_cos_econ(bool poly, double x) {
+    if (__builtin_expect(poly, 1)) return cos_econ(x);
+    return cos(x);
+}
+// (no layout hint here: RMPC measured 0.8 % slower with it, its register allocation moved)
 __device__ __forceinline__ void tilt_sincos_econ(bool poly, double x, double& s, double& c) {
     if (poly) sincos_econ(x, s, c);
     else sincos(x, &s, &c);
