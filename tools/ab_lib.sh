@@ -19,6 +19,11 @@ if d.get("saturation"):
 for k in ("rmpc_c3", "lmpc_c5", "arm_qp", "pmpc_n15"):
     if d.get(k):
         out += [k, round(d[k]["solves_per_s"]), round(d[k].get("kernel_ms", d[k]["ms_per_step"]) * 1e3, 1), "us"]
+l = d.get("lmpc_c5") or {}
+if l.get("restoration_off"):
+    out += ["c5_resto_off", round(l["restoration_off"]["solves_per_s"])]
+if l.get("policy_fused"):
+    out += ["c5_fused", round(l["policy_fused"]["solves_per_s"])]
 print(*out)
 PY
   done
