@@ -42,7 +42,7 @@ constexpr double LM_G = 9.81;     // rlmpc2.py:354
 using LmLds = OcpLdsS<5, LM_NMAXS>;
 
 #ifdef DART_STAMPS
-__device__ unsigned long long g_stamp_lm[16];
+__device__ unsigned long long g_stamp_lm[32];   // 16..23: the restoration phase (lmpc_ipm_kernel<true>)
 #endif
 
 struct Strb {           // stribeck_fric parameters (rlmpc2.py:372-376)
@@ -1362,12 +1362,14 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
 #pragma unroll
                 for (int i = 0; i < 5; ++i) rl[i] = (use && xon) ? lpr[i] : 0.0;
             }
+            STAMP(16);      // restoration start: reference point, p / n, least-square multipliers
             int rit = it + 1, rnf = 0, racc_count = 0, rstat = -2;
             bool rfirst = true, rok = false;
             double rfth = 0.0, rfph = 0.0, rdelta_last = 0.0, thr = 0.0, rth_max = 0.0, rth_min = 0.0;
             double cres[5];
             for (;; ++rit) {
                 stage();
+                STAMP(17);
                 double g[5];
                 incoming(x, up, u, xn, g);
 #pragma unroll
@@ -1455,6 +1457,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     Hk[hp(5, 5)] += eta * dru * dru + rzl * isl + rzu * isu;
                 }
                 grad_rows(false);
+                STAMP(18);
                 double delta = 0.0, dapplied = 0.0;
                 int attempt = 0;
                 bool okr = false;
@@ -1476,6 +1479,8 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     }
                     dapplied = delta;
                 }
+                STAMP(19);
+                STAMP_ADD(24, attempt + 1);
                 if (!okr) { rstat = -3; break; }
                 if (delta > 0.0) rdelta_last = delta;
                 // the step of p, n and every bound multiplier, and the fractions to the boundary
@@ -1506,6 +1511,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 };
                 resto_step();
                 pn_steps();
+                STAMP(20);
                 // barrier objective of the restoration problem and its directional derivative
                 double phir, gtdr;
                 {
@@ -1568,10 +1574,12 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     }
                     return cmp_le(tht, (1 - gam_th) * thr, thr) || cmp_le(pht - phir, -gam_ph * thr, phir);
                 };
+                STAMP(21);
                 double alr = amr;
                 bool accr = false, ftr = false;
                 for (int ls = 0; ls < 80 && !accr; ++ls) {
                     if (alr < aminr && ls > 0) break;
+                    STAMP_ADD(26, 1);
                     trial_r(alr);
                     accr = racc(alr, ftr);
                     if (!accr && ls == 0 && !(tht < thr) && a.max_soc > 0) {
@@ -1615,6 +1623,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     }
                     if (!accr) alr *= 0.5;
                 }
+                STAMP(22);
                 if (!accr) { rstat = -2; break; }      // a failed line search in the restoration phase
                 if (!ftr && rnf < kWave) {
                     if (lane == rnf) { rfth = (1 - gam_th) * thr; rfph = phir - gam_ph * thr; }
@@ -1640,6 +1649,8 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     rzu = fmax(fmin(fma(azr, dzur, rzu), 1e10 * rmu / su_), rmu / (1e10 * su_));
                 }
                 thr = tht;
+                STAMP(23);
+                STAMP_ADD(25, 1);
             }
             if (!rok) { status = rstat; it = rit; break; }
             // back to the original problem: the u-bound multipliers take the step (mu - z s_trial) / s that
@@ -1684,7 +1695,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         }
         if (uon) wo[8 * (N + 1) + 2 * k + hf] = u;
     }
-    STAMP_FLUSH_TO(g_stamp_lm, b);
+    STAMP_FLUSH32_TO(g_stamp_lm, b);
 }
 
 }  // namespace dartmpc
@@ -1729,7 +1740,7 @@ extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStre
 
 #ifdef DART_STAMPS
 extern "C" hipError_t dartmpc_read_stamps_lmpc(unsigned long long* host_out) {
-    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp_lm), sizeof(unsigned long long) * 16, 0,
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp_lm), sizeof(unsigned long long) * 32, 0,
                                hipMemcpyDeviceToHost);
 }
 #endif
