@@ -345,8 +345,10 @@ def bench_lmpc(args, torch, dev, stream, dart_mpc):
     dt_off = time.perf_counter() - t0
     st_off = ST[3:].cpu().numpy()
     s_off.close()
-    out = {"workload": "C5: LMPC batch=18, N=30, Ts=0.002, pvec~U(0.01,1.9)^34 input, reference IPOPT options "
-                       "(tol 1e-4, max_iter 50, acceptable 1e-3 x 5), cold start, IPOPT's restoration phases on",
+    out = {"workload": "C5 stress: LMPC batch=18, N=30, Ts=0.002, pvec~U(0.01,1.9)^34 input (SURVEY 8d; random "
+                       "physical parameters, harsher than the policy's), reference IPOPT options (tol 1e-4, max_iter 50, "
+                       "acceptable 1e-3 x 5), cold start, IPOPT's restoration phases on.  C5 as BASELINE.json configures "
+                       "it (the learned net inlined into the launch) is `policy_fused`",
            "solves_per_s": B * K / dt, "ms_per_step": dt / K * 1e3, "kernel_ms": kern_ms,
            "status_ok_frac": float(np.mean(st >= 0)), "status_optimal_frac": float(np.mean(st == 0)),
            "status_acceptable_frac": float(np.mean(st == 1)), "status_maxiter_frac": float(np.mean(st == -1)),
