@@ -89,7 +89,6 @@ struct LmResto {
     NodeArr<double[4], 2 * LM_NMAXS> Dinv;    // 1 / D of node k's four physical incoming rows
     NodeArr<double[20], 2 * LM_NMAXS> SV;     // a second-order correction: the plain step
     double Gs[2][LmLds::NTP];                 // the surrogate of G_{k+1} (one per half)
-    double Pw[2][24];                         // soft transform: Pt(a, q), a < 4, of the node at hand
     // per-node state of the restoration problem (node k's four physical incoming rows), kept in LDS
     // rather than registers: p, n, z_p, z_n, rp, rn, Sigma_p', Sigma_n', x_R, D_R
     NodeArr<double[40], 2 * LM_NMAXS> PN;
@@ -97,93 +96,89 @@ struct LmResto {
 
 // Backward sweep of both halves with soft physical rows (restoration phase): before the step of node
 // k, each half forms the surrogate of G_{k+1} seen through node k+1's soft rows (RL->Gs) and keeps
-// T_{k+1} for the forward map; T_0 of the soft initial rows comes last.  The transform of one node runs
-// in three lane-parallel phases of the half-wave: (1) lane e < 24 forms Pt(a, q) = Gzz - Gzu Gzu^T / Quu
-// for a = e / 6 < 4, q = e % 6; (2) lanes q < 6 factor S = Pt(ph, ph) + D^-1 = L diag(dd) L^T (each its
-// own copy) and solve column q of T = S^-1 Pt(ph, :); (3) every lane forms its packed surrogate entry
-// Pt(p, q) - Pt(p, ph) T(:, q).  G[slot N] must hold the terminal surrogate, RL->Dinv every node's 1 / D.
-// Returns false (wave-uniform) if some S or Quu is not positive definite.
+// T_{k+1} for the forward map; T_0 of the soft initial rows comes last.  The transform of one node is
+// one lane-parallel phase of the half-wave: every lane forms S = Pt(ph, ph) + D^-1 from G_{k+1}
+// (Pt = Gzz - Gzu Gzu^T / Quu), factors it S = L diag(dd) L^T (each its own copy) and solves the column
+// qv of T = S^-1 Pt(ph, :) its packed surrogate entry (pv, qv) needs, Pt(pv, qv) - Pt(pv, ph) T(:, qv);
+// the lanes of row 6 of the packed triangle store T's six columns.  (Every product is formed as the
+// earlier three-phase version formed it -- Pt(a, q) = fma(-Gzu(a) / Quu, Gzu(q), Gzz(a, q)) -- so the
+// results are the same bits, with one barrier per node instead of three.)  G[slot N] must hold the
+// terminal surrogate, RL->Dinv every node's 1 / D.  Returns false (wave-uniform) if some S or Quu is
+// not positive definite.
 __device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const RiccatiSRoles& R) {
     constexpr int NXA = LmLds::NXA, NP = LmLds::NP;
-    const int h = threadIdx.x >> 5, base = h * LM_NMAXS, e0 = threadIdx.x & 31;
+    static_assert(NXA == 5 && NP == 6, "packed row 6 = [x~ (5), u, 1] names T's six columns");
+    const int h = threadIdx.x >> 5, base = h * LM_NMAXS;
     int zi = 0;
     while (tri(zi + 1) <= R.e) ++zi;
     const int zj = R.e - tri(zi);
     const bool uent = zi == NXA || zj == NXA;                              // z index 5 = u
     const int pv = zi == NXA + 1 ? NXA : (zi < NXA ? zi : 0), qv = zj == NXA + 1 ? NXA : (zj < NXA ? zj : 0);
-    const int ea = e0 < 24 ? e0 / 6 : 0, eq = e0 < 24 ? e0 % 6 : 0;       // phase 1 entry of this lane
-    double* Pw = RL->Pw[h];
+    // the writer of T(:, qv): the lanes of packed row 6 (entries (6, zj), zj != u), each a different qv
+    const bool twrite = R.on && zi == NXA + 1 && zj != NXA;
     bool ok = true;
     auto soften = [&](int j, bool surrogate) {
         const double* Gn = S->G[j];
         const double qj = Gn[hp(NXA, NXA)];
         ok = ok && qj > 0.0 && isfinite(qj);
         const double iq = frcp(qj);
-        // phase 1: Pt(a, q), a < 4
-        {
-            const double ga = Gn[gszu<NXA>(ea)], gq = Gn[gszu<NXA>(eq)];
-            const double v = fma(-ga * iq, gq, Gn[gszz<NXA>(ea, eq)]);
-            if (e0 < 24) Pw[e0] = v;
+        const double* dinv = RL->Dinv[j];
+        double gu[4], di[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) { gu[a] = Gn[gszu<NXA>(a)]; di[a] = dinv[a]; }
+        const double gq = Gn[gszu<NXA>(qv)], gp = Gn[gszu<NXA>(pv)];
+        double P[4][4], rq[4], rp[4];          // Pt(i, c) for c <= i < 4; Pt(ph, qv); Pt(ph, pv)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int c = 0; c <= i; ++c) P[i][c] = fma(-gu[i] * iq, gu[c], Gn[gszz<NXA>(i, c)]);
+            rq[i] = fma(-gu[i] * iq, gq, Gn[gszz<NXA>(i, qv)]);
+            rp[i] = fma(-gu[i] * iq, gp, Gn[gszz<NXA>(i, pv)]);
         }
-        double pvq = 0.0;
+        const double pvq = fma(-gp * iq, gq, Gn[gszz<NXA>(pv, qv)]);
+        double L[4][4], id[4], dd[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            double t = P[c][c] + di[c];
+#pragma unroll
+            for (int m = 0; m < c; ++m) t -= L[c][m] * L[c][m] * dd[m];
+            dd[c] = t;
+            ok = ok && t > 0.0 && isfinite(t);
+            id[c] = frcp(t);
+#pragma unroll
+            for (int i = c + 1; i < 4; ++i) {
+                double u = P[i][c];
+#pragma unroll
+                for (int m = 0; m < c; ++m) u -= L[i][m] * L[c][m] * dd[m];
+                L[i][c] = u * id[c];
+            }
+        }
+        double y[4], t4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            double t = rq[i];
+#pragma unroll
+            for (int m = 0; m < i; ++m) t -= L[i][m] * y[m];
+            y[i] = t;
+        }
+#pragma unroll
+        for (int i = 3; i >= 0; --i) {
+            double t = y[i] * id[i];
+#pragma unroll
+            for (int m = i + 1; m < 4; ++m) t -= L[m][i] * t4[m];
+            t4[i] = t;
+        }
+        if (twrite) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) RL->T[j][6 * i + qv] = t4[i];
+        }
         if (surrogate) {
-            const double gp = Gn[gszu<NXA>(pv)], gq = Gn[gszu<NXA>(qv)];
-            pvq = fma(-gp * iq, gq, Gn[gszz<NXA>(pv, qv)]);
-        }
-        __syncthreads();
-        // phase 2: lanes q < 6 solve column q of T
-        if (e0 < 6) {
-            double P[4][6];
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int q = 0; q < 6; ++q) P[a][q] = Pw[6 * a + q];
-            const double* dinv = RL->Dinv[j];
-            double L[4][4], id[4], dd[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                double t = P[c][c] + dinv[c];
-#pragma unroll
-                for (int m = 0; m < c; ++m) t -= L[c][m] * L[c][m] * dd[m];
-                dd[c] = t;
-                ok = ok && t > 0.0 && isfinite(t);
-                id[c] = frcp(t);
-#pragma unroll
-                for (int i = c + 1; i < 4; ++i) {
-                    double u = P[i][c];
-#pragma unroll
-                    for (int m = 0; m < c; ++m) u -= L[i][m] * L[c][m] * dd[m];
-                    L[i][c] = u * id[c];
-                }
-            }
-            double y[4], t4[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                double t = P[i][e0];
-#pragma unroll
-                for (int m = 0; m < i; ++m) t -= L[i][m] * y[m];
-                y[i] = t;
-            }
-#pragma unroll
-            for (int i = 3; i >= 0; --i) {
-                double t = y[i] * id[i];
-#pragma unroll
-                for (int m = i + 1; m < 4; ++m) t -= L[m][i] * t4[m];
-                t4[i] = t;
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) RL->T[j][6 * i + e0] = t4[i];
-        }
-        __syncthreads();
-        // phase 3: the surrogate entry of this lane (Pt(p, a) = Pt(a, p) for the physical a)
-        if (surrogate) {
-            const double* T = RL->T[j];
             double v = pvq;
 #pragma unroll
-            for (int a = 0; a < 4; ++a) v -= Pw[6 * a + pv] * T[6 * a + qv];
+            for (int a = 0; a < 4; ++a) v -= rp[a] * t4[a];
             RL->Gs[h][R.e] = uent ? ((zi == NXA && zj == NXA) ? 1.0 : 0.0) : v;
-            __syncthreads();
         }
+        __syncthreads();
     };
     for (int k = N - 1; k >= 0; --k) {
         soften(base + k + 1, true);
