@@ -222,6 +222,7 @@ int check_cfg(const dart_mpc_config* c) {
     if (c->max_soc < 0 || c->max_soc > 8) return 0;
     if (c->pmpc_path != 0 && c->pmpc_path != 1) return 0;
     if (!(c->constr_mult_init_max >= 0.0)) return 0;
+    if (!(c->max_cpu_time >= 0.0) || c->max_cpu_time > 1e9) return 0;
     return 1;
 }
 
@@ -418,6 +419,7 @@ void dart_mpc_config_default(dart_mpc_config* c) {
     c->pmpc_path = 0;
     c->constr_mult_init_max = 1000.0;
     c->restoration = 1;
+    c->max_cpu_time = 0.05;         // rlmpc2.py:485
 }
 
 int dart_mpc_nw(int N) { return 6 * (N + 1) + 2 * N; }
@@ -632,6 +634,7 @@ int dart_lmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* state, co
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter;
     a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc; a.mult_init_max = h->cfg.constr_mult_init_max;
     a.resto = h->cfg.restoration;
+    a.max_ticks = (long long)(h->cfg.max_cpu_time * 1e8);     // s_memrealtime: 100 MHz
     if (int rc = lmpc_resto_area(h, B)) return rc;
     a.resto_buf = h->resto_buf;
     a.state = state; a.u_prev = u_prev; a.pvec = pvec; a.target = target; a.prm = prm; a.w_warm = w_warm;
@@ -780,6 +783,7 @@ int dart_lmpc_policy_solve_batch_dev(dart_mpc_handle* h, const dart_lmpc_policy_
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter;
     a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc; a.mult_init_max = h->cfg.constr_mult_init_max;
     a.resto = h->cfg.restoration;
+    a.max_ticks = (long long)(h->cfg.max_cpu_time * 1e8);     // s_memrealtime: 100 MHz
     if (int rc = lmpc_resto_area(h, B)) return rc;
     a.resto_buf = h->resto_buf;
     a.state = state; a.u_prev = u_prev; a.pvec = nullptr; a.target = target; a.prm = prm; a.w_warm = w_warm;

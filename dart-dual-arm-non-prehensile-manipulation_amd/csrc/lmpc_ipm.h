@@ -17,6 +17,7 @@ struct LmpcArgs {
     int max_soc;             // IPOPT max_soc: second-order corrections after a rejected first trial
     double mult_init_max;    // IPOPT constr_mult_init_max: > 0 least-square starting multipliers (default 1000)
     int resto;               // IPOPT's soft restoration and restoration phases after a failed line search (1)
+    long long max_ticks;     // IPOPT max_cpu_time in ticks of the 100 MHz constant clock (s_memrealtime), 0 = off
     double* resto_buf;       // [B][64][16] hand-off of instances entering them (device workspace of the handle)
     int pack;                // blocks per instance slot (set by the launcher; 8 = one XCD for small B)
     const double* state;     // [B][8]  [px, vx, py, vy, theta_x, omega_x, theta_y, omega_y]

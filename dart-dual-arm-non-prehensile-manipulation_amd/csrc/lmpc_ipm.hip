@@ -453,6 +453,14 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         policy_step_wave(a.pol, b, PL);
         pvec = PL.pv;
     }
+    // IPOPT max_cpu_time (rlmpc2.py:485): the solve's clock starts here (the resumed kernel reads the start
+    // its instance parked); 100 MHz constant clock, a scalar read, so the test below is wave-uniform
+    unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    if constexpr (RESTO)
+        t_start = (unsigned long long)a.resto_buf[(size_t)b * kWave * kLmNst + 6 * kLmNst + kLmNst - 1];
+    auto out_of_time = [&]() {
+        return a.max_ticks > 0 && (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.max_ticks;
+    };
     const bool xon = k <= N, uon = k < N;
     constexpr int NC = LmLds::NC;
     // full-state index of the subsystem's local state i
@@ -824,6 +832,8 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
             acc_count = 0;
         }
         if (it >= a.max_iter) { status = -1; break; }
+        // IPOPT Maximum_CpuTime_Exceeded (not during the least-square estimate: IPOPT's initialisation)
+        if (__builtin_expect(!lsm && out_of_time(), 0)) { status = -4; break; }
         for (; !lsm;) {
             const double cmu = fmax(c0 - mu, mu - cminw);
             if (fmax(dinf * is_d, fmax(pinf, cmu * is_c)) > 10.0 * mu || mu <= mu_min) break;
@@ -1125,7 +1135,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 for (int i = 0; i < 5; ++i) st[6 + i] = lam[i];
                 st[11] = zl; st[12] = zu; st[13] = fth; st[14] = fph;
                 st[15] = lane == 0 ? mu_it : lane == 1 ? theta : lane == 2 ? dl_it : lane == 3 ? (double)it
-                       : lane == 4 ? (double)nfilt_it : (double)acc_it;
+                       : lane == 4 ? (double)nfilt_it : lane == 5 ? (double)acc_it : (double)t_start;
                 status = kLmNeedResto;
                 break;
             }
@@ -1426,6 +1436,7 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 const double s_c = fmax(100.0, sumz / nbr) / 100.0;
                 const double errr = fmax(dinf / s_d, fmax(pinf, c0r / s_c));
                 if (rit >= a.max_iter) { rstat = -1; break; }
+                if (out_of_time()) { rstat = -4; break; }
                 if (errr <= tol && dinf <= 1.0 && pinf <= 1e-4 && c0r <= 1e-4) { rstat = -2; break; }   // local infeasibility
                 if (a.acc_iter > 0 && errr <= a.acc_tol && pinf <= 1e-2 && c0r <= 1e-2) {
                     if (++racc_count >= a.acc_iter) { rstat = -2; break; }

@@ -18,10 +18,10 @@ CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
 # DART_MPC_LIB: file name of an alternative in-tree build (A/B timing of two builds, tools/ab_lib.sh)
 LIB_PATH = os.path.join(PKG_DIR, os.path.basename(os.environ.get("DART_MPC_LIB", "libdartmpc.so")))
 
-SOLVED, ACCEPTABLE, MAXITER, LS_FAIL, INERTIA_FAIL = 0, 1, -1, -2, -3
+SOLVED, ACCEPTABLE, MAXITER, LS_FAIL, INERTIA_FAIL, MAXTIME = 0, 1, -1, -2, -3, -4
 STATUS_NAMES = {SOLVED: "Solve_Succeeded", ACCEPTABLE: "Solved_To_Acceptable_Level",
                 MAXITER: "Maximum_Iterations_Exceeded", LS_FAIL: "Restoration_Failed",
-                INERTIA_FAIL: "Error_In_Step_Computation"}
+                INERTIA_FAIL: "Error_In_Step_Computation", MAXTIME: "Maximum_CpuTime_Exceeded"}
 
 # exported symbols of include/dart_mpc.h (tests check every one is present)
 EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch", "dart_mpc_solve_batch_dev",
@@ -35,7 +35,7 @@ EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch",
            "dart_arm_solve_batch_dev", "dart_set_device", "dart_mpc_serve_start", "dart_mpc_serve_stop",
            "dart_mpc_serve_running", "dart_mpc_bind", "dart_mpc_solve_bound")
 VARIANT_PMPC, VARIANT_RMPC, VARIANT_LMPC = 0, 1, 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class DartMPCError(RuntimeError):
@@ -48,7 +48,8 @@ class Config(ctypes.Structure):
                 ("tol", ctypes.c_double), ("max_iter", ctypes.c_int32), ("B_max", ctypes.c_int32),
                 ("gravity", ctypes.c_double), ("acceptable_tol", ctypes.c_double),
                 ("acceptable_iter", ctypes.c_int32), ("max_soc", ctypes.c_int32), ("pmpc_path", ctypes.c_int32),
-                ("restoration", ctypes.c_int32), ("constr_mult_init_max", ctypes.c_double)]
+                ("restoration", ctypes.c_int32), ("constr_mult_init_max", ctypes.c_double),
+                ("max_cpu_time", ctypes.c_double)]
 
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -437,16 +438,17 @@ class LmpcSolver(Solver):
     (LMPC/src/controller/rlmpc2.py:480-489): max_iter 50, tol 1e-4, acceptable_tol 1e-3,
     acceptable_iter 5, and IPOPT's defaults max_soc 4 (second-order correction; 0 = off),
     constr_mult_init_max 1000 (least-square starting multipliers; 0 = start from 0) and its soft
-    restoration / restoration phases after a failed line search (restoration=False: status -2 there)."""
+    restoration / restoration phases after a failed line search (restoration=False: status -2 there);
+    max_cpu_time 0.05 s (rlmpc2.py:485; status -4 past it, measured per instance on the GPU clock; 0 = off)."""
 
     def __init__(self, N=20, Ts=0.002, tol=1e-4, max_iter=50, acceptable_tol=1e-3, acceptable_iter=5,
-                 B_max=1024, device=0, max_soc=4, constr_mult_init_max=1000.0, restoration=True):
+                 B_max=1024, device=0, max_soc=4, constr_mult_init_max=1000.0, restoration=True, max_cpu_time=0.05):
         self._h = ctypes.c_void_p()
         self.cfg = default_config(variant=VARIANT_LMPC, N=int(N), Ts=float(Ts), tol=float(tol), max_iter=int(max_iter),
                                   B_max=int(B_max), acceptable_tol=float(acceptable_tol),
                                   acceptable_iter=int(acceptable_iter), max_soc=int(max_soc),
                                   constr_mult_init_max=float(constr_mult_init_max),
-                                  restoration=int(bool(restoration)))
+                                  restoration=int(bool(restoration)), max_cpu_time=float(max_cpu_time))
         rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
         if rc != 0:
             raise DartMPCError(f"dart_mpc_create(LMPC) failed with code {rc} (no gfx950 device or bad config)")

@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define DART_MPC_ABI_VERSION 6
+#define DART_MPC_ABI_VERSION 7
 
 enum dart_mpc_variant {
     DART_MPC_PMPC = 0,      /* PMPC/src/controller/mpc_3d.py, N <= 63 */
@@ -113,6 +113,11 @@ typedef struct dart_mpc_config {
     double constr_mult_init_max;  /* IPOPT constr_mult_init_max (default 1000): the starting equality
                            multipliers are IPOPT's least-square estimate unless its max norm exceeds this
                            (then 0); 0 = always start from 0.  Used by PMPC, RMPC and LMPC */
+    double max_cpu_time;  /* LMPC (ABI 7): IPOPT max_cpu_time [s], default 0.05 (rlmpc2.py:485): a solve
+                           that is still running when this much wall-clock time has passed since its
+                           instance started ends with status -4 (Maximum_CpuTime_Exceeded) and the current
+                           iterate, checked where IPOPT checks it (after max_iter, each iteration and each
+                           restoration iteration); measured on the GPU's 100 MHz constant clock; 0 = off */
 } dart_mpc_config;
 
 typedef struct dart_mpc_handle dart_mpc_handle;

@@ -30,8 +30,9 @@ def test_defaults_follow_reference():
     c = _lib.default_config()
     assert (c.variant, c.N, c.Ts, c.tol, c.max_iter, c.gravity) == (0, 20, 0.002, 1e-8, 3000, -9.81)
     assert _lib.lib().dart_mpc_nw(20) == 166 and _lib.lib().dart_mpc_nw(15) == 126
-    assert _lib.lib().dart_mpc_abi_version() == 6
+    assert _lib.lib().dart_mpc_abi_version() == 7
     assert c.restoration == 1      # IPOPT's restoration phases on by default (LMPC)
+    assert c.max_cpu_time == 0.05  # rlmpc2.py:485
     assert (c.acceptable_tol, c.acceptable_iter) == (1e-6, 15)                              # IPOPT defaults
     assert _lib.lib().dart_rmpc_nw(20) == 124 and _lib.lib().dart_rmpc_nw(1) == 10      # 4(N+1) + 2N
     assert _lib.lib().dart_lmpc_nw(20) == 208 and _lib.lib().dart_lmpc_nw(30) == 308
@@ -40,7 +41,8 @@ def test_defaults_follow_reference():
 def test_create_rejects_bad_config_without_touching_a_gpu():
     from dart_mpc import _lib
     h = ctypes.c_void_p()
-    for over in (dict(N=0), dict(N=64), dict(Ts=0.0), dict(tol=-1.0), dict(B_max=0), dict(variant=7)):
+    for over in (dict(N=0), dict(N=64), dict(Ts=0.0), dict(tol=-1.0), dict(B_max=0), dict(variant=7),
+                 dict(max_cpu_time=-1.0)):
         c = _lib.default_config(**over)
         assert _lib.lib().dart_mpc_create(ctypes.byref(c), 0, ctypes.byref(h)) == -1
     for over in (dict(variant=1, N=32), dict(variant=1, N=0), dict(variant=2, N=32),   # RMPC/LMPC: N <= 31

@@ -186,3 +186,43 @@ def test_restoration_phase_same_path_as_oracle(dm, resto):
         assert np.sum(o["status"] == 0) == 718
     else:
         assert np.sum(g["status"] == -2) == 5 and np.array_equal(g["status"], o["status"])
+
+
+def test_max_cpu_time(dm):
+    """IPOPT's max_cpu_time (rlmpc2.py:485, 0.05 s): checked after max_iter at every iteration start
+    (and in the restoration iterations), measured per instance on the GPU's 100 MHz clock; past it the
+    solve ends with status -4 (Maximum_CpuTime_Exceeded) and the current iterate.
+      * a 1e-7 s cap: every instance stops at iteration 0 with the iterate the oracle returns for
+        max_iter = 0 (the start point; the least-square multipliers move no primal);
+      * the reference's 0.05 s never binds on C5 (the slowest instance, restoration phases included,
+        takes ~6 ms): bit-identical to no cap, the restoration hand-off carrying the start time;
+      * a 1 ms cap on the instances whose line search fails stops the long restoration solves early."""
+    from dart_mpc.workload import lmpc_batch
+    D = lmpc_batch(40, seed0=0)
+    args = (D["state"], D["u_prev"], D["pvec"], D["target"])
+    s = dm.LmpcSolver(N=30, B_max=1024, max_cpu_time=1e-7)
+    g = s.solve_batch(*args, want_w=True)
+    s.close()
+    o = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=8, max_iter=0)
+    assert np.all(o["status"] == -1) and np.all(o["iters"] == 0)
+    assert np.all(g["status"] == -4) and np.all(g["iters"] == 0)
+    assert np.max(np.abs(g["w"] - o["w"])) <= 1e-12 and np.max(np.abs(g["f"] - o["f"])) <= 1e-9 * np.max(np.abs(o["f"]))
+    out = {}
+    for cap in (0.05, 0.0):
+        s = dm.LmpcSolver(N=30, B_max=1024, max_cpu_time=cap)
+        out[cap] = s.solve_batch(*args)
+        s.close()
+    for key in ("u0", "f", "status", "iters"):
+        assert np.array_equal(out[0.05][key], out[0.0][key]), key
+    assert np.sum(out[0.0]["iters"] > 25) >= 2          # the restoration solves ran under the cap
+    # the instances that enter the restoration phases (oracle, phases off: -2), under a 1 ms cap
+    o2 = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=8, want_w=False, resto=False)
+    hard = np.where(o2["status"] == -2)[0]
+    sub = tuple(a[hard] for a in args)
+    s = dm.LmpcSolver(N=30, B_max=64, max_cpu_time=1e-3)
+    g = s.solve_batch(*sub)
+    s.close()
+    full = {k: out[0.0][k][hard] for k in ("status", "iters")}
+    capped = g["status"] == -4
+    assert capped.sum() >= 1 and np.all(g["iters"][capped] <= full["iters"][capped])
+    assert np.all((g["status"] == full["status"]) | capped)
