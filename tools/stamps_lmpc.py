@@ -23,7 +23,7 @@ D = lmpc_batch(1)
 s = _lib.LmpcSolver(N=30, tol=1e-8, max_iter=500, acceptable_iter=0, B_max=64)
 for rep in range(3):
     out = s.solve_batch(D["state"], D["u_prev"], D["pvec"], D["target"])
-st = np.zeros(16, dtype=np.uint64)
+st = np.zeros(32, dtype=np.uint64)     # the reader copies all 32 slots (16-26: restoration phases)
 L.dartmpc_read_stamps_lmpc(ctypes.c_void_p(st.ctypes.data))
 tot = float(st[:9].sum() + st[11:15].sum())
 it = max(1, out["iters"][0])
