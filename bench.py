@@ -53,7 +53,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-calls", type=int, default=200, help="calls of the host-pointer (PCIe-inclusive) path")
     ap.add_argument("--rmpc-steps", type=int, default=200, help="launches of the supplementary C3 RMPC line (0 = skip)")
-    ap.add_argument("--lmpc-steps", type=int, default=100, help="launches of the supplementary C5 LMPC line (0 = skip)")
+    ap.add_argument("--lmpc-steps", type=int, default=300,
+                    help="launches of the supplementary C5 stress line (0 = skip; its rate is set by the few batches with a restoration instance, so it needs a few hundred)")
     ap.add_argument("--lmpc-policy-steps", type=int, default=100,
                     help="launches of the supplementary C5 line with the policy step fused into the launch (0 = skip)")
     ap.add_argument("--arm-steps", type=int, default=200, help="launches of the supplementary arm-QP line (0 = skip)")
