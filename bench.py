@@ -547,6 +547,8 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # the CPU baselines are timed on rank 0 of a one-GPU run only (the N > 1 runs report GPU rates)
+    args.no_cpu_baseline = args.no_cpu_baseline or world > 1
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = args.dist_backend or ("nccl" if torch.cuda.is_available() else "gloo")
     host_coll = backend == "gloo"
