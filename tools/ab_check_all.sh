@@ -10,4 +10,4 @@ for lib in $LIBS; do
     -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/ab_tests_$lib.log 2>&1 || { echo "TESTS_FAILED $lib"; tail -30 gpurun_out/ab_tests_$lib.log; exit 1; }
   echo "$lib $(tail -1 gpurun_out/ab_tests_$lib.log)"
 done
-bash tools/ab_lib.sh "$LIBS" $REPS "--arm-steps 0 --rmpc-steps 1000 --lmpc-steps 300 --lmpc-policy-steps 300"
+bash tools/ab_lib.sh "$LIBS" $REPS "${EXTRA:---arm-steps 0 --rmpc-steps 1000 --lmpc-steps 300 --lmpc-policy-steps 300}"
