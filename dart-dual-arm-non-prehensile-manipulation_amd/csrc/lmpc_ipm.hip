@@ -1435,11 +1435,15 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 const double s_d = fmax(100.0, (suml + sumz) / (nA + nbr)) / 100.0;
                 const double s_c = fmax(100.0, sumz / nbr) / 100.0;
                 const double errr = fmax(dinf / s_d, fmax(pinf, c0r / s_c));
+#ifdef DART_RESTO_TRACE
+                const double errr_t = errr, dinf_t = dinf / s_d, pinf_t = pinf, c0_t = c0r / s_c;
+#endif
                 if (rit >= a.max_iter) { rstat = -1; break; }
                 if (out_of_time()) { rstat = -4; break; }
-                if (errr <= tol && dinf <= 1.0 && pinf <= 1e-4 && c0r <= 1e-4) { rstat = -2; break; }   // local infeasibility
+                // the restoration problem converged: local infeasibility (IPOPT Infeasible_Problem_Detected, 2)
+                if (errr <= tol && dinf <= 1.0 && pinf <= 1e-4 && c0r <= 1e-4) { rstat = 2; break; }
                 if (a.acc_iter > 0 && errr <= a.acc_tol && pinf <= 1e-2 && c0r <= 1e-2) {
-                    if (++racc_count >= a.acc_iter) { rstat = -2; break; }
+                    if (++racc_count >= a.acc_iter) { rstat = 2; break; }
                 } else {
                     racc_count = 0;
                 }
@@ -1630,6 +1634,72 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     if (!accr) alr *= 0.5;
                 }
                 STAMP(22);
+#ifdef DART_RESTO_TRACE
+                if (blockIdx.x == 0 && lane == 0)      // diagnostic build: the oracle's ORACLE_DEBUG line
+                    printf("  resto it %3d mu %.2e err %.2e dinf %.2e pinf %.2e c0 %.2e delta %.1e amax %.3e alpha %.3e "
+                           "th %.3e th_t %.3e phi %.6e ph_t %.6e gTd %.3e acc %d\n", rit, rmu, errr_t, dinf_t, pinf_t,
+                           c0_t, delta, amr, alr, thr, tht, phir, pht, gtdr, (int)accr);
+                {
+                    double sx = 0.0, spn = 0.0, slp = 0.0, sla = 0.0, sz = 0.0, su = 0.0;
+                    if (xon) {
+                        for (int i = 0; i < 5; ++i) { sx += fabs(dxr[i]); slp += fabs(lpr[i]); sla += fabs(rl[i]); }
+                        for (int i = 0; i < 4; ++i) { spn += fabs(dpc[i]) + fabs(dnc[i]); sz += zp[i] + zn[i]; }
+                    }
+                    if (uon) su = fabs(dUr);
+                    sx = wsum(sx); spn = wsum(spn); slp = wsum(slp); sla = wsum(sla); sz = wsum(sz); su = wsum(su);
+                    // the step against the linearised restoration rows of this lane's node (the oracle's
+                    // "resto step check"): d J dx + dn - dp + c = 0 (physical), J dx + c = 0 (copy row)
+                    double pdx[5];
+                    for (int i = 0; i < 5; ++i) pdx[i] = from_prev(dxr[i]);
+                    const double pdu = from_prev(dUr);
+                    double e1 = 0.0;
+                    if (xon) {
+                        for (int i = 0; i < 5; ++i) {
+                            double jd = dxr[i];
+                            if (k > 0) {
+                                const double* Mp = &S->M[sl - 1][0][0];
+                                for (int m = 0; m < 5; ++m) jd -= Mp[m * NC + i] * pdx[m];
+                                jd -= Mp[5 * NC + i] * pdu;
+                            }
+                            const double r = i < 4 ? dsc[i] * jd + dnc[i] - dpc[i] + cres[i] : jd + cres[i];
+                            e1 = fmax(e1, fabs(r));
+                        }
+                    }
+                    double rows[5] = {0, 0, 0, 0, 0};
+                    if (xon) {
+                        for (int i = 0; i < 5; ++i) {
+                            double jd = dxr[i];
+                            if (k > 0) {
+                                const double* Mp = &S->M[sl - 1][0][0];
+                                for (int m = 0; m < 5; ++m) jd -= Mp[m * NC + i] * pdx[m];
+                                jd -= Mp[5 * NC + i] * pdu;
+                            }
+                            rows[i] = i < 4 ? dsc[i] * jd + dnc[i] - dpc[i] + cres[i] : jd + cres[i];
+                        }
+                    }
+                    // the forward sweep against the closed-loop rows it composes: dx_k - F_{k-1} [dx_{k-1}; 1]
+                    double e2 = 0.0;
+                    if (xon && k > 0) {
+                        for (int r = 0; r < 5; ++r) {
+                            const double* Fr = S->F[sl - 1][r];
+                            double t = Fr[5];
+                            for (int j = 0; j < 5; ++j) t = fma(Fr[j], pdx[j], t);
+                            e2 = fmax(e2, fabs(dxr[r] - t));
+                        }
+                    }
+                    e2 = wmax(e2);
+                    const double e1w = wmax(e1);
+                    if (blockIdx.x == 0 && lane == 0) printf("   sweep check it %3d closed-loop %.2e\n", rit, e2);
+                    if (blockIdx.x == 0 && lane == 0) printf("   step check it %3d constraint %.2e\n", rit, e1w);
+                    if (blockIdx.x == 0 && xon && e1 > 0.05 * e1w && e1w > 1e-6)      // the rows that dominate it
+                        printf("     lane %2d (half %d node %2d) rows %.2e %.2e %.2e %.2e %.2e  dx %.3e %.3e %.3e %.3e %.3e du %.3e\n",
+                               lane, hf, k, rows[0], rows[1], rows[2], rows[3], rows[4], dxr[0], dxr[1], dxr[2], dxr[3],
+                               dxr[4], dUr);
+                    if (blockIdx.x == 0 && lane == 0)
+                        printf("   chk it %3d th %.12e phi %.12e gTd %.12e dx %.12e dpn %.12e du %.12e lamp %.12e lam %.12e "
+                               "zpn %.12e az %.12e\n", rit, thr, phir, gtdr, sx, spn, su, slp, sla, sz, azr);
+                }
+#endif
                 if (!accr) { rstat = -2; break; }      // a failed line search in the restoration phase
                 if (!ftr && rnf < kWave) {
                     if (lane == rnf) { rfth = (1 - gam_th) * thr; rfph = phir - gam_ph * thr; }

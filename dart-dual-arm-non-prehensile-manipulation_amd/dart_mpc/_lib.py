@@ -18,8 +18,8 @@ CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
 # DART_MPC_LIB: file name of an alternative in-tree build (A/B timing of two builds, tools/ab_lib.sh)
 LIB_PATH = os.path.join(PKG_DIR, os.path.basename(os.environ.get("DART_MPC_LIB", "libdartmpc.so")))
 
-SOLVED, ACCEPTABLE, MAXITER, LS_FAIL, INERTIA_FAIL, MAXTIME = 0, 1, -1, -2, -3, -4
-STATUS_NAMES = {SOLVED: "Solve_Succeeded", ACCEPTABLE: "Solved_To_Acceptable_Level",
+SOLVED, ACCEPTABLE, INFEASIBLE, MAXITER, LS_FAIL, INERTIA_FAIL, MAXTIME = 0, 1, 2, -1, -2, -3, -4
+STATUS_NAMES = {SOLVED: "Solve_Succeeded", ACCEPTABLE: "Solved_To_Acceptable_Level", INFEASIBLE: "Infeasible_Problem_Detected",
                 MAXITER: "Maximum_Iterations_Exceeded", LS_FAIL: "Restoration_Failed",
                 INERTIA_FAIL: "Error_In_Step_Computation", MAXTIME: "Maximum_CpuTime_Exceeded"}
 

@@ -41,7 +41,8 @@
  *   u0  [B][2]  first control U_opt[0] = [theta_x, theta_y] (mpc_3d.py:137-138)
  *   f   [B]     objective value at the solution ("loss")    (mpc_3d.py:134)
  *   status[B]   DART_MPC_SOLVED (0), DART_MPC_MAXITER (-1), DART_MPC_LS_FAIL (-2),
- *               DART_MPC_INERTIA_FAIL (-3), DART_MPC_MAXTIME (-4, LMPC's max_cpu_time).
+ *               DART_MPC_INERTIA_FAIL (-3), DART_MPC_MAXTIME (-4, LMPC's max_cpu_time),
+ *               DART_MPC_INFEASIBLE (2, LMPC: the restoration phase converged to local infeasibility).
  *               As in the reference (which never
  *               checks IPOPT's status, mpc_3d.py:133-138) u0 is written anyway.
  *   iters[B]    interior-point iterations taken.
@@ -75,8 +76,9 @@ enum dart_mpc_variant {
 enum dart_mpc_status {
     DART_MPC_SOLVED = 0,
     DART_MPC_ACCEPTABLE = 1,       /* IPOPT "Solved To Acceptable Level" (LMPC: acceptable_tol / _iter) */
+    DART_MPC_INFEASIBLE = 2,       /* IPOPT "Infeasible Problem Detected" (LMPC: its restoration phase converged) */
     DART_MPC_MAXITER = -1,
-    DART_MPC_LS_FAIL = -2,
+    DART_MPC_LS_FAIL = -2,         /* IPOPT "Restoration Failed" (or the failed line search, restoration = 0) */
     DART_MPC_INERTIA_FAIL = -3,
     DART_MPC_MAXTIME = -4          /* IPOPT "Maximum CpuTime Exceeded" (LMPC: dart_mpc_config.max_cpu_time, ABI 7) */
 };

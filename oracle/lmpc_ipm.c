@@ -312,7 +312,11 @@ static int soft_node(const ctx_t *C, const double Pk[NA][NA], int k, double delt
     return 1;
 }
 
-enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_MAXITER = -1, ST_LS_FAIL = -2, ST_INERTIA_FAIL = -3, ST_BAD_INPUT = -10 };
+/* IPOPT ApplicationReturnStatus values (Infeasible_Problem_Detected = 2: the restoration problem converged to a
+   point of local infeasibility; Restoration_Failed = -2: the restoration itself failed, or, with the phases
+   off, the filter line search) */
+enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_INFEASIBLE = 2, ST_MAXITER = -1, ST_LS_FAIL = -2, ST_INERTIA_FAIL = -3,
+       ST_BAD_INPUT = -10 };
 
 static double g_relax = 1e-8;
 void oracle_lmpc_set_relax(double r) { g_relax = r; }
@@ -742,7 +746,8 @@ static double soft_resto_step(const ctx_t *C, work_t *W, int nfilt, double th, d
  *     if any exceeds bound_mult_reset_threshold 1000; the equality multipliers restart at 0
  *     (constr_mult_reset_threshold 0);
  *   - the restoration problem converging (optimal or acceptable) means local infeasibility; a failed
- *     line search inside it is a restoration failure: both end the solve with status -2.
+ *     line search inside it is a restoration failure: the solve ends with status 2 (IPOPT's
+ *     Infeasible_Problem_Detected) or -2 (Restoration_Failed).
  * Returns 1 with the new iterate in W (multipliers included) and *it set to the last restoration
  * iteration, 0 with *status set.
  * --------------------------------------------------------------------------------------------- */
@@ -929,9 +934,9 @@ static int restoration(const ctx_t *C0, work_t *W, int *it_io, int max_iter, dou
         const double s_c = fmax(s_max, sum_z / nb) / s_max;
         const double err = fmax(dinf / s_d, fmax(pinf, c0 / s_c));
         if (rit >= max_iter) { *status = ST_MAXITER; break; }
-        if (err <= tol && dinf <= 1.0 && pinf <= 1e-4 && c0 <= 1e-4) { *status = ST_LS_FAIL; break; }   /* local infeasibility */
+        if (err <= tol && dinf <= 1.0 && pinf <= 1e-4 && c0 <= 1e-4) { *status = ST_INFEASIBLE; break; }   /* local infeasibility */
         if (acc_iter > 0 && err <= acc_tol && pinf <= 1e-2 && c0 <= 1e-2) {
-            if (++acc_count >= acc_iter) { *status = ST_LS_FAIL; break; }
+            if (++acc_count >= acc_iter) { *status = ST_INFEASIBLE; break; }
         } else {
             acc_count = 0;
         }
@@ -1079,6 +1084,17 @@ static int restoration(const ctx_t *C0, work_t *W, int *it_io, int max_iter, dou
 #ifdef ORACLE_DEBUG
         fprintf(stderr, "  resto it %3d mu %.2e err %.2e dinf %.2e pinf %.2e c0 %.2e delta %.1e amax %.3e alpha %.3e th %.3e th_t %.3e phi %.6e ph_t %.6e gTd %.3e acc %d\n",
                 rit, C.mu, err, dinf / s_d, pinf, c0 / s_c, delta, amax, alpha, th, th_t, phi, ph_t, gTd, accepted);
+        {
+            double sx = 0, sp_ = 0, su = 0, sl = 0, sz = 0, slam = 0;
+            for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) {
+                const int r = NA * k + i;
+                sx += fabs(V->dX[r]); sl += fabs(V->lamp[r]); slam += fabs(V->lam[r]);
+                if (i < 8) { sp_ += fabs(R->dpc[r]) + fabs(R->dnc[r]); sz += R->zp[r] + R->zn[r]; }
+            }
+            for (int j = 0; j < nU; ++j) su += fabs(V->dU[j]);
+            fprintf(stderr, "   chk it %3d th %.12e phi %.12e gTd %.12e dx %.12e dpn %.12e du %.12e lamp %.12e lam %.12e zpn %.12e az %.12e\n",
+                    rit, th, phi, gTd, sx, sp_, su, sl, slam, sz, az);
+        }
 #endif
         if (!accepted) { *status = ST_LS_FAIL; break; }     /* restoration failure */
         if (!ftype && nfilt < 256) { R->filt_th[nfilt] = (1 - gam_th) * th; R->filt_ph[nfilt] = phi - gam_ph * th; ++nfilt; }
