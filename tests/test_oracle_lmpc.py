@@ -124,3 +124,19 @@ def test_restoration_phase_recovers_failed_line_searches():
     assert np.array_equal(on["status"][same], off["status"][same])
     assert np.array_equal(on["iters"][same], off["iters"][same])
     assert np.array_equal(on["u0"][same], off["u0"][same])
+
+
+def test_restoration_reports_local_infeasibility():
+    """IPOPT's two restoration outcomes (ApplicationReturnStatus): the restoration problem converging means
+    a point of local infeasibility, Infeasible_Problem_Detected = 2; with the phases off those instances end
+    at the failed filter line search, -2.  Six stress instances of the seed-7000 batch (tools/resto_time.py)
+    take the first branch, after more iterations than the failed line search took."""
+    from dart_mpc.workload import lmpc_batch
+    D = lmpc_batch(80, seed0=7000)
+    idx = np.array([477, 509, 925, 1145, 1188, 1372])
+    args = tuple(D[k][idx] for k in ("state", "u_prev", "pvec", "target"))
+    on = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=6, want_w=False)
+    off = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=6, want_w=False, resto=False)
+    assert np.all(on["status"] == 2), on["status"]
+    assert np.all(off["status"] == -2), off["status"]
+    assert np.all(on["iters"] > off["iters"]) and np.all(on["iters"] <= 50)
