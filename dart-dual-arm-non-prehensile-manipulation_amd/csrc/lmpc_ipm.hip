@@ -84,6 +84,13 @@ struct LmShared {
 // [[Pt', 0], [0, 1]]; the incoming rows of node k+1 map x~+ <- x~+ - E T [x~+; 1] with
 // T = S^-1 Pt(ph, :) (4 x 6), and S positive definite is part of the inertia test.
 // ---------------------------------------------------------------------------------------------
+// iterative refinement of the restoration step: at most this many refinement solves per step, each
+// only while the residual of the Newton system exceeds 1e-12 of the step (IPOPT's PDFullSpaceSolver
+// refines every KKT solve).  Statuses equal to the oracle's on 99.958 % of 28,800 stress instances with
+// it, 99.747 % without (tools/parity_sweep.py); the C5 stress line pays 6 %.  0 = off
+#ifndef DART_RESTO_REFINE
+#define DART_RESTO_REFINE 3
+#endif
 struct LmResto {
     NodeArr<double[24], 2 * LM_NMAXS> T;      // T of node k's soft rows (row-major 4 x 6, value indices)
     NodeArr<double[4], 2 * LM_NMAXS> Dinv;    // 1 / D of node k's four physical incoming rows
@@ -1519,7 +1526,116 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                     }
                     amr = wmin(am); azr = wmin(a2);
                 };
+#if DART_RESTO_REFINE
+                // one step of iterative refinement of the restoration step (IPOPT's PDFullSpaceSolver refines
+                // every KKT solve): the residuals of the Newton system at (dx, du, lambda+) -- soft constraint
+                // rows and stationarity rows -- as the right-hand side of the same factorised soft system
+                // (D, Sigma and the quadratic parts unchanged), the correction added to the step
+                auto refine = [&](const double* cv) -> bool {
+                    double lpn_[5], pdx[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) { const double t = from_next(lpr[i]); lpn_[i] = uon ? t : 0.0; }
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) pdx[i] = from_prev(dxr[i]);
+                    const double pdu = from_prev(dUr);
+                    double rc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+                    if (xon) {
+                        const double* Mp = &S->M[k > 0 ? sl - 1 : sl][0][0];
+#pragma unroll
+                        for (int i = 0; i < 5; ++i) {
+                            double jd = dxr[i];
+                            if (k > 0) {
+#pragma unroll
+                                for (int m = 0; m < 5; ++m) jd -= Mp[m * NC + i] * pdx[m];
+                                jd -= Mp[5 * NC + i] * pdu;
+                            }
+                            if (i < 4) {
+                                const double dy = (lpr[i] - rl[i]) / dsc[i];
+                                const double dpi = (dy - rp[i]) / sp[i], dni = (-dy - rn[i]) / sn[i];
+                                rc[i] = dsc[i] * jd + dni - dpi + cv[i];
+                            } else {
+                                rc[i] = jd + cv[i];
+                            }
+                        }
+                    }
+                    double rs[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+                    double* GN = S->G[sl];
+                    if (uon) {
+                        const double zv[6] = {dxr[0], dxr[1], dxr[2], dxr[3], dxr[4], dUr};
+#pragma unroll
+                        for (int j = 0; j < 6; ++j) {
+                            double t = Hk[hp(6, j)];
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) t += Hk[hp(j, i)] * zv[i];
+                            if (j < 5) t += lpr[j];
+#pragma unroll
+                            for (int m = 0; m < 5; ++m) t -= Mk[j * NC + m] * lpn_[m];
+                            rs[j] = t;
+                        }
+                    } else if (k == N) {       // terminal node: G_N = [[Q_N, q_N], [q_N^T, .]] on x~
+#pragma unroll
+                        for (int j = 0; j < 5; ++j) {
+                            double t = GN[gszz<5>(5, j)];
+#pragma unroll
+                            for (int i = 0; i < 5; ++i) t += GN[gszz<5>(j, i)] * dxr[i];
+                            rs[j] = t + lpr[j];
+                        }
+                    }
+                    // done once the residual is at rounding level relative to the step and the multipliers
+                    double rmax = 0.0, smax = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) rmax = fmax(rmax, fabs(rc[i]));
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) rmax = fmax(rmax, fabs(rs[j]));
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) smax = fmax(smax, xon ? fmax(fabs(dxr[i]), fabs(lpr[i])) : 0.0);
+                    smax = fmax(smax, uon ? fabs(dUr) : 0.0);
+                    rmax = wmax(rmax); smax = wmax(smax);
+                    if (rmax <= 1e-12 * (1.0 + smax)) return false;
+                    double gsave[6];
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) gsave[j] = 0.0;
+                    if (uon) {
+#pragma unroll
+                        for (int j = 0; j < 6; ++j) { gsave[j] = Hk[hp(6, j)]; Hk[hp(6, j)] = rs[j]; }
+                    } else if (k == N) {
+#pragma unroll
+                        for (int j = 0; j < 5; ++j) { gsave[j] = GN[gszz<5>(5, j)]; GN[gszz<5>(5, j)] = rs[j]; }
+                    }
+                    double rg[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) rg[i] = xon ? (i < 4 ? rc[i] / dsc[i] : rc[i]) : 0.0;
+#pragma unroll
+                    for (int r = 0; r < 5; ++r) {
+                        const double t = from_next(rg[r]);
+                        if (uon) Mk[6 * NC + r] = -t;
+                        if (k == 0) S->dx0[hf][r] = -rg[r];
+                    }
+                    __syncthreads();
+                    (void)riccati_s_sweep_soft(S, RL, N, RR);
+                    double dx0_[5], lp0_[5];
+                    const double du0_ = dUr;
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) { dx0_[i] = dxr[i]; lp0_[i] = lpr[i]; }
+                    resto_step();
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) { dxr[i] = dx0_[i] + dxr[i]; lpr[i] = lp0_[i] + lpr[i]; }
+                    dUr = du0_ + dUr;
+                    if (uon) {
+#pragma unroll
+                        for (int j = 0; j < 6; ++j) Hk[hp(6, j)] = gsave[j];
+                    } else if (k == N) {
+#pragma unroll
+                        for (int j = 0; j < 5; ++j) GN[gszz<5>(5, j)] = gsave[j];
+                    }
+                    __syncthreads();
+                    return true;
+                };
+#endif
                 resto_step();
+#if DART_RESTO_REFINE
+                for (int rr = 0; rr < DART_RESTO_REFINE && refine(cres); ++rr) {}
+#endif
                 pn_steps();
                 STAMP(20);
                 // barrier objective of the restoration problem and its directional derivative
@@ -1615,6 +1731,9 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                             __syncthreads();
                             (void)riccati_s_sweep_soft(S, RL, N, RR);
                             resto_step();
+#if DART_RESTO_REFINE
+                            for (int rr = 0; rr < DART_RESTO_REFINE && refine(csoc); ++rr) {}
+#endif
                             pn_steps();
                             asoc = amr;
                             trial_r(asoc);
