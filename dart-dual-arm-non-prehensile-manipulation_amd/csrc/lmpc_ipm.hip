@@ -1015,6 +1015,24 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 int attempt = 0;
                 for (;;) {
                     ok = riccati_s_sweep(S, N, RR);
+#ifdef DART_RESTO_TRACE
+                    if (blockIdx.x == 0 && it <= 0 && attempt < 3) {
+                        bool fin = true;
+                        if (uon) {
+                            for (int e = 0; e < LmLds::NTP; ++e) fin = fin && isfinite(Hk[e]);
+                            for (int e = 0; e < LmLds::ND * NC; ++e) fin = fin && isfinite(Mk[e]);
+                        }
+                        const double q = S->G[sl][hp(5, 5)];
+                        const bool qbad = uon && !(q > 0.0 && isfinite(q));
+                        const unsigned long long nf = __ballot(!fin), nq = __ballot(qbad);
+                        if (lane == 0)
+                            printf("  it %d attempt %d delta %.2e ok %d  lanes with non-finite H/M %llx  lanes with Quu<=0 %llx\n",
+                                   it, attempt, delta, (int)ok, nf, nq);
+                        if (qbad && (nq & ((1ull << lane) - 1)) == 0)
+                            printf("    first bad lane %d (node %d half %d) Quu %.3e  H diag %.3e %.3e %.3e %.3e %.3e %.3e\n", lane, k,
+                                   hf, q, Hk[hp(0, 0)], Hk[hp(1, 1)], Hk[hp(2, 2)], Hk[hp(3, 3)], Hk[hp(4, 4)], Hk[hp(5, 5)]);
+                    }
+#endif
                     if (ok || soc >= 0 || ++attempt >= 60) break;
                     delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))   // IPOPT perturb_dec_fact 1/3
                                            : delta * (delta_last == 0.0 ? 100.0 : 8.0);
