@@ -252,3 +252,53 @@ def kkt_certificate(prob: RMPCProblem, w, p, act_tol=1e-6):
 # R6 / driver loop pieces ---------------------------------------------------
 RMPC_DEFAULTS = dict(N=20, Qp=80.0, Qv=2.0, Ru=0.02, Rdu=1.0, u_bounds=(-0.6, 0.6), du_bounds=(-0.06, 0.06),
                      vmax=0.2, v_eps=0.1)       # rob_ctrl.py:281-284
+
+
+# Restoration certificate ---------------------------------------------------
+# IPOPT ends at Infeasible_Problem_Detected (status 2) when its restoration problem converges: the point is
+# then a stationary point of the l1 constraint violation.  Solver-independent check: the l1 violation of the
+# linearised rows cannot decrease within a small box around the point (an LP), while at a point where the
+# filter line search merely failed it can.
+def l1_model(w, x0, up, th, prm, N=20, Ts=0.002):
+    """rows of the reference NLP at w: equality values c (x0 pin + RK4 defects) with Jacobian Jc, inequality values g with
+    bounds (lb, ub) and Jacobian Jg (du rows, velocity caps), over w = [X (4(N+1)), U (2N)]"""
+    nX, n = 4 * (N + 1), 4 * (N + 1) + 2 * N
+    X = w[:nX].reshape(N + 1, 4); U = w[nX:].reshape(N, 2)
+    c = [X[0] - x0]; Jc = [np.hstack([np.eye(4), np.zeros((4, n - 4))])]
+    for k in range(N):
+        f = lambda xu: rk4(xu[:4], xu[4:], th, prm[9], Ts)
+        xu = np.concatenate([X[k], U[k]]); h = 1e-7
+        Jf = np.stack([(f(xu + h * e) - f(xu - h * e)) / (2 * h) for e in np.eye(6)], 1)
+        c.append(X[k + 1] - f(xu))
+        J = np.zeros((4, n)); J[:, 4 * (k + 1):4 * (k + 2)] = np.eye(4)
+        J[:, 4 * k:4 * k + 4] -= Jf[:, :4]; J[:, nX + 2 * k:nX + 2 * k + 2] -= Jf[:, 4:]
+        Jc.append(J)
+    g, lb, ub, Jg = [], [], [], []
+    for k in range(N):
+        for a in range(2):
+            row = np.zeros(n); row[nX + 2 * k + a] = 1
+            if k > 0: row[nX + 2 * (k - 1) + a] = -1
+            g.append(U[k, a] - (up[a] if k == 0 else U[k - 1, a])); lb.append(prm[6]); ub.append(prm[7]); Jg.append(row)
+        for j in (1, 3):
+            row = np.zeros(n); row[4 * k + j] = 1
+            g.append(X[k, j]); lb.append(-prm[8]); ub.append(prm[8]); Jg.append(row)
+    return np.concatenate(c), np.vstack(Jc), np.array(g), np.array(lb), np.array(ub), np.array(Jg)
+
+def l1_stationarity(w, x0, up, th, prm, N=20, delta=1e-4, relax=1e-8):
+    """decrease of the linearised l1 infeasibility within |d|_inf <= delta, U box kept; and the value at d = 0"""
+    c, Jc, g, lb, ub, Jg = l1_model(w, x0, up, th, prm, N)
+    lb = lb - relax * np.maximum(1, np.abs(lb)); ub = ub + relax * np.maximum(1, np.abs(ub))
+    n, me, mi = w.size, c.size, g.size
+    # variables [d (n), ep (me), en (me), t (mi)]
+    cost = np.concatenate([np.zeros(n), np.ones(2 * me + mi)])
+    Aeq = np.hstack([Jc, -np.eye(me), np.eye(me), np.zeros((me, mi))]); beq = -c
+    Aub = np.vstack([np.hstack([Jg, np.zeros((mi, 2 * me)), -np.eye(mi)]),
+                     np.hstack([-Jg, np.zeros((mi, 2 * me)), -np.eye(mi)])])
+    bub = np.concatenate([ub - g, g - lb])
+    ulo, uhi = prm[4] - relax, prm[5] + relax
+    nX = 4 * (N + 1)
+    bounds = [(-delta, delta)] * nX + [(max(-delta, ulo - w[i]), min(delta, uhi - w[i])) for i in range(nX, n)] + [(0, None)] * (2 * me + mi)
+    from scipy.optimize import linprog
+    res = linprog(cost, A_ub=Aub, b_ub=bub, A_eq=Aeq, b_eq=beq, bounds=bounds, method='highs')
+    base = np.abs(c).sum() + np.maximum(0, g - ub).sum() + np.maximum(0, lb - g).sum()
+    return base - res.fun, base

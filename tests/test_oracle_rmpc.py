@@ -134,3 +134,51 @@ def test_second_order_correction_never_engages_on_c3():
         np.testing.assert_array_equal(a["u0"], b["u0"])
         np.testing.assert_array_equal(a["iters"], b["iters"])
         np.testing.assert_array_equal(a["status"], b["status"])
+
+
+def _spread_batch(n_seeds, factor):
+    """C3-type instances with the measured velocities scaled: a |v| above vmax at node 0 (x_0 pinned,
+    np_mpc...:88-91, caps at every node :123-127) makes the NLP locally infeasible."""
+    from dart_mpc.workload import rmpc_batch
+    D = rmpc_batch(n_seeds, seed0=0)
+    D["x0"] = D["x0"].copy()
+    D["x0"][:, [1, 3]] *= factor
+    return D
+
+
+def test_restoration_phase_leaves_feasible_solves_unchanged():
+    """IPOPT's soft restoration and restoration phases (default on) never engage on the C3 batch: every
+    solve is bit-identical with the phases off (720 instances)."""
+    from dart_mpc.workload import rmpc_batch
+    D = rmpc_batch(40, seed0=0)
+    args = (D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
+    on = oracle_lib.rmpc_solve_batch(*args, nthreads=8, want_w=False)
+    off = oracle_lib.rmpc_solve_batch(*args, nthreads=8, want_w=False, resto=False)
+    for k in ("u0", "iters", "status"):
+        np.testing.assert_array_equal(on[k], off[k])
+    assert np.all(on["status"] == 0)
+
+
+def test_restoration_phase_on_infeasible_starts():
+    """Measured velocities 2x the C3 spread (72 instances, about half of them above vmax at node 0).  With
+    the phases off the filter line search fails there (-2); IPOPT's restoration phase (oracle/rmpc_ipm.c,
+    MinC_1NrmRestorationPhase) instead converges to a point of local infeasibility, status 2
+    (Infeasible_Problem_Detected), and never fails.  Solver-independent check (rmpc_nlp.l1_stationarity): at
+    the returned point the linearised l1 violation cannot decrease within |d| <= 1e-4 (LP decrease <= 1e-7;
+    observed <= 2e-8), at the failed line search's point it can (>= 1e-4; observed >= 4.6e-4), and the
+    violation is lower there.  Instances the line search solves are unchanged."""
+    D = _spread_batch(4, 2.0)
+    args = (D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
+    on = oracle_lib.rmpc_solve_batch(*args, nthreads=8)
+    off = oracle_lib.rmpc_solve_batch(*args, nthreads=8, resto=False)
+    failed = off["status"] == -2
+    assert failed.sum() >= 20 and set(np.unique(off["status"])) <= {0, -2}
+    assert np.all(on["status"][failed] == 2), on["status"][failed]
+    for k in ("u0", "iters", "status"):
+        np.testing.assert_array_equal(on[k][~failed], off[k][~failed])
+    assert np.all(on["iters"][failed] > off["iters"][failed]) and on["iters"].max() <= 200
+    for i in np.nonzero(failed)[0][:12]:
+        p = (D["x0"][i], D["u_prev"][i], D["theta"][i], D["prm"][i])
+        dec_on, th_on = rmpc_nlp.l1_stationarity(on["w"][i], *p)
+        dec_off, th_off = rmpc_nlp.l1_stationarity(off["w"][i], *p)
+        assert dec_on <= 1e-7 and dec_off >= 1e-4 and th_on < th_off, (i, dec_on, dec_off, th_on, th_off)
