@@ -206,3 +206,27 @@ def test_same_path_as_oracle(dm, soc):
     assert np.array_equal(g["status"], o["status"])
     assert np.mean(g["iters"] == o["iters"]) >= 0.99, (g["iters"], o["iters"])
     assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6
+
+
+def test_infeasible_starts_match_oracle_without_restoration(dm):
+    """Measured velocities 2x the C3 spread (72 instances; |v| above vmax at the pinned node 0 makes the NLP
+    locally infeasible).  The kernel has no restoration phase yet: it follows the oracle with IPOPT's
+    restoration phases off (oracle_lib resto=False) -- same statuses (-2 where the filter line search fails,
+    0 elsewhere), same iterations and controls -- where IPOPT and the oracle with the phases on
+    (test_oracle_rmpc.py::test_restoration_phase_on_infeasible_starts) end at status 2 instead."""
+    from dart_mpc.workload import rmpc_batch
+    D = rmpc_batch(4, seed0=0)
+    D["x0"] = D["x0"].copy()
+    D["x0"][:, [1, 3]] *= 2.0
+    s = dm.RmpcSolver(N=20, tol=1e-8, B_max=256)
+    g = s.solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
+    s.close()
+    args = (D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
+    off = oracle_lib.rmpc_solve_batch(*args, N=20, tol=1e-8, nthreads=8, resto=False)
+    on = oracle_lib.rmpc_solve_batch(*args, N=20, tol=1e-8, nthreads=8, want_w=False)
+    assert (off["status"] == -2).sum() >= 20
+    assert np.array_equal(g["status"], off["status"])
+    assert np.mean(g["iters"] == off["iters"]) >= 0.95, (g["iters"], off["iters"])
+    ok = off["status"] == 0
+    assert np.max(np.abs(g["u0"][ok] - off["u0"][ok])) <= 1e-6
+    assert np.all(on["status"][off["status"] == -2] == 2)
