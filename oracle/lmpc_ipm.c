@@ -236,8 +236,11 @@ typedef struct resto_s {
     double M[NMAX + 1][NA][NA], Pt[NMAX + 1][NA][NA];
     double filt_th[256], filt_ph[256];
     double pt_[NA * (NMAX + 1)], nt_[NA * (NMAX + 1)];    /* trial p, n */
-    double rho, eta;
+    double rho, eta, delta;
     const double *dsc;
+    /* iterative refinement (resto_refine): residuals of the full Newton system, gradient override */
+    int ovr;
+    double gov[NMAX + 1][NZ], ex[NMAX + 1][NZ], ec[NMAX + 1][NA], ep[NA * (NMAX + 1)], en[NA * (NMAX + 1)];
 } resto_t;
 
 /* solve A X = B (n x n, nrhs columns of B stored row-major with stride NA + 1 ... ) by Gaussian
@@ -423,6 +426,7 @@ static void stage_qp(const ctx_t *C, const work_t *W, int k, double delta, doubl
             }
         }
         if (C->mode == 1) for (int a = 0; a < NZ; ++a) Hq[a][a] += delta;
+        if (R->ovr) for (int j = 0; j < NZ; ++j) gq[j] = R->gov[k][j];
         return;
     }
     for (int a = 0; a < NZ; ++a) for (int b = 0; b < NZ; ++b) Hq[a][b] = W->Hs[k][a][b];
@@ -456,6 +460,7 @@ static void terminal_qp(const ctx_t *C, const work_t *W, double delta, double Pn
             pn[i] = w * (W->X[r] - R->XR[r]);
         }
         if (C->mode == 1) { Pn[8][8] = delta; Pn[9][9] = delta; }
+        if (R->ovr) for (int i = 0; i < NA; ++i) pn[i] = R->gov[N][i];
         return;
     }
     double zN[NZ], gN[NZ];
@@ -853,6 +858,91 @@ static void resto_errors(const ctx_t *C, const work_t *W, double cres[][NA], dou
     *dinf_ = dinf; *pinf_ = pinf; *c0_ = c0; *cmin_ = cmin; *sum_l_ = sum_l; *sum_z_ = sum_z;
 }
 
+/* Iterative refinement of the restoration step (IPOPT refines every solve of its augmented system,
+   PDFullSpaceSolver; the GPU kernel refines its restoration steps the same way): the residuals of the full
+   Newton system at the step in V / R (stationarity of x and u, the scaled defect rows d J dx + dn - dp + c,
+   the p / n rows) are solved for on the same factorisation when they exceed 1e-12 (1 + |step|) (lam = 0
+   and the residuals in place of the gradients and right-hand sides), and the correction is added; at most
+   g_resto_refine times per step.  Returns 1 if a correction was made. */
+static int g_resto_refine = 3;
+void oracle_lmpc_set_resto_refine(int n) { g_resto_refine = n < 0 ? 0 : n; }
+static int resto_refine(const ctx_t *C, work_t *V, double cres[][NA], double rg[][NA]) {
+    resto_t *R = C->R; const prob_t *P = C->P; const int N = P->N, nA = NA * (N + 1), nU = NU * N;
+    double emax = 0.0, smax = 0.0;
+#define EM(v) (emax = fmax(emax, fabs(v)))
+#define SM(v) (smax = fmax(smax, fabs(v)))
+    for (int k = 0; k < N; ++k) {
+        double Hq[NZ][NZ], gq[NZ], dz[NZ];
+        stage_qp(C, V, k, R->delta, Hq, gq);
+        for (int a = 0; a < NA; ++a) dz[a] = V->dX[NA * k + a];
+        dz[10] = V->dU[NU * k]; dz[11] = V->dU[NU * k + 1];
+        for (int a = 0; a < NZ; ++a) { double t = gq[a]; for (int b = 0; b < NZ; ++b) t += Hq[a][b] * dz[b]; R->ex[k][a] = t; }
+        for (int i = 0; i < NA; ++i) R->ex[k][i] += V->lamp[NA * k + i];
+        for (int m = 0; m < NA; ++m) {
+            const double l = V->lamp[NA * (k + 1) + m];
+            for (int i = 0; i < NA; ++i) R->ex[k][i] -= V->A[k][m][i] * l;
+            R->ex[k][10] -= V->Bm[k][m][0] * l; R->ex[k][11] -= V->Bm[k][m][1] * l;
+        }
+        for (int a = 0; a < NZ; ++a) EM(R->ex[k][a]);
+    }
+    {
+        double Pn[NA][NA], pn[NA];
+        terminal_qp(C, V, R->delta, Pn, pn);
+        for (int i = 0; i < NZ; ++i) R->ex[N][i] = 0.0;
+        for (int i = 0; i < NA; ++i) {
+            double t = pn[i] + V->lamp[NA * N + i];
+            for (int j = 0; j < NA; ++j) t += Pn[i][j] * V->dX[NA * N + j];
+            R->ex[N][i] = t;
+            EM(t);
+        }
+    }
+    for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) {
+        const int r = NA * k + i;
+        double jd = V->dX[r];
+        if (k > 0) {
+            for (int m = 0; m < NA; ++m) jd -= V->A[k - 1][i][m] * V->dX[NA * (k - 1) + m];
+            for (int a = 0; a < NU; ++a) jd -= V->Bm[k - 1][i][a] * V->dU[NU * (k - 1) + a];
+        }
+        SM(V->dX[r]);
+        if (i < 8) {
+            const double d = R->dsc[r], dy = (V->lamp[r] - V->lam[r]) / d;
+            R->ec[k][i] = d * jd + R->dnc[r] - R->dpc[r] + cres[k][i];
+            R->ep[r] = R->Spd[r] * R->dpc[r] - dy + R->rp[r];
+            R->en[r] = R->Snd[r] * R->dnc[r] + dy + R->rn[r];
+            EM(R->ep[r]); EM(R->en[r]); SM(R->dpc[r]); SM(R->dnc[r]);
+        } else {
+            R->ec[k][i] = jd + cres[k][i];
+        }
+        EM(R->ec[k][i]);
+    }
+    for (int j = 0; j < nU; ++j) SM(V->dU[j]);
+#undef EM
+#undef SM
+    if (!(emax > 1e-12 * (1.0 + smax))) return 0;
+    work_t *Sv = (work_t *)malloc(sizeof(work_t));
+    resto_t *SR = (resto_t *)malloc(sizeof(resto_t));
+    memcpy(Sv, V, sizeof(work_t)); memcpy(SR, R, sizeof(resto_t));
+    memset(V->lam, 0, sizeof(double) * nA);
+    for (int i = 0; i < nA; ++i) { R->rp[i] = R->ep[i]; R->rn[i] = R->en[i]; }
+    R->ovr = 1;
+    memcpy(R->gov, R->ex, sizeof(double[NZ]) * (N + 1));
+    resto_rhs(C, V, R->ec, rg);
+    riccati_solve(C, V, rg);
+    for (int i = 0; i < nA; ++i) {
+        Sv->dX[i] += V->dX[i];
+        Sv->lamp[i] += V->lamp[i];
+        if ((i % NA) < 8) {
+            const double dy = V->lamp[i] / R->dsc[i];
+            SR->dpc[i] += (dy - R->ep[i]) / R->Spd[i];
+            SR->dnc[i] += (-dy - R->en[i]) / R->Snd[i];
+        }
+    }
+    for (int j = 0; j < nU; ++j) Sv->dU[j] += V->dU[j];
+    memcpy(V, Sv, sizeof(work_t)); memcpy(R, SR, sizeof(resto_t));
+    free(Sv); free(SR);
+    return 1;
+}
+
 static int restoration(const ctx_t *C0, work_t *W, int *it_io, int max_iter, double tol, double acc_tol, int acc_iter,
                        double th0, double phi0, int nfilt0, double tau0, double g0[][NA], int *status) {
     const prob_t *P = C0->P; const int N = P->N, nU = NU * N, nA = NA * (N + 1), nrow = 8 * (N + 1);
@@ -962,16 +1052,20 @@ static int restoration(const ctx_t *C0, work_t *W, int *it_io, int max_iter, dou
         }
         if (!ok) { *status = ST_INERTIA_FAIL; break; }
         if (delta > 0) delta_last = delta;
+        R->delta = delta;
         /* the step: Riccati for the soft rows, then p, n and every bound multiplier */
         double amax = 0, az = 0;
         #define RESTO_STEP(CV) do {                                                                   \
             resto_rhs(&C, V, CV, rg);                                                                 \
             riccati_solve(&C, V, rg);                                                                 \
-            amax = frac_to_boundary(&C, V, V->dU, tau); az = 1.0;                                     \
             for (int r = 0; r < nA; ++r) if ((r % NA) < 8) {                                         \
                 const double dy = (V->lamp[r] - V->lam[r]) / W->dsc[r];                               \
                 R->dpc[r] = (dy - R->rp[r]) / R->Spd[r];                                              \
                 R->dnc[r] = (-dy - R->rn[r]) / R->Snd[r];                                             \
+            }                                                                                         \
+            for (int rr_ = 0; rr_ < g_resto_refine && resto_refine(&C, V, CV, rg); ++rr_) {}          \
+            amax = frac_to_boundary(&C, V, V->dU, tau); az = 1.0;                                     \
+            for (int r = 0; r < nA; ++r) if ((r % NA) < 8) {                                         \
                 R->dzp[r] = C.mu / R->pc[r] - R->zp[r] - R->zp[r] / R->pc[r] * R->dpc[r];             \
                 R->dzn[r] = C.mu / R->nc[r] - R->zn[r] - R->zn[r] / R->nc[r] * R->dnc[r];             \
                 if (R->dpc[r] < 0) amax = fmin(amax, -tau * R->pc[r] / R->dpc[r]);                    \

@@ -153,6 +153,8 @@ def llib():
         L.oracle_lmpc_set_soft_resto.restype = None
         L.oracle_lmpc_set_resto.argtypes = [ctypes.c_int]
         L.oracle_lmpc_set_resto.restype = None
+        L.oracle_lmpc_set_resto_refine.argtypes = [ctypes.c_int]
+        L.oracle_lmpc_set_resto_refine.restype = None
         L.oracle_lmpc_rk4.argtypes = [ctypes.c_int, ctypes.c_double, _dp, _dp, _dp, _dp]
         L.oracle_lmpc_rk4.restype = None
         _llib = L
@@ -167,9 +169,10 @@ LMPC_PRM_DEFAULT = np.array([200.0, 2.0, 200.0, 2.0, 0.0, 0.0, 0.0, 0.0,      # 
 
 def lmpc_solve_batch(state, u_prev, pvec, target, prm=None, N=20, Ts=0.002, w_init=None, max_iter=50, tol=1e-4,
                      acc_tol=1e-3, acc_iter=5, nthreads=1, want_w=True, relax=1e-8, soc=True, mult_init_max=1000.0,
-                     resto=True):
+                     resto=True, resto_refine=3):
     """LMPC oracle; defaults are the reference's IPOPT options (rlmpc2.py:480-489).  resto=False turns
-    IPOPT's soft restoration and restoration phases off (a failed line search then ends with status -2)."""
+    IPOPT's soft restoration and restoration phases off (a failed line search then ends with status -2);
+    resto_refine caps the iterative-refinement solves per restoration step (0: none)."""
     c = lambda a: np.ascontiguousarray(a, np.float64)
     state, u_prev, pvec, target = c(state), c(u_prev), c(pvec), c(target)
     B = state.shape[0]
@@ -183,6 +186,7 @@ def lmpc_solve_batch(state, u_prev, pvec, target, prm=None, N=20, Ts=0.002, w_in
     llib().oracle_lmpc_set_mult_init_max(ctypes.c_double(float(mult_init_max)))
     llib().oracle_lmpc_set_soft_resto(int(bool(resto)))
     llib().oracle_lmpc_set_resto(int(bool(resto)))
+    llib().oracle_lmpc_set_resto_refine(int(resto_refine))
     llib().oracle_lmpc_solve_batch(B, N, Ts, _p(state), _p(u_prev), _p(pvec), _p(target), _p(prm),
                                    _p(wi) if wi is not None else None, max_iter, tol, acc_tol, acc_iter, nthreads,
                                    _p(u0), _p(f), _p(w) if want_w else None, _p(st, _ip), _p(it, _ip))
