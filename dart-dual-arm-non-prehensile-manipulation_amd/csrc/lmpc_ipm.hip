@@ -841,6 +841,11 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         if (it >= a.max_iter) { status = -1; break; }
         // IPOPT Maximum_CpuTime_Exceeded (not during the least-square estimate: IPOPT's initialisation)
         if (__builtin_expect(!lsm && out_of_time(), 0)) { status = -4; break; }
+#ifdef DART_RESTO_TRACE
+        if (lane == 0 && !lsm)
+            printf("it %3d mu %.2e err %.2e dinf %.2e pinf %.2e c0 %.2e cmin %.2e suml %.3e sumz %.3e theta %.3e\n", it, mu, err,
+                   dinf * is_d, pinf, c0 * is_c, cminw, suml, sumz, theta);
+#endif
         for (; !lsm;) {
             const double cmu = fmax(c0 - mu, mu - cminw);
             if (fmax(dinf * is_d, fmax(pinf, cmu * is_c)) > 10.0 * mu || mu <= mu_min) break;

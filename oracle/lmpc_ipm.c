@@ -622,6 +622,14 @@ static double ls_multipliers(const ctx_t *C, work_t *W) {
             for (int j = 0; j < NA; ++j) Ps[k][i][j] = Qxx[i][j] + Qux[0][i] * Ks[k][0][j] + Qux[1][i] * Ks[k][1][j];
             ps[k][i] = qx[i] + Qux[0][i] * ks[k][0] + Qux[1][i] * ks[k][1];
         }
+        /* symmetric as riccati_factor keeps it: unsymmetrised rounding let the unit-weight recursion lose its
+           positive definiteness on unstable dynamics (Quu < 0 at k = 16 of a C5 stress instance) and overflow,
+           where the dense least-squares solution is moderate (max |y| 547) */
+        for (int i = 0; i < NA; ++i) for (int j = 0; j < i; ++j) { const double t = 0.5 * (Ps[k][i][j] + Ps[k][j][i]); Ps[k][i][j] = Ps[k][j][i] = t; }
+#ifdef ORACLE_DEBUG
+        { double pm = 0, qm = 0; for (int i = 0; i < NA; ++i) { qm = fmax(qm, fabs(ps[k][i])); for (int j = 0; j < NA; ++j) pm = fmax(pm, fabs(Ps[k][i][j])); }
+          fprintf(stderr, "  lsq k %2d max|P| %.3e max|p| %.3e Quu %.3e %.3e %.3e\n", k, pm, qm, Quu[0][0], Quu[0][1], Quu[1][1]); }
+#endif
     }
     double dx[NA] = {0}, ymax = 0.0;
     for (int k = 0; k <= N; ++k) {
@@ -1333,7 +1341,11 @@ int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_pre
     }
 
     if (g_mult_init_max > 0.0) {
-        if (!(ls_multipliers(&C, W) <= g_mult_init_max)) memset(W->lam, 0, sizeof(double) * nA);
+        const double ym = ls_multipliers(&C, W);
+#ifdef ORACLE_DEBUG
+        fprintf(stderr, "least-square multipliers: max |y| %.6e (constr_mult_init_max %.0f)\n", ym, g_mult_init_max);
+#endif
+        if (!(ym <= g_mult_init_max)) memset(W->lam, 0, sizeof(double) * nA);
         linearise(&P, W);      /* the Lagrangian Hessian of iteration 0 with these multipliers */
     }
     double (*g)[NA] = (double (*)[NA])calloc(N + 1, sizeof(double[NA]));

@@ -351,7 +351,7 @@ static double ls_multipliers(const ctx_t *C, work_t *W, double *y) {
     memcpy(Ps[N], Pm, sizeof Pm); memcpy(ps[N], pv, sizeof pv);
     for (int k = N - 1; k >= 0; --k) {
         double (*A)[NX] = W->A[k], (*Bm)[NU] = W->Bm[k];
-        double PA[NX][NX], PB[NX][NU], Qxx[NX][NX], Qux[NU][NX], Quu[NU][NU], qx[NX], qu[NU], L[3];
+        double PA[NX][NX], PB[NX][NU], Qxx[NX][NX], Qux[NU][NX], Quu[NU][NU], qx[NX], qu[NU], L[3] = {1, 0, 1};
         for (int i = 0; i < NX; ++i) {
             for (int j = 0; j < NX; ++j) { double t = 0; for (int m = 0; m < NX; ++m) t += Ps[k + 1][i][m] * A[m][j]; PA[i][j] = t; }
             for (int j = 0; j < NU; ++j) { double t = 0; for (int m = 0; m < NX; ++m) t += Ps[k + 1][i][m] * Bm[m][j]; PB[i][j] = t; }
@@ -380,6 +380,7 @@ static double ls_multipliers(const ctx_t *C, work_t *W, double *y) {
             for (int j = 0; j < NX; ++j) Ps[k][i][j] = Qxx[i][j] + Qux[0][i] * Ks[k][0][j] + Qux[1][i] * Ks[k][1][j];
             ps[k][i] = qx[i] + Qux[0][i] * ks[k][0] + Qux[1][i] * ks[k][1];
         }
+        for (int i = 0; i < NX; ++i) for (int j = 0; j < i; ++j) { const double t = 0.5 * (Ps[k][i][j] + Ps[k][j][i]); Ps[k][i][j] = Ps[k][j][i] = t; }
     }
     double dx[NX] = {0}, ymax = 0.0;
     for (int k = 0; k <= N; ++k) {

@@ -700,6 +700,7 @@ static double ls_multipliers(const ctx_t *C, work_t *W) {
             for (int j = 0; j < NA; ++j) Ps[k][i][j] = Qxx[i][j] + Qux[0][i] * Ks[k][0][j] + Qux[1][i] * Ks[k][1][j];
             ps[k][i] = qx[i] + Qux[0][i] * ks[k][0] + Qux[1][i] * ks[k][1];
         }
+        for (int i = 0; i < NA; ++i) for (int j = 0; j < i; ++j) { const double t = 0.5 * (Ps[k][i][j] + Ps[k][j][i]); Ps[k][i][j] = Ps[k][j][i] = t; }
     }
     double dx[NA] = {0}, ymax = 0.0;
     for (int k = 0; k <= N; ++k) {

@@ -140,3 +140,37 @@ def test_restoration_reports_local_infeasibility():
     assert np.all(on["status"] == 2), on["status"]
     assert np.all(off["status"] == -2), off["status"]
     assert np.all(on["iters"] > off["iters"]) and np.all(on["iters"] <= 50)
+
+
+def test_least_square_multipliers_match_dense_solve():
+    """IPOPT's least-square starting multipliers (constr_mult_init_max 1000) on an unstable C5 stress draw
+    (instance 13542 of the parity sweep): the dense solution of [I J^T; J 0] [d; y] = [-r; 0] at the start point
+    (numpy lstsq, IPOPT's gradient-based row scaling) has max |y| = 547, below the cap, so IPOPT keeps the
+    estimate.  The oracle's Riccati recursion once overflowed there (an unsymmetrised P lost its positive
+    definiteness) and started from zero multipliers.  Pinned through the cap itself: just above the dense
+    max |y| the oracle's path differs from the zero-multiplier path, just below it is identical."""
+    from dart_mpc.workload import lmpc_batch
+    i = 13542
+    D = lmpc_batch(1, seed0=100000 + i // 18)
+    j = i % 18
+    args = [D[k][j:j + 1] for k in ("state", "u_prev", "pvec", "target")]
+    prm = oracle_lib.LMPC_PRM_DEFAULT
+    N = 30
+    prob = _prob(N, prm)
+    p = np.concatenate([a[0] for a in args])
+    w = np.zeros(prob.nw)                                    # the cold start (u = 0 is inside the box)
+    g = prob.objective_grad(w, p)
+    sc = 100.0 / np.abs(g).max() if np.abs(g).max() > 100.0 else 1.0
+    J = prob.constraint_jac(w, p)
+    d = np.ones(prob.ng)
+    for r in range(8, prob.ng):
+        m = max(1.0, np.abs(J[r]).max())
+        d[r] = 100.0 / m if m > 100.0 else 1.0
+    ys = np.linalg.lstsq((d[:, None] * J).T, -sc * g, rcond=None)[0]     # z_L = z_U = 1 cancel on u
+    ymax = np.abs(ys).max()
+    assert 100.0 < ymax < 1000.0, ymax
+    run = lambda cap: oracle_lib.lmpc_solve_batch(*args, N=N, nthreads=1, max_iter=3, mult_init_max=cap)
+    zero = run(0.0)
+    above, below = run(ymax * (1 + 1e-6)), run(ymax * (1 - 1e-6))
+    assert not np.array_equal(above["w"], zero["w"])
+    assert np.array_equal(below["w"], zero["w"])
