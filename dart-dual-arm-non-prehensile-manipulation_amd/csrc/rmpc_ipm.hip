@@ -59,10 +59,12 @@ struct RmShared {
 };
 
 // continuous model (np_mpc...:178-186); also returns d f / d vx|vy of rows 1, 3 and tanh values
+// (the node lane k evaluates tanh(vx / v_eps), its mirror lane k + 32 tanh(vy / v_eps) of the same node,
+// and the pair exchange both: one tanh per lane instead of two, the same bits; EXEC must be full)
 __device__ __forceinline__ void rm_f(const RmModel& m, const double* y, double sa, double sb, double* f,
-                                     double& j1vx, double& j1vy, double& j3vx, double& j3vy, double& tx, double& ty) {
-    tx = tanh_econ(y[1] * m.ie);
-    ty = tanh_econ(y[3] * m.ie);
+                                     double& j1vx, double& j1vy, double& j3vx, double& j3vy, double& tx, double& ty,
+                                     bool mir) {
+    half_pair(tanh_econ((mir ? y[3] : y[1]) * m.ie), tx, ty);
     const double* a = m.th;
     const double* c = m.th + 7;
     f[0] = y[1];
@@ -75,19 +77,19 @@ __device__ __forceinline__ void rm_f(const RmModel& m, const double* y, double s
 }
 
 // RK4 value (np_mpc...:188-193)
-__device__ __forceinline__ void rm_rk4(const RmModel& mlds, const double* x, double sa, double sb, double* xn) {
+__device__ __forceinline__ void rm_rk4(const RmModel& mlds, const double* x, double sa, double sb, double* xn, bool mir) {
     const RmModel m = mlds;     // model to registers once (LDS round trips off the stage chains)
     double k[4], y[4], acc[4], d0, d1, d2, d3, tx, ty;
-    rm_f(m, x, sa, sb, k, d0, d1, d2, d3, tx, ty);
+    rm_f(m, x, sa, sb, k, d0, d1, d2, d3, tx, ty, mir);
 #pragma unroll
     for (int i = 0; i < 4; ++i) { acc[i] = k[i]; y[i] = x[i] + m.h / 2 * k[i]; }
-    rm_f(m, y, sa, sb, k, d0, d1, d2, d3, tx, ty);
+    rm_f(m, y, sa, sb, k, d0, d1, d2, d3, tx, ty, mir);
 #pragma unroll
     for (int i = 0; i < 4; ++i) { acc[i] += 2 * k[i]; y[i] = x[i] + m.h / 2 * k[i]; }
-    rm_f(m, y, sa, sb, k, d0, d1, d2, d3, tx, ty);
+    rm_f(m, y, sa, sb, k, d0, d1, d2, d3, tx, ty, mir);
 #pragma unroll
     for (int i = 0; i < 4; ++i) { acc[i] += 2 * k[i]; y[i] = x[i] + m.h * k[i]; }
-    rm_f(m, y, sa, sb, k, d0, d1, d2, d3, tx, ty);
+    rm_f(m, y, sa, sb, k, d0, d1, d2, d3, tx, ty, mir);
 #pragma unroll
     for (int i = 0; i < 4; ++i) xn[i] = x[i] + m.h / 6 * (acc[i] + k[i]);
 }
@@ -95,7 +97,7 @@ __device__ __forceinline__ void rm_rk4(const RmModel& mlds, const double* x, dou
 // Value pass of RK4 storing per stage s the tangent coefficients sc[s] = [d f1/d vx, d f1/d vy,
 // d f3/d vx, d f3/d vy] and the tanh curvature sd[s] = [T''(vx), T''(vy)] (T = tanh(v / v_eps)).
 __device__ __forceinline__ void rm_rk4_lin(const RmModel& mlds, const double* x, double sa, double sb, double* xn,
-                                           double (*sc)[4], double (*sd)[2]) {
+                                           double (*sc)[4], double (*sd)[2], bool mir) {
     const RmModel m = mlds;     // model to registers once
     double y[4], acc[4];
 #pragma unroll
@@ -104,7 +106,7 @@ __device__ __forceinline__ void rm_rk4_lin(const RmModel& mlds, const double* x,
     for (int s = 0; s < 4; ++s) {
         const double wts = (s == 0 || s == 3) ? 1.0 : 2.0, cst = s < 2 ? 0.5 : (s == 2 ? 1.0 : 0.0);
         double k[4], j1vx, j1vy, j3vx, j3vy, tx, ty;
-        rm_f(m, y, sa, sb, k, j1vx, j1vy, j3vx, j3vy, tx, ty);
+        rm_f(m, y, sa, sb, k, j1vx, j1vy, j3vx, j3vy, tx, ty, mir);
         sc[s][0] = j1vx; sc[s][1] = j1vy; sc[s][2] = j3vx; sc[s][3] = j3vy;
         sd[s][0] = -2.0 * tx * (1.0 - tx * tx) * m.ie * m.ie;
         sd[s][1] = -2.0 * ty * (1.0 - ty * ty) * m.ie * m.ie;
@@ -374,11 +376,18 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         return xon ? f + (uon ? Ru * (uu[0] * uu[0] + uu[1] * uu[1]) + Rdu * (d0 * d0 + d1 * d1) : 0.0) : 0.0;
     };
     // incoming defect g_k of node k (6 rows: physical 4 + up copy 2) for a trial point
+    // sin / cos of both tilts of a node: the node lane takes alpha, its mirror lane beta, the pair
+    // exchange both (the same bits as two evaluations per lane)
+    auto rm_sincos2 = [&](const double* uu, double& sa, double& ca, double& sb, double& cb) {
+        double s_, c_;
+        tilt_sincos_econ(poly, mir ? uu[1] : uu[0], s_, c_);
+        half_pair(s_, sa, sb);
+        half_pair(c_, ca, cb);
+    };
     auto defects = [&](const double* xx, const double* pp, const double* uu, double* g) {
         double sa, ca, sb, cb, xn[4];
-        tilt_sincos_econ(poly, uu[0], sa, ca);
-        tilt_sincos_econ(poly, uu[1], sb, cb);
-        rm_rk4(m, xx, sa, sb, xn);
+        rm_sincos2(uu, sa, ca, sb, cb);
+        rm_rk4(m, xx, sa, sb, xn, mir);
         double f[6];
 #pragma unroll
         for (int i = 0; i < 4; ++i) f[i] = from_prev(xn[i]);
@@ -438,12 +447,11 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         double jl[6];            // J^T lambda_{k+1} (x columns 0..3, tilt 4..5)
         {
             double sa, ca, sb, cb;
-            tilt_sincos_econ(poly, u[0], sa, ca);
-            tilt_sincos_econ(poly, u[1], sb, cb);
+            rm_sincos2(u, sa, ca, sb, cb);
             // the RK4 stage data stay in registers through the adjoint and the three directions of
             // this lane (lanes k and k + 32 hold the same node: each has them without an LDS pass)
             double xn[4], huu[2], scr[4][4], sdr[4][2];
-            rm_rk4_lin(m, x, sa, sb, xn, scr, sdr);
+            rm_rk4_lin(m, x, sa, sb, xn, scr, sdr, mir);
             rm_adjoint_curv(m, scr, sdr, lamn, sa, sb, huu);
             STAMP(11);
             // lanes k and k + 32 own directions 0..2 and 3..5 of node k

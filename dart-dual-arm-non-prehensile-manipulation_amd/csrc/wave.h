@@ -105,6 +105,16 @@ __device__ __forceinline__ double half_pair_sum(double x) {
     const double c = __builtin_bit_cast(double, ((unsigned long long)rh[1] << 32) | rl[1]);
     return a + c;
 }
+// both values of a lane pair (l mod 32, l mod 32 + 32) in every lane: lo from lanes 0-31, hi from lanes
+// 32-63, by the same v_permlane32_swap_b32 pair as half_pair_sum (EXEC must be full)
+__device__ __forceinline__ void half_pair(double x, double& lo, double& hi) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+    const unsigned l32 = (unsigned)(b & 0xffffffffu), h32 = (unsigned)(b >> 32);
+    const auto rl = __builtin_amdgcn_permlane32_swap(l32, l32, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(h32, h32, false, false);
+    lo = __builtin_bit_cast(double, ((unsigned long long)rh[0] << 32) | rl[0]);
+    hi = __builtin_bit_cast(double, ((unsigned long long)rh[1] << 32) | rl[1]);
+}
 constexpr int kWaveShl1 = 0x130;   // lane k <- lane k+1 (lane 63 <- 0)
 constexpr int kWaveShr1 = 0x138;   // lane k <- lane k-1 (lane 0 <- 0)
 __device__ __forceinline__ double from_next(double x) { return dpp<kWaveShl1>(x); }
