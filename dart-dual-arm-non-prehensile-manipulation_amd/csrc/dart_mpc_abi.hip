@@ -7,7 +7,9 @@
 
 #include <cstdio>
 #include <cstring>
+#include <chrono>
 #include <mutex>
+#include <vector>
 #include <string>
 
 #include "dart_mpc.h"
@@ -176,6 +178,8 @@ struct dart_mpc_handle {
         uint32_t* mbox = nullptr;          // mapped: the 64-bit request word (pmpc_ipm.h PmpcServe)
         uint32_t* dmbox = nullptr;
         unsigned long long idle_ticks = 0;
+        double idle_s = 0.0;
+        std::chrono::steady_clock::time_point t_post;     // last request posted (or the grid launched)
     } srv;
     // PMPC in-place I/O area (dart_mpc_bind; the resident server's inputs and outputs): mapped,
     // coherent pinned memory for B_max instances at fixed addresses
@@ -189,10 +193,16 @@ struct dart_mpc_handle {
     // reference runs controllers on background threads, RMPC/dev_dual/controller/convimp.py:435)
     // are safe but take turns; one handle per thread runs them side by side.
     std::recursive_mutex mu;     // recursive: the host entries call their _dev twins
-    // LMPC: hand-off area of the instances that enter IPOPT's restoration phases (lmpc_ipm.hip,
-    // [B][64][16] doubles), grown on demand
-    double* resto_buf = nullptr;
-    size_t resto_cap = 0;
+    // LMPC: hand-off areas of the instances that enter IPOPT's restoration phases (lmpc_ipm.hip,
+    // [B][64][16] doubles), one per launch stream -- launches in flight on different streams never share
+    // one -- grown on demand by stream-ordered allocation (the old area is freed behind its last use on
+    // that stream: no device-wide synchronisation, nothing else waits)
+    struct RestoArea {
+        hipStream_t s;
+        double* buf;
+        size_t cap;
+    };
+    std::vector<RestoArea> resto;
 };
 
 namespace {
@@ -284,6 +294,7 @@ hipError_t server_launch(dart_mpc_handle* h, uint32_t seen) {
     dartmpc::PmpcServe sv{v.dmbox, v.idle_ticks};
     const hipError_t e = dartmpc_launch_pmpc_serve(&a, &sv, v.stream);
     v.running = e == hipSuccess;
+    v.t_post = std::chrono::steady_clock::now();
     return e;
 }
 
@@ -300,19 +311,26 @@ int server_stop(dart_mpc_handle* h) {
 
 // settle the stream of an earlier host PMPC call that returned on its completion words (see
 // dart_mpc_handle::pending)
-// the LMPC restoration hand-off area for B instances (device memory; a larger batch than before waits
-// for the device before the old area is freed)
-int lmpc_resto_area(dart_mpc_handle* h, int B) {
+// the LMPC restoration hand-off area for B instances of a launch on stream s (device memory, one area per
+// stream, stream-ordered growth: see dart_mpc_handle::resto)
+int lmpc_resto_area(dart_mpc_handle* h, int B, hipStream_t s, double** out) {
+    *out = nullptr;
     if (!h->cfg.restoration) return DART_MPC_OK;
     const size_t need = (size_t)B * 64 * 16;
-    if (need <= h->resto_cap) return DART_MPC_OK;
-    if (h->resto_buf) {
-        HIPCHK(h, hipDeviceSynchronize(), "hipDeviceSynchronize");
-        (void)hipFree(h->resto_buf);
-        h->resto_buf = nullptr; h->resto_cap = 0;
+    dart_mpc_handle::RestoArea* r = nullptr;
+    for (auto& e : h->resto)
+        if (e.s == s) r = &e;
+    if (!r) {
+        h->resto.push_back({s, nullptr, 0});
+        r = &h->resto.back();
     }
-    HIPCHK(h, hipMalloc((void**)&h->resto_buf, need * sizeof(double)), "hipMalloc (restoration hand-off)");
-    h->resto_cap = need;
+    if (need > r->cap) {
+        if (r->buf) HIPCHK(h, hipFreeAsync(r->buf, s), "hipFreeAsync (restoration hand-off)");
+        r->buf = nullptr; r->cap = 0;
+        HIPCHK(h, hipMallocAsync((void**)&r->buf, need * sizeof(double), s), "hipMallocAsync (restoration hand-off)");
+        r->cap = need;
+    }
+    *out = r->buf;
     return DART_MPC_OK;
 }
 
@@ -357,19 +375,42 @@ int wait_done(dart_mpc_handle* h, hipStream_t s, const volatile uint32_t* done, 
     return DART_MPC_OK;
 }
 
+// the next completion-word sequence of the handle (wraps, skipping 0; on a wrap every word is cleared so that
+// no stale one can match: the words only ever hold 0 or sequences of earlier requests)
+uint32_t next_seq(dart_mpc_handle* h) {
+    if (++h->seq == 0) {
+        std::memset(h->hdone, 0, sizeof(uint32_t) * h->cfg.B_max);
+        h->seq = 1;
+    }
+    return h->seq;
+}
+
 // post a request to the resident server (inputs already in the I/O area) and wait for its B
 // completion words; a grid that drained meanwhile (idle timeout) is relaunched and takes the request
 int served_request(dart_mpc_handle* h, int B, bool ww, bool wo) {
     auto& v = h->srv;
-    if (!v.running || hipStreamQuery(v.stream) != hipErrorNotReady) {     // drained (idle timeout)
-        HIPCHK(h, hipStreamSynchronize(v.stream), "resident server");
-        HIPCHK(h, server_launch(h, v.mbox[0]), "resident server relaunch");
+    // Every wave leaves idle_timeout after the last request it saw, each on its own clock, so near the end of
+    // an idle period part of the grid may have left while the rest still waits (and a request posted then
+    // would reset the waiting waves' timers and wait out a whole idle period for the missing ones).  The host
+    // knows when it posted last: from 90 % of the idle timeout on, it drains the grid itself (stop word) and
+    // relaunches it before posting.  Before that point no wave can have left (each wave's last request is no
+    // older than the host's last post).
+    const double since = std::chrono::duration<double>(std::chrono::steady_clock::now() - v.t_post).count();
+    if (v.running && since > 0.9 * v.idle_s - 0.002) {
+        __atomic_store_n((unsigned long long*)v.mbox, (unsigned long long)v.mbox[0] | (1ull << 56), __ATOMIC_RELEASE);
+        v.running = false;
     }
-    if (++h->seq == 0) h->seq = 1;      // (done words are only compared for equality)
-    const uint32_t sq = h->seq;
+    if (!v.running || hipStreamQuery(v.stream) != hipErrorNotReady) {     // drained (idle timeout or stop)
+        v.running = false;
+        HIPCHK(h, hipStreamSynchronize(v.stream), "resident server");
+        __atomic_store_n((unsigned long long*)v.mbox, (unsigned long long)h->seq, __ATOMIC_RELEASE);   // no stop, no request
+        HIPCHK(h, server_launch(h, h->seq), "resident server relaunch");
+    }
+    const uint32_t sq = next_seq(h);
     const unsigned long long fl = (ww ? 1ull : 0ull) | (wo ? 2ull : 0ull);
     __atomic_store_n((unsigned long long*)v.mbox, (unsigned long long)sq | ((unsigned long long)B << 32) | (fl << 48),
                      __ATOMIC_RELEASE);
+    v.t_post = std::chrono::steady_clock::now();
     for (unsigned n = 1;; ++n) {
         int bb = 0;
         while (bb < B && __atomic_load_n(h->hdone + bb, __ATOMIC_ACQUIRE) == sq) ++bb;
@@ -389,10 +430,7 @@ int served_request(dart_mpc_handle* h, int B, bool ww, bool wo) {
 
 // one launch over the I/O area (no resident server), completion words as the host entry
 int bound_launch(dart_mpc_handle* h, int B, bool ww, bool wo) {
-    if (++h->seq == 0) {
-        std::memset(h->hdone, 0, sizeof(uint32_t) * h->cfg.B_max);
-        h->seq = 1;
-    }
+    next_seq(h);
     dartmpc::PmpcArgs a = io_args(h, B, ww, wo);
     HIPCHK(h, dartmpc_launch_pmpc(&a, h->stream), "kernel launch");
     const int rc = wait_done(h, h->stream, h->hdone, B, a.seq);
@@ -541,11 +579,7 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     a.mult_init_max = h->cfg.constr_mult_init_max;
     a.x0 = d_x0; a.ref = d_ref; a.prm = d_prm; a.w_warm = d_ww;
     a.u0 = d_u0; a.f = d_f; a.w_out = d_wo; a.status = d_st; a.iters = d_it;
-    if (++h->seq == 0) {            // wrapped: clear the words so that no stale one can match
-        std::memset(h->hdone, 0, sizeof(uint32_t) * h->cfg.B_max);
-        h->seq = 1;
-    }
-    a.done = d_done; a.seq = h->seq;
+    a.done = d_done; a.seq = next_seq(h);
     HIPCHK(h, dartmpc_launch_pmpc(&a, s), "kernel launch");
     const int rc = wait_done(h, s, h->hdone, B, a.seq);
     if (rc) return rc;
@@ -569,6 +603,7 @@ int dart_rmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* x0, const
     HIPCHK(h, hipSetDevice(h->device), "hipSetDevice");
     dartmpc::RmpcArgs a;
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.g = h->cfg.gravity; a.max_iter = h->cfg.max_iter; a.mult_init_max = h->cfg.constr_mult_init_max;
+    a.resto = h->cfg.restoration; a.max_soc = h->cfg.max_soc;
     a.x0 = x0; a.u_prev = u_prev; a.theta = theta; a.rls_P = rls_P; a.rls_phi = rls_phi; a.rls_y = rls_y;
     a.rls_lambda = rls_lambda; a.Rref = Rref; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
@@ -635,8 +670,7 @@ int dart_lmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* state, co
     a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc; a.mult_init_max = h->cfg.constr_mult_init_max;
     a.resto = h->cfg.restoration;
     a.max_ticks = (long long)(h->cfg.max_cpu_time * 1e8);     // s_memrealtime: 100 MHz
-    if (int rc = lmpc_resto_area(h, B)) return rc;
-    a.resto_buf = h->resto_buf;
+    if (int rc = lmpc_resto_area(h, B, stream ? (hipStream_t)stream : h->stream, &a.resto_buf)) return rc;
     a.state = state; a.u_prev = u_prev; a.pvec = pvec; a.target = target; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     a.fuse_policy = 0;
@@ -784,8 +818,7 @@ int dart_lmpc_policy_solve_batch_dev(dart_mpc_handle* h, const dart_lmpc_policy_
     a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc; a.mult_init_max = h->cfg.constr_mult_init_max;
     a.resto = h->cfg.restoration;
     a.max_ticks = (long long)(h->cfg.max_cpu_time * 1e8);     // s_memrealtime: 100 MHz
-    if (int rc = lmpc_resto_area(h, B)) return rc;
-    a.resto_buf = h->resto_buf;
+    if (int rc = lmpc_resto_area(h, B, stream ? (hipStream_t)stream : h->stream, &a.resto_buf)) return rc;
     a.state = state; a.u_prev = u_prev; a.pvec = nullptr; a.target = target; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     HIPCHK(h, dartmpc_launch_lmpc(&a, stream ? (hipStream_t)stream : h->stream), "kernel launch");
@@ -904,6 +937,7 @@ int dart_mpc_serve_start(dart_mpc_handle* h, int B_serve, double idle_timeout_s)
     std::memset(v.mbox, 0, 256);
     v.B = B_serve;
     v.idle_ticks = (unsigned long long)(idle_timeout_s * 1.0e8);      // s_memrealtime: 100 MHz
+    v.idle_s = idle_timeout_s;
     v.mbox[0] = h->seq;
     e = server_launch(h, h->seq);
     if (e != hipSuccess) { server_release(h); return fail(h, DART_MPC_EHIP, "resident server launch", e); }
@@ -987,7 +1021,8 @@ void dart_mpc_destroy(dart_mpc_handle* h) {
     h->st.release();
     io_release(h);
     if (h->hdone) (void)hipHostFree(h->hdone);
-    if (h->resto_buf) (void)hipFree(h->resto_buf);
+    for (auto& e : h->resto)
+        if (e.buf) (void)hipFree(e.buf);       // (synchronises with the area's last use)
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }

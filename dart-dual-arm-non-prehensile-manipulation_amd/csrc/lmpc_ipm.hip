@@ -460,11 +460,13 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         policy_step_wave(a.pol, b, PL);
         pvec = PL.pv;
     }
-    // IPOPT max_cpu_time (rlmpc2.py:485): the solve's clock starts here (the resumed kernel reads the start
-    // its instance parked); 100 MHz constant clock, a scalar read, so the test below is wave-uniform
+    // IPOPT max_cpu_time (rlmpc2.py:485): the solve's clock starts here; the resumed kernel continues it from
+    // the time its instance had spent when it was handed over (the wait for the rest of the first launch is
+    // not counted: the cap is per-instance GPU time); 100 MHz constant clock, a scalar read, so the test
+    // below is wave-uniform
     unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     if constexpr (RESTO)
-        t_start = (unsigned long long)a.resto_buf[(size_t)b * kWave * kLmNst + 6 * kLmNst + kLmNst - 1];
+        t_start -= (unsigned long long)a.resto_buf[(size_t)b * kWave * kLmNst + 6 * kLmNst + kLmNst - 1];
     auto out_of_time = [&]() {
         return a.max_ticks > 0 && (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.max_ticks;
     };
@@ -1165,7 +1167,8 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
                 for (int i = 0; i < 5; ++i) st[6 + i] = lam[i];
                 st[11] = zl; st[12] = zu; st[13] = fth; st[14] = fph;
                 st[15] = lane == 0 ? mu_it : lane == 1 ? theta : lane == 2 ? dl_it : lane == 3 ? (double)it
-                       : lane == 4 ? (double)nfilt_it : lane == 5 ? (double)acc_it : (double)t_start;
+                       : lane == 4 ? (double)nfilt_it : lane == 5 ? (double)acc_it
+                       : (double)(__builtin_amdgcn_s_memrealtime() - t_start);     // elapsed ticks
                 status = kLmNeedResto;
                 break;
             }

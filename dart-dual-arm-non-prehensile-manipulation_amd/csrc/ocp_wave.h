@@ -133,18 +133,28 @@ __device__ __forceinline__ bool quu_inverse(const double* Gk, double& i00, doubl
 // (m = s ^ x, x = 0..7; row 7 of every M column is the zero pad).  The 17 entries with a u_prev
 // index are copied from H_k by lanes that write no product entry.  G[N] must hold the terminal
 // surrogate.  Returns false (wave-uniform) if some Quu is not positive definite (inertia correction).
+struct AugRoles {
+    int cg, s, e;        // z column of the lane's group, lane in the group, packed entry written
+    bool prod;           // a product entry (else a u_prev entry copied from H_k, or the pad slot)
+    int goff[8];         // G_{k+1}(zs, z(n)) offsets of the value indices n
+    int gsu0, gsu1;      // Gzu(s, 0), Gzu(s, 1)
+    int cs;              // z column of the lane's value index s
+};
+
 template <class L>
-__device__ bool riccati_sweep_aug(L* S, int N) {
-    constexpr int NXA = L::NXA, NP = L::NP, NC = L::NC, ND = L::ND, NX = NXA - 2;
-    static_assert(ND == NXA + 3 && NP <= 8 && NC == 8, "two inputs, value dimension <= 8, M columns padded to 8");
+__device__ __forceinline__ AugRoles aug_roles() {
+    constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, NX = NXA - 2;
+    static_assert(ND == NXA + 3 && NP <= 8 && L::NC == 8, "two inputs, value dimension <= 8, M columns padded to 8");
+    AugRoles R;
     const int lane = threadIdx.x;
     const int g = lane >> 3, s = lane & 7;
     const int ge = g < NP ? g : NP - 1, se = s < NP ? s : NP - 1;          // clamped (idle lanes stay finite)
-    const int cg = ge < NX ? ge : ge + 2, cs = se < NX ? se : se + 2;     // z columns of the groups
+    R.cg = ge < NX ? ge : ge + 2; R.cs = se < NX ? se : se + 2;           // z columns of the groups
+    R.s = s;
     const int zs = se < NXA ? se : ND - 1;                                // z index of value index s
     // the packed entry this lane writes: a product entry (c(g), c(s)), s <= g < NP; or a u_prev entry
     // copied from H_k (q-th of the 17, enumerated row by row); or none
-    const bool prod = g < NP && s <= g;
+    R.prod = g < NP && s <= g;
     int q = -1;
     if (g >= NP) q = s;                                                   // lanes 56..63: q = 0..7
     else if (s > g) q = 8 + g * 7 - g * (g - 1) / 2 + (s - g - 1);        // upper-triangle lanes
@@ -160,71 +170,249 @@ __device__ bool riccati_sweep_aug(L* S, int N) {
     }
     // lanes with no entry write the pad slot NT (straight-line stores, no exec masking)
     static_assert(L::NTP > L::NT, "a pad slot after the packed entries");
-    const int e = prod ? hp(cg, cs) : (ecopy >= 0 ? ecopy : L::NT);
+    R.e = R.prod ? hp(R.cg, R.cs) : (ecopy >= 0 ? ecopy : L::NT);
     // G_{k+1}(zs, z(n)) of the value indices n: packed row zs for z(n) <= zs, else column zs of row z(n)
-    int goff[NP];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+        const int zn = n < NXA ? n : ND - 1;
+        R.goff[n] = zn <= zs ? tri(zs) + zn : tri(zn) + zs;
+    }
+    R.gsu0 = hp(NXA, zs); R.gsu1 = hp(NXA + 1, zs);
+    return R;
+}
+
+// One node step: G_k from M_k, H_k and the value function held in Gn (G_{k+1}, or its soft-row
+// surrogate); ok &= Quu of Gn positive definite.  Ends with a barrier.
+template <class L>
+__device__ __forceinline__ void aug_node_step(L* S, int k, const double* Gn, const AugRoles& R, bool& ok) {
+    constexpr int NXA = L::NXA, NP = L::NP, NC = L::NC;
+    // off the chain: the two M columns and the H entry of this lane
+    const double* Mk = &S->M[k][0][0];
+    double a[NP], b[8];
+#pragma unroll
+    for (int m = 0; m < NP; ++m) a[m] = Mk[R.cg * NC + m];
+#pragma unroll
+    for (int x = 0; x < 8; ++x) b[x] = Mk[R.cs * NC + (R.s ^ x)];
+    const double hk = S->H[k][R.e];
+    // phase 1: every read of G_{k+1} issued before the first product
+    double gz[NP], gu0[NP], gu1[NP];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) { gu0[n] = Gn[gzu<NXA>(n, 0)]; gu1[n] = Gn[gzu<NXA>(n, 1)]; }
+#pragma unroll
+    for (int n = 0; n < NP; ++n) gz[n] = Gn[R.goff[n]];
+    const double gs0 = Gn[R.gsu0], gs1 = Gn[R.gsu1];
+    const double q00 = Gn[hp(NXA, NXA)], q01 = Gn[hp(NXA + 1, NXA)], q11 = Gn[hp(NXA + 1, NXA + 1)];
+    double t0 = 0.0, t1 = 0.0, w0 = 0.0, w1 = 0.0;
 #pragma unroll
     for (int n = 0; n < NP; ++n) {
-        const int zn = n < NXA ? n : ND - 1;
-        goff[n] = zn <= zs ? tri(zs) + zn : tri(zn) + zs;
+        w0 = fma(gu0[n], a[n], w0);
+        w1 = fma(gu1[n], a[n], w1);
     }
-    const int gsu0 = hp(NXA, zs), gsu1 = hp(NXA + 1, zs);                 // Gzu(s, 0), Gzu(s, 1)
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+        if (n & 1) t1 = fma(gz[n], a[n], t1);
+        else t0 = fma(gz[n], a[n], t0);
+    }
+    // r = Quu^-1 Guz(:, s) depends on G_{k+1} alone: it runs beside the products with a_g
+    const double det = fma(q00, q11, -q01 * q01);
+    ok = ok && (q00 > 0.0) && (det > 0.0) && isfinite(det);
+    const double idet = frcp(det);
+    const double r0 = fma(q11, gs0, -q01 * gs1) * idet, r1 = fma(q00, gs1, -q01 * gs0) * idet;
+    const double u = (t0 + t1) - fma(r0, w0, r1 * w1);
+    // phase 2: u_g[s ^ x] of the 8-lane group
+    const double m7 = dpp<0x141>(u);                                 // row_half_mirror: lane s <- 7 - s
+    const double ux[8] = {u, dpp<0xB1>(u), dpp<0x4E>(u), dpp<0x1B>(u), dpp<0x1B>(m7), dpp<0x4E>(m7),
+                          dpp<0xB1>(m7), m7};
+    double p0 = hk, p1 = 0.0;
+#pragma unroll
+    for (int x = 0; x < 8; x += 2) { p0 = fma(b[x], ux[x], p0); p1 = fma(b[x + 1], ux[x + 1], p1); }
+    // all reads of G_{k+1} and M_k precede the write of G_k (distinct rows: no hazard)
+    S->G[k][R.e] = R.prod ? p0 + p1 : hk;
+    __syncthreads();
+}
+
+template <class L>
+__device__ bool riccati_sweep_aug(L* S, int N) {
+    constexpr int NXA = L::NXA;
+    const AugRoles R = aug_roles<L>();
     bool ok = true;
-    for (int k = N - 1; k >= 0; --k) {
-        // off the chain: the two M columns and the H entry of this lane
-        const double* Mk = &S->M[k][0][0];
-        double a[NP], b[8];
-#pragma unroll
-        for (int m = 0; m < NP; ++m) a[m] = Mk[cg * NC + m];
-#pragma unroll
-        for (int x = 0; x < 8; ++x) b[x] = Mk[cs * NC + (s ^ x)];
-        const double hk = S->H[k][e];
-        // phase 1: every read of G_{k+1} issued before the first product
-        const double* Gn = S->G[k + 1];
-        double gz[NP], gu0[NP], gu1[NP];
-#pragma unroll
-        for (int n = 0; n < NP; ++n) { gu0[n] = Gn[gzu<NXA>(n, 0)]; gu1[n] = Gn[gzu<NXA>(n, 1)]; }
-#pragma unroll
-        for (int n = 0; n < NP; ++n) gz[n] = Gn[goff[n]];
-        const double gs0 = Gn[gsu0], gs1 = Gn[gsu1];
-        const double q00 = Gn[hp(NXA, NXA)], q01 = Gn[hp(NXA + 1, NXA)], q11 = Gn[hp(NXA + 1, NXA + 1)];
-        double t0 = 0.0, t1 = 0.0, w0 = 0.0, w1 = 0.0;
-#pragma unroll
-        for (int n = 0; n < NP; ++n) {
-            w0 = fma(gu0[n], a[n], w0);
-            w1 = fma(gu1[n], a[n], w1);
-        }
-#pragma unroll
-        for (int n = 0; n < NP; ++n) {
-            if (n & 1) t1 = fma(gz[n], a[n], t1);
-            else t0 = fma(gz[n], a[n], t0);
-        }
-        // r = Quu^-1 Guz(:, s) depends on G_{k+1} alone: it runs beside the products with a_g
-        const double det = fma(q00, q11, -q01 * q01);
-        ok = ok && (q00 > 0.0) && (det > 0.0) && isfinite(det);
-        const double idet = frcp(det);
-        const double r0 = fma(q11, gs0, -q01 * gs1) * idet, r1 = fma(q00, gs1, -q01 * gs0) * idet;
-        const double u = (t0 + t1) - fma(r0, w0, r1 * w1);
-        // phase 2: u_g[s ^ x] of the 8-lane group
-        const double m7 = dpp<0x141>(u);                                 // row_half_mirror: lane s <- 7 - s
-        const double ux[8] = {u, dpp<0xB1>(u), dpp<0x4E>(u), dpp<0x1B>(u), dpp<0x1B>(m7), dpp<0x4E>(m7),
-                              dpp<0xB1>(m7), m7};
-        double p0 = hk, p1 = 0.0;
-#pragma unroll
-        for (int x = 0; x < 8; x += 2) { p0 = fma(b[x], ux[x], p0); p1 = fma(b[x + 1], ux[x + 1], p1); }
-        // all reads of G_{k+1} and M_k precede the write of G_k (distinct rows: no hazard)
-        S->G[k][e] = prod ? p0 + p1 : hk;
-        __syncthreads();
-    }
+    for (int k = N - 1; k >= 0; --k) aug_node_step<L>(S, k, S->G[k + 1], R, ok);
     double i00, i01, i11;
     return quu_inverse<NXA>(S->G[0], i00, i01, i11) && ok;
 }
 
+// ------------------------------------------------------------------------------------------
+// Soft rows (IPOPT's restoration phase, rmpc_ipm.hip): the first NS rows of node j's incoming defect are
+// soft, J dx - D dlam = rhs.  In the recursion the value function of node j is then seen through them:
+// eliminating the row slack w (Hessian D^-1 on value indices ph = 0..NS-1) from V(x~ + w) gives
+//   Pt' = P (I + D P)^-1 (over the value indices [x~; 1], P the Schur complement of G_j on u),
+// and the node step runs unchanged on the surrogate [[Pt', 0], [0, I_u]] (Gs).  With S = P(ph, ph) + D^-1
+// (positive definite: part of the inertia test) and W = S^-1 D^-1 every block is formed without
+// cancellation, whatever the mix of nearly hard (D^-1 huge) and nearly free (D^-1 tiny) rows -- the
+// Woodbury form P - P(:, ph) S^-1 P(ph, :) loses all accuracy on a free row's block at mu ~ 1e-9
+// (D^-1 spans 1e-7 ... 1e15 there):
+//   Pt'(ph, ph) = P(ph, ph) W,   Pt'(r, ph) = P(r, ph) W,   Pt'(r, r') = P(r, r') - P(r, ph) S^-1 P(ph, r')
+// (r, r' the other value indices).  The incoming rows of node j map x~+ <- y with
+//   y(ph) = W x~+(ph) - S^-1 P(ph, r) [x~+(r); 1] = Y [x~+; 1],  Y (NS x NP) kept per node.
+template <class L, int NS>
+struct AugSoftLds {
+    NodeArr<double[NS * L::NP], L::NMAXS> T;  // Y_j row-major NS x NP (value indices)
+    NodeArr<double[NS], L::NMAXS> Dinv;       // 1 / D of node j's soft rows
+    alignas(16) double Gs[L::NTP];            // the surrogate of G_{k+1}
+};
+
+// the constant u rows of the surrogate (Gzu = 0, Quu = I); call once before the soft sweeps
+template <class L, int NS>
+__device__ __forceinline__ void aug_soft_init(AugSoftLds<L, NS>* RS) {
+    constexpr int NXA = L::NXA;
+    for (int e = threadIdx.x; e < L::NTP; e += 64) {
+        int i = 0;
+        while (tri(i + 1) <= e) ++i;
+        const int j = e - tri(i);
+        const bool ui = i == NXA || i == NXA + 1, uj = j == NXA || j == NXA + 1;
+        if (ui || uj || e >= L::NT) RS->Gs[e] = (ui && i == j) ? 1.0 : 0.0;
+    }
+    __syncthreads();
+}
+
+// Node j's soft rows seen from G_j: lane e < tri(NP) owns the packed value entry (pv, qv), qv <= pv; every
+// such lane forms S from G_j, factors it S = L diag(dd) L^T (its own copy) and solves one system S t = b for
+// its entry -- b = e_qv (both indices soft: Pt'(pv, qv) = D^-1_qv P(pv, ph) t), b = P(ph, pv) (pv not soft,
+// qv soft: Pt'(pv, qv) = D^-1_qv t_qv), b = P(ph, qv) (neither: Pt'(pv, qv) = P(pv, qv) - P(pv, ph) t); the
+// diagonal soft lanes store Y's column qv (D^-1_qv t), the lanes of the homogeneous row with qv not soft store
+// -t.  With `surrogate` every lane stores Pt'(pv, qv) into Gs.  ok &= (Quu of G_j and S positive definite).
+// Ends with a barrier.
+template <class L, int NS>
+__device__ __forceinline__ void aug_soften(L* S, AugSoftLds<L, NS>* RS, int j, bool surrogate, bool& ok) {
+    constexpr int NXA = L::NXA, NP = L::NP, NV = tri(NP);
+    const int e0 = (int)threadIdx.x < NV ? (int)threadIdx.x : NV - 1;
+    int pv = 0;
+    while (tri(pv + 1) <= e0) ++pv;
+    const int qv = e0 - tri(pv);
+    const bool act = (int)threadIdx.x < NV;
+    const bool ps = pv < NS, qs = qv < NS;          // (qv <= pv: qs whenever ps)
+    const double* Gn = S->G[j];
+    const double q00 = Gn[hp(NXA, NXA)], q01 = Gn[hp(NXA + 1, NXA)], q11 = Gn[hp(NXA + 1, NXA + 1)];
+    const double det = fma(q00, q11, -q01 * q01);
+    ok = ok && (q00 > 0.0) && (det > 0.0) && isfinite(det);
+    const double idet = frcp(det);
+    const double i00 = q11 * idet, i01 = -q01 * idet, i11 = q00 * idet;
+    // w(a) = Quu^-1 Gzu(a, :); P(a, b) = Gzz(a, b) - Gzu(b, :) w(a)
+    double ga0[NS], ga1[NS], wa0[NS], wa1[NS];
+#pragma unroll
+    for (int a = 0; a < NS; ++a) {
+        ga0[a] = Gn[gzu<NXA>(a, 0)]; ga1[a] = Gn[gzu<NXA>(a, 1)];
+        wa0[a] = fma(i00, ga0[a], i01 * ga1[a]); wa1[a] = fma(i01, ga0[a], i11 * ga1[a]);
+    }
+    const int bc = (!ps && qs) ? pv : qv;           // the column of P(ph, :) on the right-hand side
+    const double gq0 = Gn[gzu<NXA>(qv, 0)], gq1 = Gn[gzu<NXA>(qv, 1)];
+    const double gp0 = Gn[gzu<NXA>(pv, 0)], gp1 = Gn[gzu<NXA>(pv, 1)];
+    const double gb0 = Gn[gzu<NXA>(bc, 0)], gb1 = Gn[gzu<NXA>(bc, 1)];
+    const double wq0 = fma(i00, gq0, i01 * gq1), wq1 = fma(i01, gq0, i11 * gq1);
+    double P[NS][NS], rb[NS], rp[NS], di[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+#pragma unroll
+        for (int c = 0; c <= i; ++c) P[i][c] = Gn[gzz<NXA>(i, c)] - fma(ga0[i], wa0[c], ga1[i] * wa1[c]);
+        rb[i] = Gn[gzz<NXA>(i, bc)] - fma(gb0, wa0[i], gb1 * wa1[i]);     // P(i, bc)
+        rp[i] = Gn[gzz<NXA>(i, pv)] - fma(gp0, wa0[i], gp1 * wa1[i]);     // P(i, pv)
+        di[i] = RS->Dinv[j][i];
+    }
+    const double pvq = Gn[gzz<NXA>(pv, qv)] - fma(gp0, wq0, gp1 * wq1);
+    double Lm[NS][NS], id[NS], dd[NS];
+#pragma unroll
+    for (int c = 0; c < NS; ++c) {
+        double t = P[c][c] + di[c];
+#pragma unroll
+        for (int m = 0; m < c; ++m) t -= Lm[c][m] * Lm[c][m] * dd[m];
+        dd[c] = t;
+        ok = ok && t > 0.0 && isfinite(t);
+        id[c] = 1.0 / t;
+#pragma unroll
+        for (int i = c + 1; i < NS; ++i) {
+            double u = P[i][c];
+#pragma unroll
+            for (int m = 0; m < c; ++m) u -= Lm[i][m] * Lm[c][m] * dd[m];
+            Lm[i][c] = u * id[c];
+        }
+    }
+    double y[NS], t4[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        double t = qs && ps ? (i == qv ? 1.0 : 0.0) : rb[i];
+#pragma unroll
+        for (int m = 0; m < i; ++m) t -= Lm[i][m] * y[m];
+        y[i] = t;
+    }
+#pragma unroll
+    for (int i = NS - 1; i >= 0; --i) {
+        double t = y[i] * id[i];
+#pragma unroll
+        for (int m = i + 1; m < NS; ++m) t -= Lm[m][i] * t4[m];
+        t4[i] = t;
+    }
+    double dq = 0.0, tq = 0.0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        if (i == qv) { dq = di[i]; tq = t4[i]; }
+    }
+    if (act && ps && pv == qv) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) RS->T[j][NP * i + qv] = dq * t4[i];
+    }
+    if (act && !qs && pv == NP - 1) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) RS->T[j][NP * i + qv] = -t4[i];
+    }
+    if (surrogate && act) {
+        double v;
+        if (ps) {             // both soft: D^-1_qv P(pv, ph) S^-1 e_qv  (P(pv, i) = P[max][min])
+            v = 0.0;
+#pragma unroll
+            for (int a = 0; a < NS; ++a) v = fma(rp[a], t4[a], v);
+            v *= dq;
+        } else if (qs) {      // pv not soft, qv soft: D^-1_qv (S^-1 P(ph, pv))_qv
+            v = dq * tq;
+        } else {
+            v = pvq;
+#pragma unroll
+            for (int a = 0; a < NS; ++a) v -= rp[a] * t4[a];
+        }
+        RS->Gs[gzz<NXA>(pv, qv)] = v;
+    }
+    __syncthreads();
+}
+
+// Backward sweep with the soft rows of every node (restoration phase): before the step of node k the
+// surrogate of G_{k+1} seen through node k+1's soft rows, Y_{k+1} kept for the forward map; Y_0 of the soft
+// initial rows last.  G[N] must hold the terminal surrogate, RS->Dinv every node's 1 / D, the u rows of
+// RS->Gs their constants (aug_soft_init).  Returns false (wave-uniform) if some S or Quu is not positive
+// definite.
+template <class L, int NS>
+__device__ bool riccati_sweep_aug_soft(L* S, AugSoftLds<L, NS>* RS, int N) {
+    const AugRoles R = aug_roles<L>();
+    bool ok = true;
+    for (int k = N - 1; k >= 0; --k) {
+        aug_soften<L, NS>(S, RS, k + 1, true, ok);
+        aug_node_step<L>(S, k, RS->Gs, R, ok);
+    }
+    aug_soften<L, NS>(S, RS, 0, false, ok);
+    return !wany(!ok);
+}
+
+struct NoPost {
+    __device__ void operator()(int, int) const {}
+};
+template <class P> struct IsNoPost { static constexpr bool value = false; };
+template <> struct IsNoPost<NoPost> { static constexpr bool value = true; };
+
 // Gains and closed-loop matrices for the forward sweep, lanes k and k + 32 per node (N <= 32): both
 // form [K | k] = -Quu^-1 Guz, lane k writes it, and the rows of Phi_k = A_k + B_k K_k, f_k = c_k + B_k k_k
 // split between them.  Ends with a barrier.
-template <class L>
-__device__ void closed_loop(L* S, int N) {
+// post(k) (restoration phase: the rows mapped through node k+1's soft rows) runs on the node lanes k < N
+// after every row of F_k is written, before the pair maps are composed.
+template <class L, class Post = NoPost>
+__device__ void closed_loop(L* S, int N, Post post = Post()) {
     constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, RH = (NXA + 1) / 2;
     const int k = threadIdx.x & 31, rb = threadIdx.x >= 32 ? RH : 0;
     if (k < N) {
@@ -259,6 +447,10 @@ __device__ void closed_loop(L* S, int N) {
         }
     }
     __syncthreads();
+    if constexpr (!IsNoPost<Post>::value) {
+        if (k < N && threadIdx.x < 32) post(k);
+        __syncthreads();
+    }
     compose_pairs<1, L::NMAXS, NXA, 1>(S->F, S->F2, N);   // NXA floor(N / 2) tasks: one round over the wave for N <= 21 (RMPC), two beyond
 }
 
@@ -478,9 +670,6 @@ __device__ bool riccati_s_sweep(L* S, int N, const RiccatiSRoles& R) {
     return !wany(!ok);
 }
 
-struct NoPost {
-    __device__ void operator()(int, int) const {}
-};
 // [K | k] = -Guz / Quu and [Phi | f] of every node, lane 32 h + k per node (k < N); post(slot, k) then
 // runs on each node's lane before the pair maps are composed (the LMPC restoration phase maps the rows
 // through its soft defect rows there).  Ends with a barrier.

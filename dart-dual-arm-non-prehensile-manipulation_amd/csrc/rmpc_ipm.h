@@ -11,6 +11,8 @@ struct RmpcArgs {
     int max_iter;
     double mult_init_max;   // IPOPT constr_mult_init_max: > 0 least-square starting multipliers (default 1000)
     int pack;                // blocks per instance slot (set by the launcher; 8 = one XCD for small B)
+    int resto;               // IPOPT's soft restoration and restoration phases (1 default; 0: a failed line search ends at -2)
+    int max_soc;             // IPOPT max_soc of the restoration phase's line search (default 4)
     const double* x0;        // [B][4]
     const double* u_prev;    // [B][2]
     double* theta;           // [B][14] theta_hat (in), or RLS theta (in/out) when rls_P != nullptr

@@ -23,6 +23,15 @@
 // slack rows of the node three and three (slacks, slack multipliers, their steps and barrier terms);
 // the node-coupled Riccati and forward sweeps run through LDS with the lanes sharing each node's dense
 // algebra (ocp_wave.h).
+//
+// IPOPT's soft restoration and restoration phases (oracle/rmpc_ipm.c `soft_resto_step`, `restoration`):
+// a measured |v| above vmax at the pinned node 0 (np_mpc...:123-127) makes the NLP locally infeasible and
+// the filter line search fails.  rmpc_ipm_kernel<false> (every solve) carries no restoration code: an
+// instance whose line search fails ends with the internal status kRmNeedResto and writes nothing else.  The
+// launcher always follows it with rmpc_ipm_kernel<true> on the same stream; its blocks return at once unless
+// their instance was handed over, the others solve the instance again from its start (the same iterates up
+// to the failure) with both phases available, to the end of the solve.  No state crosses the hand-off but
+// the status word in the caller's output array, so launches on different streams cannot interfere.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -40,6 +49,8 @@ constexpr int RM_NIQ = 6;         // inequality rows per node: du_x, du_y, vx-vm
 constexpr int RM_NQ = 3;          // of them per lane: rows 0..2 on lane k, rows 3..5 on its mirror lane k + 32
 static_assert(2 * RM_NQ == RM_NIQ, "the node and mirror lanes split the rows evenly");
 using RmLds = OcpLds<6, RM_NMAXS>;
+using RmSoft = AugSoftLds<RmLds, 4>;     // restoration: the four physical rows of every defect are soft
+constexpr int kRmNeedResto = -100;      // hand-off of an instance to rmpc_ipm_kernel<true>
 
 #ifdef DART_STAMPS
 __device__ unsigned long long g_stamp_rm[16];
@@ -56,6 +67,46 @@ struct RmShared {
     double rls_Pphi[2][7], rls_phiP[2][7];
     RmModel model;                            // uniform, read at the use sites (keeps VGPRs free)
     NodeArr<double[8], RM_NMAXS + 1> JL;      // J^T lambda staging, primal residual maxima
+};
+
+// Restoration-phase state in LDS (rmpc_ipm_kernel<true> only).  PN: node k's four physical incoming rows
+// (written by the node lane): p, n, z_p, z_n, rp, rn, Sigma_p', Sigma_n'; x_R, D_R of the states, u_R, D_R of
+// the tilts, and the original problem's u-bound multipliers at the start.  Q: each lane's three inequality
+// rows: p, n, z_p, z_n, rp, rn, Sigma_s', Sigma_p', Sigma_n', sigma, off, psi, and the original slack and
+// slack-bound multipliers at the start.  SV / SV2: a parked step (second-order correction, refinement).
+enum { P_PC = 0, P_NC = 4, P_ZP = 8, P_ZN = 12, P_RP = 16, P_RN = 20, P_SP = 24, P_SN = 28, P_XR = 32, P_DRX = 36,
+       P_UR = 40, P_DRU = 42, P_ZL0 = 44, P_ZU0 = 46, P_N = 48 };
+enum { Q_QP = 0, Q_QN = 3, Q_ZQP = 6, Q_ZQN = 9, Q_RQP = 12, Q_RQN = 15, Q_SS = 18, Q_SP = 21, Q_SN = 24, Q_SIG = 27,
+       Q_OFF = 30, Q_PSI = 33, Q_S0 = 36, Q_VL0 = 39, Q_VU0 = 42, Q_N = 45 };
+enum { V_DX = 0, V_LP = 6, V_DU = 12, V_DY = 14, V_DS = 17, V_DQP = 20, V_DQN = 23, V_DPC = 26, V_DNC = 30, V_N = 34 };
+struct RmResto {
+    RmSoft soft;
+    NodeArr<double[P_N], RM_NMAXS + 1> PN;
+    NodeArr<double[Q_N], kWave> Q;
+    NodeArr<double[V_N], kWave> SV, SV2;
+};
+
+// closed-loop rows of node k mapped through node k+1's soft rows: [Phi | f](r) <- Y(r, :) [[Phi | f]; 0 1]
+struct RmSoftPost {
+    RmLds* S;
+    const RmSoft* R;
+    __device__ void operator()(int k) const {
+        const double* Y = R->T[k + 1];
+        double F[6][7];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int j = 0; j < 7; ++j) F[r][j] = S->F[k][r][j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                double t = j == 6 ? Y[7 * r + 6] : 0.0;
+#pragma unroll
+                for (int a = 0; a < 6; ++a) t = fma(Y[7 * r + a], F[a][j], t);
+                S->F[k][r][j] = t;
+            }
+    }
 };
 
 // continuous model (np_mpc...:178-186); also returns d f / d vx|vy of rows 1, 3 and tanh values
@@ -230,12 +281,21 @@ __device__ __forceinline__ void rm_iq3(const double* z, double vmax, bool mir, d
     c[2] = mir ? -z[3] - vmax : z[1] - vmax;
 }
 
+template <bool RESTO>
 __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     __shared__ RmShared SH;
     RmLds* S = &SH.ocp;
+    RmResto* RL = nullptr;
+    if constexpr (RESTO) {
+        __shared__ RmResto RSH;
+        RL = &RSH;
+    }
     STAMP_DECL
     if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
     const int b = blockIdx.x / a.pack;
+    if constexpr (RESTO) {
+        if (a.status[b] != kRmNeedResto) return;     // wave-uniform: solved by rmpc_ipm_kernel<false>
+    }
     // lane k and its mirror lane k + 32 both own node k: the node work runs on both, the slack rows are
     // split (rm_iq3), and sums over the wave count the node terms on the node lanes only
     const int lane = threadIdx.x;
@@ -248,7 +308,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     const double ulo = pr[4], uhi = pr[5], dulo = pr[6], duhi = pr[7], vmax = pr[8], veps = pr[9];
 
     // ---------------- fused RLS update (np_mpc...:17-27, rob_ctrl.py:340-343) -----------------
-    if (a.rls_P) {
+    if (!RESTO && a.rls_P) {      // (<true> re-solves with the theta <false> updated in place)
         double* Pg = a.rls_P + 98 * b;
         const double* ph = a.rls_phi + 7 * b;
         const double lamr = a.rls_lambda;
@@ -436,7 +496,14 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     // variables of the reference NLP), the slack columns eliminated with weight 1 (Hessian C^T C,
     // gradient C^T r_s, r_s = -v_L + v_U), r = scaled grad f - z_L + z_U, zero defects; the equality
     // multipliers are the step's new multipliers, y_d = C dz + r_s.  Mirrors oracle/rmpc_ipm.c.
-    for (it = a.mult_init_max > 0.0 ? -1 : 0; it < a.max_iter; ++it) {
+    int in_soft = 0, soft_count = 0;      // IPOPT's soft restoration phase (BacktrackingLineSearch; <true>)
+    bool go_resto = false;
+    double phi_rs = 0.0;
+    int it_next = a.mult_init_max > 0.0 ? -1 : 0;
+    // <true>: the iteration loop is left for each restoration phase, which runs after it (outside the loop,
+    // so that its registers do not burden the iterations) and re-enters it at the next iteration
+    for (;;) {
+    for (it = it_next; it < a.max_iter; ++it) {
         const bool lsm = it < 0;
         // ---------------- derivatives, residuals, optimality error ---------------------------
         // stage data go to LDS as soon as they exist (Jacobian columns, dynamics Hessian, defect
@@ -545,7 +612,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
             const double cmu = fmax(c0 - mu, mu - cminw);
             if (fmax(dinf * is_d, fmax(pinf, cmu * is_c)) > 10.0 * mu || mu <= mu_min) break;
             mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
-            nfilt = 0;
+            nfilt = 0; in_soft = 0;       // BacktrackingLineSearch::Reset: the filter and the soft phase
 #pragma unroll
             for (int i = 0; i < RM_NQ; ++i) {
                 const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
@@ -769,7 +836,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         const bool tiny = wmaxf(tnl) < 2.2e-15f;
         STAMP(6);
         int ls = 0;
-        for (; ls < 80; ++ls) {
+        for (; ls < 80 && !in_soft; ++ls) {
             double xt[4], pt[2], ut[2], st_[RM_NQ], gt[6];
 #pragma unroll
             for (int i = 0; i < 4; ++i) xt[i] = fma(alpha, dx[i], x[i]);
@@ -805,8 +872,150 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         }
         STAMP_ADD(10, ls + 1);
         STAMP(7);
-        if (!accepted) { status = -2; break; }
-        if (!ftype && nfilt < kWave) {
+#ifdef DART_RESTO_TRACE
+        if (RESTO && blockIdx.x == 0 && lane == 0)      // diagnostic build: the oracle's ORACLE_DEBUG line
+            printf("it %3d mu %.2e dinf %.2e pinf %.2e c0 %.2e delta %.1e amax %.3e alpha %.3e az %.3e th %.2e\n", it, mu,
+                   dinf * is_d, pinf, c0 * is_c, delta, amax, alpha, az, theta);
+#endif
+        if constexpr (!RESTO) {
+            // a failed line search: IPOPT's restoration phases in rmpc_ipm_kernel<true> (or status -2 without)
+            if (!accepted) { status = a.resto ? kRmNeedResto : -2; break; }
+        }
+        bool soft = false;
+        if constexpr (RESTO) {
+            // ---------------- IPOPT's soft restoration phase (BacktrackingLineSearch::TrySoftRestoStep) ----
+            // the line search failed, or the soft phase is on: the primal-dual step damped only by the
+            // fractions to the boundary (one length for x, s, lambda, y and the bound multipliers) is taken if
+            // the original filter accepts it with alpha_primal_test = 0 (the phase ends) or if it cuts the
+            // primal-dual system error at mu by the factor 0.9999; at most max_soft_resto_iters = 10 steps
+            if (!accepted) {
+                if (!in_soft) {         // PrepareRestoPhaseStart: the current point enters the filter
+                    if (nfilt < kWave) {
+                        if (lane == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
+                        ++nfilt;
+                    }
+                    soft_count = 0;
+                }
+                if (!(in_soft && ++soft_count > 10)) {
+                    const double as = fmin(amax, az);
+                    double th_s, ph_s;
+                    {
+                        double xt[4], pt[2], ut[2], st_[RM_NQ], gt[6];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) xt[i] = fma(as, dx[i], x[i]);
+                        pt[0] = fma(as, dx[4], up[0]); pt[1] = fma(as, dx[5], up[1]);
+                        ut[0] = fma(as, dU[0], u[0]); ut[1] = fma(as, dU[1], u[1]);
+#pragma unroll
+                        for (int i = 0; i < RM_NQ; ++i) st_[i] = fma(as, dS[i], s[i]);
+                        defects(xt, pt, ut, gt);
+                        double zt[8] = {xt[0], xt[1], xt[2], xt[3], pt[0], pt[1], ut[0], ut[1]}, ct[RM_NQ];
+                        rm_iq3(zt, vmax, mir, ct);
+                        double thl = 0.0;
+#pragma unroll
+                        for (int i = 0; i < 6; ++i) thl += nod && xon ? fabs(gt[i]) : 0.0;
+#pragma unroll
+                        for (int i = 0; i < RM_NQ; ++i) thl += uon ? fabs(ct[i] - st_[i]) : 0.0;
+                        double phl = nod ? sc * cost_val(xt, ut, pt) : 0.0;
+                        phl -= uon ? mu * log_fast(barrier_args(ut, st_)) : 0.0;
+                        th_s = wsum_rl(thl); ph_s = wsum_rl(phl);
+                    }
+                    bool orig = th_s < th_max && isfinite(ph_s) && !wany(lane < nfilt && th_s >= fth && ph_s >= fph);
+                    orig = orig && (cmp_le(th_s, (1 - gam_th) * theta, theta) || cmp_le(ph_s - phi, -gam_ph * theta, phi));
+                    bool take = orig;
+                    if (!take && isfinite(ph_s)) {
+                        // IPOPT's primal-dual system error at mu (l1 norms of the primal infeasibility, the dual
+                        // infeasibility and z s - mu, added) at the current point and at the trial point with
+                        // every multiplier moved by the same step
+                        double pd[2];
+#pragma unroll 1
+                        for (int pass = 0; pass < 2; ++pass) {
+                            const double al = pass ? as : 0.0;
+                            double xx[4], pp[2], uu[2], ss[RM_NQ], lm[6], yy[RM_NQ], wl[RM_NQ], wu[RM_NQ], zzl[2], zzu[2];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) xx[i] = fma(al, dx[i], x[i]);
+                            pp[0] = fma(al, dx[4], up[0]); pp[1] = fma(al, dx[5], up[1]);
+#pragma unroll
+                            for (int j = 0; j < 2; ++j) {
+                                uu[j] = uon ? fma(al, dU[j], u[j]) : u[j];
+                                zzl[j] = fma(al, dzl[j], zl[j]); zzu[j] = fma(al, dzu[j], zu[j]);
+                            }
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) lm[i] = xon ? fma(al, lamp[i] - lam[i], lam[i]) : 0.0;
+#pragma unroll
+                            for (int i = 0; i < RM_NQ; ++i) {
+                                ss[i] = fma(al, dS[i], s[i]); yy[i] = fma(al, dY[i], yq[i]);
+                                wl[i] = fma(al, dvl[i], vl[i]); wu[i] = fma(al, dvu[i], vu[i]);
+                            }
+                            double lmn[6], jl_[6], xn_[4];
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) { const double t = from_next(lm[i]); lmn[i] = uon ? t : 0.0; }
+                            {
+                                double sa, ca, sb, cb, huu[2], scr[4][4], sdr[4][2];
+                                rm_sincos2(uu, sa, ca, sb, cb);
+                                rm_rk4_lin(m, xx, sa, sb, xn_, scr, sdr, mir);
+                                rm_adjoint_curv(m, scr, sdr, lmn, sa, sb, huu);
+                                if (uon) rm_directions(m, scr, sdr, lmn, huu, m.gz * ca, m.gz * cb, mir ? 3 : 0, Mk, Hk, SH.JL[k]);
+                                __syncthreads();
+#pragma unroll
+                                for (int i = 0; i < 6; ++i) jl_[i] = uon ? SH.JL[sr][i] : 0.0;
+                                __syncthreads();
+                            }
+                            double cdef[6], gg[6];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) { const double t = from_next(xx[i]); cdef[i] = xn_[i] - t; }
+                            { const double t0 = from_next(pp[0]), t1 = from_next(pp[1]); cdef[4] = uu[0] - t0; cdef[5] = uu[1] - t1; }
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) {
+                                const double t = from_prev(cdef[i]);
+                                gg[i] = k == 0 ? (i < 4 ? xx[i] - x0[i] : pp[i - 4] - upv[i - 4]) : -t;
+                            }
+                            double gl[8];
+                            cost_grad(xx, uu, pp, gl);
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) gl[j] *= sc;
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) gl[i] += lm[i];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) gl[j] -= jl_[j];
+                            gl[6] -= jl_[4] + lmn[4]; gl[7] -= jl_[5] + lmn[5];
+                            double yo[RM_NQ];
+#pragma unroll
+                            for (int i = 0; i < RM_NQ; ++i) yo[i] = __shfl_xor(yy[i], 32);
+                            gl[6] += yy[0]; gl[4] -= yy[0]; gl[7] += yy[1]; gl[5] -= yy[1];
+                            gl[1] += yy[2] - yo[0]; gl[3] += yo[1] - yo[2];
+                            gl[6] += -zzl[0] + zzu[0]; gl[7] += -zzl[1] + zzu[1];
+                            double tot = 0.0;
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) tot += nod && (j < 6 ? xon : uon) ? fabs(gl[j]) : 0.0;
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) tot += nod && xon ? fabs(gg[i]) : 0.0;
+                            if (uon && nod) tot += fabs(zzl[0] * (uu[0] - lo) - mu) + fabs(zzu[0] * (hi - uu[0]) - mu) +
+                                                   fabs(zzl[1] * (uu[1] - lo) - mu) + fabs(zzu[1] * (hi - uu[1]) - mu);
+                            if (uon) {
+                                const double zz2[8] = {xx[0], xx[1], xx[2], xx[3], pp[0], pp[1], uu[0], uu[1]};
+                                double cz2[RM_NQ];
+                                rm_iq3(zz2, vmax, mir, cz2);
+#pragma unroll
+                                for (int i = 0; i < RM_NQ; ++i) {
+                                    tot += fabs(-yy[i] - wl[i] + wu[i]) + fabs(cz2[i] - ss[i]);
+                                    if (tw[i]) tot += fabs(wl[i] * (ss[i] - sL[i]) - mu);
+                                    tot += fabs(wu[i] * (sU[i] - ss[i]) - mu);
+                                }
+                            }
+                            pd[pass] = wsum_rl(tot);
+                        }
+                        take = pd[1] <= 0.9999 * pd[0];
+                    }
+                    if (take) {
+                        accepted = true; soft = true; alpha = as; az = as; th_t = th_s;
+                        in_soft = orig ? 0 : 1;
+                        if (orig) soft_count = 0;
+                    }
+                }
+            }
+            if (!accepted) { phi_rs = phi; go_resto = true; break; }
+        }
+        if (!soft && !ftype && nfilt < kWave) {
             if (lane == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
             ++nfilt;
         }
@@ -838,8 +1047,991 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         theta = th_t;
         STAMP(8);
     }
+    if (!RESTO || !go_resto) break;
+    go_resto = false;
+    // ---------------- IPOPT's restoration phase (MinC_1NrmRestorationPhase) -------------------------------
+    // (oracle/rmpc_ipm.c `restoration`): min rho sum(p + n) + eta/2 |D_R (x - x_R)|^2 over the reference NLP's
+    // variables, s.t. c(x) + n - p = 0 on the physical defect rows (x_0 pinning included; the u_{k-1} copy
+    // rows stay hard), d(x) - s + n - p = 0 on the inequality rows with the slack bounds kept, p, n >= 0, the
+    // U box; rho 1000, eta = sqrt(mu_R), D_R = 1 / max(1, |x_R|).  Start: mu_R = max(mu, |(c, d - s)|_inf),
+    // closed-form p, n, z = mu_R / p, bound multipliers min(rho, z), least-square equality multipliers.  The
+    // problem is solved by the same algorithm (its own filter and mu, inertia correction, second-order
+    // correction, iterative refinement of every step); it returns when the original problem's theta falls to
+    // 0.9 of its start value at a point the original filter accepts.  Defect rows: soft rows of the Riccati
+    // recursion (riccati_sweep_aug_soft); inequality rows: slack, p and n in series, eliminated per stage,
+    // y + dy = sigma (C dz + r) + off with 1 / sigma = 1 / Sigma_s' + 1 / Sigma_p' + 1 / Sigma_n'.
+    {
+        RmResto& RS = *RL;
+        RmSoft* const SR = &RS.soft;
+        double* const pn = RS.PN[xon ? k : RM_NMAXS];      // node k's physical rows (written by the node lane)
+        double* const q = RS.Q[lane];                      // this lane's three inequality rows
+        const double mu0 = mu, th0 = theta, phi0 = phi_rs, tau0 = fmax(0.99, 1.0 - mu0), rho = 1000.0;
+        const double nbr = 24.0 * N + 8.0 * (N + 1);       // bound-multiplier count of the restoration problem
+        aug_soft_init<RmLds, 4>(SR);
+        if (nod) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { pn[P_XR + i] = x[i]; pn[P_DRX + i] = 1.0 / fmax(1.0, fabs(x[i])); }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                pn[P_UR + j] = u[j]; pn[P_DRU + j] = 1.0 / fmax(1.0, fabs(u[j]));
+                pn[P_ZL0 + j] = zl[j]; pn[P_ZU0 + j] = zu[j];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < RM_NQ; ++i) { q[Q_S0 + i] = s[i]; q[Q_VL0 + i] = vl[i]; q[Q_VU0 + i] = vu[i]; }
+        double rmu, eta;
+        {   // RestoIterateInitializer
+            double g0[6], cz[RM_NQ];
+            defects(x, up, u, g0);
+            const double zz[8] = {x[0], x[1], x[2], x[3], up[0], up[1], u[0], u[1]};
+            rm_iq3(zz, vmax, mir, cz);
+            double cmx = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) cmx = fmax(cmx, nod && xon ? fabs(g0[i]) : 0.0);
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) cmx = fmax(cmx, uon ? fabs(cz[i] - s[i]) : 0.0);
+            rmu = fmax(mu0, wmax(cmx));
+            eta = sqrt(rmu);
+            auto pn_init = [&](double c, double& p, double& n) {
+                const double aa = rmu / (2.0 * rho) - 0.5 * c, bb = c * rmu / (2.0 * rho);
+                n = aa + sqrt(aa * aa + bb); p = c + n;
+            };
+            if (nod) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    double p = 1.0, n = 1.0;
+                    if (xon) pn_init(g0[i], p, n);
+                    pn[P_PC + i] = p; pn[P_NC + i] = n;
+                    pn[P_ZP + i] = xon ? rmu / p : 0.0; pn[P_ZN + i] = xon ? rmu / n : 0.0;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) {
+                double p = 1.0, n = 1.0;
+                if (uon) pn_init(cz[i] - s[i], p, n);
+                q[Q_QP + i] = p; q[Q_QN + i] = n;
+                q[Q_ZQP + i] = uon ? rmu / p : 0.0; q[Q_ZQN + i] = uon ? rmu / n : 0.0;
+                vl[i] = fmin(rho, vl[i]); vu[i] = fmin(rho, vu[i]);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) { zl[j] = fmin(rho, zl[j]); zu[j] = fmin(rho, zu[j]); }
+        }
+        __syncthreads();
+        // the derivative pass at the current point with the next node's multipliers lmn: Jacobian columns into
+        // M~, the dynamics Hessian into H~, jl = J^T lmn (x columns 0..3, tilts 4..5), xn = x+ of node k
+        double lmn[6], jl[6], xn[4], hd[6];
+        auto rderiv = [&]() {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { const double t = from_next(lam[i]); lmn[i] = uon ? t : 0.0; }
+            double sa, ca, sb, cb, huu[2], scr[4][4], sdr[4][2];
+            rm_sincos2(u, sa, ca, sb, cb);
+            rm_rk4_lin(m, x, sa, sb, xn, scr, sdr, mir);
+            rm_adjoint_curv(m, scr, sdr, lmn, sa, sb, huu);
+            if (uon) rm_directions(m, scr, sdr, lmn, huu, m.gz * ca, m.gz * cb, mir ? 3 : 0, Mk, Hk, SH.JL[k]);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 6; ++i) jl[i] = uon ? SH.JL[sr][i] : 0.0;
+            const int dg[6] = {0, 1, 2, 3, 6, 7};
+#pragma unroll
+            for (int i = 0; i < 6; ++i) hd[i] = uon ? Hk[hp(dg[i], dg[i])] : 0.0;
+            __syncthreads();
+        };
+        // incoming defects of node k (6 rows) from x+ of every node
+        auto incoming = [&](double* g) {
+            double cdef[6];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { const double t = from_next(x[i]); cdef[i] = xn[i] - t; }
+            { const double t0 = from_next(up[0]), t1 = from_next(up[1]); cdef[4] = u[0] - t0; cdef[5] = u[1] - t1; }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double t = from_prev(cdef[i]);
+                g[i] = k == 0 ? (i < 4 ? x[i] - x0[i] : up[i - 4] - upv[i - 4]) : -t;
+            }
+        };
+        // the inequality rows (shift delta; lsq: the least-square multipliers' unit weights): Sigma's, sigma,
+        // off, psi into Q
+        auto iq_terms = [&](double delta, bool lsq) {
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) {
+                double Ss = 1.0, ps = 0.0, Sp = 1.0, Sn = 1.0, rp = 0.0, rn = 0.0, yv = 0.0;
+                if (uon) {
+                    if (lsq) {
+                        ps = -vl[i] + vu[i]; rp = rho - q[Q_ZQP + i]; rn = rho - q[Q_ZQN + i];
+                    } else {
+                        const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
+                        Ss = (tw[i] ? vl[i] / dl : 0.0) + vu[i] / du_ + delta;
+                        ps = (tw[i] ? -rmu / dl : 0.0) + rmu / du_;
+                        Sp = q[Q_ZQP + i] / q[Q_QP + i] + delta; Sn = q[Q_ZQN + i] / q[Q_QN + i] + delta;
+                        rp = q[Q_RQP + i]; rn = q[Q_RQN + i]; yv = yq[i];
+                    }
+                }
+                const double sg = 1.0 / (1.0 / Ss + 1.0 / Sp + 1.0 / Sn);
+                q[Q_SS + i] = Ss; q[Q_SP + i] = Sp; q[Q_SN + i] = Sn; q[Q_SIG + i] = sg; q[Q_PSI + i] = ps;
+                q[Q_OFF + i] = uon ? sg * (ps / Ss + yv * (1.0 / Sp + 1.0 / Sn) - rn / Sn + rp / Sp) : 0.0;
+            }
+        };
+        // stage Hessians (node lanes) and the terminal surrogate's Hessian; after iq_terms
+        auto assemble_H = [&](double delta, bool lsq) {
+            double sg[RM_NQ], so[RM_NQ];
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) sg[i] = q[Q_SIG + i];
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) so[i] = __shfl_xor(sg[i], 32);
+            if (uon && nod) {
+                if (lsq) {
+                    for (int e = 0; e < RmLds::NT; ++e) Hk[e] = 0.0;
+                    Hk[hp(0, 0)] = 1.0; Hk[hp(2, 2)] = 1.0;
+                    Hk[hp(1, 1)] = 1.0 + sg[2] + so[0];
+                    Hk[hp(3, 3)] = 1.0 + so[1] + so[2];
+                    Hk[hp(6, 6)] = 1.0 + sg[0]; Hk[hp(7, 7)] = 1.0 + sg[1];
+                    Hk[hp(4, 4)] = sg[0]; Hk[hp(5, 5)] = sg[1];
+                } else {
+                    double w[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) w[i] = eta * pn[P_DRX + i] * pn[P_DRX + i];
+                    double wu[2];
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        wu[j] = eta * pn[P_DRU + j] * pn[P_DRU + j] + zl[j] / (u[j] - lo) + zu[j] / (hi - u[j]);
+                    Hk[hp(0, 0)] = hd[0] + w[0] + delta;
+                    Hk[hp(1, 1)] = hd[1] + w[1] + sg[2] + so[0] + delta;
+                    Hk[hp(2, 2)] = hd[2] + w[2] + delta;
+                    Hk[hp(3, 3)] = hd[3] + w[3] + so[1] + so[2] + delta;
+                    Hk[hp(6, 6)] = hd[4] + wu[0] + sg[0] + delta;
+                    Hk[hp(7, 7)] = hd[5] + wu[1] + sg[1] + delta;
+                    Hk[hp(4, 4)] = sg[0] + delta; Hk[hp(5, 5)] = sg[1] + delta;
+                }
+                Hk[hp(6, 4)] = -sg[0]; Hk[hp(7, 5)] = -sg[1];
+            }
+            if (k == N && nod) {   // terminal surrogate: [[eta D_R^2 + delta, grad], [grad^T, 0]], Quu = I
+                double* GN = S->G[N];
+                for (int e = 0; e < RmLds::NT; ++e) GN[e] = 0.0;
+#pragma unroll
+                for (int i = 0; i < 6; ++i)
+                    GN[hp(i, i)] = i < 4 ? (lsq ? 1.0 : eta * pn[P_DRX + i] * pn[P_DRX + i] + delta) : (lsq ? 0.0 : delta);
+                GN[hp(6, 6)] = 1.0; GN[hp(7, 7)] = 1.0;
+            }
+        };
+        // gradient rows: the proximity and barrier terms (or the override ov of a refinement solve), plus
+        // C^T (sigma rin + offv) of the inequality rows; the terminal surrogate's gradient row
+        auto assemble_g = [&](const double* rin, const double* offv, const double* ov, bool lsq) {
+            double tq[RM_NQ], to[RM_NQ];
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) tq[i] = uon ? q[Q_SIG + i] * rin[i] + offv[i] : 0.0;
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) to[i] = __shfl_xor(tq[i], 32);
+            double gq[8];
+            if (ov) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) gq[j] = ov[j];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) gq[i] = eta * pn[P_DRX + i] * pn[P_DRX + i] * (x[i] - pn[P_XR + i]);
+                gq[4] = 0.0; gq[5] = 0.0;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    gq[6 + j] = eta * pn[P_DRU + j] * pn[P_DRU + j] * (u[j] - pn[P_UR + j]);
+                    gq[6 + j] += lsq ? -zl[j] + zu[j] : -rmu / (u[j] - lo) + rmu / (hi - u[j]);
+                }
+            }
+            if (uon && nod) {
+                gq[6] += tq[0]; gq[4] -= tq[0]; gq[7] += tq[1]; gq[5] -= tq[1];
+                gq[1] += tq[2] - to[0];
+                gq[3] += to[1] - to[2];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) Hk[hp(8, j)] = gq[j];
+            }
+            if (k == N && nod) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) S->G[N][hp(8, j)] = j < 4 ? gq[j] : (ov ? ov[j] : 0.0);
+            }
+        };
+        // soft rows of node k's physical incoming rows (shift delta): Sigma_p', Sigma_n', 1 / D
+        auto soft_set = [&](double delta, bool lsq) {
+            if (nod) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const double sp_ = lsq ? 1.0 : pn[P_ZP + i] / pn[P_PC + i] + delta;
+                    const double sn_ = lsq ? 1.0 : pn[P_ZN + i] / pn[P_NC + i] + delta;
+                    pn[P_SP + i] = sp_; pn[P_SN + i] = sn_;
+                    if (xon) SR->Dinv[k][i] = 1.0 / (1.0 / sp_ + 1.0 / sn_);
+                }
+            }
+        };
+        // right-hand side of the soft rows: rg = cgv - (rnv / Sigma_n' - rpv / Sigma_p') + D lamv (physical),
+        // cgv (copy rows), into the defect column of M~ and dx~_0
+        auto soft_rhs = [&](const double* cgv, const double* lamv, const double* rpv, const double* rnv) {
+            double rg[6];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const double sp_ = pn[P_SP + i], sn_ = pn[P_SN + i];
+                rg[i] = cgv[i] - (rnv[i] / sn_ - rpv[i] / sp_) + (1.0 / sp_ + 1.0 / sn_) * lamv[i];
+            }
+            rg[4] = cgv[4]; rg[5] = cgv[5];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+                const double t = from_next(rg[r]);
+                if (uon && nod) Mk[8 * RmLds::NC + r] = -t;
+                if (k == 0 && nod) S->dx0[r] = -rg[r];
+            }
+        };
+        // the step from the factorised soft system: dx~_0 and the closed-loop rows through the soft rows,
+        // forward sweep, du = [K | k] [dx~; 1], lambda+ = -(P dx~ + p) with the unsoftened value function
+        double dx[6], dU[2], lamp[6], dY[RM_NQ], dS[RM_NQ], dqp[RM_NQ], dqn[RM_NQ], dpc[4], dnc[4];
+        auto rstep = [&]() {
+            if (k == 0 && nod) {
+                double d0[6];
+#pragma unroll
+                for (int r = 0; r < 6; ++r) d0[r] = S->dx0[r];
+                const double* Y0 = SR->T[0];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    double t = Y0[7 * r + 6];
+#pragma unroll
+                    for (int aa = 0; aa < 6; ++aa) t = fma(Y0[7 * r + aa], d0[aa], t);
+                    S->dx0[r] = t;
+                }
+            }
+            __syncthreads();
+            closed_loop(S, N, RmSoftPost{S, SR});
+            forward_sweep(S, N, k, dx);
+            const double* K0 = S->KK[uon ? k : 0][0];
+            const double* K1 = S->KK[uon ? k : 0][1];
+            double d0 = K0[6], d1 = K1[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) { d0 = fma(K0[j], dx[j], d0); d1 = fma(K1[j], dx[j], d1); }
+            dU[0] = uon ? d0 : 0.0; dU[1] = uon ? d1 : 0.0;
+            node_multiplier(S, xon ? k : 0, dx, dU, lamp);
+        };
+        // the eliminated rows' steps: y + dy = sigma (C dz + rin) + offv, ds, dp, dn of the inequality rows,
+        // dp, dn of the physical defect rows
+        auto rdirs = [&](const double* rin, const double* offv, const double* psv, const double* rqpv,
+                         const double* rqnv, const double* yv, const double* lamv, const double* rpv, const double* rnv) {
+            const double dz[8] = {dx[0], dx[1], dx[2], dx[3], dx[4], dx[5], dU[0], dU[1]};
+            double cdz[RM_NQ];
+            rm_iq3(dz, 0.0, mir, cdz);
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) {
+                const double yn = q[Q_SIG + i] * (cdz[i] + rin[i]) + offv[i];
+                dY[i] = uon ? yn - yv[i] : 0.0;
+                dS[i] = uon ? (yn - psv[i]) / q[Q_SS + i] : 0.0;
+                dqp[i] = uon ? (dY[i] - rqpv[i]) / q[Q_SP + i] : 0.0;
+                dqn[i] = uon ? (-dY[i] - rqnv[i]) / q[Q_SN + i] : 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const double dl = lamp[i] - lamv[i];
+                dpc[i] = xon ? (dl - rpv[i]) / pn[P_SP + i] : 0.0;
+                dnc[i] = xon ? (-dl - rnv[i]) / pn[P_SN + i] : 0.0;
+            }
+        };
+        auto park = [&](double* v) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { v[V_DX + i] = dx[i]; v[V_LP + i] = lamp[i]; }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) v[V_DU + j] = dU[j];
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) { v[V_DY + i] = dY[i]; v[V_DS + i] = dS[i]; v[V_DQP + i] = dqp[i]; v[V_DQN + i] = dqn[i]; }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { v[V_DPC + i] = dpc[i]; v[V_DNC + i] = dnc[i]; }
+        };
+        auto unpark = [&](const double* v, bool add) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                dx[i] = add ? dx[i] + v[V_DX + i] : v[V_DX + i];
+                lamp[i] = add ? lamp[i] + v[V_LP + i] : v[V_LP + i];
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) dU[j] = add ? dU[j] + v[V_DU + j] : v[V_DU + j];
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) {
+                dY[i] = add ? dY[i] + v[V_DY + i] : v[V_DY + i];
+                dS[i] = add ? dS[i] + v[V_DS + i] : v[V_DS + i];
+                dqp[i] = add ? dqp[i] + v[V_DQP + i] : v[V_DQP + i];
+                dqn[i] = add ? dqn[i] + v[V_DQN + i] : v[V_DQN + i];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                dpc[i] = add ? dpc[i] + v[V_DPC + i] : v[V_DPC + i];
+                dnc[i] = add ? dnc[i] + v[V_DNC + i] : v[V_DNC + i];
+            }
+        };
+        const double zero6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+
+        // ---- least-square equality multipliers of the restoration problem (unit weights on x, u, s, p, n) ----
+        {
+            if (nod) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { pn[P_RP + i] = rho - pn[P_ZP + i]; pn[P_RN + i] = rho - pn[P_ZN + i]; }
+            }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) lam[i] = 0.0;
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) yq[i] = 0.0;
+            rderiv();
+            iq_terms(0.0, true);
+            assemble_H(0.0, true);
+            assemble_g(zero6, q + Q_OFF, nullptr, true);
+            soft_set(0.0, true);
+            soft_rhs(zero6, zero6, pn + P_RP, pn + P_RN);
+            __syncthreads();
+            (void)riccati_sweep_aug_soft<RmLds, 4>(S, SR, N);      // unit weights: positive definite
+            rstep();
+            double ym = 0.0;
+            bool fin = true;
+            const double dz[8] = {dx[0], dx[1], dx[2], dx[3], dx[4], dx[5], dU[0], dU[1]};
+            double cdz[RM_NQ], yd[RM_NQ];
+            rm_iq3(dz, 0.0, mir, cdz);
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) {
+                yd[i] = uon ? q[Q_SIG + i] * cdz[i] + q[Q_OFF + i] : 0.0;
+                ym = fmax(ym, fabs(yd[i]));
+                fin = fin && isfinite(yd[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                if (i < 4) ym = fmax(ym, nod && xon ? fabs(lamp[i]) : 0.0);
+                fin = fin && (!xon || isfinite(lamp[i]));
+            }
+            const bool use = !wany(!fin) && wmax(ym) <= 1e3;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) lam[i] = (use && xon) ? lamp[i] : 0.0;
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) yq[i] = use ? yd[i] : 0.0;
+        }
+        int rit = it + 1, rnf = 0, rstat = -2;
+        bool rfirst = true, rok = false;
+        double rfth = 0.0, rfph = 0.0, rdelta_last = 0.0, thr = 0.0, rth_max = 0.0, rth_min = 0.0;
+        double cg[6], cr[RM_NQ];
+        for (;; ++rit) {
+            rderiv();
+            {
+                double g[6], cz[RM_NQ];
+                incoming(g);
+                const double zz[8] = {x[0], x[1], x[2], x[3], up[0], up[1], u[0], u[1]};
+                rm_iq3(zz, vmax, mir, cz);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) cg[i] = i < 4 ? g[i] + pn[P_NC + i] - pn[P_PC + i] : g[i];
+#pragma unroll
+                for (int i = 0; i < RM_NQ; ++i) cr[i] = uon ? cz[i] - s[i] + q[Q_QN + i] - q[Q_QP + i] : 0.0;
+                if (rfirst) {
+                    double t = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) t += nod && xon ? fabs(cg[i]) : 0.0;
+#pragma unroll
+                    for (int i = 0; i < RM_NQ; ++i) t += uon ? fabs(cr[i]) : 0.0;
+                    thr = wsum_rl(t);
+                    rth_max = 1e4 * fmax(1.0, thr); rth_min = 1e-4 * fmax(1.0, thr);
+                } else {
+                    // RestoConvergenceCheck: the original problem's progress at the current point
+                    double t = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) t += nod && xon ? fabs(g[i]) : 0.0;
+#pragma unroll
+                    for (int i = 0; i < RM_NQ; ++i) t += uon ? fabs(cz[i] - s[i]) : 0.0;
+                    const double tho = wsum_rl(t);
+                    if (tho <= 0.9 * th0) {
+                        double pl = nod ? sc * cost_val(x, u, up) : 0.0;
+                        double pa = 1.0;
+                        if (uon) {
+                            const double pb = (u[0] - lo) * (hi - u[0]) * (u[1] - lo) * (hi - u[1]) * ((s[0] - sL[0]) * (s[1] - sL[1]));
+                            pa = nod ? pb : 1.0;
+#pragma unroll
+                            for (int i = 0; i < RM_NQ; ++i) pa *= sU[i] - s[i];
+                        }
+                        pl -= uon ? mu0 * log_fast(pa) : 0.0;
+                        const double pho = wsum_rl(pl);
+                        bool accp = isfinite(pho) && !wany(lane < nfilt && tho >= fth && pho >= fph);
+                        accp = accp && (cmp_le(tho, (1 - gam_th) * th0, th0) || cmp_le(pho - phi0, -gam_ph * th0, phi0));
+                        if (accp) { rok = true; theta = tho; break; }
+                    }
+                }
+            }
+            rfirst = false;
+            // ---- optimality error of the restoration problem ----
+            double dinf = 0.0, pinf = 0.0, c0r = 0.0, cminr = 1e300, suml = 0.0, sumz = 0.0;
+            {
+                double gl[8];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) gl[i] = eta * pn[P_DRX + i] * pn[P_DRX + i] * (x[i] - pn[P_XR + i]);
+                gl[4] = 0.0; gl[5] = 0.0;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) gl[6 + j] = eta * pn[P_DRU + j] * pn[P_DRU + j] * (u[j] - pn[P_UR + j]);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) gl[i] += lam[i];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) gl[j] -= jl[j];
+                gl[6] -= jl[4] + lmn[4]; gl[7] -= jl[5] + lmn[5];
+                double yo[RM_NQ];
+#pragma unroll
+                for (int i = 0; i < RM_NQ; ++i) yo[i] = __shfl_xor(yq[i], 32);
+                gl[6] += yq[0]; gl[4] -= yq[0]; gl[7] += yq[1]; gl[5] -= yq[1];
+                gl[1] += yq[2] - yo[0]; gl[3] += yo[1] - yo[2];
+                gl[6] += -zl[0] + zu[0]; gl[7] += -zl[1] + zu[1];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) dinf = fmax(dinf, nod && (j < 6 ? xon : uon) ? fabs(gl[j]) : 0.0);
+                if (uon) {
+#pragma unroll
+                    for (int i = 0; i < RM_NQ; ++i) {
+                        const double y = yq[i];
+                        dinf = fmax(dinf, fabs(-y - vl[i] + vu[i]));
+                        dinf = fmax(dinf, fmax(fabs(rho - q[Q_ZQP + i] - y), fabs(rho - q[Q_ZQN + i] + y)));
+                        pinf = fmax(pinf, fabs(cr[i]));
+                        if (tw[i]) {
+                            const double cl = vl[i] * (s[i] - sL[i]);
+                            c0r = fmax(c0r, cl); cminr = fmin(cminr, cl); sumz += vl[i];
+                        }
+                        const double cu = vu[i] * (sU[i] - s[i]), cp = q[Q_ZQP + i] * q[Q_QP + i], cn = q[Q_ZQN + i] * q[Q_QN + i];
+                        c0r = fmax(c0r, fmax(cu, fmax(cp, cn))); cminr = fmin(cminr, fmin(cu, fmin(cp, cn)));
+                        sumz += vu[i] + q[Q_ZQP + i] + q[Q_ZQN + i];
+                        suml += fabs(y);
+                    }
+                    if (nod) {
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const double cl = zl[j] * (u[j] - lo), cu = zu[j] * (hi - u[j]);
+                            c0r = fmax(c0r, fmax(cl, cu)); cminr = fmin(cminr, fmin(cl, cu));
+                            sumz += zl[j] + zu[j];
+                        }
+                    }
+                }
+                if (nod && xon) {
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) { pinf = fmax(pinf, fabs(cg[i])); suml += fabs(lam[i]); }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        dinf = fmax(dinf, fmax(fabs(rho - pn[P_ZP + i] - lam[i]), fabs(rho - pn[P_ZN + i] + lam[i])));
+                        const double cp = pn[P_ZP + i] * pn[P_PC + i], cn = pn[P_ZN + i] * pn[P_NC + i];
+                        c0r = fmax(c0r, fmax(cp, cn)); cminr = fmin(cminr, fmin(cp, cn));
+                        sumz += pn[P_ZP + i] + pn[P_ZN + i];
+                    }
+                }
+                dinf = wmax(dinf); pinf = wmax(pinf); c0r = wmax(c0r); cminr = wmin(cminr);
+                suml = wsum_rl(suml); sumz = wsum_rl(sumz);
+            }
+            const double s_d = fmax(100.0, (suml + sumz) / (nA + nI + nbr)) / 100.0;
+            const double s_c = fmax(100.0, sumz / nbr) / 100.0;
+            const double errr = fmax(dinf / s_d, fmax(pinf, c0r / s_c));
+            if (rit >= a.max_iter) { rstat = -1; break; }
+            // the restoration problem converged: local infeasibility (IPOPT Infeasible_Problem_Detected, 2)
+            if (errr <= tol && dinf <= 1.0 && pinf <= 1e-4 && c0r <= 1e-4) { rstat = 2; break; }
+            for (;;) {
+                const double cmu = fmax(c0r - rmu, rmu - cminr);
+                if (fmax(dinf / s_d, fmax(pinf, cmu / s_c)) > 10.0 * rmu || rmu <= mu_min) break;
+                rmu = fmax(mu_min, fmin(0.2 * rmu, rmu * sqrt(rmu)));
+                eta = sqrt(rmu);
+                rnf = 0;
+            }
+            const double taur = fmax(0.99, 1.0 - rmu);
+            if (nod) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    pn[P_RP + i] = rho - rmu / pn[P_PC + i] - lam[i];
+                    pn[P_RN + i] = rho - rmu / pn[P_NC + i] + lam[i];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) {
+                q[Q_RQP + i] = uon ? rho - rmu / q[Q_QP + i] - yq[i] : 0.0;
+                q[Q_RQN + i] = uon ? rho - rmu / q[Q_QN + i] + yq[i] : 0.0;
+            }
+            // ---- the step: plain (with inertia correction) or a second-order correction pass, one solve site;
+            //      each solve refined iteratively (IPOPT's PDFullSpaceSolver) ----
+            double delta = 0.0, amr = 1.0, azr = 1.0, phir = 0.0, gtdr = 0.0, aminr = 0.0, alr = 1.0;
+            double csg[6], csr[RM_NQ], cgt[6], crt[RM_NQ], tht = 0.0, pht = 0.0, th_prev = 0.0;
+            bool accr = false, ftr = false, okr = true;
+            int soc = -1, ls = 0;
+            // fractions to the boundary of the primal step (amr) and of every bound multiplier (azr)
+            auto pn_steps = [&]() {
+                double am = 1.0, a2 = 1.0;
+                if (nod && xon) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const double p = pn[P_PC + i], n = pn[P_NC + i], zp = pn[P_ZP + i], zn = pn[P_ZN + i];
+                        if (dpc[i] < 0) am = fmin(am, -taur * p / dpc[i]);
+                        if (dnc[i] < 0) am = fmin(am, -taur * n / dnc[i]);
+                        const double dzp = rmu / p - zp - zp / p * dpc[i], dzn = rmu / n - zn - zn / n * dnc[i];
+                        if (dzp < 0) a2 = fmin(a2, -taur * zp / dzp);
+                        if (dzn < 0) a2 = fmin(a2, -taur * zn / dzn);
+                    }
+                }
+                if (uon) {
+                    if (nod) {
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const double sl_ = u[j] - lo, su_ = hi - u[j];
+                            if (dU[j] < 0) am = fmin(am, -taur * sl_ / dU[j]);
+                            if (dU[j] > 0) am = fmin(am, taur * su_ / dU[j]);
+                            const double dzl_ = rmu / sl_ - zl[j] - zl[j] / sl_ * dU[j];
+                            const double dzu_ = rmu / su_ - zu[j] + zu[j] / su_ * dU[j];
+                            if (dzl_ < 0) a2 = fmin(a2, -taur * zl[j] / dzl_);
+                            if (dzu_ < 0) a2 = fmin(a2, -taur * zu[j] / dzu_);
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < RM_NQ; ++i) {
+                        const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
+                        if (tw[i] && dS[i] < 0) am = fmin(am, -taur * dl / dS[i]);
+                        if (dS[i] > 0) am = fmin(am, taur * du_ / dS[i]);
+                        const double p = q[Q_QP + i], n = q[Q_QN + i], zp = q[Q_ZQP + i], zn = q[Q_ZQN + i];
+                        if (dqp[i] < 0) am = fmin(am, -taur * p / dqp[i]);
+                        if (dqn[i] < 0) am = fmin(am, -taur * n / dqn[i]);
+                        if (tw[i]) {
+                            const double dv = rmu / dl - vl[i] - vl[i] / dl * dS[i];
+                            if (dv < 0) a2 = fmin(a2, -taur * vl[i] / dv);
+                        }
+                        const double dv = rmu / du_ - vu[i] + vu[i] / du_ * dS[i];
+                        if (dv < 0) a2 = fmin(a2, -taur * vu[i] / dv);
+                        const double dzp = rmu / p - zp - zp / p * dqp[i], dzn = rmu / n - zn - zn / n * dqn[i];
+                        if (dzp < 0) a2 = fmin(a2, -taur * zp / dzp);
+                        if (dzn < 0) a2 = fmin(a2, -taur * zn / dzn);
+                    }
+                }
+                amr = wmin(am); azr = wmin(a2);
+            };
+            // one refinement pass: the residuals of the full Newton system at the step (stationarity of z, the
+            // soft defect rows, the p / n rows of both kinds, the inequality and slack rows) solved for on the
+            // same factorisation and added, while they exceed 1e-12 (1 + |step|); returns false when done
+            auto refine = [&](const double* cgv, const double* crv) -> bool {
+                double lpn_[6], pdx[6], pdu[2];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) { const double t = from_next(lamp[i]); lpn_[i] = uon ? t : 0.0; }
+#pragma unroll
+                for (int i = 0; i < 6; ++i) pdx[i] = from_prev(dx[i]);
+                pdu[0] = from_prev(dU[0]); pdu[1] = from_prev(dU[1]);
+                double ex[8], ec[6], ep[4], en[4], eq[RM_NQ], eqp[RM_NQ], eqn[RM_NQ], es[RM_NQ];
+                double emax = 0.0, smax = 0.0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ex[j] = 0.0;
+                if (uon && nod) {
+                    const double dz[8] = {dx[0], dx[1], dx[2], dx[3], dx[4], dx[5], dU[0], dU[1]};
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        double t = Hk[hp(8, j)];
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) t = fma(Hk[hp(j, i)], dz[i], t);
+                        if (j < 6) t += lamp[j];
+#pragma unroll
+                        for (int mm = 0; mm < 6; ++mm) t -= Mk[j * RmLds::NC + mm] * lpn_[mm];
+                        ex[j] = t;
+                        emax = fmax(emax, fabs(t));
+                    }
+                } else if (k == N && nod) {
+                    const double* GN = S->G[N];
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) {
+                        double t = GN[hp(8, j)];
+#pragma unroll
+                        for (int i = 0; i < 6; ++i) t = fma(GN[hp(j, i)], dx[i], t);
+                        ex[j] = t + lamp[j];
+                        emax = fmax(emax, fabs(ex[j]));
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 6; ++i) ec[i] = 0.0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { ep[i] = 0.0; en[i] = 0.0; }
+                if (nod && xon) {
+                    const double* Mp = &S->M[k > 0 ? k - 1 : 0][0][0];
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) {
+                        double jd = dx[i];
+                        if (k > 0) {
+#pragma unroll
+                            for (int mm = 0; mm < 6; ++mm) jd -= Mp[mm * RmLds::NC + i] * pdx[mm];
+                            jd -= Mp[6 * RmLds::NC + i] * pdu[0];
+                            jd -= Mp[7 * RmLds::NC + i] * pdu[1];
+                        }
+                        smax = fmax(smax, fabs(dx[i]));
+                        if (i < 4) {
+                            const double dl = lamp[i] - lam[i];
+                            ec[i] = jd + dnc[i] - dpc[i] + cgv[i];
+                            ep[i] = pn[P_SP + i] * dpc[i] - dl + pn[P_RP + i];
+                            en[i] = pn[P_SN + i] * dnc[i] + dl + pn[P_RN + i];
+                            emax = fmax(emax, fmax(fabs(ep[i]), fabs(en[i])));
+                            smax = fmax(smax, fmax(fabs(dpc[i]), fabs(dnc[i])));
+                        } else {
+                            ec[i] = jd + cgv[i];
+                        }
+                        emax = fmax(emax, fabs(ec[i]));
+                    }
+                }
+                {
+                    const double dz[8] = {dx[0], dx[1], dx[2], dx[3], dx[4], dx[5], dU[0], dU[1]};
+                    double cdz[RM_NQ];
+                    rm_iq3(dz, 0.0, mir, cdz);
+#pragma unroll
+                    for (int i = 0; i < RM_NQ; ++i) {
+                        eq[i] = uon ? cdz[i] - dS[i] + dqn[i] - dqp[i] + crv[i] : 0.0;
+                        eqp[i] = uon ? q[Q_SP + i] * dqp[i] - dY[i] + q[Q_RQP + i] : 0.0;
+                        eqn[i] = uon ? q[Q_SN + i] * dqn[i] + dY[i] + q[Q_RQN + i] : 0.0;
+                        es[i] = uon ? q[Q_SS + i] * dS[i] - (yq[i] + dY[i]) + q[Q_PSI + i] : 0.0;
+                        emax = fmax(emax, fmax(fmax(fabs(eq[i]), fabs(eqp[i])), fmax(fabs(eqn[i]), fabs(es[i]))));
+                        smax = fmax(smax, fmax(fabs(dS[i]), fmax(fabs(dqp[i]), fabs(dqn[i]))));
+                    }
+                }
+                if (uon && nod) smax = fmax(smax, fmax(fabs(dU[0]), fabs(dU[1])));
+                emax = wmax(emax); smax = wmax(smax);
+#ifdef DART_RESTO_TRACE
+                {
+                    double e1 = 0.0, e2 = 0.0, e3 = 0.0, e4 = 0.0;
+                    for (int j = 0; j < 8; ++j) e1 = fmax(e1, fabs(ex[j]));
+                    for (int i = 0; i < 6; ++i) e2 = fmax(e2, fabs(ec[i]));
+                    for (int i = 0; i < 4; ++i) e3 = fmax(e3, fmax(fabs(ep[i]), fabs(en[i])));
+                    for (int i = 0; i < RM_NQ; ++i) e4 = fmax(e4, fmax(fmax(fabs(eq[i]), fabs(eqp[i])), fmax(fabs(eqn[i]), fabs(es[i]))));
+                    e1 = wmax(e1); e2 = wmax(e2); e3 = wmax(e3); e4 = wmax(e4);
+                    double dmn = 1e300, dmx = 0.0, smx = 0.0;
+                    if (nod && xon) for (int i = 0; i < 4; ++i) { dmn = fmin(dmn, SR->Dinv[k][i]); dmx = fmax(dmx, SR->Dinv[k][i]); }
+                    if (uon) for (int i = 0; i < RM_NQ; ++i) smx = fmax(smx, q[Q_SIG + i]);
+                    dmn = wmin(dmn); dmx = wmax(dmx); smx = wmax(smx);
+                    if (blockIdx.x == 0 && lane == 0)
+                        printf("     refine emax %.3e (stat %.2e defect %.2e pn %.2e iq %.2e) smax %.3e  Dinv [%.2e, %.2e] sigma max %.2e\n",
+                               emax, e1, e2, e3, e4, smax, dmn, dmx, smx);
+                }
+#endif
+                if (!(emax > 1e-12 * (1.0 + smax))) return false;
+                // the correction solve: lambda = y = 0, the residuals as gradient and right-hand sides
+                park(RS.SV2[lane]);
+                double gsave[8], offc[RM_NQ];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) gsave[j] = (uon && nod) ? Hk[hp(8, j)] : (k == N && nod && j < 6 ? S->G[N][hp(8, j)] : 0.0);
+#pragma unroll
+                for (int i = 0; i < RM_NQ; ++i)
+                    offc[i] = uon ? q[Q_SIG + i] * (es[i] / q[Q_SS + i] - eqn[i] / q[Q_SN + i] + eqp[i] / q[Q_SP + i]) : 0.0;
+                assemble_g(eq, offc, ex, false);
+                soft_rhs(ec, zero6, ep, en);
+                __syncthreads();
+                (void)riccati_sweep_aug_soft<RmLds, 4>(S, SR, N);
+                rstep();
+                rdirs(eq, offc, es, eqp, eqn, zero6, zero6, ep, en);
+                unpark(RS.SV2[lane], true);
+                if (uon && nod) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) Hk[hp(8, j)] = gsave[j];
+                } else if (k == N && nod) {
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) S->G[N][hp(8, j)] = gsave[j];
+                }
+                __syncthreads();
+                return true;
+            };
+            // trial point of the restoration problem at step al: constraint values cgt / crt, theta, barrier
+            auto trial_r = [&](double al) {
+                double xt[4], pt[2], ut[2], st_[RM_NQ], gt[6];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xt[i] = fma(al, dx[i], x[i]);
+                pt[0] = fma(al, dx[4], up[0]); pt[1] = fma(al, dx[5], up[1]);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) ut[j] = uon ? fma(al, dU[j], u[j]) : u[j];
+#pragma unroll
+                for (int i = 0; i < RM_NQ; ++i) st_[i] = fma(al, dS[i], s[i]);
+                defects(xt, pt, ut, gt);
+                const double zt[8] = {xt[0], xt[1], xt[2], xt[3], pt[0], pt[1], ut[0], ut[1]};
+                double ct[RM_NQ];
+                rm_iq3(zt, vmax, mir, ct);
+                double thl = 0.0, phl = 0.0, lb = 0.0;
+                bool inside = true;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    if (i < 4) {
+                        const double p = fma(al, dpc[i], pn[P_PC + i]), n = fma(al, dnc[i], pn[P_NC + i]);
+                        cgt[i] = gt[i] + n - p;
+                        if (nod && xon) {
+                            const double e = pn[P_DRX + i] * (xt[i] - pn[P_XR + i]);
+                            phl += rho * (p + n) + 0.5 * eta * e * e;
+                            inside = inside && p > 0.0 && n > 0.0;
+                            lb += log_fast(p) + log_fast(n);
+                        }
+                    } else {
+                        cgt[i] = gt[i];
+                    }
+                    thl += nod && xon ? fabs(cgt[i]) : 0.0;
+                }
+                if (uon) {
+#pragma unroll
+                    for (int i = 0; i < RM_NQ; ++i) {
+                        const double p = fma(al, dqp[i], q[Q_QP + i]), n = fma(al, dqn[i], q[Q_QN + i]);
+                        crt[i] = ct[i] - st_[i] + n - p;
+                        thl += fabs(crt[i]);
+                        phl += rho * (p + n);
+                        const double dl = st_[i] - sL[i], du_ = sU[i] - st_[i];
+                        inside = inside && p > 0.0 && n > 0.0 && du_ > 0.0 && (!tw[i] || dl > 0.0);
+                        lb += log_fast(p) + log_fast(n) + (tw[i] ? log_fast(dl) : 0.0) + log_fast(du_);
+                    }
+                    if (nod) {
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const double e = pn[P_DRU + j] * (ut[j] - pn[P_UR + j]);
+                            phl += 0.5 * eta * e * e;
+                            inside = inside && ut[j] > lo && ut[j] < hi;
+                            lb += log_fast(ut[j] - lo) + log_fast(hi - ut[j]);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < RM_NQ; ++i) crt[i] = 0.0;
+                }
+                phl = inside ? phl - rmu * lb : __builtin_inf();
+                tht = wsum_rl(thl); pht = wsum_rl(phl);
+            };
+            auto racc = [&](double al_test, bool& ft) {
+                const bool in_f = !(tht < rth_max) || !isfinite(pht) || wany(lane < rnf && tht >= rfth && pht >= rfph);
+                if (in_f) return false;
+                const bool sw = gtdr < 0.0 && al_test * pow(-gtdr, s_ph) > pow(thr, s_th);
+                if (thr <= rth_min && sw) {
+                    if (cmp_le(pht, phir + eta_ph * al_test * gtdr, phir)) { ft = true; return true; }
+                    return false;
+                }
+                return cmp_le(tht, (1 - gam_th) * thr, thr) || cmp_le(pht - phir, -gam_ph * thr, phir);
+            };
+            for (;;) {
+                if (soc < 0) {
+                    int attempt = 0;
+                    for (;;) {
+                        iq_terms(delta, false);
+                        assemble_H(delta, false);
+                        assemble_g(cr, q + Q_OFF, nullptr, false);
+                        soft_set(delta, false);
+                        soft_rhs(cg, lam, pn + P_RP, pn + P_RN);
+                        __syncthreads();
+                        okr = riccati_sweep_aug_soft<RmLds, 4>(S, SR, N);
+                        if (okr || ++attempt >= 60) break;
+                        delta = (attempt == 1) ? (rdelta_last == 0.0 ? 1e-4 : fmax(1e-20, rdelta_last * (1.0 / 3.0)))
+                                               : delta * (rdelta_last == 0.0 ? 100.0 : 8.0);
+                    }
+                    if (!okr) break;
+                    if (delta > 0.0) rdelta_last = delta;
+                } else {
+                    assemble_g(csr, q + Q_OFF, nullptr, false);
+                    soft_rhs(csg, lam, pn + P_RP, pn + P_RN);
+                    __syncthreads();
+                    (void)riccati_sweep_aug_soft<RmLds, 4>(S, SR, N);
+                }
+                rstep();
+                rdirs(soc < 0 ? cr : csr, q + Q_OFF, q + Q_PSI, q + Q_RQP, q + Q_RQN, yq, lam, pn + P_RP, pn + P_RN);
+                for (int rr = 0; rr < 3 && refine(soc < 0 ? cg : csg, soc < 0 ? cr : csr); ++rr) {}
+                pn_steps();
+                double al_try;
+                if (soc < 0) {
+                    // barrier objective of the restoration problem and its directional derivative
+                    double pl = 0.0, gd = 0.0, lb = 0.0;
+                    if (nod && xon) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const double p = pn[P_PC + i], n = pn[P_NC + i];
+                            const double w = eta * pn[P_DRX + i] * pn[P_DRX + i];
+                            const double e = pn[P_DRX + i] * (x[i] - pn[P_XR + i]);
+                            pl += rho * (p + n) + 0.5 * eta * e * e;
+                            lb += log_fast(p) + log_fast(n);
+                            gd += w * (x[i] - pn[P_XR + i]) * dx[i] + (rho - rmu / p) * dpc[i] + (rho - rmu / n) * dnc[i];
+                        }
+                    }
+                    if (uon) {
+#pragma unroll
+                        for (int i = 0; i < RM_NQ; ++i) {
+                            const double p = q[Q_QP + i], n = q[Q_QN + i];
+                            pl += rho * (p + n);
+                            lb += log_fast(p) + log_fast(n) + (tw[i] ? log_fast(s[i] - sL[i]) : 0.0) + log_fast(sU[i] - s[i]);
+                            gd += (rho - rmu / p) * dqp[i] + (rho - rmu / n) * dqn[i] + q[Q_PSI + i] * dS[i];
+                        }
+                        if (nod) {
+#pragma unroll
+                            for (int j = 0; j < 2; ++j) {
+                                const double w = eta * pn[P_DRU + j] * pn[P_DRU + j];
+                                const double e = pn[P_DRU + j] * (u[j] - pn[P_UR + j]);
+                                pl += 0.5 * eta * e * e;
+                                lb += log_fast(u[j] - lo) + log_fast(hi - u[j]);
+                                gd += (w * (u[j] - pn[P_UR + j]) - rmu / (u[j] - lo) + rmu / (hi - u[j])) * dU[j];
+                            }
+                        }
+                    }
+                    phir = wsum_rl(pl - rmu * lb); gtdr = wsum_rl(gd);
+                    aminr = gam_th;
+                    if (gtdr < 0) aminr = fmin(gam_th, fmin(gam_ph * thr / (-gtdr), pow(thr, s_th) / pow(-gtdr, s_ph)));
+                    aminr *= gam_al;
+                    alr = amr;
+                    al_try = alr;
+                } else {
+                    al_try = amr;
+                }
+                bool resolve = false;
+                for (;;) {
+                    trial_r(al_try);
+                    if (soc < 0) {
+                        if (racc(alr, ftr)) { accr = true; break; }
+                        if (ls == 0 && a.max_soc > 0 && !(tht < thr)) {
+                            // second-order correction on the restoration problem's constraints; the plain step
+                            // is parked in LDS
+                            park(RS.SV[lane]);
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) csg[i] = fma(alr, cg[i], cgt[i]);
+#pragma unroll
+                            for (int i = 0; i < RM_NQ; ++i) csr[i] = fma(alr, cr[i], crt[i]);
+                            th_prev = tht; soc = 0; resolve = true;
+                            break;
+                        }
+                    } else {
+                        bool ft = false;
+                        if (racc(alr, ft)) { accr = true; ftr = ft; alr = al_try; break; }
+                        if (soc + 1 < a.max_soc && tht <= 0.99 * th_prev) {
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) csg[i] = fma(al_try, csg[i], cgt[i]);
+#pragma unroll
+                            for (int i = 0; i < RM_NQ; ++i) csr[i] = fma(al_try, csr[i], crt[i]);
+                            th_prev = tht; ++soc; resolve = true;
+                            break;
+                        }
+                        // the corrections failed: back to the plain step and its multiplier steps
+                        unpark(RS.SV[lane], false);
+                        const double amr_keep = amr;
+                        pn_steps();
+                        amr = amr_keep;
+                        soc = -1;
+                    }
+                    ++ls;
+                    alr *= 0.5;
+                    if (alr < aminr || ls >= 80) break;
+                    al_try = alr;
+                }
+                if (!resolve) break;
+            }
+#ifdef DART_RESTO_TRACE
+            if (blockIdx.x == 0 && lane == 0)
+                printf("  resto it %3d mu %.2e err %.2e dinf %.2e pinf %.2e c0 %.2e delta %.1e amax %.3e alpha %.3e th %.3e "
+                       "th_t %.3e acc %d\n", rit, rmu, errr, dinf / s_d, pinf, c0r / s_c, delta, amr, alr, thr, tht, (int)accr);
+#endif
+            if (!okr) { rstat = -3; break; }
+            if (!accr) { rstat = -2; break; }      // a failed line search in the restoration phase
+            if (!ftr && rnf < kWave) {
+                if (lane == rnf) { rfth = (1 - gam_th) * thr; rfph = phir - gam_ph * thr; }
+                ++rnf;
+            }
+            // ---- accept the trial point ----
+            if (nod && xon) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const double p = fma(alr, dpc[i], pn[P_PC + i]), n = fma(alr, dnc[i], pn[P_NC + i]);
+                    const double zp = pn[P_ZP + i], zn = pn[P_ZN + i];
+                    const double dzp = rmu / pn[P_PC + i] - zp - zp / pn[P_PC + i] * dpc[i];
+                    const double dzn = rmu / pn[P_NC + i] - zn - zn / pn[P_NC + i] * dnc[i];
+                    pn[P_PC + i] = p; pn[P_NC + i] = n;
+                    pn[P_ZP + i] = fmax(fmin(fma(azr, dzp, zp), 1e10 * rmu / p), rmu / (1e10 * p));
+                    pn[P_ZN + i] = fmax(fmin(fma(azr, dzn, zn), 1e10 * rmu / n), rmu / (1e10 * n));
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = xon ? fma(alr, dx[i], x[i]) : x[i];
+            up[0] = xon ? fma(alr, dx[4], up[0]) : up[0];
+            up[1] = xon ? fma(alr, dx[5], up[1]) : up[1];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) lam[i] = xon ? fma(alr, lamp[i] - lam[i], lam[i]) : 0.0;
+            if (uon) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const double sl_ = u[j] - lo, su_ = hi - u[j];
+                    const double dzl_ = rmu / sl_ - zl[j] - zl[j] / sl_ * dU[j];
+                    const double dzu_ = rmu / su_ - zu[j] + zu[j] / su_ * dU[j];
+                    u[j] = fma(alr, dU[j], u[j]);
+                    const double nl = u[j] - lo, nu = hi - u[j];
+                    zl[j] = fmax(fmin(fma(azr, dzl_, zl[j]), 1e10 * rmu / nl), rmu / (1e10 * nl));
+                    zu[j] = fmax(fmin(fma(azr, dzu_, zu[j]), 1e10 * rmu / nu), rmu / (1e10 * nu));
+                }
+#pragma unroll
+                for (int i = 0; i < RM_NQ; ++i) {
+                    const double dl = s[i] - sL[i], du_ = sU[i] - s[i];
+                    const double dvl_ = tw[i] ? rmu / dl - vl[i] - vl[i] / dl * dS[i] : 0.0;
+                    const double dvu_ = rmu / du_ - vu[i] + vu[i] / du_ * dS[i];
+                    const double p0 = q[Q_QP + i], n0 = q[Q_QN + i], zp = q[Q_ZQP + i], zn = q[Q_ZQN + i];
+                    const double dzp = rmu / p0 - zp - zp / p0 * dqp[i], dzn = rmu / n0 - zn - zn / n0 * dqn[i];
+                    const double p = fma(alr, dqp[i], p0), n = fma(alr, dqn[i], n0);
+                    s[i] = fma(alr, dS[i], s[i]);
+                    yq[i] = fma(alr, dY[i], yq[i]);
+                    q[Q_QP + i] = p; q[Q_QN + i] = n;
+                    q[Q_ZQP + i] = fmax(fmin(fma(azr, dzp, zp), 1e10 * rmu / p), rmu / (1e10 * p));
+                    q[Q_ZQN + i] = fmax(fmin(fma(azr, dzn, zn), 1e10 * rmu / n), rmu / (1e10 * n));
+                    const double nl = s[i] - sL[i], nu = sU[i] - s[i];
+                    if (tw[i]) vl[i] = fmax(fmin(fma(azr, dvl_, vl[i]), 1e10 * rmu / nl), rmu / (1e10 * nl));
+                    vu[i] = fmax(fmin(fma(azr, dvu_, vu[i]), 1e10 * rmu / nu), rmu / (1e10 * nu));
+                }
+            }
+            thr = tht;
+            __syncthreads();
+        }
+        if (!rok) { status = rstat; it = rit; break; }
+        // back to the original problem: the bound multipliers take the step (mu - z s_trial) / s that pretends
+        // the restoration's progress was one Newton step, cut by the fraction to the boundary (tau of the
+        // original iteration) and all reset to 1 if one exceeds 1000; the equality multipliers restart at 0
+        {
+            double a2 = 1.0, dzlo[2] = {0.0, 0.0}, dzuo[2] = {0.0, 0.0}, dvlo[RM_NQ], dvuo[RM_NQ];
+            double zl0[2], zu0[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) { zl0[j] = pn[P_ZL0 + j]; zu0[j] = pn[P_ZU0 + j]; }
+            if (uon) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const double ur = pn[P_UR + j];
+                    dzlo[j] = (mu0 - zl0[j] * (u[j] - lo)) / (ur - lo);
+                    dzuo[j] = (mu0 - zu0[j] * (hi - u[j])) / (hi - ur);
+                    if (dzlo[j] < 0) a2 = fmin(a2, -tau0 * zl0[j] / dzlo[j]);
+                    if (dzuo[j] < 0) a2 = fmin(a2, -tau0 * zu0[j] / dzuo[j]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) {
+                const double s0 = q[Q_S0 + i], v0l = q[Q_VL0 + i], v0u = q[Q_VU0 + i];
+                dvlo[i] = uon && tw[i] ? (mu0 - v0l * (s[i] - sL[i])) / (s0 - sL[i]) : 0.0;
+                dvuo[i] = uon ? (mu0 - v0u * (sU[i] - s[i])) / (sU[i] - s0) : 0.0;
+                if (dvlo[i] < 0) a2 = fmin(a2, -tau0 * v0l / dvlo[i]);
+                if (dvuo[i] < 0) a2 = fmin(a2, -tau0 * v0u / dvuo[i]);
+            }
+            const double azo = wmin(a2);
+            double zmx = 0.0;
+            if (uon) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    zl[j] = fma(azo, dzlo[j], zl0[j]); zu[j] = fma(azo, dzuo[j], zu0[j]);
+                    zmx = fmax(zmx, fmax(zl[j], zu[j]));
+                }
+#pragma unroll
+                for (int i = 0; i < RM_NQ; ++i) {
+                    vl[i] = tw[i] ? fma(azo, dvlo[i], q[Q_VL0 + i]) : 0.0;
+                    vu[i] = fma(azo, dvuo[i], q[Q_VU0 + i]);
+                    zmx = fmax(zmx, fmax(vl[i], vu[i]));
+                }
+            }
+            const bool reset = wmax(zmx) > 1e3;
+            if (uon) {
+#pragma unroll
+                for (int i = 0; i < RM_NQ; ++i) {
+                    if (reset) { vl[i] = tw[i] ? 1.0 : 0.0; vu[i] = 1.0; }
+                    const double nl = s[i] - sL[i], nu = sU[i] - s[i];
+                    if (tw[i]) vl[i] = fmax(fmin(vl[i], 1e10 * mu0 / nl), mu0 / (1e10 * nl));
+                    vu[i] = fmax(fmin(vu[i], 1e10 * mu0 / nu), mu0 / (1e10 * nu));
+                }
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if (reset) { zl[j] = 1.0; zu[j] = 1.0; }
+                    const double nl = u[j] - lo, nu = hi - u[j];
+                    zl[j] = fmax(fmin(zl[j], 1e10 * mu0 / nl), mu0 / (1e10 * nl));
+                    zu[j] = fmax(fmin(zu[j], 1e10 * mu0 / nu), mu0 / (1e10 * nu));
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) lam[i] = 0.0;
+#pragma unroll
+            for (int i = 0; i < RM_NQ; ++i) yq[i] = 0.0;
+        }
+        in_soft = 0; soft_count = 0;
+        it_next = rit;
+        __syncthreads();
+    }
+    }
 
     // ---------------- outputs -------------------------------------------------------------
+    if (!RESTO && status == kRmNeedResto) {     // handed over: rmpc_ipm_kernel<true> writes the outputs
+        if (lane == 0) a.status[b] = status;
+        return;
+    }
     const double fval = wsum_rl(nod ? cost_val(x, u, up) : 0.0);
     if (lane == 0) {
         a.u0[2 * b] = u[0]; a.u0[2 * b + 1] = u[1];
@@ -898,7 +2090,11 @@ extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStre
     if (args->N < 1 || args->N >= dartmpc::RM_NMAXS) return hipErrorInvalidValue;
     dartmpc::RmpcArgs a = *args;
     a.pack = (a.B <= 32) ? 8 : 1;            // blocks go round-robin over the 8 XCDs: one XCD, one L2 for the code
-    hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel, dim3(a.B * a.pack), dim3(dartmpc::kWave), 0, stream, a);
+    hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel<false>, dim3(a.B * a.pack), dim3(dartmpc::kWave), 0, stream, a);
+    if (a.resto) {      // the instances whose line search failed, with IPOPT's restoration phases
+        if (hipError_t e = hipGetLastError()) return e;
+        hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel<true>, dim3(a.B * a.pack), dim3(dartmpc::kWave), 0, stream, a);
+    }
     return hipGetLastError();
 }
 

@@ -35,7 +35,7 @@ EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch",
            "dart_arm_solve_batch_dev", "dart_set_device", "dart_mpc_serve_start", "dart_mpc_serve_stop",
            "dart_mpc_serve_running", "dart_mpc_bind", "dart_mpc_solve_bound")
 VARIANT_PMPC, VARIANT_RMPC, VARIANT_LMPC = 0, 1, 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class DartMPCError(RuntimeError):
@@ -381,14 +381,18 @@ class Bound:
 
 
 class RmpcSolver(Solver):
-    """``dart_mpc_handle`` of variant RMPC (regressor NMPC + fused RLS), N <= 31."""
+    """``dart_mpc_handle`` of variant RMPC (regressor NMPC + fused RLS), N <= 31.  Defaults are the
+    reference's options (np_mpc...:158-162: max_iter 200) and IPOPT's: constr_mult_init_max 1000, its soft
+    restoration / restoration phases after a failed line search (restoration=False: status -2 there; a measured
+    |v| above vmax at the pinned node 0 ends at status 2 with them) and max_soc 4 in the restoration phase."""
 
     def __init__(self, N=20, Ts=0.002, tol=1e-8, max_iter=200, B_max=1024, device=0, gravity=-9.81,
-                 constr_mult_init_max=1000.0):
+                 constr_mult_init_max=1000.0, restoration=True, max_soc=4):
         self._h = ctypes.c_void_p()
         self.cfg = default_config(variant=VARIANT_RMPC, N=int(N), Ts=float(Ts), tol=float(tol),
                                   max_iter=int(max_iter), B_max=int(B_max), gravity=float(gravity),
-                                  constr_mult_init_max=float(constr_mult_init_max))
+                                  constr_mult_init_max=float(constr_mult_init_max),
+                                  restoration=int(bool(restoration)), max_soc=int(max_soc))
         rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
         if rc != 0:
             raise DartMPCError(f"dart_mpc_create(RMPC) failed with code {rc} (no gfx950 device or bad config)")

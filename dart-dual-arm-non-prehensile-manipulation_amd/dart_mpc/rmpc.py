@@ -162,5 +162,7 @@ class RMPCStep:
                                        Rref[None], c.params()[None], w_warm=c.w0[None], want_w=True,
                                        rls_P=self.P[None], rls_phi=phi[None], rls_y=y[None], rls_lambda=self.lam)
         self.theta, self.P = out["theta"][0], out["rls_P"][0]
-        c.w0 = out["w"][0]
+        c.w0 = out["w"][0]          # whatever the status (np_mpc...:214-217: an infeasible start's iterate too)
+        c.last_status = int(out["status"][0])
+        c.last_iters = int(out["iters"][0])
         return out["u0"][0].copy(), np.array([out["f"][0]])

@@ -42,7 +42,8 @@
  *   f   [B]     objective value at the solution ("loss")    (mpc_3d.py:134)
  *   status[B]   DART_MPC_SOLVED (0), DART_MPC_MAXITER (-1), DART_MPC_LS_FAIL (-2),
  *               DART_MPC_INERTIA_FAIL (-3), DART_MPC_MAXTIME (-4, LMPC's max_cpu_time),
- *               DART_MPC_INFEASIBLE (2, LMPC: the restoration phase converged to local infeasibility).
+ *               DART_MPC_INFEASIBLE (2, RMPC / LMPC: the restoration phase converged to local
+ *               infeasibility, e.g. an RMPC start with a measured |v| above vmax at the pinned node 0).
  *               As in the reference (which never
  *               checks IPOPT's status, mpc_3d.py:133-138) u0 is written anyway.
  *   iters[B]    interior-point iterations taken.
@@ -65,7 +66,7 @@
 extern "C" {
 #endif
 
-#define DART_MPC_ABI_VERSION 7
+#define DART_MPC_ABI_VERSION 8
 
 enum dart_mpc_variant {
     DART_MPC_PMPC = 0,      /* PMPC/src/controller/mpc_3d.py, N <= 63 */
@@ -76,7 +77,7 @@ enum dart_mpc_variant {
 enum dart_mpc_status {
     DART_MPC_SOLVED = 0,
     DART_MPC_ACCEPTABLE = 1,       /* IPOPT "Solved To Acceptable Level" (LMPC: acceptable_tol / _iter) */
-    DART_MPC_INFEASIBLE = 2,       /* IPOPT "Infeasible Problem Detected" (LMPC: its restoration phase converged) */
+    DART_MPC_INFEASIBLE = 2,       /* IPOPT "Infeasible Problem Detected" (RMPC / LMPC: the restoration phase converged) */
     DART_MPC_MAXITER = -1,
     DART_MPC_LS_FAIL = -2,         /* IPOPT "Restoration Failed" (or the failed line search, restoration = 0) */
     DART_MPC_INERTIA_FAIL = -3,
@@ -105,15 +106,17 @@ typedef struct dart_mpc_config {
     double acceptable_tol;   /* IPOPT acceptable_tol; used by LMPC (rlmpc2.py:487: 1e-3) */
     int32_t acceptable_iter; /* IPOPT acceptable_iter, 0 = off; used by LMPC (rlmpc2.py:488: 5) */
     int32_t max_soc;    /* IPOPT max_soc (second-order corrections per line search), default 4, 0 = off,
-                           <= 8; used by PMPC and LMPC (the reference leaves IPOPT's default,
-                           mpc_3d.py:82, rlmpc2.py:480-489) */
+                           <= 8; used by PMPC, LMPC and RMPC's restoration phase (the reference leaves
+                           IPOPT's default, mpc_3d.py:82, np_mpc...:158-162, rlmpc2.py:480-489) */
     int32_t pmpc_path;  /* PMPC only (ABI 5): 0 = IPOPT's path on the full 6-state NLP (default; the z
                            defect rows of mpc_3d.py:37, :48 in theta, the filter, the error measures and
                            the second-order correction); 1 = the reduced (x, y) path, opt-in: same KKT
                            point to the tolerance, fewer iterations, but not IPOPT's iterates */
-    int32_t restoration;  /* LMPC (ABI 6): 1 = IPOPT's soft restoration and restoration phases after a
-                           failed filter line search (default; MinC_1NrmRestorationPhase, the fallback of
-                           every nlpsol call, rlmpc2.py:480-489); 0 = stop with status -2 there */
+    int32_t restoration;  /* LMPC (ABI 6), RMPC (ABI 8): 1 = IPOPT's soft restoration and restoration
+                           phases after a failed filter line search (default; MinC_1NrmRestorationPhase,
+                           the fallback of every nlpsol call, np_mpc...:158-162, rlmpc2.py:480-489); 0 = stop
+                           with status -2 there.  RMPC: the failed instances of a launch are re-solved by a
+                           second kernel on the same stream */
     double constr_mult_init_max;  /* IPOPT constr_mult_init_max (default 1000): the starting equality
                            multipliers are IPOPT's least-square estimate unless its max norm exceeds this
                            (then 0); 0 = always start from 0.  Used by PMPC, RMPC and LMPC */

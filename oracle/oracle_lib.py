@@ -102,14 +102,18 @@ def rlib():
         L.oracle_rmpc_set_soc.restype = None
         L.oracle_rmpc_set_resto.argtypes = [ctypes.c_int]
         L.oracle_rmpc_set_resto.restype = None
+        L.oracle_rmpc_set_slack_shift.argtypes = [ctypes.c_int]
+        L.oracle_rmpc_set_slack_shift.restype = None
         _rlib = L
     return _rlib
 
 
 def rmpc_solve_batch(x0, u_prev, theta, Rref, prm, N=20, Ts=0.002, w_init=None, max_iter=200, tol=1e-8,
-                     nthreads=1, want_w=True, relax=1e-8, soc=True, mult_init_max=1000.0, resto=True):
+                     nthreads=1, want_w=True, relax=1e-8, soc=True, mult_init_max=1000.0, resto=True, slack_shift=False):
     """resto: IPOPT's soft restoration and restoration phases (default on, as IPOPT); off, a failed filter
-    line search ends the solve at status -2."""
+    line search ends the solve at status -2.  soc: max_soc of the original and the restoration line
+    searches.  slack_shift: IPOPT's inertia shift of the slack block (delta_s = delta_x; off by default,
+    never engaged on the RMPC workloads)."""
     c = lambda a: np.ascontiguousarray(a, np.float64)
     x0, u_prev, theta, Rref, prm = c(x0), c(u_prev), c(theta), c(Rref), c(prm)
     B = x0.shape[0]
@@ -121,6 +125,7 @@ def rmpc_solve_batch(x0, u_prev, theta, Rref, prm, N=20, Ts=0.002, w_init=None, 
     rlib().oracle_rmpc_set_soc(_max_soc(soc))
     rlib().oracle_rmpc_set_mult_init_max(ctypes.c_double(float(mult_init_max)))
     rlib().oracle_rmpc_set_resto(int(bool(resto)))
+    rlib().oracle_rmpc_set_slack_shift(int(bool(slack_shift)))
     rlib().oracle_rmpc_solve_batch(B, N, Ts, _p(x0), _p(u_prev), _p(theta), _p(Rref), _p(prm),
                                    _p(wi) if wi is not None else None, max_iter, tol, nthreads,
                                    _p(u0), _p(f), _p(w) if want_w else None, _p(st, _ip), _p(it, _ip))

@@ -165,6 +165,7 @@ typedef struct {
     double sL[NIQ], sU[NIQ];                            /* relaxed slack bounds (+-inf as +-1e300) */
     struct resto_s *Rs;     /* restoration phase data (NULL: the original problem) */
     int mode;               /* 0 original problem, 1 restoration Newton step, 2 restoration least-square multipliers */
+    double ds_shift;        /* inertia shift of the slack block in the original problem's step (slack_shift) */
 } ctx_t;
 
 /* IPOPT ApplicationReturnStatus values (Infeasible_Problem_Detected = 2: the restoration problem converged to a
@@ -269,8 +270,16 @@ static int soft_node(const ctx_t *C, const double Pk[NA][NA], int k, double delt
 static double g_relax = 1e-8;
 void oracle_rmpc_set_relax(double r) { g_relax = r; }
 /* second-order correction on/off (IPOPT default on; off mirrors the GPU kernel's line search) */
-static int g_max_soc = 4;      /* IPOPT max_soc (second-order corrections per line search) */
+static int g_max_soc = 4;      /* IPOPT max_soc (second-order corrections per line search; the restoration
+                                  phase's line search reads the same option) */
 void oracle_rmpc_set_soc(int max_soc) { g_max_soc = max_soc < 0 ? 0 : max_soc; }
+/* IPOPT shifts the slack block of its KKT system by the same inertia perturbation as the x block
+   (delta_s = delta_x, PDPerturbationHandler).  Off by default here and in the kernel: the original problem's
+   inertia correction never engages on the RMPC workloads (C3 and its 2x / 3x / 6x velocity spreads), and
+   tests/test_oracle_rmpc.py checks that turning the shift on leaves every solve bit-identical.  The
+   restoration phase always shifts its slack, p and n blocks (resto_iq_terms). */
+static int g_slack_shift = 0;
+void oracle_rmpc_set_slack_shift(int on) { g_slack_shift = on; }
 
 static void stage_z(const double *X, const double *U, int k, double *z) {
     for (int i = 0; i < NA; ++i) z[i] = X[NA * k + i];
@@ -444,6 +453,7 @@ static void stage_qp(const ctx_t *C, const work_t *W, int k, double rr[NIQ], dou
         double cr[NZ], sig, psi;
         iq_row(i, cr);
         slack_terms(C, W, k, i, &sig, &psi);
+        sig += C->ds_shift;
         for (int a = 0; a < NZ; ++a) {
             if (cr[a] == 0.0) continue;
             for (int b = 0; b < NZ; ++b) Hq[a][b] += sig * cr[a] * cr[b];
@@ -631,7 +641,7 @@ static double dual_steps(const ctx_t *C, work_t *W, int nU, double tau) {
         slack_terms(C, W, k, i, &sig, &psi);
         /* dy from the eliminated system: y + dy = Sigma*ds + psi' with psi' = -mu/(s-sL)+mu/(sU-s)
            (the restoration's riccati_solve has set it from the soft row) */
-        if (!C->Rs) W->dy[k][i] = sig * ds + psi - W->y[k][i];
+        if (!C->Rs) W->dy[k][i] = (sig + C->ds_shift) * ds + psi - W->y[k][i];
         if (C->sL[i] > -1e299) {
             double d = s - C->sL[i];
             W->dvL[k][i] = C->mu / d - W->vL[k][i] - W->vL[k][i] / d * ds;
@@ -1096,7 +1106,7 @@ static int restoration(const ctx_t *C0, work_t *W, int *it_io, int max_iter, dou
     double (*cr)[NIQ] = calloc(N, sizeof(double[NIQ])), (*crt)[NIQ] = calloc(N, sizeof(double[NIQ]));
     double (*csr)[NIQ] = calloc(N, sizeof(double[NIQ]));
     ctx_t C = *C0;
-    C.Rs = R; C.mode = 1;
+    C.Rs = R; C.mode = 1; C.ds_shift = 0.0;
     R->rho = 1000.0;
     int ok_out = 0;
     /* RestoIpoptNLP: reference point and D_R */
@@ -1285,12 +1295,12 @@ static int restoration(const ctx_t *C0, work_t *W, int *it_io, int max_iter, dou
             if (alpha < amin && ls > 0) break;
             RESTO_TRIAL(alpha);
             RESTO_ACCEPT(alpha, accepted);
-            if (!accepted && ls == 0 && !(th_t < th)) {
+            if (!accepted && ls == 0 && !(th_t < th) && g_max_soc > 0) {
                 /* second-order correction on the restoration problem's constraints */
                 memcpy(Sv, V, sizeof(work_t)); memcpy(SR, R, sizeof(resto_t));
                 double asoc = alpha, th_old = 0.0;
                 memcpy(csg, cg, szg); memcpy(csr, cr, szr);
-                for (int c = 0; c < 4; ++c) {
+                for (int c = 0; c < g_max_soc; ++c) {
                     if (c > 0 && !(th_t <= kap_soc * th_old)) break;
                     th_old = th_t;
                     for (int k = 0; k <= N; ++k) for (int i = 0; i < NA; ++i) csg[k][i] = asoc * csg[k][i] + cgt[k][i];
@@ -1536,10 +1546,12 @@ int oracle_rmpc_solve(int N, double Ts, const double *x0, const double *u_prev, 
         }
         const double tau = fmax(0.99, 1.0 - C.mu);
         double delta = 0.0;
+        C.ds_shift = 0.0;
         int ok = riccati_factor(&C, W, r, 0.0);
         for (int attempt = 0; !ok && attempt < 60; ++attempt) {
             delta = (attempt == 0) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))   /* perturb_dec_fact 1/3 */
                                    : delta * (delta_last == 0.0 ? 100.0 : 8.0);
+            C.ds_shift = g_slack_shift ? delta : 0.0;
             ok = riccati_factor(&C, W, r, delta);
         }
         if (!ok) { status = ST_INERTIA_FAIL; break; }

@@ -30,8 +30,8 @@ def test_defaults_follow_reference():
     c = _lib.default_config()
     assert (c.variant, c.N, c.Ts, c.tol, c.max_iter, c.gravity) == (0, 20, 0.002, 1e-8, 3000, -9.81)
     assert _lib.lib().dart_mpc_nw(20) == 166 and _lib.lib().dart_mpc_nw(15) == 126
-    assert _lib.lib().dart_mpc_abi_version() == 7
-    assert c.restoration == 1      # IPOPT's restoration phases on by default (LMPC)
+    assert _lib.lib().dart_mpc_abi_version() == 8
+    assert c.restoration == 1      # IPOPT's restoration phases on by default (RMPC, LMPC)
     assert c.max_cpu_time == 0.05  # rlmpc2.py:485
     assert (c.acceptable_tol, c.acceptable_iter) == (1e-6, 15)                              # IPOPT defaults
     assert _lib.lib().dart_rmpc_nw(20) == 124 and _lib.lib().dart_rmpc_nw(1) == 10      # 4(N+1) + 2N

@@ -60,6 +60,29 @@ def test_idle_timeout_drains_and_restarts():
         s.serve_stop()
 
 
+def test_requests_near_the_idle_timeout():
+    """Requests posted around the idle timeout (0.2 s) -- where part of the grid may have left on its own
+    clock while the rest still waits -- are answered promptly and correctly: the host drains and relaunches
+    the grid itself from 90 % of the timeout on, so no request meets a partly drained grid and waits out a
+    further idle period."""
+    import dart_mpc
+    from dart_mpc.workload import pmpc_batch
+    S, T, P = pmpc_batch(1)
+    with dart_mpc.Solver(N=20, tol=1e-8, B_max=18) as s:
+        base = s.solve_batch(S, T, P)
+        s.serve_start(B_serve=18, idle_timeout=0.2)
+        worst = 0.0
+        for gap in (0.15, 0.17, 0.178, 0.182, 0.19, 0.195, 0.2, 0.205, 0.21, 0.22, 0.3):
+            time.sleep(gap)
+            t0 = time.perf_counter()
+            got = s.solve_batch(S, T, P)
+            worst = max(worst, time.perf_counter() - t0)
+            np.testing.assert_array_equal(got["u0"], base["u0"])
+            np.testing.assert_array_equal(got["iters"], base["iters"])
+        assert worst < 0.1, worst          # a request that waited for a partly drained grid takes >= 0.2 s
+        s.serve_stop()
+
+
 def test_two_threads_share_a_served_handle():
     import dart_mpc
     from dart_mpc.workload import pmpc_batch
