@@ -201,7 +201,7 @@ def _max_over_ranks(vals, dev, host_coll):
     return [float(x) for x in t.cpu()]
 
 
-def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False):
+def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False, coll=None):
     """C4 (BASELINE.json configs[3]): PMPC 18 configs x 64 seeds = 1152 instances, N=20, sharded over the
     ranks in contiguous blocks (dart_mpc.parallel.shard_bounds).  One step = every rank solves its block,
     packs [u0, f, status] and joins one all_gather_into_tensor (RCCL over xGMI) of the padded blocks.
@@ -210,6 +210,9 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False):
     import torch.distributed as dist
     from dart_mpc.parallel import RESULT_COLS, shard_bounds
     from dart_mpc.workload import pmpc_batch
+    # the collective runs whenever a process group exists -- also at N = 1 with --dist-backend nccl, where
+    # the gather is one RCCL all_gather_into_tensor over a world of one
+    coll = (world > 1) if coll is None else coll
     Bg, K, N = 18 * 64, args.c4_steps, args.N
     S, T, P = pmpc_batch(n_seeds=64, seed0=300000)
     lo, hi = shard_bounds(Bg, world, rank)
@@ -236,11 +239,11 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False):
             block[:n, 0:2].copy_(U0)
             block[:n, 2].copy_(FV)
             block[:n, 3].copy_(ST)
-            if world > 1 and host_coll:
+            if coll and host_coll:
                 fh = full.cpu()     # gloo rehearsal: the gather runs on host copies
                 dist.all_gather_into_tensor(fh, block.cpu())
                 full.copy_(fh)
-            elif world > 1:
+            elif coll:
                 dist.all_gather_into_tensor(full, block)
             else:
                 full.copy_(block)
@@ -249,24 +252,24 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False):
         for _ in range(3):
             step(gather)
         torch.cuda.synchronize()
-        if world > 1:
+        if coll:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(K):
             step(gather)
         torch.cuda.synchronize()
-        if world > 1:
+        if coll:
             dist.barrier()
         t = time.perf_counter() - t0
-        return _max_over_ranks([t], dev, host_coll)[0] if world > 1 else t
+        return _max_over_ranks([t], dev, host_coll)[0] if coll else t
 
     dt_solve = timed(False)      # the solves alone (with and without the gather)
     dt = timed(True)
     res = full.cpu().numpy()[:Bg]
     # every rank finds its own block, bit for bit, at its offset of the gathered result
     mine = bool(np.array_equal(res[lo:hi], block[:n].cpu().numpy()))
-    if world > 1:
+    if coll:
         mine = _max_over_ranks([0.0 if mine else 1.0], dev, host_coll)[0] == 0.0
     solver.close()
     if rank != 0:
@@ -279,7 +282,9 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False):
     return {"workload": "C4: PMPC 18 configs x 64 seeds = 1152 instances, N=20, tol 1e-8, cold start, contiguous "
                         "blocks over the ranks + all_gather_into_tensor of [u0, f, status] (RCCL)",
             "global_batch": Bg, "per_rank": per, "n_gpus": world, "scaling": "strong", "steps": K,
-            "solves_per_s": Bg * K / dt, "ms_per_step": dt / K * 1e3, "gather_in_timed_region": world > 1,
+            "solves_per_s": Bg * K / dt, "ms_per_step": dt / K * 1e3, "gather_in_timed_region": coll,
+            "gather": ("RCCL all_gather_into_tensor on device tensors" if coll and not host_coll
+                       else "gloo all_gather_into_tensor on host copies" if coll else "local copy (no process group)"),
             "solves_per_s_without_gather": Bg * K / dt_solve, "ms_per_step_without_gather": dt_solve / K * 1e3,
             "status_ok_frac": float(np.mean(res[:, 3] == 0)), "rank_blocks_consistent": mine,
             "max_abs_u0_err_vs_oracle_same_tol": float(np.max(np.abs(res[:, 0:2] - same["u0"]))),
@@ -553,7 +558,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = args.dist_backend or ("nccl" if torch.cuda.is_available() else "gloo")
     host_coll = backend == "gloo"
-    if world > 1:
+    # a process group for N > 1, and at N = 1 when --dist-backend is given (bench_c4's RCCL gather then runs
+    # over a world of one: the collective path exercised on a one-GPU box)
+    coll = world > 1 or args.dist_backend is not None
+    if coll:
+        if world == 1:
+            import socket
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                so = socket.socket(); so.bind(("127.0.0.1", 0)); os.environ["MASTER_PORT"] = str(so.getsockname()[1]); so.close()
+            os.environ.setdefault("RANK", "0"); os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group(backend)
     # one rank per GPU; a gloo rehearsal with more ranks than cards shares them round robin
     ndev = max(1, torch.cuda.device_count())
@@ -766,7 +780,7 @@ def main():
         hs.close()
 
     # supplementary C4 (BASELINE.json configs[3]): 1152 instances sharded over the ranks + result gather
-    c4 = bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll) if args.c4_steps > 0 else None
+    c4 = bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll, coll) if args.c4_steps > 0 else None
 
     # supplementary PMPC line at the DART driver's horizon (N = 15)
     n15 = None
@@ -827,7 +841,7 @@ def main():
             "config": {"workload": "C2: PMPC batch=18 object configs (3 shapes x 2 masses x 3 frictions), "
                                    "N=20, Ts=0.002, cold start, IPOPT tol 1e-8; one rank per GPU",
                        "batch_per_gpu": B, "N": N, "parallelism": f"instance-sharded x{world}",
-                       **({"dist_backend": backend} if world > 1 else {})},
+                       **({"dist_backend": backend} if coll else {})},
             "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "kernel": "pmpc_ipm_kernel", "kernel_ms": kern_ms, "issue": issue,
@@ -848,7 +862,7 @@ def main():
             "arm_qp": arm,
         }
         print(json.dumps(line))
-    if world > 1:
+    if coll:
         dist.destroy_process_group()
 
 

@@ -58,3 +58,48 @@ def test_two_ranks_hip_solve_and_gather_equal_single_launch():
         np.testing.assert_array_equal(u0, one["u0"])
         np.testing.assert_array_equal(f, one["f"])
         np.testing.assert_array_equal(st, one["status"])
+
+
+def _nccl_one(port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "dart-dual-arm-non-prehensile-manipulation_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import dart_mpc
+    from dart_mpc.parallel import solve_sharded
+    from dart_mpc.workload import pmpc_batch
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    backend = dist.get_backend()
+    S, T, P = pmpc_batch(64)
+    solver = dart_mpc.Solver(N=20, Ts=0.002, tol=1e-8, B_max=S.shape[0], device=0)
+    u0, f, st = solve_sharded(solver.solve_batch, S, T, P, 1, 0, device=torch.device("cuda", 0))
+    solver.close()
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((backend, u0, f, st))
+
+
+def test_rccl_world_of_one_gather_equals_single_launch():
+    """RCCL on the hardware there is: a "nccl" (= RCCL on ROCm) process group of world size 1 on the one GPU;
+    parallel.solve_sharded solves C4's 1152 instances and gathers the packed results as device tensors with
+    all_gather_into_tensor -- bit-equal to one launch over the batch."""
+    import torch.multiprocessing as mp
+    import dart_mpc
+    from dart_mpc.workload import pmpc_batch
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_one, args=(_free_port(), q))
+    p.start()
+    backend, u0, f, st = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and backend == "nccl"
+    S, T, P = pmpc_batch(64)
+    s = dart_mpc.Solver(N=20, Ts=0.002, tol=1e-8, B_max=S.shape[0])
+    one = s.solve_batch(S, T, P)
+    s.close()
+    np.testing.assert_array_equal(u0, one["u0"])
+    np.testing.assert_array_equal(f, one["f"])
+    np.testing.assert_array_equal(st, one["status"])
