@@ -53,7 +53,9 @@ def _p(a, t=_dp):
 
 
 def solve_batch(states, targets, params, N=20, Ts=0.002, max_iter=200, tol=1e-9, nthreads=1, want_w=True, soc=True,
-                mult_init_max=1000.0):
+                mult_init_max=1000.0, resto=True):
+    """PMPC oracle.  resto: IPOPT's soft restoration and restoration phases (default on, as IPOPT); off, a
+    failed filter line search ends the solve at status -2."""
     states = np.ascontiguousarray(states, np.float64)
     targets = np.ascontiguousarray(targets, np.float64)
     params = np.ascontiguousarray(params, np.float64)
@@ -66,6 +68,7 @@ def solve_batch(states, targets, params, N=20, Ts=0.002, max_iter=200, tol=1e-9,
     it = np.zeros(B, np.int32)
     lib().oracle_pmpc_set_soc(_max_soc(soc))
     lib().oracle_pmpc_set_mult_init_max(ctypes.c_double(float(mult_init_max)))
+    lib().oracle_pmpc_set_resto(int(bool(resto)))
     lib().oracle_pmpc_solve_batch(B, N, Ts, _p(states), _p(targets), _p(params), max_iter, tol, nthreads,
                                   _p(u0), _p(f), _p(w) if want_w else None, _p(st, _ip), _p(it, _ip))
     return dict(u0=u0, f=f, w=w, status=st, iters=it)

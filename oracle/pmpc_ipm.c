@@ -23,7 +23,13 @@
  *     IPOPT's constants) with the second-order correction (max_soc 4).
  *   Deviations (documented in DESIGN.md): the KKT system is solved by an
  *   exact stage-wise Riccati recursion instead of MUMPS (same Newton step up
- *   to rounding); no restoration phase (status -2 where IPOPT would enter it).
+ *   to rounding).
+ *   A failed filter line search goes through IPOPT's soft restoration phase and
+ *   then its restoration phase (MinC_1NrmRestorationPhase, as restated in
+ *   rmpc_ipm.c / lmpc_ipm.c: every defect row soft with its p / n pair,
+ *   least-square multipliers, its own filter and mu, second-order correction,
+ *   iterative refinement of every step): status 2 when the restoration problem
+ *   converges to a point of local infeasibility, -2 when its line search fails.
  *
  * Exact first/second derivatives of the RK4 map are taken with second-order
  * forward "jets" (value, gradient, Hessian in the 8 stage variables x,u).
@@ -188,9 +194,85 @@ typedef struct {
 
 enum { ST_SOLVED = 0, ST_MAXITER = -1, ST_LS_FAIL = -2, ST_INERTIA_FAIL = -3, ST_BAD_INPUT = -10 };
 
+struct resto_s;
 typedef struct {
     const prob_t *P; const double *state, *ref; double sc, mu, lo, hi; int N;
+    struct resto_s *Rs;     /* restoration phase data (NULL: the original problem) */
+    int mode;               /* 0 original problem, 1 restoration Newton step, 2 restoration least-square multipliers */
 } ctx_t;
+
+/* IPOPT's restoration phase for this NLP (MinC_1NrmRestorationPhase; restated as in rmpc_ipm.c, whose
+ * commentary applies): min rho sum(p + n) + eta/2 ||D_R (x - x_R)||^2 s.t. c(x) + n - p = 0 on every defect
+ * row (x_0 pinning included), p, n >= 0, the U box.  In the Newton system the rows become soft rows
+ * J dx - D dlam = rhs with D = 1/S_p + 1/S_n, absorbed by the Riccati recursion (soft_node). */
+typedef struct resto_s {
+    double pc[NX * (NMAX + 1)], nc[NX * (NMAX + 1)], zp[NX * (NMAX + 1)], zn[NX * (NMAX + 1)];
+    double dpc[NX * (NMAX + 1)], dnc[NX * (NMAX + 1)], dzp[NX * (NMAX + 1)], dzn[NX * (NMAX + 1)];
+    double rp[NX * (NMAX + 1)], rn[NX * (NMAX + 1)], D[NX * (NMAX + 1)], Spd[NX * (NMAX + 1)], Snd[NX * (NMAX + 1)];
+    double pt_[NX * (NMAX + 1)], nt_[NX * (NMAX + 1)];
+    double XR[NX * (NMAX + 1)], UR[NU * NMAX], DRx[NX * (NMAX + 1)], DRu[NU * NMAX];
+    double M[NMAX + 1][NX][NX], Pt[NMAX + 1][NX][NX];
+    double filt_th[256], filt_ph[256];
+    double rho, eta, delta;
+    int ovr;                                              /* refinement: gradient override gov */
+    double gov[NMAX + 1][NZ], ex[NMAX + 1][NZ], ec[NMAX + 1][NX], ep[NX * (NMAX + 1)], en[NX * (NMAX + 1)];
+} resto_t;
+
+/* A X = B by Gaussian elimination with partial pivoting (n x n, nrhs columns); A and B are overwritten */
+static void gauss_solve(int n, double A[NX][NX], double B[NX][NX], int nrhs) {
+    for (int c = 0; c < n; ++c) {
+        int piv = c;
+        for (int r = c + 1; r < n; ++r) if (fabs(A[r][c]) > fabs(A[piv][c])) piv = r;
+        if (piv != c) {
+            for (int j = 0; j < n; ++j) { double t = A[c][j]; A[c][j] = A[piv][j]; A[piv][j] = t; }
+            for (int j = 0; j < nrhs; ++j) { double t = B[c][j]; B[c][j] = B[piv][j]; B[piv][j] = t; }
+        }
+        for (int r = c + 1; r < n; ++r) {
+            const double f = A[r][c] / A[c][c];
+            if (f == 0.0) continue;
+            for (int j = c; j < n; ++j) A[r][j] -= f * A[c][j];
+            for (int j = 0; j < nrhs; ++j) B[r][j] -= f * B[c][j];
+        }
+    }
+    for (int c = n - 1; c >= 0; --c)
+        for (int j = 0; j < nrhs; ++j) {
+            double t = B[c][j];
+            for (int m = c + 1; m < n; ++m) t -= A[c][m] * B[m][j];
+            B[c][j] = t / A[c][c];
+        }
+}
+/* x <- M_k^-1 x (trans 0), x <- M_k^-T x (trans 1) */
+static void soft_apply(const resto_t *R, int k, int trans, double *x) {
+    double A[NX][NX], Bv[NX][NX];
+    for (int i = 0; i < NX; ++i) for (int j = 0; j < NX; ++j) A[i][j] = trans ? R->M[k][j][i] : R->M[k][i][j];
+    for (int i = 0; i < NX; ++i) Bv[i][0] = x[i];
+    gauss_solve(NX, A, Bv, 1);
+    for (int i = 0; i < NX; ++i) x[i] = Bv[i][0];
+}
+/* soft defect rows of node k (shift delta): D, M = I + D P_k, P~_k = M^-T P_k; 0 when S = P_k + D^-1 is not
+   positive definite (wrong inertia) */
+static int soft_node(const ctx_t *C, const double Pk[NX][NX], int k, double delta) {
+    resto_t *R = C->Rs;
+    for (int i = 0; i < NX; ++i) {
+        const int r = NX * k + i;
+        if (C->mode == 2) { R->Spd[r] = 1.0; R->Snd[r] = 1.0; }
+        else { R->Spd[r] = R->zp[r] / R->pc[r] + delta; R->Snd[r] = R->zn[r] / R->nc[r] + delta; }
+        R->D[r] = 1.0 / R->Spd[r] + 1.0 / R->Snd[r];
+        for (int j = 0; j < NX; ++j) R->M[k][i][j] = (i == j) + R->D[r] * Pk[i][j];
+    }
+    double A[NX][NX], Bm[NX][NX];
+    for (int i = 0; i < NX; ++i) for (int j = 0; j < NX; ++j) { A[i][j] = R->M[k][j][i]; Bm[i][j] = Pk[i][j]; }
+    gauss_solve(NX, A, Bm, NX);
+    for (int i = 0; i < NX; ++i) for (int j = 0; j < NX; ++j) R->Pt[k][i][j] = 0.5 * (Bm[i][j] + Bm[j][i]);
+    double L[NX][NX];
+    for (int i = 0; i < NX; ++i) for (int j = 0; j <= i; ++j) {
+        double t = Pk[i][j] + (i == j ? 1.0 / R->D[NX * k + i] : 0.0);
+        for (int m = 0; m < j; ++m) t -= L[i][m] * L[j][m];
+        if (i == j) { if (!(t > 0.0)) return 0; L[i][i] = sqrt(t); }
+        else L[i][j] = t / L[j][j];
+    }
+    return 1;
+}
 
 /* constraint residuals g (N+1 blocks) at (X,U); returns l1 norm */
 static double constraints(const ctx_t *C, const double *X, const double *U, double g[][NX]) {
@@ -218,13 +300,27 @@ static double barrier_obj(const ctx_t *C, const double *X, const double *U) {
 /* Riccati factorisation of the KKT matrix (Hessian blocks + delta*I).  Returns 0 on wrong inertia. */
 static int riccati_factor(const ctx_t *C, work_t *W, double delta) {
     const prob_t *P = C->P; const int N = C->N; const double sc = C->sc;
+    const resto_t *Rs = C->Rs;
+    static const double H0[NZ][NZ];        /* (least-square system: no dynamics Hessian) */
     double (*Pn)[NX] = W->Pm[N];
     for (int i = 0; i < NX; ++i) for (int j = 0; j < NX; ++j) Pn[i][j] = 0.0;
-    Pn[0][0] = Pn[2][2] = sc * 2 * P->Qp; Pn[1][1] = Pn[3][3] = sc * 2 * P->Qv;
-    for (int i = 0; i < NX; ++i) Pn[i][i] += delta;
+    if (C->mode == 0) {
+        Pn[0][0] = Pn[2][2] = sc * 2 * P->Qp; Pn[1][1] = Pn[3][3] = sc * 2 * P->Qv;
+        for (int i = 0; i < NX; ++i) Pn[i][i] += delta;
+    } else {
+        for (int i = 0; i < NX; ++i) {
+            const int r = NX * N + i;
+            Pn[i][i] = C->mode == 1 ? Rs->eta * Rs->DRx[r] * Rs->DRx[r] + delta : 1.0;
+        }
+    }
     for (int k = N - 1; k >= 0; --k) {
-        double (*A)[NX] = W->A[k], (*Bm)[NU] = W->Bm[k], (*Hk)[NZ] = W->H[k];
+        double (*A)[NX] = W->A[k], (*Bm)[NU] = W->Bm[k];
+        const double (*Hk)[NZ] = C->mode == 2 ? H0 : (const double (*)[NZ])W->H[k];
         double (*Pp)[NX] = W->Pm[k + 1];
+        if (Rs) {
+            if (!soft_node(C, (const double (*)[NX])W->Pm[k + 1], k + 1, delta)) return 0;
+            Pp = C->Rs->Pt[k + 1];
+        }
         double PA[NX][NX], PB[NX][NU], Qxx[NX][NX], Quu[NU][NU];
         for (int i = 0; i < NX; ++i) {
             for (int j = 0; j < NX; ++j) { double s = 0; for (int m = 0; m < NX; ++m) s += Pp[i][m] * A[m][j]; PA[i][j] = s; }
@@ -234,13 +330,22 @@ static int riccati_factor(const ctx_t *C, work_t *W, double delta) {
             for (int j = 0; j < NX; ++j) { double s = Hk[i][j]; for (int m = 0; m < NX; ++m) s += A[m][i] * PA[m][j]; Qxx[i][j] = s; }
             Qxx[i][i] += delta;
         }
-        Qxx[0][0] += sc * 2 * P->Qp; Qxx[2][2] += sc * 2 * P->Qp; Qxx[1][1] += sc * 2 * P->Qv; Qxx[3][3] += sc * 2 * P->Qv;
+        if (C->mode == 0) {
+            Qxx[0][0] += sc * 2 * P->Qp; Qxx[2][2] += sc * 2 * P->Qp; Qxx[1][1] += sc * 2 * P->Qv; Qxx[3][3] += sc * 2 * P->Qv;
+        } else {        /* restoration: the proximity term (mode 1), unit weights (mode 2) */
+            for (int i = 0; i < NX; ++i) {
+                const int r = NX * k + i;
+                Qxx[i][i] += C->mode == 1 ? Rs->eta * Rs->DRx[r] * Rs->DRx[r] : 1.0;
+            }
+        }
         for (int a = 0; a < NU; ++a) {
             const int j = NU * k + a;
             double sl = W->U[j] - C->lo, su = C->hi - W->U[j];
             for (int i = 0; i < NX; ++i) { double s = Hk[NX + a][i]; for (int m = 0; m < NX; ++m) s += Bm[m][a] * PA[m][i]; W->Qux[k][a][i] = s; }
             for (int b = 0; b < NU; ++b) { double s = Hk[NX + a][NX + b]; for (int m = 0; m < NX; ++m) s += Bm[m][a] * PB[m][b]; Quu[a][b] = s; }
-            Quu[a][a] += sc * 2 * P->R + W->zL[j] / sl + W->zU[j] / su + delta;
+            if (C->mode == 0) Quu[a][a] += sc * 2 * P->R + W->zL[j] / sl + W->zU[j] / su + delta;
+            else if (C->mode == 1) Quu[a][a] += Rs->eta * Rs->DRu[j] * Rs->DRu[j] + W->zL[j] / sl + W->zU[j] / su + delta;
+            else Quu[a][a] += 1.0;
         }
         if (!chol2(Quu[0][0], 0.5 * (Quu[0][1] + Quu[1][0]), Quu[1][1], W->Lq[k])) return 0;
         for (int i = 0; i < NX; ++i) {
@@ -251,26 +356,59 @@ static int riccati_factor(const ctx_t *C, work_t *W, double delta) {
             W->Pm[k][i][j] = Qxx[i][j] + W->Qux[k][0][i] * W->K[k][0][j] + W->Qux[k][1][i] * W->K[k][1][j];
         for (int i = 0; i < NX; ++i) for (int j = 0; j < i; ++j) { double s = 0.5 * (W->Pm[k][i][j] + W->Pm[k][j][i]); W->Pm[k][i][j] = W->Pm[k][j][i] = s; }
     }
+    if (Rs) return soft_node(C, (const double (*)[NX])W->Pm[0], 0, delta);     /* the soft initial-state rows */
     return 1;
 }
 
 /* Solve the factorised KKT system for constraint RHS rg (the linearised constraints read
  * J d = -rg) and the barrier-gradient RHS at the current point.  Fills dX, dU, lamp. */
-static void riccati_solve(const ctx_t *C, work_t *W, double rg[][NX]) {
-    const prob_t *P = C->P; const int N = C->N; const double sc = C->sc, mu = C->mu;
-    double gx[NX];
-    cost_grad_x(P, W->X + NX * N, C->ref, gx);
-    for (int i = 0; i < NX; ++i) W->pv[N][i] = sc * gx[i];
-    for (int k = N - 1; k >= 0; --k) {
-        double (*A)[NX] = W->A[k], (*Bm)[NU] = W->Bm[k], (*Pp)[NX] = W->Pm[k + 1], *pp = W->pv[k + 1];
-        double h[NX], qx[NX], qu[NU], kf[2];
-        for (int i = 0; i < NX; ++i) { double s = pp[i]; for (int m = 0; m < NX; ++m) s -= Pp[i][m] * rg[k + 1][m]; h[i] = s; }
+/* the stage gradient over z = [x; u] (restoration: the proximity term plus the box barrier (mode 1) or -z_L + z_U
+   (mode 2), or the refinement's override) */
+static void stage_grad(const ctx_t *C, const work_t *W, int k, double *gq) {
+    const prob_t *P = C->P; const double sc = C->sc, mu = C->mu;
+    if (C->mode == 0) {
+        double gx[NX];
         cost_grad_x(P, W->X + NX * k, C->ref, gx);
-        for (int i = 0; i < NX; ++i) { double s = sc * gx[i]; for (int m = 0; m < NX; ++m) s += A[m][i] * h[m]; qx[i] = s; }
-        for (int a = 0; a < NU; ++a) {
+        for (int i = 0; i < NX; ++i) gq[i] = sc * gx[i];
+        for (int a = 0; a < NU && k < C->N; ++a) {
             const int j = NU * k + a;
             double sl = W->U[j] - C->lo, su = C->hi - W->U[j];
-            double s = sc * 2 * P->R * W->U[j] - mu / sl + mu / su;
+            gq[NX + a] = sc * 2 * P->R * W->U[j] - mu / sl + mu / su;
+        }
+        return;
+    }
+    const resto_t *R = C->Rs;
+    if (R->ovr) { for (int j = 0; j < NZ; ++j) gq[j] = R->gov[k][j]; return; }
+    for (int i = 0; i < NX; ++i) {
+        const int r = NX * k + i;
+        gq[i] = R->eta * R->DRx[r] * R->DRx[r] * (W->X[r] - R->XR[r]);
+    }
+    for (int a = 0; a < NU && k < C->N; ++a) {
+        const int j = NU * k + a;
+        double sl = W->U[j] - C->lo, su = C->hi - W->U[j];
+        gq[NX + a] = R->eta * R->DRu[j] * R->DRu[j] * (W->U[j] - R->UR[j]);
+        gq[NX + a] += C->mode == 1 ? -mu / sl + mu / su : -W->zL[j] + W->zU[j];
+    }
+}
+
+static void riccati_solve(const ctx_t *C, work_t *W, double rg[][NX]) {
+    const int N = C->N;
+    const resto_t *R = C->Rs;
+    double gN[NZ];
+    stage_grad(C, W, N, gN);
+    for (int i = 0; i < NX; ++i) W->pv[N][i] = gN[i];
+    for (int k = N - 1; k >= 0; --k) {
+        double (*A)[NX] = W->A[k], (*Bm)[NU] = W->Bm[k], (*Pp)[NX] = W->Pm[k + 1], *pp = W->pv[k + 1], ppt[NX];
+        if (R) {
+            memcpy(ppt, pp, sizeof ppt); soft_apply(R, k + 1, 1, ppt);
+            pp = ppt; Pp = (double (*)[NX])R->Pt[k + 1];
+        }
+        double h[NX], qx[NX], qu[NU], kf[2], gq[NZ];
+        for (int i = 0; i < NX; ++i) { double s = pp[i]; for (int m = 0; m < NX; ++m) s -= Pp[i][m] * rg[k + 1][m]; h[i] = s; }
+        stage_grad(C, W, k, gq);
+        for (int i = 0; i < NX; ++i) { double s = gq[i]; for (int m = 0; m < NX; ++m) s += A[m][i] * h[m]; qx[i] = s; }
+        for (int a = 0; a < NU; ++a) {
+            double s = gq[NX + a];
             for (int m = 0; m < NX; ++m) s += Bm[m][a] * h[m];
             qu[a] = s;
         }
@@ -278,7 +416,8 @@ static void riccati_solve(const ctx_t *C, work_t *W, double rg[][NX]) {
         W->kff[k][0] = -kf[0]; W->kff[k][1] = -kf[1];
         for (int i = 0; i < NX; ++i) W->pv[k][i] = qx[i] + W->Qux[k][0][i] * W->kff[k][0] + W->Qux[k][1][i] * W->kff[k][1];
     }
-    for (int i = 0; i < NX; ++i) W->dX[i] = -rg[0][i];
+    for (int i = 0; i < NX; ++i) W->dX[i] = -rg[0][i] - (R ? R->D[i] * W->pv[0][i] : 0.0);
+    if (R) soft_apply(R, 0, 0, W->dX);
     for (int k = 0; k < N; ++k) {
         double *dx = W->dX + NX * k, *du = W->dU + NU * k;
         for (int a = 0; a < NU; ++a) { double s = W->kff[k][a]; for (int i = 0; i < NX; ++i) s += W->K[k][a][i] * dx[i]; du[a] = s; }
@@ -286,8 +425,10 @@ static void riccati_solve(const ctx_t *C, work_t *W, double rg[][NX]) {
             double s = -rg[k + 1][i];
             for (int m = 0; m < NX; ++m) s += W->A[k][i][m] * dx[m];
             for (int a = 0; a < NU; ++a) s += W->Bm[k][i][a] * du[a];
+            if (R) s -= R->D[NX * (k + 1) + i] * W->pv[k + 1][i];
             W->dX[NX * (k + 1) + i] = s;
         }
+        if (R) soft_apply(R, k + 1, 0, W->dX + NX * (k + 1));
     }
     for (int k = 0; k <= N; ++k) for (int i = 0; i < NX; ++i) {
         double s = W->pv[k][i]; for (int m = 0; m < NX; ++m) s += W->Pm[k][i][m] * W->dX[NX * k + m];
@@ -403,6 +544,448 @@ static double ls_multipliers(const ctx_t *C, work_t *W, double *y) {
 
 static double g_mult_init_max = 1e3;   /* IPOPT constr_mult_init_max (default 1000; 0 = zero multipliers) */
 void oracle_pmpc_set_mult_init_max(double m) { g_mult_init_max = m; }
+/* IPOPT's soft restoration and restoration phases on / off (off: a failed line search ends at -2) */
+static int g_resto = 1;
+void oracle_pmpc_set_resto(int on) { g_resto = on; }
+enum { ST_INFEASIBLE = 2 };
+
+/* the dynamics Jacobians (A, Bm) and the lambda-weighted RK4 Hessians at the iterate in W */
+static void linearise(const prob_t *P, work_t *W, int N) {
+    for (int k = 0; k < N; ++k) {
+        double xn[NX], nl[NX];
+        for (int i = 0; i < NX; ++i) nl[i] = -W->lam[NX * (k + 1) + i];
+        rk4_derivs(P, W->X + NX * k, W->U + NU * k, nl, xn, W->A[k], W->Bm[k], W->H[k]);
+    }
+}
+
+/* IPOPT's primal-dual system error at C->mu (curr_primal_dual_system_error): l1 norms of the primal
+   infeasibility g, of the dual infeasibility (x and u rows) and of the U box's z s - mu, added */
+static double pd_error(const ctx_t *C, const work_t *W, double g[][NX]) {
+    const prob_t *P = C->P; const int N = C->N;
+    double l1 = 0.0;
+    for (int k = 0; k <= N; ++k) {
+        double gx[NX];
+        cost_grad_x(P, W->X + NX * k, C->ref, gx);
+        for (int i = 0; i < NX; ++i) {
+            double r = C->sc * gx[i] + W->lam[NX * k + i];
+            if (k < N) for (int m = 0; m < NX; ++m) r -= W->A[k][m][i] * W->lam[NX * (k + 1) + m];
+            l1 += fabs(r) + fabs(g[k][i]);
+        }
+        if (k < N) for (int a = 0; a < NU; ++a) {
+            const int j = NU * k + a;
+            double r = C->sc * 2 * P->R * W->U[j] - W->zL[j] + W->zU[j];
+            for (int m = 0; m < NX; ++m) r -= W->Bm[k][m][a] * W->lam[NX * (k + 1) + m];
+            l1 += fabs(r) + fabs(W->zL[j] * (W->U[j] - C->lo) - C->mu) + fabs(W->zU[j] * (C->hi - W->U[j]) - C->mu);
+        }
+    }
+    return l1;
+}
+
+/* IPOPT's soft restoration phase (BacktrackingLineSearch::TrySoftRestoStep, soft_resto_pderror_reduction_factor
+   0.9999): the primal-dual step damped only by the fraction to the boundary (one length for x, lambda, z),
+   taken if the original filter accepts it with alpha_primal_test = 0 (*orig = 1) or if it reduces the
+   primal-dual system error.  Returns the step length (0: rejected); the trial point is left in Xt / Ut, gt. */
+static double soft_resto_step(const ctx_t *C, work_t *W, int nfilt, double th, double phi, double th_max, double tau,
+                              double curr_pd, double *th_t, double *ph_t, int *orig) {
+    const prob_t *P = C->P; const int N = C->N, nU = NU * N, ng = NX * (N + 1);
+    const double gam_th = 1e-5, gam_ph = 1e-8;
+    const double a = fmin(frac_to_boundary(C, W, W->dU, tau), bound_dual_step(C, W, nU, tau));
+    for (int i = 0; i < ng; ++i) W->Xt[i] = W->X[i] + a * W->dX[i];
+    for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + a * W->dU[j];
+    *th_t = constraints(C, W->Xt, W->Ut, W->gt);
+    *ph_t = barrier_obj(C, W->Xt, W->Ut);
+    *orig = 0;
+    int in_filter = !(*th_t < th_max) || !isfinite(*ph_t);
+    for (int q = 0; q < nfilt && !in_filter; ++q) in_filter = *th_t >= W->filt_th[q] && *ph_t >= W->filt_ph[q];
+    if (!in_filter && (LE(*th_t, (1 - gam_th) * th, th) || LE(*ph_t - phi, -gam_ph * th, phi))) { *orig = 1; return a; }
+    if (!isfinite(*ph_t)) return 0.0;
+    work_t *S = (work_t *)malloc(sizeof(work_t));
+    memcpy(S, W, sizeof(work_t));
+    memcpy(W->X, S->Xt, sizeof(double) * ng); memcpy(W->U, S->Ut, sizeof(double) * nU);
+    for (int i = 0; i < ng; ++i) W->lam[i] = S->lam[i] + a * (S->lamp[i] - S->lam[i]);
+    for (int j = 0; j < nU; ++j) { W->zL[j] = S->zL[j] + a * S->dzL[j]; W->zU[j] = S->zU[j] + a * S->dzU[j]; }
+    linearise(P, W, N);
+    const double pd = pd_error(C, W, S->gt);
+    memcpy(W, S, sizeof(work_t));
+    free(S);
+    return pd <= 0.9999 * curr_pd ? a : 0.0;
+}
+
+/* ---- the restoration phase (oracle/rmpc_ipm.c `restoration` has the commentary; every defect row soft) ---- */
+/* constraint values of the restoration problem c + n - p (all rows); returns their l1 norm */
+static double resto_cons(const ctx_t *C, const double *X, const double *U, const double *pc, const double *nc,
+                         double g[][NX], double cg[][NX]) {
+    const int N = C->N;
+    constraints(C, X, U, g);
+    double th = 0.0;
+    for (int k = 0; k <= N; ++k) for (int i = 0; i < NX; ++i) {
+        const int r = NX * k + i;
+        cg[k][i] = g[k][i] + nc[r] - pc[r];
+        th += fabs(cg[k][i]);
+    }
+    return th;
+}
+/* soft-row right-hand sides rg = c - (rn / S_n - rp / S_p) + D lam */
+static void resto_rhs(const ctx_t *C, const work_t *W, double cg[][NX], double rg[][NX]) {
+    const resto_t *R = C->Rs;
+    for (int k = 0; k <= C->N; ++k) for (int i = 0; i < NX; ++i) {
+        const int r = NX * k + i;
+        rg[k][i] = cg[k][i] - (R->rn[r] / R->Snd[r] - R->rp[r] / R->Spd[r]) + R->D[r] * W->lam[r];
+    }
+}
+static double resto_barrier(const ctx_t *C, const double *X, const double *U, const double *pc, const double *nc) {
+    const resto_t *R = C->Rs; const int N = C->N;
+    double f = 0.0, lb = 0.0;
+    for (int k = 0; k <= N; ++k) for (int i = 0; i < NX; ++i) {
+        const int r = NX * k + i;
+        const double e = R->DRx[r] * (X[r] - R->XR[r]);
+        f += R->rho * (pc[r] + nc[r]) + 0.5 * R->eta * e * e;
+        if (!(pc[r] > 0) || !(nc[r] > 0)) return INFINITY;
+        lb += log(pc[r]) + log(nc[r]);
+    }
+    for (int j = 0; j < NU * N; ++j) {
+        const double e = R->DRu[j] * (U[j] - R->UR[j]);
+        f += 0.5 * R->eta * e * e;
+        double sl = U[j] - C->lo, su = C->hi - U[j];
+        if (!(sl > 0) || !(su > 0)) return INFINITY;
+        lb += log(sl) + log(su);
+    }
+    return f - C->mu * lb;
+}
+/* optimality-error measures of the restoration problem at the iterate in W (A, Bm there) */
+static void resto_errors(const ctx_t *C, const work_t *W, double cg[][NX], double *dinf_, double *pinf_, double *c0_,
+                         double *cmin_, double *sum_l_, double *sum_z_) {
+    const resto_t *R = C->Rs; const int N = C->N;
+    double dinf = 0, pinf = 0, c0 = 0, cmin = INFINITY, sum_l = 0, sum_z = 0;
+#define CMPL(v) do { const double cv_ = (v); c0 = fmax(c0, cv_); cmin = fmin(cmin, cv_); } while (0)
+    for (int k = 0; k <= N; ++k) {
+        for (int i = 0; i < NX; ++i) {
+            const int r = NX * k + i;
+            double gl = R->eta * R->DRx[r] * R->DRx[r] * (W->X[r] - R->XR[r]) + W->lam[r];
+            if (k < N) for (int m = 0; m < NX; ++m) gl -= W->A[k][m][i] * W->lam[NX * (k + 1) + m];
+            dinf = fmax(dinf, fabs(gl));
+            pinf = fmax(pinf, fabs(cg[k][i]));
+            sum_l += fabs(W->lam[r]);
+            dinf = fmax(dinf, fmax(fabs(R->rho - R->zp[r] - W->lam[r]), fabs(R->rho - R->zn[r] + W->lam[r])));
+            CMPL(R->zp[r] * R->pc[r]); CMPL(R->zn[r] * R->nc[r]);
+            sum_z += R->zp[r] + R->zn[r];
+        }
+        if (k < N) for (int a = 0; a < NU; ++a) {
+            const int j = NU * k + a;
+            double gl = R->eta * R->DRu[j] * R->DRu[j] * (W->U[j] - R->UR[j]) - W->zL[j] + W->zU[j];
+            for (int m = 0; m < NX; ++m) gl -= W->Bm[k][m][a] * W->lam[NX * (k + 1) + m];
+            dinf = fmax(dinf, fabs(gl));
+            CMPL(W->zL[j] * (W->U[j] - C->lo)); CMPL(W->zU[j] * (C->hi - W->U[j]));
+            sum_z += W->zL[j] + W->zU[j];
+        }
+    }
+#undef CMPL
+    *dinf_ = dinf; *pinf_ = pinf; *c0_ = c0; *cmin_ = cmin; *sum_l_ = sum_l; *sum_z_ = sum_z;
+}
+/* Iterative refinement of the restoration step (rmpc_ipm.c resto_refine): the residuals of the full Newton
+   system (stationarity of x and u, the soft defect rows, the p / n rows) solved for on the same factorisation
+   when they exceed 1e-12 (1 + |step|), and added.  Returns 1 if a correction was made. */
+static int resto_refine(const ctx_t *Cm, work_t *V, double cg[][NX], double rg[][NX]) {
+    resto_t *R = Cm->Rs; const int N = Cm->N, ng = NX * (N + 1), nU = NU * N;
+    double emax = 0.0, smax = 0.0;
+#define EM(v) (emax = fmax(emax, fabs(v)))
+#define SM(v) (smax = fmax(smax, fabs(v)))
+    for (int k = 0; k <= N; ++k) {
+        double gq[NZ];
+        stage_grad(Cm, V, k, gq);
+        for (int i = 0; i < NX; ++i) {
+            const int r = NX * k + i;
+            double t = gq[i] + (R->eta * R->DRx[r] * R->DRx[r] + R->delta) * V->dX[r] + V->lamp[r];
+            if (k < N) {
+                for (int b = 0; b < NZ; ++b) t += V->H[k][i][b] * (b < NX ? V->dX[NX * k + b] : V->dU[NU * k + b - NX]);
+                for (int m = 0; m < NX; ++m) t -= V->A[k][m][i] * V->lamp[NX * (k + 1) + m];
+            }
+            R->ex[k][i] = t; EM(t);
+        }
+        if (k < N) for (int a = 0; a < NU; ++a) {
+            const int j = NU * k + a;
+            double sl = V->U[j] - Cm->lo, su = Cm->hi - V->U[j];
+            double t = gq[NX + a] + (R->eta * R->DRu[j] * R->DRu[j] + V->zL[j] / sl + V->zU[j] / su + R->delta) * V->dU[j];
+            for (int b = 0; b < NZ; ++b) t += V->H[k][NX + a][b] * (b < NX ? V->dX[NX * k + b] : V->dU[NU * k + b - NX]);
+            for (int m = 0; m < NX; ++m) t -= V->Bm[k][m][a] * V->lamp[NX * (k + 1) + m];
+            R->ex[k][NX + a] = t; EM(t);
+        }
+    }
+    for (int k = 0; k <= N; ++k) for (int i = 0; i < NX; ++i) {
+        const int r = NX * k + i;
+        double jd = V->dX[r];
+        if (k > 0) {
+            for (int m = 0; m < NX; ++m) jd -= V->A[k - 1][i][m] * V->dX[NX * (k - 1) + m];
+            for (int a = 0; a < NU; ++a) jd -= V->Bm[k - 1][i][a] * V->dU[NU * (k - 1) + a];
+        }
+        const double dl = V->lamp[r] - V->lam[r];
+        R->ec[k][i] = jd + R->dnc[r] - R->dpc[r] + cg[k][i];
+        R->ep[r] = R->Spd[r] * R->dpc[r] - dl + R->rp[r];
+        R->en[r] = R->Snd[r] * R->dnc[r] + dl + R->rn[r];
+        EM(R->ec[k][i]); EM(R->ep[r]); EM(R->en[r]);
+        SM(V->dX[r]); SM(R->dpc[r]); SM(R->dnc[r]);
+    }
+    for (int j = 0; j < nU; ++j) SM(V->dU[j]);
+#undef EM
+#undef SM
+    if (!(emax > 1e-12 * (1.0 + smax))) return 0;
+    work_t *Sv = (work_t *)malloc(sizeof(work_t));
+    resto_t *SR = (resto_t *)malloc(sizeof(resto_t));
+    memcpy(Sv, V, sizeof(work_t)); memcpy(SR, R, sizeof(resto_t));
+    memset(V->lam, 0, sizeof(double) * ng);
+    for (int i = 0; i < ng; ++i) { R->rp[i] = R->ep[i]; R->rn[i] = R->en[i]; }
+    R->ovr = 1;
+    memcpy(R->gov, R->ex, sizeof(double[NZ]) * (N + 1));
+    resto_rhs(Cm, V, R->ec, rg);
+    riccati_solve(Cm, V, rg);
+    for (int i = 0; i < ng; ++i) {
+        Sv->dX[i] += V->dX[i];
+        Sv->lamp[i] += V->lamp[i];
+        SR->dpc[i] += (V->lamp[i] - R->ep[i]) / R->Spd[i];
+        SR->dnc[i] += (-V->lamp[i] - R->en[i]) / R->Snd[i];
+    }
+    for (int j = 0; j < nU; ++j) Sv->dU[j] += V->dU[j];
+    memcpy(V, Sv, sizeof(work_t)); memcpy(R, SR, sizeof(resto_t));
+    free(Sv); free(SR);
+    return 1;
+}
+
+static int restoration(const ctx_t *C0, work_t *W, int *it_io, int max_iter, double tol, double th0, double phi0,
+                       int nfilt0, double tau0, double g0[][NX], int *status) {
+    const prob_t *P = C0->P; const int N = C0->N, nU = NU * N, ng = NX * (N + 1);
+    const double gam_th = 1e-5, gam_ph = 1e-8, s_th = 1.1, s_ph = 2.3, gam_al = 0.05, kap_soc = 0.99;
+    const double mu_min = tol / 10, s_max = 100.0;
+    resto_t *R = (resto_t *)calloc(1, sizeof(resto_t));
+    work_t *V = (work_t *)malloc(sizeof(work_t));
+    work_t *Sv = (work_t *)malloc(sizeof(work_t));
+    resto_t *SR = (resto_t *)malloc(sizeof(resto_t));
+    memcpy(V, W, sizeof(work_t));
+    const size_t szg = sizeof(double[NX]) * (N + 1);
+    double (*g)[NX] = calloc(N + 1, sizeof(double[NX])), (*gt)[NX] = calloc(N + 1, sizeof(double[NX]));
+    double (*cg)[NX] = calloc(N + 1, sizeof(double[NX])), (*cgt)[NX] = calloc(N + 1, sizeof(double[NX]));
+    double (*csg)[NX] = calloc(N + 1, sizeof(double[NX])), (*rg)[NX] = calloc(N + 1, sizeof(double[NX]));
+    ctx_t C = *C0;
+    C.Rs = R; C.mode = 1;
+    R->rho = 1000.0;
+    int ok_out = 0;
+    for (int i = 0; i < ng; ++i) { R->XR[i] = W->X[i]; R->DRx[i] = 1.0 / fmax(1.0, fabs(W->X[i])); }
+    for (int j = 0; j < nU; ++j) { R->UR[j] = W->U[j]; R->DRu[j] = 1.0 / fmax(1.0, fabs(W->U[j])); }
+    double cmax = 0.0;
+    for (int k = 0; k <= N; ++k) for (int i = 0; i < NX; ++i) cmax = fmax(cmax, fabs(g0[k][i]));
+    C.mu = fmax(C0->mu, cmax);
+    R->eta = sqrt(C.mu);
+    for (int i = 0; i < ng; ++i) {
+        const double c = g0[i / NX][i % NX];
+        const double a_ = C.mu / (2.0 * R->rho) - 0.5 * c, b_ = c * C.mu / (2.0 * R->rho);
+        R->nc[i] = a_ + sqrt(a_ * a_ + b_); R->pc[i] = c + R->nc[i];
+        R->zp[i] = C.mu / R->pc[i]; R->zn[i] = C.mu / R->nc[i];
+    }
+    for (int j = 0; j < nU; ++j) { V->zL[j] = fmin(R->rho, W->zL[j]); V->zU[j] = fmin(R->rho, W->zU[j]); }
+    /* least-square equality multipliers of the restoration problem (unit weights on x, u, p, n) */
+    linearise(P, V, N);
+    {
+        C.mode = 2;
+        for (int i = 0; i < ng; ++i) { R->rp[i] = R->rho - R->zp[i]; R->rn[i] = R->rho - R->zn[i]; }
+        memset(V->lam, 0, sizeof(double) * ng);
+        riccati_factor(&C, V, 0.0);              /* unit weights: every Quu >= I */
+        resto_rhs(&C, V, cg, rg);                /* cg = 0 */
+        riccati_solve(&C, V, rg);
+        double ym = 0.0;
+        for (int i = 0; i < ng; ++i) { ym = fmax(ym, fabs(V->lamp[i])); if (!isfinite(V->lamp[i])) ym = INFINITY; }
+        if (ym <= 1e3) memcpy(V->lam, V->lamp, sizeof(double) * ng);
+        C.mode = 1;
+    }
+    double th = resto_cons(&C, V->X, V->U, R->pc, R->nc, g, cg);
+    const double th_max = 1e4 * fmax(1.0, th), th_min = 1e-4 * fmax(1.0, th);
+    int nfilt = 0, rit = *it_io + 1, first = 1;
+    double delta_last = 0.0;
+    for (;; ++rit) {
+        linearise(P, V, N);
+        if (!first) {       /* the original problem's progress at the current point */
+            const double tho = constraints(C0, V->X, V->U, gt);
+            if (tho <= 0.9 * th0) {
+                const double pho = barrier_obj(C0, V->X, V->U);
+                int acc = isfinite(pho);
+                for (int q = 0; q < nfilt0 && acc; ++q) acc = !(tho >= W->filt_th[q] && pho >= W->filt_ph[q]);
+                acc = acc && (LE(tho, (1 - gam_th) * th0, th0) || LE(pho - phi0, -gam_ph * th0, phi0));
+                if (acc) { ok_out = 1; break; }
+            }
+        }
+        first = 0;
+        double dinf, pinf, c0, cmin, sum_l, sum_z;
+        resto_errors(&C, V, cg, &dinf, &pinf, &c0, &cmin, &sum_l, &sum_z);
+        const double nb = 4.0 * N + 2.0 * ng;
+        const double s_d = fmax(s_max, (sum_l + sum_z) / (ng + nb)) / s_max;
+        const double s_c = fmax(s_max, sum_z / nb) / s_max;
+        const double err = fmax(dinf / s_d, fmax(pinf, c0 / s_c));
+        if (rit >= max_iter) { *status = ST_MAXITER; break; }
+        if (err <= tol && dinf <= 1.0 && pinf <= 1e-4 && c0 <= 1e-4) { *status = ST_INFEASIBLE; break; }
+        for (;;) {
+            const double cmu = fmax(c0 - C.mu, C.mu - cmin);
+            if (fmax(dinf / s_d, fmax(pinf, cmu / s_c)) > 10.0 * C.mu || C.mu <= mu_min) break;
+            C.mu = fmax(mu_min, fmin(0.2 * C.mu, pow(C.mu, 1.5)));
+            R->eta = sqrt(C.mu);
+            nfilt = 0;
+        }
+        const double tau = fmax(0.99, 1.0 - C.mu);
+        for (int i = 0; i < ng; ++i) {
+            R->rp[i] = R->rho - C.mu / R->pc[i] - V->lam[i];
+            R->rn[i] = R->rho - C.mu / R->nc[i] + V->lam[i];
+        }
+        double delta = 0.0;
+        int ok = riccati_factor(&C, V, 0.0);
+        for (int attempt = 0; !ok && attempt < 60; ++attempt) {
+            delta = (attempt == 0) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))
+                                   : delta * (delta_last == 0.0 ? 100.0 : 8.0);
+            ok = riccati_factor(&C, V, delta);
+        }
+        if (!ok) { *status = ST_INERTIA_FAIL; break; }
+        if (delta > 0) delta_last = delta;
+        R->delta = delta;
+        double amax = 0, az = 0;
+#define PN_DUALS() do {                                                                                 \
+            az = bound_dual_step(&C, V, nU, tau);                                                       \
+            for (int i = 0; i < ng; ++i) {                                                              \
+                R->dzp[i] = C.mu / R->pc[i] - R->zp[i] - R->zp[i] / R->pc[i] * R->dpc[i];               \
+                R->dzn[i] = C.mu / R->nc[i] - R->zn[i] - R->zn[i] / R->nc[i] * R->dnc[i];               \
+                if (R->dzp[i] < 0) az = fmin(az, -tau * R->zp[i] / R->dzp[i]);                          \
+                if (R->dzn[i] < 0) az = fmin(az, -tau * R->zn[i] / R->dzn[i]);                          \
+            }                                                                                           \
+        } while (0)
+#define RESTO_STEP(CG) do {                                                                             \
+            resto_rhs(&C, V, CG, rg);                                                                   \
+            riccati_solve(&C, V, rg);                                                                   \
+            for (int i = 0; i < ng; ++i) {                                                              \
+                const double dy_ = V->lamp[i] - V->lam[i];                                              \
+                R->dpc[i] = (dy_ - R->rp[i]) / R->Spd[i];                                               \
+                R->dnc[i] = (-dy_ - R->rn[i]) / R->Snd[i];                                              \
+            }                                                                                           \
+            for (int rr_ = 0; rr_ < 3 && resto_refine(&C, V, CG, rg); ++rr_) {}                         \
+            amax = frac_to_boundary(&C, V, V->dU, tau);                                                 \
+            for (int i = 0; i < ng; ++i) {                                                              \
+                if (R->dpc[i] < 0) amax = fmin(amax, -tau * R->pc[i] / R->dpc[i]);                      \
+                if (R->dnc[i] < 0) amax = fmin(amax, -tau * R->nc[i] / R->dnc[i]);                      \
+            }                                                                                           \
+            PN_DUALS();                                                                                 \
+        } while (0)
+        RESTO_STEP(cg);
+        const double phi = resto_barrier(&C, V->X, V->U, R->pc, R->nc);
+        double gTd = 0.0;
+        for (int i = 0; i < ng; ++i) {
+            gTd += R->eta * R->DRx[i] * R->DRx[i] * (V->X[i] - R->XR[i]) * V->dX[i];
+            gTd += (R->rho - C.mu / R->pc[i]) * R->dpc[i] + (R->rho - C.mu / R->nc[i]) * R->dnc[i];
+        }
+        for (int j = 0; j < nU; ++j)
+            gTd += (R->eta * R->DRu[j] * R->DRu[j] * (V->U[j] - R->UR[j]) - C.mu / (V->U[j] - C.lo) + C.mu / (C.hi - V->U[j])) * V->dU[j];
+        double amin = gam_th;
+        if (gTd < 0) amin = fmin(gam_th, fmin(gam_ph * th / (-gTd), pow(th, s_th) / pow(-gTd, s_ph)));
+        amin *= gam_al;
+        double alpha = amax, th_t = 0, ph_t = 0;
+        int accepted = 0, ftype = 0;
+#define RESTO_TRIAL(AL) do {                                                                            \
+            for (int i = 0; i < ng; ++i) V->Xt[i] = V->X[i] + (AL) * V->dX[i];                         \
+            for (int j = 0; j < nU; ++j) V->Ut[j] = V->U[j] + (AL) * V->dU[j];                         \
+            for (int i = 0; i < ng; ++i) { R->pt_[i] = R->pc[i] + (AL) * R->dpc[i]; R->nt_[i] = R->nc[i] + (AL) * R->dnc[i]; } \
+            th_t = resto_cons(&C, V->Xt, V->Ut, R->pt_, R->nt_, gt, cgt);                               \
+            ph_t = resto_barrier(&C, V->Xt, V->Ut, R->pt_, R->nt_);                                      \
+        } while (0)
+#define RESTO_ACCEPT(AL, ACC) do {                                                                      \
+            int in_f_ = !(th_t < th_max) || !isfinite(ph_t);                                            \
+            for (int q = 0; q < nfilt && !in_f_; ++q) in_f_ = th_t >= R->filt_th[q] && ph_t >= R->filt_ph[q]; \
+            (ACC) = 0;                                                                                  \
+            if (!in_f_) {                                                                               \
+                const int sw_ = gTd < 0 && (AL) * pow(-gTd, s_ph) > pow(th, s_th);                      \
+                if (th <= th_min && sw_) { if (LE(ph_t, phi + 1e-8 * (AL) * gTd, phi)) { (ACC) = 1; ftype = 1; } } \
+                else (ACC) = LE(th_t, (1 - gam_th) * th, th) || LE(ph_t - phi, -gam_ph * th, phi);     \
+            }                                                                                           \
+        } while (0)
+        for (int ls = 0; ls < 80 && !accepted; ++ls) {
+            if (alpha < amin && ls > 0) break;
+            RESTO_TRIAL(alpha);
+            RESTO_ACCEPT(alpha, accepted);
+            if (!accepted && ls == 0 && !(th_t < th) && g_max_soc > 0) {
+                /* second-order correction on the restoration problem's constraints */
+                memcpy(Sv, V, sizeof(work_t)); memcpy(SR, R, sizeof(resto_t));
+                double asoc = alpha, th_old = 0.0;
+                memcpy(csg, cg, szg);
+                for (int c = 0; c < g_max_soc; ++c) {
+                    if (c > 0 && !(th_t <= kap_soc * th_old)) break;
+                    th_old = th_t;
+                    for (int k = 0; k <= N; ++k) for (int i = 0; i < NX; ++i) csg[k][i] = asoc * csg[k][i] + cgt[k][i];
+                    RESTO_STEP(csg);
+                    asoc = amax;
+                    RESTO_TRIAL(asoc);
+                    int acc;
+                    RESTO_ACCEPT(alpha, acc);
+                    if (acc) { accepted = 1; alpha = asoc; break; }
+                }
+                if (!accepted) {    /* back to the plain direction and its multiplier steps */
+                    memcpy(V, Sv, sizeof(work_t)); memcpy(R, SR, sizeof(resto_t));
+                    PN_DUALS();
+                }
+            }
+            if (!accepted) alpha *= 0.5;
+        }
+#ifdef ORACLE_DEBUG
+        fprintf(stderr, "  resto it %3d mu %.2e err %.2e dinf %.2e pinf %.2e c0 %.2e delta %.1e amax %.3e alpha %.3e th %.3e th_t %.3e acc %d\n",
+                rit, C.mu, err, dinf / s_d, pinf, c0 / s_c, delta, amax, alpha, th, th_t, accepted);
+#endif
+        if (!accepted) { *status = ST_LS_FAIL; break; }     /* restoration failure */
+        if (!ftype && nfilt < 256) { R->filt_th[nfilt] = (1 - gam_th) * th; R->filt_ph[nfilt] = phi - gam_ph * th; ++nfilt; }
+        memcpy(V->X, V->Xt, sizeof(double) * ng);
+        memcpy(V->U, V->Ut, sizeof(double) * nU);
+        memcpy(cg, cgt, szg);
+        th = th_t;
+        for (int i = 0; i < ng; ++i) V->lam[i] += alpha * (V->lamp[i] - V->lam[i]);
+#define KSIG(z, s, m) fmax(fmin((z), 1e10 * (m) / (s)), (m) / (1e10 * (s)))
+        for (int i = 0; i < ng; ++i) {
+            R->pc[i] = R->pt_[i]; R->nc[i] = R->nt_[i];
+            R->zp[i] = KSIG(R->zp[i] + az * R->dzp[i], R->pc[i], C.mu);
+            R->zn[i] = KSIG(R->zn[i] + az * R->dzn[i], R->nc[i], C.mu);
+        }
+        for (int j = 0; j < nU; ++j) {
+            V->zL[j] = KSIG(V->zL[j] + az * V->dzL[j], V->U[j] - C.lo, C.mu);
+            V->zU[j] = KSIG(V->zU[j] + az * V->dzU[j], C.hi - V->U[j], C.mu);
+        }
+#undef RESTO_ACCEPT
+#undef RESTO_TRIAL
+#undef RESTO_STEP
+#undef PN_DUALS
+    }
+    if (ok_out) {
+        /* back to the original problem: the u-bound multipliers by the pretended Newton step (mu - z s_trial) / s
+           cut by the fraction to the boundary, reset to 1 above 1000; equality multipliers 0 */
+        const double mu0 = C0->mu;
+        double az = 1.0, zmax = 0.0;
+        for (int j = 0; j < nU; ++j) {
+            W->dzL[j] = (mu0 - W->zL[j] * (V->U[j] - C0->lo)) / (W->U[j] - C0->lo);
+            W->dzU[j] = (mu0 - W->zU[j] * (C0->hi - V->U[j])) / (C0->hi - W->U[j]);
+            if (W->dzL[j] < 0) az = fmin(az, -tau0 * W->zL[j] / W->dzL[j]);
+            if (W->dzU[j] < 0) az = fmin(az, -tau0 * W->zU[j] / W->dzU[j]);
+        }
+        for (int j = 0; j < nU; ++j) {
+            W->zL[j] += az * W->dzL[j]; W->zU[j] += az * W->dzU[j];
+            zmax = fmax(zmax, fmax(W->zL[j], W->zU[j]));
+        }
+        if (zmax > 1e3) for (int j = 0; j < nU; ++j) { W->zL[j] = 1.0; W->zU[j] = 1.0; }
+        memcpy(W->X, V->X, sizeof(double) * ng);
+        memcpy(W->U, V->U, sizeof(double) * nU);
+        memset(W->lam, 0, sizeof(double) * ng);
+        for (int j = 0; j < nU; ++j) {
+            W->zL[j] = KSIG(W->zL[j], W->U[j] - C0->lo, mu0);
+            W->zU[j] = KSIG(W->zU[j], C0->hi - W->U[j], mu0);
+        }
+        *it_io = rit - 1;
+    } else {
+        memcpy(W->X, V->X, sizeof(double) * ng);
+        memcpy(W->U, V->U, sizeof(double) * nU);
+        *it_io = rit;
+    }
+#undef KSIG
+    free(g); free(gt); free(cg); free(cgt); free(csg); free(rg);
+    free(V); free(Sv); free(SR); free(R);
+    return ok_out;
+}
 
 int oracle_pmpc_solve(int N, double Ts, const double *state, const double *target, const double *prm,
                       const double *w_init, int max_iter, double tol,
@@ -434,7 +1017,7 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
         for (int i = 0; i < NX; ++i) gmax = fmax(gmax, fabs(gx[i]));
         if (k < N) for (int j = 0; j < NU; ++j) gmax = fmax(gmax, fabs(2 * P.R * W->U[NU * k + j]));
     }
-    ctx_t C = {&P, state, target, gmax > 100.0 ? 100.0 / gmax : 1.0, 0.1, lo, hi, N};
+    ctx_t C = {&P, state, target, gmax > 100.0 ? 100.0 / gmax : 1.0, 0.1, lo, hi, N, NULL, 0};
     double (*g)[NX] = (double (*)[NX])calloc(N + 1, sizeof(double[NX]));
 
     if (g_mult_init_max > 0.0) {
@@ -447,7 +1030,7 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
     }
     double th = constraints(&C, W->X, W->U, g);
     const double th_max = 1e4 * fmax(1.0, th), th_min = 1e-4 * fmax(1.0, th);
-    int nfilt = 0, status = ST_MAXITER, it;
+    int nfilt = 0, status = ST_MAXITER, it, in_soft = 0, soft_count = 0;
     double delta_last = 0.0;
     for (it = 0; it < max_iter; ++it) {
         /* ---- derivatives at the current point ------------------------------- */
@@ -486,7 +1069,7 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
                 cmu = fmax(cmu, fmax(fabs(W->zL[j] * (W->U[j] - lo) - C.mu), fabs(W->zU[j] * (hi - W->U[j]) - C.mu)));
             if (fmax(dinf / s_d, fmax(pinf, cmu / s_c)) > kappa_eps * C.mu || C.mu <= mu_min) break;
             C.mu = fmax(mu_min, fmin(kappa_mu * C.mu, pow(C.mu, theta_mu)));
-            nfilt = 0;                                     /* filter reset on barrier update */
+            nfilt = 0; in_soft = 0;           /* BacktrackingLineSearch::Reset: the filter and the soft phase */
         }
         const double tau = fmax(0.99, 1.0 - C.mu);
 
@@ -523,7 +1106,7 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
         for (int i = 0; i < ng; ++i) tn = fmax(tn, fabs(W->dX[i]) / (1.0 + fabs(W->X[i])));
         for (int j = 0; j < nU; ++j) tn = fmax(tn, fabs(W->dU[j]) / (1.0 + fabs(W->U[j])));
         const int tiny = tn < 10.0 * 2.220446049250313e-16;
-        for (int ls = 0; ls < 80 && !accepted; ++ls) {
+        for (int ls = 0; ls < 80 && !accepted && !in_soft; ++ls) {
             if (alpha < amin && ls > 0) break;
             for (int i = 0; i < ng; ++i) W->Xt[i] = W->X[i] + alpha * W->dX[i];
             for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + alpha * W->dU[j];
@@ -569,8 +1152,33 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
                 it, C.mu, dinf / s_d, pinf, c0 / s_c, delta, amax, alpha, az, used_soc, th);
 #endif
         (void)used_soc;
-        if (!accepted) { status = ST_LS_FAIL; break; }   /* IPOPT would enter restoration here */
-        if (!ftype && nfilt < 256) { W->filt_th[nfilt] = (1 - gam_th) * th; W->filt_ph[nfilt] = phi - gam_ph * th; ++nfilt; }
+        int soft = 0;
+        if (!accepted && g_resto) {
+            /* IPOPT's soft restoration phase: at most 10 steps; on entry the current point goes into the filter */
+            if (!in_soft) {
+                if (nfilt < 256) { W->filt_th[nfilt] = (1 - gam_th) * th; W->filt_ph[nfilt] = phi - gam_ph * th; ++nfilt; }
+                soft_count = 0;
+            }
+            if (!(in_soft && ++soft_count > 10)) {
+                int orig = 0;
+                const double a = soft_resto_step(&C, W, nfilt, th, phi, th_max, tau, pd_error(&C, W, g), &th_t, &ph_t, &orig);
+                if (a > 0.0) {
+                    accepted = 1; soft = 1; alpha = a; az = a;
+                    in_soft = !orig;
+                    if (orig) soft_count = 0;
+                }
+            }
+            if (!accepted) {
+                /* IPOPT's restoration phase */
+                int rst = ST_LS_FAIL;
+                if (!restoration(&C, W, &it, max_iter, tol, th, phi, nfilt, tau, g, &rst)) { status = rst; break; }
+                th = constraints(&C, W->X, W->U, g);
+                in_soft = 0; soft_count = 0;
+                continue;
+            }
+        }
+        if (!accepted) { status = ST_LS_FAIL; break; }   /* (restoration phases off) */
+        if (!soft && !ftype && nfilt < 256) { W->filt_th[nfilt] = (1 - gam_th) * th; W->filt_ph[nfilt] = phi - gam_ph * th; ++nfilt; }
         memcpy(W->X, W->Xt, sizeof(double) * ng);
         memcpy(W->U, W->Ut, sizeof(double) * nU);
         memcpy(g, W->gt, sizeof(double) * ng);

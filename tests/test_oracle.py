@@ -98,3 +98,31 @@ def test_workload_is_seeded_and_matches_survey():
     np.testing.assert_array_equal(config_params(0), [0.05, 600, 5, 0.1, -0.6, 0.6])     # cube, mu 0.05
     np.testing.assert_array_equal(config_params(17), [0.2, 200, 2, 0.2, -0.6, 0.6])     # sphere, mu 0.2
     assert config_name(4) == "cube_m2_mu0.1"
+
+
+@pytest.mark.parametrize("N,soc", [(31, 4), (20, 0)])
+def test_c_oracle_restoration_phases(N, soc):
+    """IPOPT's soft restoration and restoration phases in the PMPC oracle (TrySoftRestoStep,
+    MinC_1NrmRestorationPhase; oracle/pmpc_ipm.c restoration()).  C4's 1152 instances at the reference
+    tol 1e-8: at N = 31 three, and with the second-order correction off about a tenth, fail the filter
+    line search; IPOPT (and the oracle with the phases on) solves every one.  Instances that never enter a
+    restoration phase take the identical path with the phases on or off; the restored ones end at a KKT
+    point (the certificate of pmpc_nlp.py, tolerances of an interior-point answer at tol 1e-8)."""
+    import oracle_lib
+    from dart_mpc.workload import pmpc_batch
+    S, T, P = pmpc_batch(64)
+    kw = dict(N=N, Ts=0.002, tol=1e-8, max_iter=3000, nthreads=8, soc=soc)
+    on = oracle_lib.solve_batch(S, T, P, resto=True, **kw)
+    off = oracle_lib.solve_batch(S, T, P, resto=False, **kw)
+    assert np.all(on["status"] == 0)
+    failed = off["status"] != 0
+    assert failed.any() and np.all(off["status"][failed] == -2)
+    same = ~failed
+    np.testing.assert_array_equal(on["iters"][same], off["iters"][same])
+    np.testing.assert_array_equal(on["u0"][same], off["u0"][same])
+    for i in np.flatnonzero(failed)[:12]:
+        mu, qp, qv, r, lo, hi = P[i]
+        prob = PMPCProblem(N=N, Ts=0.002, Qp=qp, Qv=qv, R=r, mu=mu, u_bounds=(lo, hi))
+        c = kkt_certificate(prob, on["w"][i], np.concatenate([S[i], T[i]]), act_tol=1e-5)
+        assert c["primal"] <= 1e-8 and c["bound"] == 0.0, i
+        assert c["stat_free"] <= 1e-6 * max(1.0, c["grad_scale"]) and c["stat_sign"] <= 1e-6 * max(1.0, c["grad_scale"]), i
