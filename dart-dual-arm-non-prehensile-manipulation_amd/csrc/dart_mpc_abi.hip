@@ -14,6 +14,7 @@
 
 #include "dart_mpc.h"
 #include "pmpc_ipm.h"
+#include "pmpc_model.h"
 #include "rmpc_ipm.h"
 #include "lmpc_ipm.h"
 #include "lmpc_policy.h"
@@ -272,8 +273,14 @@ hipError_t ensure_io(dart_mpc_handle* h) {
     return hipSuccess;
 }
 
+// IPOPT's restoration phases for PMPC launches of this handle (pmpc_resto.hip: IPOPT's path, N <= 31);
+// `mode` 1 for launches that queue the restoration kernel behind the solve, 2 for the resident server
+int pmpc_resto_mode(const dart_mpc_handle* h, int mode) {
+    return (h->cfg.restoration && h->cfg.pmpc_path == 0 && h->cfg.N <= 31) ? mode : 0;
+}
+
 // kernel arguments reading / writing the I/O area
-dartmpc::PmpcArgs io_args(dart_mpc_handle* h, int B, bool ww, bool wo) {
+dartmpc::PmpcArgs io_args(dart_mpc_handle* h, int B, bool ww, bool wo, int resto_mode = 1) {
     const auto& o = h->io;
     dartmpc::PmpcArgs a;
     a.B = B; a.N = h->cfg.N; a.Ts = h->cfg.Ts; a.tol = h->cfg.tol; a.max_iter = h->cfg.max_iter; a.g = h->cfg.gravity;
@@ -283,13 +290,14 @@ dartmpc::PmpcArgs io_args(dart_mpc_handle* h, int B, bool ww, bool wo) {
     a.u0 = (double*)o.dout; a.f = (double*)(o.dout + o.off_f); a.w_out = wo ? (double*)(o.dout + o.off_wo) : nullptr;
     a.status = (int32_t*)(o.dout + o.off_st); a.iters = (int32_t*)(o.dout + o.off_it);
     a.done = h->ddone; a.seq = h->seq;
+    a.resto = pmpc_resto_mode(h, resto_mode);
     return a;
 }
 
 // (re)launch the resident grid; it takes every request with a sequence other than `seen`
 hipError_t server_launch(dart_mpc_handle* h, uint32_t seen) {
     auto& v = h->srv;
-    dartmpc::PmpcArgs a = io_args(h, v.B, true, true);     // the flags of each request select w_warm / w_out
+    dartmpc::PmpcArgs a = io_args(h, v.B, true, true, 2);  // the flags of each request select w_warm / w_out
     a.seq = seen;
     dartmpc::PmpcServe sv{v.dmbox, v.idle_ticks};
     const hipError_t e = dartmpc_launch_pmpc_serve(&a, &sv, v.stream);
@@ -353,6 +361,7 @@ int launch(dart_mpc_handle* h, int B, const double* x0, const double* ref, const
     a.x0 = x0; a.ref = ref; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     a.done = nullptr; a.seq = 0;
+    a.resto = pmpc_resto_mode(h, 1);
     HIPCHK(h, dartmpc_launch_pmpc(&a, s), "kernel launch");
     return DART_MPC_OK;
 }
@@ -385,6 +394,25 @@ uint32_t next_seq(dart_mpc_handle* h) {
     return h->seq;
 }
 
+// A served request's instances that the resident grid handed over (status kPmNeedResto: IPOPT's restoration
+// phases): the grid is drained (its waves hold the SIMDs while they wait for requests) and pmpc_resto_kernel
+// runs over the I/O area on the server's stream; the next request relaunches the grid.
+int served_resto(dart_mpc_handle* h, int B, bool ww, bool wo) {
+    auto& v = h->srv;
+    const int32_t* st = (const int32_t*)(h->io.hout + h->io.off_st);
+    bool any = false;
+    for (int b = 0; b < B && !any; ++b) any = __atomic_load_n(st + b, __ATOMIC_ACQUIRE) == dartmpc::kPmNeedResto;
+    if (!any) return DART_MPC_OK;
+    __atomic_store_n((unsigned long long*)v.mbox, (unsigned long long)v.mbox[0] | (1ull << 56), __ATOMIC_RELEASE);
+    v.running = false;
+    HIPCHK(h, hipStreamSynchronize(v.stream), "resident server");
+    dartmpc::PmpcArgs a = io_args(h, B, ww, wo, 1);
+    a.done = nullptr;
+    HIPCHK(h, dartmpc_launch_pmpc_resto(&a, v.stream), "restoration kernel launch");
+    HIPCHK(h, hipStreamSynchronize(v.stream), "restoration kernel");
+    return DART_MPC_OK;
+}
+
 // post a request to the resident server (inputs already in the I/O area) and wait for its B
 // completion words; a grid that drained meanwhile (idle timeout) is relaunched and takes the request
 int served_request(dart_mpc_handle* h, int B, bool ww, bool wo) {
@@ -414,11 +442,11 @@ int served_request(dart_mpc_handle* h, int B, bool ww, bool wo) {
     for (unsigned n = 1;; ++n) {
         int bb = 0;
         while (bb < B && __atomic_load_n(h->hdone + bb, __ATOMIC_ACQUIRE) == sq) ++bb;
-        if (bb == B) return DART_MPC_OK;
+        if (bb == B) return served_resto(h, B, ww, wo);
         if ((n & 1023) == 0 && hipStreamQuery(v.stream) != hipErrorNotReady) {
             bb = 0;
             while (bb < B && __atomic_load_n(h->hdone + bb, __ATOMIC_ACQUIRE) == sq) ++bb;
-            if (bb == B) return DART_MPC_OK;
+            if (bb == B) return served_resto(h, B, ww, wo);
             v.running = false;
             HIPCHK(h, hipStreamSynchronize(v.stream), "resident server");
             // the grid drained before it saw the request: relaunch with the request already posted
@@ -580,6 +608,7 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     a.x0 = d_x0; a.ref = d_ref; a.prm = d_prm; a.w_warm = d_ww;
     a.u0 = d_u0; a.f = d_f; a.w_out = d_wo; a.status = d_st; a.iters = d_it;
     a.done = d_done; a.seq = next_seq(h);
+    a.resto = pmpc_resto_mode(h, 1);
     HIPCHK(h, dartmpc_launch_pmpc(&a, s), "kernel launch");
     const int rc = wait_done(h, s, h->hdone, B, a.seq);
     if (rc) return rc;

@@ -400,6 +400,68 @@ __device__ bool riccati_sweep_aug_soft(L* S, AugSoftLds<L, NS>* RS, int N) {
     return !wany(!ok);
 }
 
+// ------------------------------------------------------------------------------------------
+// Node step for stages whose M columns may all be non-zero (the PMPC restoration kernel, pmpc_resto.hip:
+// x~ = the six states, no u_prev block).  Two LDS phases: lane NP i + s (i < ND, s < NP) forms
+// u_i[s] = (Pt_{k+1} a_i)[s] = (Gzz a_i)[s] - Gzu(s, :) Quu^-1 (Guz a_i), a_i column i of M_k, parked in U
+// (ND rows of stride NC); then lane e < NT forms the packed entry G_k(i, j) = H_k(i, j) + a_j^T u_i.
+// ok &= Quu of Gn positive definite.  Two barriers.
+template <class L>
+__device__ __forceinline__ void gen_node_step(L* S, int k, const double* Gn, double* U, bool& ok) {
+    constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, NC = L::NC;
+    static_assert(ND * NP <= 64 && NP <= NC, "one lane per (stage column, value index)");
+    const int lane = threadIdx.x;
+    const double* Mk = &S->M[k][0][0];
+    const double q00 = Gn[hp(NXA, NXA)], q01 = Gn[hp(NXA + 1, NXA)], q11 = Gn[hp(NXA + 1, NXA + 1)];
+    const double det = fma(q00, q11, -q01 * q01);
+    ok = ok && (q00 > 0.0) && (det > 0.0) && isfinite(det);
+    {
+        const int l = lane < ND * NP ? lane : ND * NP - 1;
+        const int i = l / NP, s = l - i * NP;
+        double t = 0.0, w0 = 0.0, w1 = 0.0;
+#pragma unroll
+        for (int n = 0; n < NP; ++n) {
+            const double an = Mk[i * NC + n];
+            t = fma(Gn[gzz<NXA>(s, n)], an, t);
+            w0 = fma(Gn[gzu<NXA>(n, 0)], an, w0);
+            w1 = fma(Gn[gzu<NXA>(n, 1)], an, w1);
+        }
+        const double gs0 = Gn[gzu<NXA>(s, 0)], gs1 = Gn[gzu<NXA>(s, 1)];
+        const double r0 = fma(q11, gs0, -q01 * gs1) / det, r1 = fma(q00, gs1, -q01 * gs0) / det;
+        if (lane < ND * NP) U[i * NC + s] = t - fma(r0, w0, r1 * w1);
+    }
+    __syncthreads();
+    if (lane < L::NT) {
+        int i = 0;
+        while (tri(i + 1) <= lane) ++i;
+        const int j = lane - tri(i);
+        double gv = S->H[k][lane];
+#pragma unroll
+        for (int m = 0; m < NP; ++m) gv = fma(Mk[j * NC + m], U[i * NC + m], gv);
+        S->G[k][lane] = gv;
+    }
+    __syncthreads();
+}
+
+// backward sweeps with gen_node_step: plain, and with the soft rows of every node (as riccati_sweep_aug[_soft])
+template <class L>
+__device__ bool riccati_sweep_gen(L* S, int N, double* U) {
+    bool ok = true;
+    for (int k = N - 1; k >= 0; --k) gen_node_step<L>(S, k, S->G[k + 1], U, ok);
+    double i00, i01, i11;
+    return quu_inverse<L::NXA>(S->G[0], i00, i01, i11) && ok;
+}
+template <class L, int NS>
+__device__ bool riccati_sweep_gen_soft(L* S, AugSoftLds<L, NS>* RS, int N, double* U) {
+    bool ok = true;
+    for (int k = N - 1; k >= 0; --k) {
+        aug_soften<L, NS>(S, RS, k + 1, true, ok);
+        gen_node_step<L>(S, k, RS->Gs, U, ok);
+    }
+    aug_soften<L, NS>(S, RS, 0, false, ok);
+    return !wany(!ok);
+}
+
 struct NoPost {
     __device__ void operator()(int, int) const {}
 };

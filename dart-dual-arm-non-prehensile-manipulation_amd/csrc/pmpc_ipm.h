@@ -13,6 +13,11 @@ struct PmpcArgs {
     int reduced;            // 1: the reduced (x, y) path (dart_mpc_config.pmpc_path), 0: IPOPT's path
     double mult_init_max;   // IPOPT constr_mult_init_max: > 0 least-square starting multipliers (default 1000)
     int pack;               // blocks per instance slot: 8 packs a small batch onto one XCD (launcher)
+    // IPOPT's restoration phases (N <= 31, IPOPT's path): 0 off (a failed line search ends at -2); 1 an
+    // instance whose line search fails is handed to pmpc_resto_kernel (status kPmNeedResto, no other output,
+    // no completion word), which dartmpc_launch_pmpc queues behind the solve on the same stream; 2 the same
+    // hand-off with the completion word written (the resident server: the host runs the restoration kernel)
+    int resto;
     const double* x0;       // [B][6]   device
     const double* ref;      // [B][6]
     const double* prm;      // [B][6]  mu, Qp, Qv, R, u_lo, u_hi
@@ -41,4 +46,5 @@ struct PmpcServe {
 extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStream_t stream);
 extern "C" hipError_t dartmpc_launch_pmpc_serve(const dartmpc::PmpcArgs* args, const dartmpc::PmpcServe* sv,
                                                hipStream_t stream);
+extern "C" hipError_t dartmpc_launch_pmpc_resto(const dartmpc::PmpcArgs* args, hipStream_t stream);
 extern "C" hipError_t dartmpc_wave_selftest(double* d_out, hipStream_t stream);

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include "pmpc_ipm.h"
+#include "pmpc_model.h"
 #include "stamps.h"
 #include "wave.h"
 
@@ -49,35 +50,6 @@ __device__ unsigned long long g_stamp_seq[16];
 #else
 #define STAMP_FLUSH(b) STAMP_FLUSH_TO(g_stamp, b)
 #endif
-
-// ---------------------------------------------------------------------------
-// model pieces
-// ---------------------------------------------------------------------------
-// mpc_3d.py:87-97, one axis:  pdot = v,  vdot = g sin(theta) - mu v
-__device__ __forceinline__ void axis_rhs(double g, double mu, double s, double v, double& dp, double& dv) {
-    dp = v;
-    dv = g * s - mu * v;
-}
-// mpc_3d.py:99-104 on one axis with s = sin(theta) held constant
-__device__ __forceinline__ void axis_rk4(double h, double g, double mu, double s, double p, double v,
-                                         double& pn, double& vn) {
-    double k1p, k1v, k2p, k2v, k3p, k3v, k4p, k4v;
-    axis_rhs(g, mu, s, v, k1p, k1v);
-    axis_rhs(g, mu, s, v + h / 2 * k1v, k2p, k2v);
-    axis_rhs(g, mu, s, v + h / 2 * k2v, k3p, k3v);
-    axis_rhs(g, mu, s, v + h * k3v, k4p, k4v);
-    pn = p + h / 6 * (k1p + 2 * k2p + 2 * k3p + k4p);
-    vn = v + h / 6 * (k1v + 2 * k2v + 2 * k3v + k4v);
-}
-// z sub-state (mpc_3d.py:93-97): pzdot = vz_new, vzdot = (vz_new - vz)/Ts, literal RK4
-__device__ __forceinline__ void z_rk4(double h, double w, double pz, double vz, double& pzn, double& vzn) {
-    const double k1v = (w - vz) / h;
-    const double k2v = (w - (vz + h / 2 * k1v)) / h;
-    const double k3v = (w - (vz + h / 2 * k2v)) / h;
-    const double k4v = (w - (vz + h * k3v)) / h;
-    pzn = pz + h / 6 * (w + 2 * w + 2 * w + w);
-    vzn = vz + h / 6 * (k1v + 2 * k2v + 2 * k3v + k4v);
-}
 
 // DPP move with an identity fill (FILL = 0.0 or 1.0) for lanes whose source is outside the row or
 // masked out.  With every row enabled a zero half comes from bound_ctrl (the DPP writes 0 where the
@@ -852,7 +824,8 @@ __device__ __forceinline__ void pmpc_solve(const PmpcArgs& a, const int b) {
         STAMP_ADD(10, ls + 1);
         STAMP_ADD(15, soc > 0 ? 1 : 0);
         STAMP(6);
-        if (PM_EXPECT(!accepted, 0)) { status = -2; break; }   // IPOPT would enter its restoration phase here
+        // a failed line search: IPOPT's restoration phases in pmpc_resto_kernel (or status -2 without)
+        if (PM_EXPECT(!accepted, 0)) { status = a.resto ? kPmNeedResto : -2; break; }
         if (!ftype && nfilt < kWave) {
             if (lane == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
             ++nfilt;
@@ -875,6 +848,14 @@ __device__ __forceinline__ void pmpc_solve(const PmpcArgs& a, const int b) {
     }
 
     // -------- outputs ---------------------------------------------------------------
+    if (PM_EXPECT(status == kPmNeedResto, 0)) {     // handed over: pmpc_resto_kernel writes the outputs
+        if (lane == 0) a.status[b] = status;
+        if (a.done && a.resto == 2) {
+            __threadfence_system();
+            if (lane == 0) __hip_atomic_store(a.done + b, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
     // objective (mpc_3d.py:44-46, :63-66), unscaled
     double fl = 0.0;
 #pragma unroll
@@ -1082,9 +1063,9 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
         const char* e = getenv("DART_PMPC_QSCAN_MAX_B");
         return e ? atoi(e) : (1 << 30);
     }();
-    if (a.N <= 15 && a.B <= qscan_max_b)
-        return dartmpc_launch_pmpc_seq(&a, grid.x, stream, 1);
-    else if (a.N <= 23 && a.B <= qscan_max_b) {
+    if (a.N <= 15 && a.B <= qscan_max_b) {
+        if (hipError_t e = dartmpc_launch_pmpc_seq(&a, grid.x, stream, 1)) return e;
+    } else if (a.N <= 23 && a.B <= qscan_max_b) {
         if (a.reduced)
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
         else
@@ -1094,8 +1075,13 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
         else
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
-    } else
-        return dartmpc_launch_pmpc_seq(&a, grid.x, stream, 0);
+    } else {
+        if (hipError_t e = dartmpc_launch_pmpc_seq(&a, grid.x, stream, 0)) return e;
+    }
+    if (a.resto == 1) {       // the instances whose line search failed, with IPOPT's restoration phases
+        if (hipError_t e = hipGetLastError()) return e;
+        return dartmpc_launch_pmpc_resto(&a, stream);
+    }
     return hipGetLastError();
 }
 

@@ -200,18 +200,22 @@ class Solver:
     """Owns one ``dart_mpc_handle`` (device workspace + stream) for a fixed N/Ts/tol.  ``max_soc`` is
     IPOPT's second-order-correction count (default 4, as ``mpc_3d.py:82`` leaves it; 0 = off).
     ``path``: "ipopt" (default) follows IPOPT's iterates on the full 6-state NLP; "reduced" is the
-    faster opt-in that solves the (x, y) problem and rolls z out afterwards (same KKT point)."""
+    faster opt-in that solves the (x, y) problem and rolls z out afterwards (same KKT point).
+    ``restoration``: IPOPT's soft restoration and restoration phases after a failed filter line search
+    (IPOPT's path, N <= 31; pmpc_resto.hip); off, or on the reduced path or beyond N = 31, such an instance
+    ends at status -2."""
 
     PATHS = {"ipopt": 0, "reduced": 1}
 
     def __init__(self, N=20, Ts=0.002, tol=1e-8, max_iter=3000, B_max=1024, device=0, gravity=-9.81, max_soc=4,
-                 path="ipopt", constr_mult_init_max=1000.0):
+                 path="ipopt", constr_mult_init_max=1000.0, restoration=True):
         self._h = ctypes.c_void_p()
         if path not in self.PATHS:
             raise DartMPCError(f"unknown PMPC path {path!r} (expected one of {sorted(self.PATHS)})")
         self.cfg = default_config(N=int(N), Ts=float(Ts), tol=float(tol), max_iter=int(max_iter), B_max=int(B_max),
                                   gravity=float(gravity), max_soc=int(max_soc), pmpc_path=self.PATHS[path],
-                                  constr_mult_init_max=float(constr_mult_init_max))
+                                  constr_mult_init_max=float(constr_mult_init_max),
+                                  restoration=int(bool(restoration)))
         rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
         if rc != 0:
             raise DartMPCError(f"dart_mpc_create failed with code {rc} (no gfx950 device or bad config)")
@@ -228,6 +232,8 @@ class Solver:
         want_w, w[B,nw] arrays that are filled and returned instead of fresh ones."""
         x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 6)
         B = x0.shape[0]
+        if out is not None:
+            self._check_out(out, B, want_w)
         if w_warm is None and not want_w and B > 0:
             return self._solve_staged(B, x0, ref, prm, out)
         ref = np.ascontiguousarray(ref, np.float64).reshape(B, 6)
@@ -236,11 +242,6 @@ class Solver:
         if out is not None:
             u0, f, st, it = out["u0"], out["f"], out["status"], out["iters"]
             w = out.get("w") if want_w else None
-            if (u0.shape != (B, 2) or f.shape != (B,) or st.shape != (B,) or it.shape != (B,) or st.dtype != np.int32
-                    or it.dtype != np.int32 or not all(a.flags.c_contiguous for a in (u0, f, st, it))):
-                raise DartMPCError("out= arrays do not match the batch")
-            if want_w and (w is None or w.shape != (B, self.nw)):
-                raise DartMPCError("out['w'] must be a [B, nw] array when want_w")
         else:
             u0 = np.empty((B, 2)); f = np.empty(B)
             w = np.empty((B, self.nw)) if want_w else None
@@ -250,6 +251,18 @@ class Solver:
         if rc != 0:
             self._err(rc, "dart_mpc_solve_batch")
         return dict(u0=u0, f=f, w=w, status=st, iters=it)
+
+    def _check_out(self, out, B, want_w):
+        """out= arrays: shapes of the batch, float64 u0 / f (/ w), int32 status / iters, C-contiguous."""
+        u0, f, st, it = out["u0"], out["f"], out["status"], out["iters"]
+        if (u0.shape != (B, 2) or f.shape != (B,) or st.shape != (B,) or it.shape != (B,) or u0.dtype != np.float64
+                or f.dtype != np.float64 or st.dtype != np.int32 or it.dtype != np.int32
+                or not all(a.flags.c_contiguous for a in (u0, f, st, it))):
+            raise DartMPCError("out= arrays do not match the batch")
+        if want_w:
+            w = out.get("w")
+            if w is None or w.shape != (B, self.nw) or w.dtype != np.float64 or not w.flags.c_contiguous:
+                raise DartMPCError("out['w'] must be a C-contiguous float64 [B, nw] array when want_w")
 
     def _solve_staged(self, B, x0, ref, prm, out):
         """Cold-start call without w: inputs copied into per-batch-size buffers whose pointers are
