@@ -129,9 +129,95 @@ def test_same_path_as_oracle(dm, max_soc, mult_init):
         # (with the correction off, IPOPT's line search crawls through hundreds of tiny steps on some
         # instances, and rounding-level differences shift a few of those long paths by an iteration)
         assert np.mean(g["iters"] == o["iters"]) >= (0.99 if max_soc else 0.97), (n_seeds, g["iters"], o["iters"])
-        ok = o["status"] == 0       # (with the correction off IPOPT's line search fails on ~7 % of C4)
-        assert np.mean(ok) >= (0.99 if max_soc else 0.5)
-        assert np.max(np.abs(g["u0"] - o["u0"])[ok]) <= 1e-6, (n_seeds, np.max(np.abs(g["u0"] - o["u0"])[ok]))
+        # every instance solved: with the correction off the filter line search fails on ~9 % of C4, and
+        # IPOPT's restoration phases (pmpc_resto.hip) take those instances to the solution
+        assert np.all(o["status"] == 0) and np.all(g["status"] == 0)
+        assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6, (n_seeds, np.max(np.abs(g["u0"] - o["u0"])))
+
+
+@pytest.mark.parametrize("N,max_soc", [(31, 4), (15, 0), (31, 0)])
+def test_restoration_phases_same_path_as_oracle(dm, N, max_soc):
+    """IPOPT's soft restoration and restoration phases (pmpc_resto.hip; oracle/pmpc_ipm.c soft_resto_step,
+    restoration) on C4's 1152 instances at tol 1e-8: at N = 31 three instances, with the second-order
+    correction off ~8-13 %, fail the filter line search (the oracle with the phases off ends them at -2).  The
+    register kernel hands those to the restoration kernel, which solves them again from the start: every
+    instance ends with the oracle's status (0); the restored ones take the oracle's iterations (>= 95 %) and
+    reach its u0 within 1e-8; the others are untouched (u0 within 1e-6, >= 99 % the same iterations)."""
+    import oracle_lib
+    from dart_mpc.workload import pmpc_batch
+    S, T, P = pmpc_batch(64)
+    s = dm.Solver(N=N, Ts=0.002, tol=1e-8, B_max=S.shape[0], max_soc=max_soc)
+    g = s.solve_batch(S, T, P)
+    s.close()
+    kw = dict(N=N, Ts=0.002, tol=1e-8, max_iter=3000, nthreads=8, want_w=False, soc=max_soc)
+    o = oracle_lib.solve_batch(S, T, P, **kw)
+    off = oracle_lib.solve_batch(S, T, P, resto=False, **kw)
+    rest = off["status"] != 0
+    assert rest.sum() >= 3 and np.all(off["status"][rest] == -2)
+    assert np.array_equal(g["status"], o["status"]) and np.all(o["status"] == 0)
+    du = np.abs(g["u0"] - o["u0"]).max(axis=1)
+    assert np.mean(g["iters"][rest] == o["iters"][rest]) >= 0.95, (g["iters"][rest], o["iters"][rest])
+    assert du[rest].max() <= 1e-8, du[rest].max()
+    assert np.mean(g["iters"][~rest] == o["iters"][~rest]) >= 0.99
+    assert du[~rest].max() <= 1e-6
+
+
+def test_restoration_off_keeps_the_failed_line_search(dm):
+    """restoration=False: an instance whose filter line search fails ends at status -2 (IPOPT with the
+    restoration phases unavailable), on the oracle's instances; the others are solved as with them on."""
+    import oracle_lib
+    from dart_mpc.workload import pmpc_batch
+    S, T, P = pmpc_batch(64)
+    s = dm.Solver(N=20, Ts=0.002, tol=1e-8, B_max=S.shape[0], max_soc=0, restoration=False)
+    g = s.solve_batch(S, T, P)
+    s.close()
+    off = oracle_lib.solve_batch(S, T, P, N=20, Ts=0.002, tol=1e-8, max_iter=3000, nthreads=8, want_w=False, soc=0,
+                                 resto=False)
+    assert np.array_equal(g["status"], off["status"]) and np.sum(off["status"] == -2) > 50
+    ok = off["status"] == 0
+    assert np.max(np.abs(g["u0"] - off["u0"])[ok]) <= 1e-6
+
+
+def test_restoration_through_every_entry(dm):
+    """The hand-off works on every PMPC entry: the host entry (completion words written by the restoration
+    kernel), the device entry (dart_mpc_solve_batch_dev on a caller stream), the bound in-place area and the
+    resident server (the host drains the grid and runs the restoration kernel): the same outputs everywhere."""
+    import torch
+    from dart_mpc.workload import pmpc_batch
+    import oracle_lib
+    S, T, P = pmpc_batch(4)
+    B = S.shape[0]
+    off = oracle_lib.solve_batch(S, T, P, N=20, Ts=0.002, tol=1e-8, nthreads=8, want_w=False, soc=0, resto=False)
+    assert np.sum(off["status"] == -2) >= 3          # instances that go through the restoration kernel
+    s = dm.Solver(N=20, Ts=0.002, tol=1e-8, B_max=B, max_soc=0)
+    ref = s.solve_batch(S, T, P, want_w=True)
+    assert np.sum(ref["status"] == 0) == B
+    stg = s.solve_batch(S, T, P)                    # staged host path
+    for k in ("u0", "f", "status", "iters"):
+        assert np.array_equal(stg[k], ref[k]), k
+    dev = torch.device("cuda:0")
+    d = {n: torch.from_numpy(np.ascontiguousarray(a)).to(dev) for n, a in (("x0", S), ("ref", T), ("prm", P))}
+    u0 = torch.empty((B, 2), dtype=torch.float64, device=dev); f = torch.empty(B, dtype=torch.float64, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev); it = torch.empty(B, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    s.solve_batch_dev(B, d["x0"].data_ptr(), d["ref"].data_ptr(), d["prm"].data_ptr(), u0.data_ptr(), f.data_ptr(),
+                      st.data_ptr(), it.data_ptr())
+    s.sync()
+    assert np.array_equal(st.cpu().numpy(), ref["status"]) and np.array_equal(it.cpu().numpy(), ref["iters"])
+    assert np.array_equal(u0.cpu().numpy(), ref["u0"])
+    bd = s.bind()
+    bd.x0[:B] = S; bd.ref[:B] = T; bd.prm[:B] = P
+    bd.solve(B)
+    assert np.array_equal(bd.status[:B], ref["status"]) and np.array_equal(bd.u0[:B], ref["u0"])
+    s.serve_start(B)
+    try:
+        for _ in range(2):
+            sv = s.solve_batch(S, T, P)
+            for k in ("u0", "f", "status", "iters"):
+                assert np.array_equal(sv[k], ref[k]), k
+    finally:
+        s.serve_stop()
+    s.close()
 
 
 def test_reduced_path_opt_in(dm):
@@ -183,7 +269,7 @@ def test_scan_and_sequential_riccati_agree(dm, N):
     status, take the same iterations and agree to 1e-9; with DART_PMPC_QSCAN_MAX_B the big launch
     would run the sequential Riccati sweep (tools/c4_ab.sh).  N covers every scan instantiation: one-row (N <= 15, the DART driver's
     horizon), SHORT2 (16 <= N <= 23, both ends) and the full scan (N = 24, 31).  (At N = 31 IPOPT's filter
-    line search fails on 3 of the 1152 instances, oracle and kernel alike: status -2, restoration.)"""
+    line search fails on 3 of the 1152 instances, and the restoration kernel solves them: every status 0.)"""
     from dart_mpc.workload import pmpc_batch
     S, T, P = pmpc_batch(64)
     s = dm.Solver(N=N, Ts=0.002, tol=1e-8, B_max=2 * S.shape[0])
@@ -196,11 +282,10 @@ def test_scan_and_sequential_riccati_agree(dm, N):
     st_small = np.concatenate([o["status"] for o in small])
     np.testing.assert_array_equal(big["status"][:B], big["status"][B:])
     np.testing.assert_array_equal(big["status"][:B], st_small)
-    assert np.mean(st_small == 0) >= 0.99
+    assert np.all(st_small == 0)
     np.testing.assert_array_equal(big["iters"][:B], big["iters"][B:])
     assert np.mean(big["iters"][:B] == it_small) >= 0.99
-    ok = st_small == 0
-    assert np.max(np.abs(big["u0"][:B] - u_small)[ok]) <= 1e-9
+    assert np.max(np.abs(big["u0"][:B] - u_small)) <= 1e-9
 
 
 def test_symmetry_and_rest_properties(dm):
