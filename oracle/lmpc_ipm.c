@@ -1290,6 +1290,9 @@ static double bound_dual_step(const ctx_t *C, work_t *W, int nU, double tau) {
     return az;
 }
 
+#ifdef ORACLE_RICCATI_PROBE
+static void riccati_probe(const ctx_t *C, work_t *W);
+#endif
 int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_prev, const double *pvec,
                       const double *target, const double *prm, const double *w_init, int max_iter, double tol,
                       double acc_tol, int acc_iter, double *u0, double *fval, double *w_out, int32_t *iters_out) {
@@ -1381,6 +1384,9 @@ int oracle_lmpc_solve(int N, double Ts, const double *state, const double *u_pre
             nfilt = 0; in_soft = 0;      /* BacktrackingLineSearch::Reset: the filter and the soft phase */
         }
         const double tau = fmax(0.99, 1.0 - C.mu);
+#ifdef ORACLE_RICCATI_PROBE
+        if (it == 0) riccati_probe(&C, W);      /* diagnostic build (tools/lmpc_riccati_probe.c) */
+#endif
         double delta = 0.0;
         int ok = riccati_factor(&C, W, 0.0);
         for (int attempt = 0; !ok && attempt < 60; ++attempt) {

@@ -26,18 +26,18 @@ def _nw(N):
 
 
 def _same_outcome(g, o, min_conv):
-    """Path parity with the oracle: on every instance IPOPT solves (status 0 / 1) the kernel ends with the same
-    status after the same number of iterations with |du0| <= 1e-6; where IPOPT does not converge (max_iter
-    or a failed restoration, after restoration phases with Hessian shifts up to 1e3 and steps of 1e-6,
-    where rounding at 1e-16 decides the path) the kernel does not converge either."""
+    """Path parity with the oracle: every instance ends with the oracle's status.  Where IPOPT solves it
+    (status 0 / 1) the kernel also takes the same number of iterations with |du0| <= 1e-6; where IPOPT does not
+    converge (max_iter -1, local infeasibility 2, a failed restoration -2) the statuses are equal too.  (The
+    parity sweep's two iteration-0 inertia disagreements, tools/lmpc_riccati_probe.c, are not in these batches:
+    their Riccati recursion is indeterminate even in quad precision)"""
     conv = np.isin(o["status"], (0, 1))
     assert conv.sum() >= min_conv, conv.sum()
-    bad = np.where(g["status"][conv] != o["status"][conv])[0]
-    assert bad.size == 0, (bad, g["status"][conv][bad], o["status"][conv][bad])
+    bad = np.where(g["status"] != o["status"])[0]
+    assert bad.size == 0, (bad, g["status"][bad], o["status"][bad], g["iters"][bad], o["iters"][bad])
     bad = np.where(g["iters"][conv] != o["iters"][conv])[0]
     assert bad.size == 0, (bad, g["iters"][conv][bad], o["iters"][conv][bad])
     assert np.max(np.abs(g["u0"][conv] - o["u0"][conv])) <= 1e-6
-    assert not np.any(np.isin(g["status"][~conv], (0, 1)))
 
 
 def test_goldens_tight_tol(dm, lmpc_goldens):
