@@ -13,11 +13,19 @@ Per client: one request is taken per round, so each client's replies stay in its
 starved.  Clients may have different objects and weights (their ``params`` dicts, as passed to
 ``mpc_worker``); clients are grouped by (N, Ts), one GPU handle per group.  A client leaves with
 ``"STOP"``; the server returns when every client has left.
+
+Waiting on many queues uses only their public API: one forwarding thread per client blocks in
+``state_queue.get()`` and hands each message, stamped with its arrival time, to one in-process inbox.
+The ``solve_time`` of a reply is that request's own time in the server, from its arrival to its reply
+(the batch it waited for and the solve), the server-side counterpart of the worker's timed
+``mpc.solve`` (:44-46).
 """
 from __future__ import annotations
 
+import queue
+import threading
 import time
-from multiprocessing.connection import wait
+from collections import deque
 
 import numpy as np
 
@@ -57,37 +65,54 @@ def mpc_batch_server(model_path, clients, idle_timeout=1.0, device=0, tol=1e-8, 
         s = solver_factory(N, Ts, len(g["clients"]))
         g["solver"], g["bound"] = s, s.bind()
 
+    inbox = queue.Queue()
+
+    def forward(i, q):
+        while True:
+            item = q.get()
+            inbox.put((i, item, time.perf_counter()))
+            if isinstance(item, str) and item == "STOP":
+                return
+
+    for i, c in enumerate(clients):
+        threading.Thread(target=forward, args=(i, c[2]), daemon=True, name=f"mpc-client-{i}").start()
     active = set(range(len(clients)))
+    backlog = {i: deque() for i in active}       # arrived, not yet taken (one per client per round)
     sizes = []
     try:
         while active:
-            wait([clients[i][2]._reader for i in active])
+            if not any(backlog[i] for i in active):
+                i, item, t = inbox.get()
+                backlog[i].append((item, t))
+            while True:
+                try:
+                    i, item, t = inbox.get_nowait()
+                except queue.Empty:
+                    break
+                backlog[i].append((item, t))
             pending = {}
             for i in sorted(active):
-                q = clients[i][2]
-                if not q._reader.poll():
+                if not backlog[i]:
                     continue
-                item = q.get()
+                item, t = backlog[i].popleft()
                 if isinstance(item, str) and item == "STOP":
                     active.discard(i)
                     continue
-                pending[i] = item
+                pending[i] = (item, t)
             for g in groups.values():
                 idx = [i for i in g["clients"] if i in pending]
                 if not idx:
                     continue
                 bd, B = g["bound"], len(idx)
                 for r, i in enumerate(idx):
-                    state, target = pending[i]
+                    state, target = pending[i][0]
                     bd.x0[r] = state
                     bd.ref[r] = target
                     bd.prm[r] = prm[i]
-                t0 = time.time()
                 bd.solve(B)
-                dt = time.time() - t0
                 sizes.append(B)
                 for r, i in enumerate(idx):
-                    clients[i][3].put((bd.u0[r].copy(), np.array([bd.f[r]]), dt))
+                    clients[i][3].put((bd.u0[r].copy(), np.array([bd.f[r]]), time.perf_counter() - pending[i][1]))
     finally:
         for g in groups.values():
             g["solver"].close()

@@ -54,7 +54,10 @@ def test_c3_batch_vs_oracle(dm, tol, u0_bound, U_bound):
     assert np.max(np.abs(out["u0"] - ref["u0"])) <= u0_bound
     assert np.max(np.abs(out["w"][:, 84:] - ref["w"][:, 84:])) <= U_bound
     assert np.allclose(out["f"], ref["f"], rtol=1e-6, atol=1e-10)
-    assert np.max(np.abs(out["iters"] - ref["iters"])) <= 10, (out["iters"], ref["iters"])
+    # the same path as the oracle (test_same_path_as_oracle's bound): equal iteration counts, bar at most one
+    # instance where rounding near the end shifts convergence by one iteration
+    d = np.abs(out["iters"] - ref["iters"])
+    assert np.sum(d != 0) <= 1 and d.max() <= 1, (out["iters"], ref["iters"])
 
 
 def test_wide_tilt_box_library_trig_path(dm):
