@@ -112,11 +112,12 @@ typedef struct dart_mpc_config {
                            defect rows of mpc_3d.py:37, :48 in theta, the filter, the error measures and
                            the second-order correction); 1 = the reduced (x, y) path, opt-in: same KKT
                            point to the tolerance, fewer iterations, but not IPOPT's iterates */
-    int32_t restoration;  /* LMPC (ABI 6), RMPC (ABI 8): 1 = IPOPT's soft restoration and restoration
-                           phases after a failed filter line search (default; MinC_1NrmRestorationPhase,
-                           the fallback of every nlpsol call, np_mpc...:158-162, rlmpc2.py:480-489); 0 = stop
-                           with status -2 there.  RMPC: the failed instances of a launch are re-solved by a
-                           second kernel on the same stream */
+    int32_t restoration;  /* LMPC (ABI 6), RMPC and PMPC (ABI 8): 1 = IPOPT's soft restoration and
+                           restoration phases after a failed filter line search (default;
+                           MinC_1NrmRestorationPhase, the fallback of every nlpsol call, mpc_3d.py:82,
+                           np_mpc...:158-162, rlmpc2.py:480-489); 0 = stop with status -2 there.  RMPC and
+                           PMPC: the failed instances of a launch are re-solved by a second kernel queued on
+                           the same stream (PMPC: IPOPT's path, N <= 31; the reduced path and N > 31 keep -2) */
     double constr_mult_init_max;  /* IPOPT constr_mult_init_max (default 1000): the starting equality
                            multipliers are IPOPT's least-square estimate unless its max norm exceeds this
                            (then 0); 0 = always start from 0.  Used by PMPC, RMPC and LMPC */
