@@ -2,7 +2,9 @@
 at the reference's options -- PMPC tol 1e-8 (C2/C4 workload), RMPC tol 1e-8 (C3), LMPC tol 1e-4 / max_iter 50
 / acceptable 1e-3 x 5 with IPOPT's restoration phases (C5 stress workload).  Per variant: instances, status
 agreement, iteration agreement, max |du0| over the instances the oracle solves (status 0 / 1) and the
-status counts of both.  Usage: python tools/parity_sweep.py [pmpc_seeds rmpc_seeds lmpc_seeds]"""
+status counts of both.  Round 4 adds the restoration phases: RMPC with the C3 velocities spread 3x (infeasible starts) and PMPC at
+N = 31 and with max_soc = 0 (instances whose filter line search fails).
+Usage: python tools/parity_sweep.py [pmpc_seeds rmpc_seeds lmpc_seeds [rmpc_spread_seeds]]"""
 import os
 import sys
 import time
@@ -16,7 +18,7 @@ import dart_mpc  # noqa: E402
 from dart_mpc.workload import lmpc_batch, pmpc_batch, rmpc_batch  # noqa: E402
 
 NT = max(1, min(16, len(os.sched_getaffinity(0))))
-ns = [int(a) for a in sys.argv[1:4]] if len(sys.argv) > 3 else [640, 160, 160]
+ns = [int(a) for a in sys.argv[1:5]] if len(sys.argv) > 3 else [640, 160, 160, 80]
 
 
 def report(name, g, o, solved):
@@ -57,4 +59,33 @@ g = s.solve_batch(*args)
 s.close()
 o = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=NT, want_w=False)
 report("LMPC C5 stress (seeds 100000+, restoration on)", g, o, lambda st: np.isin(st, (0, 1)))
+
+# the restoration phases of RMPC and PMPC (round 4): infeasible RMPC starts (measured velocities 3x the C3
+# spread: |v| > vmax at the pinned node 0) and PMPC instances whose filter line search fails (N = 31 at the
+# defaults; max_soc = 0 at N = 20)
+if len(ns) > 3 or len(sys.argv) <= 4:
+    n_r = ns[3] if len(ns) > 3 else 80
+    D = rmpc_batch(n_r, seed0=200000)
+    D["x0"] = D["x0"].copy(); D["x0"][:, [1, 3]] *= 3.0
+    args = (D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
+    s = dart_mpc.RmpcSolver(N=20, tol=1e-8, B_max=len(D["x0"]))
+    g = s.solve_batch(*args)
+    s.close()
+    o = oracle_lib.rmpc_solve_batch(*args, N=20, tol=1e-8, nthreads=NT)
+    report("RMPC C3 velocities x3 (seeds 200000+, restoration)", g, o, lambda st: st == 0)
+    inf = (o["status"] == 2) & (g["status"] == 2)
+    if inf.any():
+        du = np.abs(g["u0"] - o["u0"]).max(axis=1)[inf]
+        print(f"    status 2 by both {int(inf.sum())}: |du0| median {np.median(du):.2e}, 99 % {np.quantile(du, 0.99):.2e}, "
+              f"max {du.max():.2e}", flush=True)
+    for N, soc, seeds in ((31, 4, 128), (20, 0, 32)):
+        S, T, P = pmpc_batch(seeds, seed0=300000)
+        s = dart_mpc.Solver(N=N, Ts=0.002, tol=1e-8, B_max=S.shape[0], max_soc=soc)
+        g = s.solve_batch(S, T, P)
+        s.close()
+        o = oracle_lib.solve_batch(S, T, P, N=N, Ts=0.002, tol=1e-8, max_iter=3000, nthreads=NT, want_w=False, soc=soc)
+        off = oracle_lib.solve_batch(S, T, P, N=N, Ts=0.002, tol=1e-8, max_iter=3000, nthreads=NT, want_w=False, soc=soc,
+                                     resto=False)
+        report(f"PMPC N={N} max_soc={soc} (seeds 300000+; {int(np.sum(off['status'] != 0))} need restoration)", g, o,
+               lambda st: st == 0)
 print(f"({time.time() - t0:.0f} s, oracle on {NT} threads)")
