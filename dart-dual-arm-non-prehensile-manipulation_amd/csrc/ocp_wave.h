@@ -194,6 +194,11 @@ __device__ __forceinline__ void aug_node_step(L* S, int k, const double* Gn, con
 #pragma unroll
     for (int x = 0; x < 8; ++x) b[x] = Mk[R.cs * NC + (R.s ^ x)];
     const double hk = S->H[k][R.e];
+    // the phase-2 column of M_k issued with the G_{k+1} reads (an empty asm use keeps the scheduler from
+    // sinking these loads behind phase 1, where their latency would sit on the node chain; C3 -1.7% kernel
+    // time, profiles/r04/pin_b_ab.txt)
+#pragma unroll
+    for (int x = 0; x < 8; ++x) asm volatile("" : "+v"(b[x]));
     // phase 1: every read of G_{k+1} issued before the first product
     double gz[NP], gu0[NP], gu1[NP];
 #pragma unroll
