@@ -241,6 +241,7 @@ __device__ bool riccati_sweep_aug(L* S, int N) {
     constexpr int NXA = L::NXA;
     const AugRoles R = aug_roles<L>();
     bool ok = true;
+    // (unrolled by two like riccati_s_sweep, this kernel spills: C3 -20 %, profiles/r04/node_unroll_ab.txt)
     for (int k = N - 1; k >= 0; --k) aug_node_step<L>(S, k, S->G[k + 1], R, ok);
     double i00, i01, i11;
     return quu_inverse<NXA>(S->G[0], i00, i01, i11) && ok;
@@ -694,44 +695,58 @@ __device__ RiccatiSRoles riccati_s_roles() {
 
 // Backward sweep of both halves over nodes N-1 .. 0; G[slot N] must hold each half's terminal
 // surrogate.  Returns false (wave-uniform) if some Quu of either half is not positive.
+// One node step of both halves (riccati_s_sweep): straight-line body, every lane active (lanes past NT
+// recompute entry 0 and store the same value): the loads of H_k and M_k do not wait on G_{k+1}, and Quu's
+// reciprocal is taken after the products, so one LDS latency per node stays on the chain.  Ends with a
+// barrier.
+template <class L>
+__device__ __forceinline__ void s_node_step(L* S, int sk, const RiccatiSRoles& R, bool& ok) {
+    constexpr int NXA = L::NXA, NP = L::NP;
+    const double hk = S->H[sk][R.e];
+    const double* Mk = &S->M[sk][0][0];
+    double vi[NP], vj[NP];
+#pragma unroll
+    for (int m = 0; m < NP; ++m) { vi[m] = Mk[R.ci + m]; vj[m] = Mk[R.cj + m]; }
+    const double* Gn = S->G[sk + 1];
+    double t[NP], b = 0.0, c = 0.0;
+#pragma unroll
+    for (int m = 0; m < NP; ++m) t[m] = 0.0;
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+#pragma unroll
+        for (int m = 0; m < NP; ++m) t[m] = fma(Gn[gszz<NXA>(m, n)], vj[n], t[m]);
+        b = fma(vi[n], Gn[gszu<NXA>(n)], b);
+        c = fma(vj[n], Gn[gszu<NXA>(n)], c);
+    }
+    double ga = hk, gb = 0.0;
+#pragma unroll
+    for (int m = 0; m < NP; m += 2) {
+        ga = fma(vi[m], t[m], ga);
+        if (m + 1 < NP) gb = fma(vi[m + 1], t[m + 1], gb);
+    }
+    const double q = Gn[hp(NXA, NXA)];
+    ok = ok && q > 0.0 && isfinite(q);
+    const double g = (ga + gb) - b * c * frcp(q);
+    // all reads of G_{k+1} and M_k precede the write of G_k (distinct slots: no hazard)
+    S->G[sk][R.e] = g;
+    __syncthreads();
+}
+
+// Backward sweep of both halves over nodes N-1 .. 0; G[slot N] must hold each half's terminal
+// surrogate.  Returns false (wave-uniform) if some Quu of either half is not positive.  Two nodes per
+// loop trip: the second node's LDS addresses are immediate offsets of the first's (C5 +0.3 %,
+// profiles/r04/node_unroll_ab.txt).
 template <class L>
 __device__ bool riccati_s_sweep(L* S, int N, const RiccatiSRoles& R) {
-    constexpr int NXA = L::NXA, NP = L::NP;
+    constexpr int NXA = L::NXA;
     const int base = (threadIdx.x >> 5) * L::NMAXS;
     bool ok = true;
-    for (int k = N - 1; k >= 0; --k) {
-        // straight-line body, every lane active (lanes past NT recompute entry 0 and store the same
-        // value): the loads of H_k and M_k do not wait on G_{k+1}, and Quu's reciprocal is taken
-        // after the products, so one LDS latency per node stays on the chain
-        const double hk = S->H[base + k][R.e];
-        const double* Mk = &S->M[base + k][0][0];
-        double vi[NP], vj[NP];
-#pragma unroll
-        for (int m = 0; m < NP; ++m) { vi[m] = Mk[R.ci + m]; vj[m] = Mk[R.cj + m]; }
-        const double* Gn = S->G[base + k + 1];
-        double t[NP], b = 0.0, c = 0.0;
-#pragma unroll
-        for (int m = 0; m < NP; ++m) t[m] = 0.0;
-#pragma unroll
-        for (int n = 0; n < NP; ++n) {
-#pragma unroll
-            for (int m = 0; m < NP; ++m) t[m] = fma(Gn[gszz<NXA>(m, n)], vj[n], t[m]);
-            b = fma(vi[n], Gn[gszu<NXA>(n)], b);
-            c = fma(vj[n], Gn[gszu<NXA>(n)], c);
-        }
-        double ga = hk, gb = 0.0;
-#pragma unroll
-        for (int m = 0; m < NP; m += 2) {
-            ga = fma(vi[m], t[m], ga);
-            if (m + 1 < NP) gb = fma(vi[m + 1], t[m + 1], gb);
-        }
-        const double q = Gn[hp(NXA, NXA)];
-        ok = ok && q > 0.0 && isfinite(q);
-        const double g = (ga + gb) - b * c * frcp(q);
-        // all reads of G_{k+1} and M_k precede the write of G_k (distinct slots: no hazard)
-        S->G[base + k][R.e] = g;
-        __syncthreads();
+    int k = N - 1;
+    for (; k >= 1; k -= 2) {
+        s_node_step<L>(S, base + k, R, ok);
+        s_node_step<L>(S, base + k - 1, R, ok);
     }
+    if (k == 0) s_node_step<L>(S, base, R, ok);
     const double q0 = S->G[base][hp(NXA, NXA)];
     ok = ok && q0 > 0.0 && isfinite(q0);
     return !wany(!ok);
