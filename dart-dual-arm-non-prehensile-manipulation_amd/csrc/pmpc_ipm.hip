@@ -912,8 +912,8 @@ __device__ __forceinline__ void pmpc_solve(const PmpcArgs& a, const int b) {
     STAMP_FLUSH(b);
 }
 
-template <int NAX, bool QSCAN, bool ONEROW = false, bool SHORT2 = false, bool RED = false>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu((QSCAN || NAX == 2) ? 1 : 2)))
+template <int NAX, bool QSCAN, bool ONEROW = false, bool SHORT2 = false, bool RED = false, bool OCC2 = false>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(OCC2 ? 2 : ((QSCAN || NAX == 2) ? 1 : 2))))
 void pmpc_ipm_kernel(PmpcArgs a) {
     // small batches: the launcher deals 8 blocks per instance and only every 8th works, so all
     // instances land on one XCD (blocks go round-robin over the 8 XCDs) and share its L2 for the code
@@ -1063,15 +1063,34 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
         const char* e = getenv("DART_PMPC_QSCAN_MAX_B");
         return e ? atoi(e) : (1 << 30);
     }();
+    // From two instances per SIMD of the device on (2048 on MI355X), batches of 16 <= N <= 31 take the scan
+    // build compiled for two waves per SIMD (40 VGPRs spilled, 164 B of scratch): the second wave fills the
+    // first's dependency stalls (VALU busy ~63 % alone).  Below that, one wave per SIMD and no spills win
+    // (N = 20, B = 1152: 10.8 against 9.4 M solves/s; even at 1536; B = 2048: 15.2 against 13.7 M; 18432:
+    // 20.5-20.9 against 17.8 M; N = 31, 18432: 6.4 against 6.1 M); the one-row build (N <= 15) loses with it
+    // (18432: 19.4-19.7 against 19.9 M) and stays at one wave.  profiles/r04/occ2_ab.txt;
+    // DART_PMPC_OCC2_MIN_B overrides the threshold (experiments).
+    static const int occ2_min_b = [] {
+        if (const char* e = getenv("DART_PMPC_OCC2_MIN_B")) return atoi(e);
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            return 1 << 30;
+        return 2 * 4 * cus;
+    }();
+    const bool occ2 = !a.reduced && a.B >= occ2_min_b;
     if (a.N <= 15 && a.B <= qscan_max_b) {
         if (hipError_t e = dartmpc_launch_pmpc_seq(&a, grid.x, stream, 1)) return e;
     } else if (a.N <= 23 && a.B <= qscan_max_b) {
-        if (a.reduced)
+        if (occ2)
+            hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+        else if (a.reduced)
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
         else
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
     } else if (a.N <= 31 && a.B <= qscan_max_b) {
-        if (a.reduced)
+        if (occ2)
+            hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, false, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+        else if (a.reduced)
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
         else
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true>), grid, dim3(dartmpc::kWave), 0, stream, a);

@@ -12,7 +12,7 @@ ARGS="--steps 200 --warmup 20 --no-cpu-baseline --host-calls 0 --n15-steps 0 --r
 for r in $(seq 1 $REPS); do
   for th in off 1024; do
     for sb in 4096 18432; do
-      if [ $th = off ]; then unset DART_PMPC_OCC2_MIN_B; else export DART_PMPC_OCC2_MIN_B=$th; fi
+      if [ $th = off ]; then export DART_PMPC_OCC2_MIN_B=1000000000; else export DART_PMPC_OCC2_MIN_B=$th; fi
       timeout -k 10 180 python bench.py $ARGS --saturation-batch $sb > gpurun_out/occ2.json 2>gpurun_out/occ2.err || exit $?
       python - "$th" "$sb" <<'PY'
 import json, sys
