@@ -19,7 +19,7 @@ SRC = os.path.join(ROOT, "gpurun_out", f"sq_{TAG}")
 DST = os.path.join(ROOT, "profiles", TAG, "sq_summary.json")
 
 # label: (kernel-name prefix, grid size of the headline launch, working waves per launch)
-KERNELS = {"PMPC C2": ("void dartmpc::pmpc_ipm_kernel<1, true, false, true, false>", 9216, 18),
+KERNELS = {"PMPC C2": ("void dartmpc::pmpc_ipm_kernel<1, true, false, true, false", 9216, 18),
            "RMPC C3": ("void dartmpc::rmpc_ipm_kernel<false>", 9216, 18),
            "LMPC C5": ("void dartmpc::lmpc_ipm_kernel<false>", 9216, 18),
            "arm QP": ("void dartmpc::arm_qp_kernel<7>", 2304, 36)}
