@@ -147,8 +147,9 @@ __device__ __forceinline__ void mat4_scan_level(double* T) {
 //   per SIMD (throughput regime)
 //   ONEROW: N <= 15, every axis fits one 16-lane DPP row and the scans need no cross-row step (the
 //   DART driver's default horizon is 15, main_parallel_enhanced.py:171-196)
-//   SHORT2: 16 <= N <= 23, the suffix of node 16 spans at most 8 lanes, so the quadratic scan stops
+//   SHORT2: N <= 23, the suffix of node 16 spans at most 8 lanes, so the quadratic scan stops
 //   after 3 in-row levels and finishes rows 0 / 2 with two 4 x 2 compositions (no 4th 4 x 4 level)
+//   (16 <= N <= 23 at one wave per SIMD; its two-wave instantiation, OCC2, also serves large N <= 15 batches)
 //   Occupancy: the sequential NAX == 1 build is the throughput variant and must fit two waves per
 //   SIMD (<= 256 registers); the ILP-oriented scheduler of this file (Makefile) would otherwise spend
 //   the whole register file on one wave
@@ -1063,13 +1064,14 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
         const char* e = getenv("DART_PMPC_QSCAN_MAX_B");
         return e ? atoi(e) : (1 << 30);
     }();
-    // From two instances per SIMD of the device on (2048 on MI355X), batches of 16 <= N <= 31 take the scan
-    // build compiled for two waves per SIMD (40 VGPRs spilled, 164 B of scratch): the second wave fills the
+    // From two instances per SIMD of the device on (2048 on MI355X), batches of N <= 31 take the scan build
+    // compiled for two waves per SIMD (40 VGPRs spilled, 164 B of scratch): the second wave fills the
     // first's dependency stalls (VALU busy ~63 % alone).  Below that, one wave per SIMD and no spills win
     // (N = 20, B = 1152: 10.8 against 9.4 M solves/s; even at 1536; B = 2048: 15.2 against 13.7 M; 18432:
-    // 20.5-20.9 against 17.8 M; N = 31, 18432: 6.4 against 6.1 M); the one-row build (N <= 15) loses with it
-    // (18432: 19.4-19.7 against 19.9 M) and stays at one wave.  profiles/r04/occ2_ab.txt;
-    // DART_PMPC_OCC2_MIN_B overrides the threshold (experiments).
+    // 20.5-20.9 against 17.8 M; N = 31, 18432: 6.4 against 6.1 M).  N <= 15 takes the short-scan build there
+    // (the one-row build loses at two waves, 19.4-19.7 against 19.9 M; the short-scan one wins, 2048: 15.4-15.5
+    // against 15.0 M, 18432: 22.2-22.8 against 20.0 M).  profiles/r04/occ2_ab.txt; DART_PMPC_OCC2_MIN_B
+    // overrides the threshold (experiments).
     static const int occ2_min_b = [] {
         if (const char* e = getenv("DART_PMPC_OCC2_MIN_B")) return atoi(e);
         int dev = 0, cus = 0;
@@ -1078,12 +1080,12 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
         return 2 * 4 * cus;
     }();
     const bool occ2 = !a.reduced && a.B >= occ2_min_b;
-    if (a.N <= 15 && a.B <= qscan_max_b) {
+    if (a.N <= 23 && occ2) {        // (N <= 15 too: the short-scan build at two waves beats the one-row build at one)
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+    } else if (a.N <= 15 && a.B <= qscan_max_b) {
         if (hipError_t e = dartmpc_launch_pmpc_seq(&a, grid.x, stream, 1)) return e;
     } else if (a.N <= 23 && a.B <= qscan_max_b) {
-        if (occ2)
-            hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
-        else if (a.reduced)
+        if (a.reduced)
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
         else
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
