@@ -226,7 +226,8 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False, c
     ST = torch.empty(n, dtype=torch.int32, device=dev)
     IT = torch.empty(n, dtype=torch.int32, device=dev)
     block = torch.zeros((per, RESULT_COLS), dtype=dt64, device=dev)
-    full = torch.zeros((world * per, RESULT_COLS), dtype=dt64, device=dev)
+    # without a collective the gathered result of one rank is its block: the same buffer
+    full = torch.zeros((world * per, RESULT_COLS), dtype=dt64, device=dev) if coll else block
     solver = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=max(1, n), device=dev.index, path=args.pmpc_path)
     sp = stream.cuda_stream
 
@@ -236,17 +237,14 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False, c
         if not gather:
             return
         with torch.cuda.stream(stream):
-            block[:n, 0:2].copy_(U0)
-            block[:n, 2].copy_(FV)
-            block[:n, 3].copy_(ST)
+            # [u0, f, status] rows in one kernel
+            torch.cat((U0, FV.unsqueeze(1), ST.unsqueeze(1).to(dt64)), dim=1, out=block[:n])
             if coll and host_coll:
                 fh = full.cpu()     # gloo rehearsal: the gather runs on host copies
                 dist.all_gather_into_tensor(fh, block.cpu())
                 full.copy_(fh)
             elif coll:
                 dist.all_gather_into_tensor(full, block)
-            else:
-                full.copy_(block)
 
     def timed(gather):
         for _ in range(3):
@@ -284,7 +282,7 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False, c
             "global_batch": Bg, "per_rank": per, "n_gpus": world, "scaling": "strong", "steps": K,
             "solves_per_s": Bg * K / dt, "ms_per_step": dt / K * 1e3, "gather_in_timed_region": coll,
             "gather": ("RCCL all_gather_into_tensor on device tensors" if coll and not host_coll
-                       else "gloo all_gather_into_tensor on host copies" if coll else "local copy (no process group)"),
+                       else "gloo all_gather_into_tensor on host copies" if coll else "none: one rank, its packed block is the result"),
             "solves_per_s_without_gather": Bg * K / dt_solve, "ms_per_step_without_gather": dt_solve / K * 1e3,
             "status_ok_frac": float(np.mean(res[:, 3] == 0)), "rank_blocks_consistent": mine,
             "max_abs_u0_err_vs_oracle_same_tol": float(np.max(np.abs(res[:, 0:2] - same["u0"]))),
@@ -546,6 +544,11 @@ def bench_arm(args, torch, dev, stream, dart_mpc):
 
 def main():
     args = parse()
+    # stdout carries exactly one JSON line (rank 0): everything else written to fd 1 -- Python prints and the
+    # libraries' own output (RCCL prints a version banner there when a communicator starts) -- goes to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
     import dart_mpc
@@ -873,7 +876,8 @@ def main():
             "lmpc_c5": lmpc,
             "arm_qp": arm,
         }
-        print(json.dumps(line))
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     if coll:
         dist.destroy_process_group()
 
