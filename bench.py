@@ -571,12 +571,14 @@ def main():
             if "MASTER_PORT" not in os.environ:
                 so = socket.socket(); so.bind(("127.0.0.1", 0)); os.environ["MASTER_PORT"] = str(so.getsockname()[1]); so.close()
             os.environ.setdefault("RANK", "0"); os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group(backend)
     # one rank per GPU; a gloo rehearsal with more ranks than cards shares them round robin
     ndev = max(1, torch.cuda.device_count())
     local = local % ndev if host_coll else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if coll:
+        # RCCL: the rank's device named explicitly (a guessed rank -> GPU mapping can hang)
+        dist.init_process_group(backend, **({} if host_coll else {"device_id": dev}))
 
     B, N, K, W = args.batch, args.N, args.steps, args.warmup
     n_seeds_step = max(1, -(-B // 18))
