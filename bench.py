@@ -41,7 +41,12 @@ METRIC = "MPC solves/sec (horizon N=20, batch=18 objects) at 1/2/4/8 GPUs; max |
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU).  Under torchrun it must equal WORLD_SIZE; without torchrun and > 1, "
+                         "bench.py starts the N rank processes itself (default: WORLD_SIZE, else 1)")
+    ap.add_argument("--plumbing-only", action="store_true",
+                    help="run the multi-rank plumbing (process group, barrier + max-over-ranks timing, the C4 "
+                         "shard / gather) on the CPU without solving: a launcher self-test")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=18, help="instances per step per GPU (18 = the metric's config)")
@@ -60,6 +65,8 @@ def parse():
     ap.add_argument("--arm-steps", type=int, default=200, help="launches of the supplementary arm-QP line (0 = skip)")
     ap.add_argument("--n15-steps", type=int, default=200,
                     help="launches of the supplementary PMPC line at the driver's horizon N=15 (0 = skip)")
+    ap.add_argument("--resto-steps", type=int, default=10,
+                    help="launches per line of the supplementary PMPC restoration lines (0 = skip)")
     ap.add_argument("--c4-steps", type=int, default=50,
                     help="steps of the supplementary C4 line (1152 instances sharded over the ranks + gather; 0 = skip)")
     ap.add_argument("--dist-backend", default=None,
@@ -290,6 +297,73 @@ def bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll=False, c
             "max_abs_u0_err_vs_exact_optimum_first36": float(np.max(np.abs(res[:36, 0:2] - ref["u0"]))),
             "note_exact_optimum": "IPOPT's own stopping point at tol 1e-8 sits ~mu/z inside weakly active bounds: "
                                   "the oracle at tol 1e-8 is as far from the tol-1e-11 optimum"}
+
+
+def bench_pmpc_restoration(args, torch, dev, stream, dart_mpc):
+    """PMPC launches that contain instances needing IPOPT's restoration phases (pmpc_resto.h): C4's 1152
+    instances at N = 31 with the default options (a few fail the filter line search) and at N = 20 with
+    max_soc = 0 (about one in ten), against the same launches with the phases off (restoration = False: those
+    instances stop at -2, the cost of a launch without restoration); and C2-size batches of 18 that hold one such
+    instance (the restoration runs in the solving wave).  The restored controls are checked against the oracle."""
+    from dart_mpc.workload import pmpc_batch
+    K = args.resto_steps
+    S, T, P = pmpc_batch(n_seeds=64, seed0=300000)
+    B = S.shape[0]
+    dt64 = torch.float64
+    X0, RF, PR = (torch.tensor(a, dtype=dt64, device=dev).contiguous() for a in (S, T, P))
+    U0 = torch.empty((B, 2), dtype=dt64, device=dev); FV = torch.empty(B, dtype=dt64, device=dev)
+    ST = torch.empty(B, dtype=torch.int32, device=dev); IT = torch.empty(B, dtype=torch.int32, device=dev)
+    sp = stream.cuda_stream
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_lib   # checker only
+
+    def timed(solver, n, k):
+        def launch():
+            solver.solve_batch_dev(n, X0.data_ptr(), RF.data_ptr(), PR.data_ptr(), U0.data_ptr(), FV.data_ptr(),
+                                   ST.data_ptr(), IT.data_ptr(), stream=sp)
+        launch()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            launch()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / k
+
+    out = {}
+    for name, N, soc in (("c4_n31_default", 31, 4), ("c4_n20_max_soc0", 20, 0)):
+        on = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=B, device=dev.index, max_soc=soc)
+        off = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=B, device=dev.index, max_soc=soc, restoration=False)
+        t_off = timed(off, B, K)
+        rest = ST.cpu().numpy() == -2
+        t_on = timed(on, B, K)
+        st, u0, it = ST.cpu().numpy(), U0.cpu().numpy(), IT.cpu().numpy()
+        idx = np.flatnonzero(rest)
+        o = oracle_lib.solve_batch(S[idx], T[idx], P[idx], N=N, Ts=0.002, tol=args.tol, max_iter=3000, nthreads=8,
+                                   want_w=False, soc=soc)
+        line = {"instances": B, "restored": int(rest.sum()), "ms_per_launch": t_on * 1e3,
+                "ms_per_launch_restoration_off": t_off * 1e3, "ratio_to_restoration_off": t_on / t_off,
+                "status_ok_frac": float(np.mean(st == 0)), "restored_iters_mean": float(it[idx].mean()),
+                "restored_status_equal_to_oracle": bool(np.array_equal(st[idx], o["status"])),
+                "restored_max_abs_u0_err_vs_oracle": float(np.max(np.abs(u0[idx] - o["u0"])))}
+        # a C2-size batch of 18 holding one such instance (the restoration in the solving wave)
+        if idx.size:
+            sel = np.concatenate([idx[:1], np.flatnonzero(~rest)[:17]])
+            for a, src in ((X0, S), (RF, T), (PR, P)):
+                a[:18].copy_(torch.tensor(src[sel], dtype=dt64, device=dev))
+            s18 = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=18, device=dev.index, max_soc=soc)
+            o18 = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=18, device=dev.index, max_soc=soc,
+                                  restoration=False)
+            line["b18_one_restored_ms"] = timed(s18, 18, K) * 1e3
+            line["b18_one_restored_status"] = int(ST[0].item())
+            line["b18_restoration_off_ms"] = timed(o18, 18, K) * 1e3
+            s18.close(); o18.close()
+            for a, src in ((X0, S), (RF, T), (PR, P)):
+                a.copy_(torch.tensor(src, dtype=dt64, device=dev))
+        out[name] = line
+        on.close(); off.close()
+    out["note"] = ("one launch per call, inputs resident in HBM; a launch lasts as long as its slowest instance, and a "
+                   "restored instance is solved again from its start on the LDS Riccati engine (pmpc_resto.h)")
+    return out
 
 
 def bench_lmpc(args, torch, dev, stream, dart_mpc):
@@ -542,20 +616,121 @@ def bench_arm(args, torch, dev, stream, dart_mpc):
     return out
 
 
+def _spawn_ranks(n):
+    """`--gpus N` (N > 1) without torchrun: start the N rank processes here, in the environment torchrun
+    gives them (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free MASTER_PORT), and return the
+    exit status.  This parent never imports torch, so nothing has touched a GPU when the children start;
+    rank r takes GPU r (LOCAL_RANK).  If a rank fails, the others (which may wait in a collective) are
+    stopped by their PIDs.  The rank-0 JSON line reaches stdout from rank 0 itself.  This replaces
+    PMPC/main_parallel_enhanced.py:200-207's one-worker Process spawn with one process per GPU."""
+    import signal
+    import socket
+    import subprocess
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.send_signal(signal.SIGTERM)
+            for p in procs:
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        time.sleep(0.05)
+    for p in procs:
+        if rc == 0 and p.returncode:
+            rc = p.returncode
+    return rc
+
+
+def _world_from_env(args):
+    """(world, rank) of this process; spawns the ranks itself for `--gpus N > 1` outside torchrun (returns
+    None after they finished, with the exit status in the second slot)."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        return None, _spawn_ranks(args.gpus)
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (torchrun --nproc-per-node must "
+                         f"equal --gpus)\n")
+        return None, 2
+    return world, int(os.environ.get("RANK", "0"))
+
+
+def plumbing_main(args, world, rank, json_fd):
+    """--plumbing-only: the multi-rank path without a GPU or a solve.  Every rank joins a gloo process group,
+    fills its C4 block (contiguous ceil(1152 / world) instances, dart_mpc.parallel.shard_bounds) with rows that
+    are a function of the global instance index, all-gathers the blocks and checks that every rank's rows sit
+    at its offset bit for bit; timing is barrier + max over ranks, as in main()."""
+    import torch
+    import torch.distributed as dist
+    from dart_mpc.parallel import RESULT_COLS, shard_bounds
+    if world > 1:
+        dist.init_process_group("gloo")
+    Bg = 18 * 64
+    lo, hi = shard_bounds(Bg, world, rank)
+    per, n = -(-Bg // world), hi - lo
+    block = torch.zeros((per, RESULT_COLS), dtype=torch.float64)
+    idx = torch.arange(lo, hi, dtype=torch.float64)
+    for c in range(RESULT_COLS):
+        block[:n, c] = idx * (c + 1) + 0.25 * c
+    full = torch.zeros((world * per, RESULT_COLS), dtype=torch.float64)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    if world > 1:
+        dist.all_gather_into_tensor(full, block)
+        dist.barrier()
+    else:
+        full.copy_(block)
+    t = time.perf_counter() - t0
+    res = full[:Bg].numpy()
+    mine = bool(np.array_equal(res[lo:hi], block[:n].numpy()))
+    want = np.stack([np.arange(Bg) * (c + 1) + 0.25 * c for c in range(RESULT_COLS)], axis=1)
+    every = bool(np.array_equal(res, want))
+    if world > 1:
+        t, bad = _max_over_ranks([t, 0.0 if (mine and every) else 1.0], "cpu", True)
+        mine = every = bad == 0.0
+        dist.destroy_process_group()
+    if rank == 0:
+        line = {"metric": METRIC, "value": None, "unit": "solves/s", "n_gpus": world, "plumbing_only": True,
+                "pmpc_c4": {"global_batch": Bg, "per_rank": per, "n_gpus": world, "gather_s": t,
+                            "rank_blocks_consistent": mine, "gathered_equals_global_rows": every,
+                            "gather": "gloo all_gather_into_tensor on host tensors"}}
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
+    return 0
+
+
 def main():
     args = parse()
+    world, rank = _world_from_env(args)
+    if world is None:
+        sys.exit(rank)
     # stdout carries exactly one JSON line (rank 0): everything else written to fd 1 -- Python prints and the
     # libraries' own output (RCCL prints a version banner there when a communicator starts) -- goes to stderr
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
+    if args.plumbing_only:
+        sys.exit(plumbing_main(args, world, rank, json_fd))
     import torch
     import torch.distributed as dist
     import dart_mpc
     from dart_mpc.workload import pmpc_batch
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     # the CPU baselines are timed on rank 0 of a one-GPU run only (the N > 1 runs report GPU rates)
     args.no_cpu_baseline = args.no_cpu_baseline or world > 1
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -697,7 +872,7 @@ def main():
         sat_tflops = float(si.double().sum()) * F_ITER_PMPC / (ms * 1e-3) / 1e12
         saturation = {"batch": Bs, "ms_per_launch": ms, "solves_per_s": Bs / (ms * 1e-3),
                       "ok_frac": float((ss == 0).float().mean()), "iters_mean": float(si.double().mean()),
-                      "roofline": {"bound": "fp64", "achieved": sat_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                      "roofline": {"bound": "fp64-valu", "achieved": sat_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                                    "frac": sat_tflops / FP64_PEAK_TFLOPS,
                                    "note": "same algorithmic FLOP count as the headline; the chip filled with "
                                            f"{Bs} waves instead of 18"}}
@@ -787,6 +962,11 @@ def main():
     # supplementary C4 (BASELINE.json configs[3]): 1152 instances sharded over the ranks + result gather
     c4 = bench_c4(args, torch, dev, stream, dart_mpc, world, rank, host_coll, coll) if args.c4_steps > 0 else None
 
+    # supplementary: PMPC launches holding instances that need IPOPT's restoration phases
+    pmpc_resto = None
+    if rank == 0 and args.resto_steps > 0:
+        pmpc_resto = bench_pmpc_restoration(args, torch, dev, stream, dart_mpc)
+
     # supplementary PMPC line at the DART driver's horizon (N = 15)
     n15 = None
     if rank == 0 and args.n15_steps > 0:
@@ -824,7 +1004,7 @@ def main():
             pi = json.load(fh)["kernels"]["PMPC C2"]["per_instance"]
         issue = {"bound": "VALU issue of one wave per instance", "valu_busy_frac": pi["valu_busy_frac"],
                  "valu_insts_per_solve": pi["valu_insts"], "cycles_per_valu_inst": pi["cycles_per_valu_inst"],
-                 "source": os.path.relpath(sq[-1], ROOT)}
+                 "mfma_busy_frac": pi.get("mfma_busy_frac"), "source": os.path.relpath(sq[-1], ROOT)}
 
     if rank == 0:
         value = world * B * K / elapsed
@@ -858,12 +1038,14 @@ def main():
                                    "N=20, Ts=0.002, cold start, IPOPT tol 1e-8; one rank per GPU",
                        "batch_per_gpu": B, "N": N, "parallelism": f"instance-sharded x{world}",
                        **({"dist_backend": backend} if coll else {})},
-            "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
+            "roofline": {"bound": "fp64-valu", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "kernel": "pmpc_ipm_kernel", "kernel_ms": kern_ms, "issue": issue,
-                         "note": "FP64 compute roof (vector = matrix on gfx950); algorithmic FLOP = "
-                                 "sum(iters) x 6.0e4 per launch; time = one HIP event pair around the K "
-                                 "back-to-back launches of the timed loop / K; algorithmic HBM bytes = 176 per solve"},
+                         "note": "FP64 vector compute roof (78.6 TFLOP/s; the FP64 MFMA rate is the same on gfx950 "
+                                 "and no MFMA instruction is issued: issue.mfma_busy_frac, SQ_VALU_MFMA_BUSY_CYCLES); "
+                                 "algorithmic FLOP = sum(iters) x 6.0e4 per launch; time = one HIP event pair around "
+                                 "the K back-to-back launches of the timed loop / K; algorithmic HBM bytes = 176 per "
+                                 "solve"},
             "cpu_baseline": cpu_baseline,
             "north_star_ratio": ratio,
             "max_abs_u0_err_vs_exact_optimum": max_du,
@@ -873,6 +1055,7 @@ def main():
             "host_path_pcie_inclusive": host_path,
             "host_inclusive_8d": host_incl,
             "pmpc_c4": c4,
+            "pmpc_restoration": pmpc_resto,
             "pmpc_n15": n15,
             "rmpc_c3": rmpc,
             "lmpc_c5": lmpc,

@@ -35,4 +35,4 @@ def achieved_tflops(iters_sum: float, f_iter: float, seconds: float) -> float:
 
 def roofline(iters_sum: float, f_iter: float, seconds: float, **extra) -> dict:
     a = achieved_tflops(iters_sum, f_iter, seconds)
-    return dict(bound="fp64", achieved=a, peak=FP64_PEAK_TFLOPS, unit="TFLOP/s", frac=a / FP64_PEAK_TFLOPS, **extra)
+    return dict(bound="fp64-valu", achieved=a, peak=FP64_PEAK_TFLOPS, unit="TFLOP/s", frac=a / FP64_PEAK_TFLOPS, **extra)

@@ -273,10 +273,30 @@ hipError_t ensure_io(dart_mpc_handle* h) {
     return hipSuccess;
 }
 
-// IPOPT's restoration phases for PMPC launches of this handle (pmpc_resto.hip: IPOPT's path, N <= 31);
-// `mode` 1 for launches that queue the restoration kernel behind the solve, 2 for the resident server
+// IPOPT's restoration phases for PMPC launches of this handle (pmpc_resto.h: IPOPT's path, N <= 31);
+// `mode` 1 for launches whose restoration runs on the device without the host (the launcher runs it in the
+// solving wave for B <= 32, else queues pmpc_resto_kernel behind the solve), 2 for launches whose handed-over
+// instances the host sees in their completion words (it launches the kernel only then: host_resto)
 int pmpc_resto_mode(const dart_mpc_handle* h, int mode) {
     return (h->cfg.restoration && h->cfg.pmpc_path == 0 && h->cfg.N <= 31) ? mode : 0;
+}
+
+// the mode of a host-entry launch of B instances: in the solving wave (small batches), else host-driven
+int host_resto_mode(const dart_mpc_handle* h, int B) { return pmpc_resto_mode(h, B <= 32 ? 1 : 2); }
+
+// After the completion words of a host-driven (mode 2) launch: pmpc_resto_kernel for the handed-over
+// instances (status kPmNeedResto, read from mapped host memory), only if there is one -- no restoration
+// dispatch follows a batch that needs none
+int host_resto(dart_mpc_handle* h, dartmpc::PmpcArgs a, const int32_t* host_status, hipStream_t s) {
+    if (a.resto != 2) return DART_MPC_OK;
+    bool any = false;
+    for (int b = 0; b < a.B && !any; ++b)
+        any = __atomic_load_n(host_status + b, __ATOMIC_ACQUIRE) == dartmpc::kPmNeedResto;
+    if (!any) return DART_MPC_OK;
+    a.done = nullptr;
+    HIPCHK(h, dartmpc_launch_pmpc_resto(&a, s), "restoration kernel launch");
+    HIPCHK(h, hipStreamSynchronize(s), "restoration kernel");
+    return DART_MPC_OK;
 }
 
 // kernel arguments reading / writing the I/O area
@@ -329,7 +349,21 @@ int lmpc_resto_area(dart_mpc_handle* h, int B, hipStream_t s, double** out) {
     for (auto& e : h->resto)
         if (e.s == s) r = &e;
     if (!r) {
+        // at most kMaxRestoAreas streams keep an area: the least recently used one is freed (a caller that makes
+        // a new stream per call does not grow device memory without bound).  Its stream may be gone by now, so the
+        // area is freed with hipFree, which waits for the device's outstanding work first (this rare path only).
+        constexpr size_t kMaxRestoAreas = 8;
+        if (h->resto.size() >= kMaxRestoAreas) {
+            dart_mpc_handle::RestoArea old = h->resto.front();
+            h->resto.erase(h->resto.begin());
+            if (old.buf) HIPCHK(h, hipFree(old.buf), "hipFree (restoration hand-off)");
+        }
         h->resto.push_back({s, nullptr, 0});
+        r = &h->resto.back();
+    } else if (r != &h->resto.back()) {     // most recently used last
+        dart_mpc_handle::RestoArea cur = *r;
+        h->resto.erase(h->resto.begin() + (r - h->resto.data()));
+        h->resto.push_back(cur);
         r = &h->resto.back();
     }
     if (need > r->cap) {
@@ -424,7 +458,8 @@ int served_request(dart_mpc_handle* h, int B, bool ww, bool wo) {
     // relaunches it before posting.  Before that point no wave can have left (each wave's last request is no
     // older than the host's last post).
     const double since = std::chrono::duration<double>(std::chrono::steady_clock::now() - v.t_post).count();
-    if (v.running && since > 0.9 * v.idle_s - 0.002) {
+    // (the 2 ms margin is capped at half the idle timeout, so that short timeouts still serve from the grid)
+    if (v.running && since > std::fmax(0.9 * v.idle_s - 0.002, 0.5 * v.idle_s)) {
         __atomic_store_n((unsigned long long*)v.mbox, (unsigned long long)v.mbox[0] | (1ull << 56), __ATOMIC_RELEASE);
         v.running = false;
     }
@@ -459,9 +494,10 @@ int served_request(dart_mpc_handle* h, int B, bool ww, bool wo) {
 // one launch over the I/O area (no resident server), completion words as the host entry
 int bound_launch(dart_mpc_handle* h, int B, bool ww, bool wo) {
     next_seq(h);
-    dartmpc::PmpcArgs a = io_args(h, B, ww, wo);
+    dartmpc::PmpcArgs a = io_args(h, B, ww, wo, B <= 32 ? 1 : 2);
     HIPCHK(h, dartmpc_launch_pmpc(&a, h->stream), "kernel launch");
-    const int rc = wait_done(h, h->stream, h->hdone, B, a.seq);
+    int rc = wait_done(h, h->stream, h->hdone, B, a.seq);
+    if (rc == DART_MPC_OK) rc = host_resto(h, a, (const int32_t*)(h->io.hout + h->io.off_st), h->stream);
     if (rc == DART_MPC_OK) h->pending = h->stream;
     return rc;
 }
@@ -608,9 +644,10 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     a.x0 = d_x0; a.ref = d_ref; a.prm = d_prm; a.w_warm = d_ww;
     a.u0 = d_u0; a.f = d_f; a.w_out = d_wo; a.status = d_st; a.iters = d_it;
     a.done = d_done; a.seq = next_seq(h);
-    a.resto = pmpc_resto_mode(h, 1);
+    a.resto = host_resto_mode(h, B);
     HIPCHK(h, dartmpc_launch_pmpc(&a, s), "kernel launch");
-    const int rc = wait_done(h, s, h->hdone, B, a.seq);
+    int rc = wait_done(h, s, h->hdone, B, a.seq);
+    if (rc == DART_MPC_OK) rc = host_resto(h, a, S.host_of(d_st), s);
     if (rc) return rc;
     h->pending = s;
     S.take(u0, d_u0, 2 * B); S.take(f, d_f, B); S.take(w_out, d_wo, nw * B);

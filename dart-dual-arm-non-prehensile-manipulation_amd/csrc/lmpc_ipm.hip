@@ -429,24 +429,15 @@ __device__ __forceinline__ double sub_direction(const LmSub& m, const double (*s
     return dot;
 }
 
-// RESTO = false: the fast kernel of every solve; an instance whose filter line search fails parks the
-// state of that iteration's start in a.resto_buf and ends with status kLmNeedResto.  RESTO = true: the
-// same solve with IPOPT's soft restoration and restoration phases inline (their registers would spill
-// the fast kernel's loop); launched right after it, only flagged instances run: they redo the setup,
-// reload the parked state and continue from the failed iteration.
+// The solve of instance b by the calling wave; returns true when <false> handed the instance over.
 template <bool RESTO>
-__global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
+__device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     LmShared& SH = *reinterpret_cast<LmShared*>(smem);
     LmLds* S = &SH.ocp;
     LmResto* RL = reinterpret_cast<LmResto*>(smem + kLmRestoOff);
     const RiccatiSRoles RR = riccati_s_roles<LmLds>();
     STAMP_DECL
-    if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
-    const int b = blockIdx.x / a.pack;
-    if constexpr (RESTO) {
-        if (a.status[b] != kLmNeedResto) return;     // wave-uniform: the instance was solved by <false>
-    }
     const int lane = threadIdx.x;
     const int hf = lane >> 5;                  // subsystem: 0 = x [px, vx, th_y, om_y; a], 1 = y [py, vy, th_x, om_x; b]
     const int k = lane & 31;                   // shooting node
@@ -1917,6 +1908,42 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
         if (uon) wo[8 * (N + 1) + 2 * k + hf] = u;
     }
     STAMP_FLUSH32_TO(g_stamp_lm, b);
+    return !RESTO && status == kLmNeedResto;
+}
+
+// IPOPT's restoration phases for instance b in the wave that handed it over (batches of at most 32, one
+// instance per CU): lmpc_solve<true> resumes from the parked state as lmpc_ipm_kernel<true> would behind a
+// second launch.  A call, not inlined, so that the fast kernel keeps its register allocation; the launch
+// arguments are read from the kernel's argument segment (LmpcArgs is its first argument).  The policy
+// prologue's LDS (fused C5 launches) is dead by then: the restoration state takes its place, and the policy's
+// parameter vector is read back from model_params, as by the second launch.
+__device__ __noinline__ void lmpc_resto_tail(const int b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const LmpcArgs __attribute__((address_space(4))) KernArgs;
+    const LmpcArgs a = *(KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    __threadfence_block();
+    __syncthreads();            // the parked state and the policy's parameter vector (global stores) first
+    lmpc_solve<true>(a, b);
+#endif
+}
+
+// RESTO = false: the fast kernel of every solve; an instance whose filter line search fails parks the state
+// of that iteration's start in a.resto_buf and ends with status kLmNeedResto.  RESTO = true: the same solve
+// with IPOPT's soft restoration and restoration phases inline (their registers would spill the fast kernel's
+// loop); launched right after it for batches above 32, only flagged instances run: they redo the setup,
+// reload the parked state and continue from the failed iteration.  FUSE (batches of at most 32): the flagged
+// instances continue in lmpc_resto_tail in the same launch.
+template <bool RESTO, bool FUSE = false>
+__global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
+    if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
+    const int b = blockIdx.x / a.pack;
+    if constexpr (RESTO) {
+        if (a.status[b] != kLmNeedResto) return;     // wave-uniform: the instance was solved by <false>
+    }
+    const bool handed = lmpc_solve<RESTO>(a, b);
+    if constexpr (FUSE) {
+        if (__builtin_expect(handed, 0)) lmpc_resto_tail(b);
+    }
 }
 
 }  // namespace dartmpc
@@ -1943,6 +1970,9 @@ extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStre
             if (e == hipSuccess)
                 e = hipFuncSetAttribute((const void*)dartmpc::lmpc_ipm_kernel<true>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)dartmpc::lmpc_ipm_kernel<false, true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
             attr_set[dev] = true;
         }
@@ -1951,6 +1981,12 @@ extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStre
     a.pack = (a.B <= 32) ? 8 : 1;            // one XCD (and its L2) for the code of a small batch
     // the policy prologue's LDS only when the launch runs it (the opt-in above covers the maximum)
     const size_t lds_launch = a.fuse_policy ? dartmpc::kLmPolicyLdsOff + sizeof(dartmpc::PolicyLds) : sizeof(dartmpc::LmShared);
+    if (a.resto && a.pack == 8) {   // restoration in the wave that hands the instance over: one launch
+        const size_t lds_r = dartmpc::kLmRestoOff + sizeof(dartmpc::LmResto);
+        hipLaunchKernelGGL((dartmpc::lmpc_ipm_kernel<false, true>), dim3(a.B * a.pack), dim3(dartmpc::kWave),
+                           lds_launch > lds_r ? lds_launch : lds_r, stream, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(dartmpc::lmpc_ipm_kernel<false>, dim3(a.B * a.pack), dim3(dartmpc::kWave), lds_launch, stream, a);
     // IPOPT's restoration phases for the instances the first launch handed off (the others return at once)
     if (a.resto)

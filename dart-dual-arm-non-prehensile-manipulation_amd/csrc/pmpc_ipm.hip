@@ -30,6 +30,7 @@
 
 #include "pmpc_ipm.h"
 #include "pmpc_model.h"
+#include "pmpc_resto.h"
 #include "stamps.h"
 #include "wave.h"
 
@@ -157,13 +158,14 @@ __device__ __forceinline__ void mat4_scan_level(double* T) {
 //   error measures leave the z rows out and there is no second-order correction, z is rolled out from
 //   the final controls.  Same KKT point, fewer iterations, but not IPOPT's iterates.
 // the solve of instance b by the calling wave (the body of pmpc_ipm_kernel and of the resident
-// server pmpc_serve_kernel)
+// server pmpc_serve_kernel); true when the instance was handed over to IPOPT's restoration phases
+// (status kPmNeedResto, no other output)
 // branch-layout hints for the cold paths of the loop (inertia retries, the sequential fallback of the
 // scan, the least-square iteration, second-order corrections, failures): C2 +2.1 % (A/B); the one-row
 // build (N <= 15) measured 1 % slower with them and goes without
 #define PM_EXPECT(x, v) (ONEROW ? (bool)(x) : (bool)__builtin_expect((long)(bool)(x), (v)))
 template <int NAX, bool QSCAN, bool ONEROW, bool SHORT2, bool RED>
-__device__ __forceinline__ void pmpc_solve(const PmpcArgs& a, const int b) {
+__device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
     STAMP_DECL
     const int lane = threadIdx.x;
     const int k = NAX == 1 ? (lane & 31) : lane;            // shooting node of this lane
@@ -849,13 +851,13 @@ __device__ __forceinline__ void pmpc_solve(const PmpcArgs& a, const int b) {
     }
 
     // -------- outputs ---------------------------------------------------------------
-    if (PM_EXPECT(status == kPmNeedResto, 0)) {     // handed over: pmpc_resto_kernel writes the outputs
+    if (PM_EXPECT(status == kPmNeedResto, 0)) {     // handed over: pmpc_resto_solve writes the outputs
         if (lane == 0) a.status[b] = status;
         if (a.done && a.resto == 2) {
             __threadfence_system();
             if (lane == 0) __hip_atomic_store(a.done + b, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        return;
+        return true;
     }
     // objective (mpc_3d.py:44-46, :63-66), unscaled
     double fl = 0.0;
@@ -911,15 +913,39 @@ __device__ __forceinline__ void pmpc_solve(const PmpcArgs& a, const int b) {
     }
     STAMP(8);
     STAMP_FLUSH(b);
+    return false;
 }
 
-template <int NAX, bool QSCAN, bool ONEROW = false, bool SHORT2 = false, bool RED = false, bool OCC2 = false>
+// IPOPT's restoration phases for instance b in the wave that handed it over (resto mode 3, batches of at
+// most 32): a call, not inlined, so that the register kernel keeps its own register allocation; the
+// launch arguments are read from the kernel's argument segment (PmpcArgs is the kernel's first argument;
+// the resident server passes its request's sequence and w_warm / w_out flags, which its waves change).
+// The kernel takes pmpc_resto_solve's LDS (PrShared), which costs nothing at one instance per CU.
+__device__ __noinline__ void pmpc_resto_tail(const int b, const uint32_t seq, const uint32_t fl) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const PmpcArgs __attribute__((address_space(4))) KernArgs;
+    PmpcArgs a = *(KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    a.seq = seq;
+    if (!(fl & 1u)) a.w_warm = nullptr;
+    if (!(fl & 2u)) a.w_out = nullptr;
+    __syncthreads();            // the hand-off's status store (lane 0) is the only prior write
+    pmpc_resto_solve(a, b);
+#endif
+}
+
+// FUSE: resto mode 3, the handed-over instance continues in pmpc_resto_tail (no second launch)
+template <int NAX, bool QSCAN, bool ONEROW = false, bool SHORT2 = false, bool RED = false, bool OCC2 = false,
+          bool FUSE = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(OCC2 ? 2 : ((QSCAN || NAX == 2) ? 1 : 2))))
 void pmpc_ipm_kernel(PmpcArgs a) {
     // small batches: the launcher deals 8 blocks per instance and only every 8th works, so all
     // instances land on one XCD (blocks go round-robin over the 8 XCDs) and share its L2 for the code
     if (blockIdx.x % a.pack) return;
-    pmpc_solve<NAX, QSCAN, ONEROW, SHORT2, RED>(a, blockIdx.x / a.pack);
+    const int b = blockIdx.x / a.pack;
+    const bool handed = pmpc_solve<NAX, QSCAN, ONEROW, SHORT2, RED>(a, b);
+    if constexpr (FUSE) {
+        if (PM_EXPECT(handed, 0)) pmpc_resto_tail(b, a.seq, 3u);
+    }
 }
 
 // Resident solver (dart_mpc_serve_start): the waves of one launch stay on the GPU and take request
@@ -929,7 +955,9 @@ void pmpc_ipm_kernel(PmpcArgs a) {
 // wanted) | stop << 56.  Inputs and outputs live at fixed mapped addresses (the PmpcArgs pointers).  Every
 // wave leaves the loop on stop or after sv.idle_ticks of s_memrealtime (100 MHz) without a request,
 // so the grid always drains.
-template <int NAX, bool ONEROW, bool SHORT2>
+// FUSE (B_serve <= 32, resto mode 3): a handed-over instance continues in pmpc_resto_tail, so the grid stays
+// resident through a restoration
+template <int NAX, bool ONEROW, bool SHORT2, bool FUSE = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1)))
 void pmpc_serve_kernel(PmpcArgs a, PmpcServe sv) {
     if (blockIdx.x % a.pack) return;
@@ -957,7 +985,10 @@ void pmpc_serve_kernel(PmpcArgs a, PmpcServe sv) {
             r.B = (int)B; r.seq = sq;
             r.w_warm = (fl & 1u) ? a.w_warm : nullptr;
             r.w_out = (fl & 2u) ? a.w_out : nullptr;
-            pmpc_solve<NAX, true, ONEROW, SHORT2, false>(r, b);
+            const bool handed = pmpc_solve<NAX, true, ONEROW, SHORT2, false>(r, b);
+            if constexpr (FUSE) {
+                if (PM_EXPECT(handed, 0)) pmpc_resto_tail(b, sq, fl);
+            }
         }
         t_last = __builtin_amdgcn_s_memrealtime();
     }
@@ -997,7 +1028,10 @@ __global__ __launch_bounds__(kWave) void wave_selftest_kernel(double* out) {
 // SIMD, used once B exceeds the scan limit or N > 31
 template <bool RED>
 static void launch_seq(const dartmpc::PmpcArgs* a, unsigned grid, hipStream_t stream, int onerow) {
-    if (onerow)
+    if (onerow && !RED && a->resto == 3)
+        hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, true, false, false, false, true>), dim3(grid),
+                           dim3(dartmpc::kWave), 0, stream, *a);
+    else if (onerow)
         hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, true, false, RED>), dim3(grid), dim3(dartmpc::kWave), 0,
                            stream, *a);
     else if (a->N <= 31)
@@ -1015,8 +1049,12 @@ extern "C" hipError_t dartmpc_launch_pmpc_seq(const dartmpc::PmpcArgs* a, unsign
 }
 extern "C" hipError_t dartmpc_launch_pmpc_serve_onerow(const dartmpc::PmpcArgs* a, const dartmpc::PmpcServe* sv,
                                                       unsigned grid, hipStream_t stream) {
-    hipLaunchKernelGGL((dartmpc::pmpc_serve_kernel<1, true, false>), dim3(grid), dim3(dartmpc::kWave), 0, stream, *a,
-                       *sv);
+    if (a->resto == 3)
+        hipLaunchKernelGGL((dartmpc::pmpc_serve_kernel<1, true, false, true>), dim3(grid), dim3(dartmpc::kWave), 0,
+                           stream, *a, *sv);
+    else
+        hipLaunchKernelGGL((dartmpc::pmpc_serve_kernel<1, true, false>), dim3(grid), dim3(dartmpc::kWave), 0, stream,
+                           *a, *sv);
     return hipGetLastError();
 }
 #ifdef DART_STAMPS
@@ -1038,11 +1076,21 @@ extern "C" hipError_t dartmpc_launch_pmpc_serve(const dartmpc::PmpcArgs* args, c
     if (args->B <= 0 || args->N > 31) return hipErrorInvalidValue;
     dartmpc::PmpcArgs a = *args;
     a.pack = (a.B <= 32) ? 8 : 1;
+    // B_serve <= 32: the restoration phases run in the wave that handed the instance over (mode 3); larger
+    // servers hand it to the host (mode 2: dart_mpc_abi.hip served_resto)
+    if (a.resto && a.pack == 8) a.resto = 3;
+    else if (a.resto) a.resto = 2;
     const unsigned grid = (unsigned)(a.B * a.pack);
     if (a.N <= 15) return dartmpc_launch_pmpc_serve_onerow(&a, sv, grid, stream);
-    if (a.N <= 23)
+    if (a.N <= 23 && a.resto == 3)
+        hipLaunchKernelGGL((dartmpc::pmpc_serve_kernel<1, false, true, true>), dim3(grid), dim3(dartmpc::kWave), 0,
+                           stream, a, *sv);
+    else if (a.N <= 23)
         hipLaunchKernelGGL((dartmpc::pmpc_serve_kernel<1, false, true>), dim3(grid), dim3(dartmpc::kWave), 0, stream, a,
                            *sv);
+    else if (a.resto == 3)
+        hipLaunchKernelGGL((dartmpc::pmpc_serve_kernel<1, false, false, true>), dim3(grid), dim3(dartmpc::kWave), 0,
+                           stream, a, *sv);
     else
         hipLaunchKernelGGL((dartmpc::pmpc_serve_kernel<1, false, false>), dim3(grid), dim3(dartmpc::kWave), 0, stream, a,
                            *sv);
@@ -1079,19 +1127,27 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
             return 1 << 30;
         return 2 * 4 * cus;
     }();
-    const bool occ2 = !a.reduced && a.B >= occ2_min_b;
+    const bool occ2 = !a.reduced && a.B >= occ2_min_b && a.B <= qscan_max_b;
+    // batches of at most 32 (one XCD, one instance per CU): IPOPT's restoration phases run in the wave that
+    // handed the instance over (resto mode 3, pmpc_resto_tail), so no restoration launch follows the solve
+    if (a.resto == 1 && a.pack == 8 && !a.reduced && a.N <= 31) a.resto = 3;
+    const bool fuse = a.resto == 3;
     if (a.N <= 23 && occ2) {        // (N <= 15 too: the short-scan build at two waves beats the one-row build at one)
         hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
     } else if (a.N <= 15 && a.B <= qscan_max_b) {
         if (hipError_t e = dartmpc_launch_pmpc_seq(&a, grid.x, stream, 1)) return e;
     } else if (a.N <= 23 && a.B <= qscan_max_b) {
-        if (a.reduced)
+        if (fuse)
+            hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true, false, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+        else if (a.reduced)
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
         else
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
     } else if (a.N <= 31 && a.B <= qscan_max_b) {
         if (occ2)
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, false, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+        else if (fuse)
+            hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, false, false, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
         else if (a.reduced)
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
         else

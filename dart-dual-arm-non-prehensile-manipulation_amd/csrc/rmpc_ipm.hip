@@ -281,21 +281,23 @@ __device__ __forceinline__ void rm_iq3(const double* z, double vmax, bool mir, d
     c[2] = mir ? -z[3] - vmax : z[1] - vmax;
 }
 
+// The LDS of the solve (one instance per workgroup), at namespace scope so that the main solve and the
+// restoration solve of a fused launch (rmpc_resto_tail) share it: a kernel is given the blocks its code reaches
+// (70.6 KB without the restoration phases, 151.7 KB with them)
+__shared__ RmShared g_rm_sh;
+__shared__ RmResto g_rm_resto;
+
+// The solve of instance b by the calling wave.  RESTO = false: the kernel of every launch, without IPOPT's
+// restoration phases; an instance whose filter line search fails is handed over (status kRmNeedResto, no other
+// output) and the function returns true.  RESTO = true: the solve of a handed-over instance again from its
+// start, with both phases available (no state crosses the hand-off).
 template <bool RESTO>
-__global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
-    __shared__ RmShared SH;
+__device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
+    RmShared& SH = g_rm_sh;
     RmLds* S = &SH.ocp;
     RmResto* RL = nullptr;
-    if constexpr (RESTO) {
-        __shared__ RmResto RSH;
-        RL = &RSH;
-    }
+    if constexpr (RESTO) RL = &g_rm_resto;
     STAMP_DECL
-    if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
-    const int b = blockIdx.x / a.pack;
-    if constexpr (RESTO) {
-        if (a.status[b] != kRmNeedResto) return;     // wave-uniform: solved by rmpc_ipm_kernel<false>
-    }
     // lane k and its mirror lane k + 32 both own node k: the node work runs on both, the slack rows are
     // split (rm_iq3), and sums over the wave count the node terms on the node lanes only
     const int lane = threadIdx.x;
@@ -2028,9 +2030,9 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     }
 
     // ---------------- outputs -------------------------------------------------------------
-    if (!RESTO && status == kRmNeedResto) {     // handed over: rmpc_ipm_kernel<true> writes the outputs
+    if (!RESTO && status == kRmNeedResto) {     // handed over: rmpc_solve<true> writes the outputs
         if (lane == 0) a.status[b] = status;
-        return;
+        return true;
     }
     const double fval = wsum_rl(nod ? cost_val(x, u, up) : 0.0);
     if (lane == 0) {
@@ -2046,6 +2048,37 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
         if (nod && uon) { wo[4 * (N + 1) + 2 * k] = u[0]; wo[4 * (N + 1) + 2 * k + 1] = u[1]; }
     }
     STAMP_FLUSH_TO(g_stamp_rm, b);
+    return false;
+}
+
+// IPOPT's restoration phases for instance b in the wave that handed it over (batches of at most 32, one
+// instance per CU): a call, not inlined, so that rmpc_ipm_kernel<false>'s register allocation stays its own;
+// the launch arguments are read from the kernel's argument segment (RmpcArgs is its first argument).  The RLS
+// update of the launch has already been applied to theta / rls_P in place, and the restoration solve reads
+// the updated theta, as rmpc_ipm_kernel<true> does behind a separate launch.
+__device__ __noinline__ void rmpc_resto_tail(const int b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const RmpcArgs __attribute__((address_space(4))) KernArgs;
+    const RmpcArgs a = *(KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    __threadfence_block();
+    __syncthreads();            // the RLS update's theta stores (any lane) before the re-solve reads them
+    rmpc_solve<true>(a, b);
+#endif
+}
+
+// RESTO: the handed-over instances of a launch (queued behind rmpc_ipm_kernel<false> for batches above 32);
+// FUSE: rmpc_ipm_kernel<false> whose handed-over instances continue in rmpc_resto_tail (no second launch)
+template <bool RESTO, bool FUSE = false>
+__global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
+    if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
+    const int b = blockIdx.x / a.pack;
+    if constexpr (RESTO) {
+        if (a.status[b] != kRmNeedResto) return;     // wave-uniform: solved by rmpc_ipm_kernel<false>
+    }
+    const bool handed = rmpc_solve<RESTO>(a, b);
+    if constexpr (FUSE) {
+        if (__builtin_expect(handed, 0)) rmpc_resto_tail(b);
+    }
 }
 
 // Standalone batched RLS.update (np_mpc...:17-27): one p = 7 filter per workgroup, lanes as entries.
@@ -2090,6 +2123,11 @@ extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStre
     if (args->N < 1 || args->N >= dartmpc::RM_NMAXS) return hipErrorInvalidValue;
     dartmpc::RmpcArgs a = *args;
     a.pack = (a.B <= 32) ? 8 : 1;            // blocks go round-robin over the 8 XCDs: one XCD, one L2 for the code
+    if (a.resto && a.pack == 8) {   // restoration in the wave that hands the instance over: one launch
+        hipLaunchKernelGGL((dartmpc::rmpc_ipm_kernel<false, true>), dim3(a.B * a.pack), dim3(dartmpc::kWave), 0,
+                           stream, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel<false>, dim3(a.B * a.pack), dim3(dartmpc::kWave), 0, stream, a);
     if (a.resto) {      // the instances whose line search failed, with IPOPT's restoration phases
         if (hipError_t e = hipGetLastError()) return e;

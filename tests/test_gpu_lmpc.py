@@ -184,6 +184,12 @@ def test_restoration_phase_same_path_as_oracle(dm, resto):
     if resto:
         assert not np.any(np.isin(o["status"], (2, -2))) and np.sum(np.isin(g["status"], (2, -2))) <= 1
         assert np.sum(o["status"] == 0) == 718
+        # batches of 18 (C5's size): the restoration continues in the wave that handed the instance over
+        # (lmpc_resto_tail, one launch) -- the same outcome
+        s = dm.LmpcSolver(N=30, B_max=18)
+        parts = [s.solve_batch(*(a[i:i + 18] for a in args)) for i in range(0, 720, 18)]
+        s.close()
+        _same_outcome({k: np.concatenate([p_[k] for p_ in parts]) for k in ("status", "iters", "u0")}, o, min_conv=715)
     else:
         assert np.sum(g["status"] == -2) == 5 and np.array_equal(g["status"], o["status"])
 

@@ -249,6 +249,61 @@ def test_restoration_through_every_entry(dm):
     s.close()
 
 
+@pytest.mark.parametrize("N,B", [(20, 1), (20, 18), (20, 32), (15, 18), (31, 18)])
+def test_restoration_in_the_solving_wave_small_batches(dm, N, B):
+    """Batches of at most 32 run IPOPT's restoration phases in the wave that handed the instance over (resto mode
+    3: pmpc_resto_tail, one launch, no restoration dispatch behind it; the resident server's waves likewise, so
+    the grid stays resident).  Batches mixing restored and regular instances (max_soc = 0: the oracle with the
+    phases off ends the restored ones at -2) take the oracle's path on every entry: statuses equal, iterations
+    equal on the restored ones (>= 95 % overall), u0 within 1e-8 there and 1e-6 elsewhere; the device entry,
+    the bound area and the resident server return the host entry's outputs bit for bit, w included."""
+    import torch
+    import oracle_lib
+    from dart_mpc.workload import pmpc_batch
+    S, T, P = pmpc_batch(4)
+    kw = dict(N=N, Ts=0.002, tol=1e-8, max_iter=3000, nthreads=8, soc=0)
+    off = oracle_lib.solve_batch(S, T, P, want_w=False, resto=False, **kw)
+    hard, easy = np.flatnonzero(off["status"] == -2), np.flatnonzero(off["status"] == 0)
+    assert hard.size >= 3
+    sel = np.concatenate([hard[:max(1, B // 3)], easy])[:B]
+    S, T, P = S[sel], T[sel], P[sel]
+    rest = np.isin(sel, hard)
+    o = oracle_lib.solve_batch(S, T, P, want_w=True, **kw)
+    s = dm.Solver(N=N, Ts=0.002, tol=1e-8, B_max=B, max_soc=0)
+    g = s.solve_batch(S, T, P, want_w=True)
+    assert np.array_equal(g["status"], o["status"]) and np.all(o["status"] == 0)
+    assert np.array_equal(g["iters"][rest], o["iters"][rest]), (g["iters"][rest], o["iters"][rest])
+    assert np.mean(g["iters"] == o["iters"]) >= 0.95
+    du = np.abs(g["u0"] - o["u0"]).max(axis=1)
+    assert du[rest].max() <= 1e-8 and du.max() <= 1e-6, du
+    dev = torch.device("cuda:0")
+    d = {n: torch.from_numpy(np.ascontiguousarray(a)).to(dev) for n, a in (("x0", S), ("ref", T), ("prm", P))}
+    u0 = torch.empty((B, 2), dtype=torch.float64, device=dev); f = torch.empty(B, dtype=torch.float64, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev); it = torch.empty(B, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    s.solve_batch_dev(B, d["x0"].data_ptr(), d["ref"].data_ptr(), d["prm"].data_ptr(), u0.data_ptr(), f.data_ptr(),
+                      st.data_ptr(), it.data_ptr())
+    s.sync()
+    assert np.array_equal(st.cpu().numpy(), g["status"]) and np.array_equal(it.cpu().numpy(), g["iters"])
+    assert np.array_equal(u0.cpu().numpy(), g["u0"])
+    bd = s.bind()
+    bd.x0[:B] = S; bd.ref[:B] = T; bd.prm[:B] = P
+    bd.solve(B)
+    assert np.array_equal(bd.status[:B], g["status"]) and np.array_equal(bd.u0[:B], g["u0"])
+    s.serve_start(B)
+    try:
+        for _ in range(2):
+            sv = s.solve_batch(S, T, P, want_w=True)
+            for k in ("u0", "f", "status", "iters", "w"):
+                assert np.array_equal(sv[k], g[k]), k
+        sv = s.solve_batch(S, T, P)            # without w_out (the request's flags reach the restoration)
+        assert np.array_equal(sv["u0"], g["u0"]) and np.array_equal(sv["iters"], g["iters"])
+        assert s.serving()                     # a restoration no longer drains the resident grid
+    finally:
+        s.serve_stop()
+    s.close()
+
+
 def test_reduced_path_opt_in(dm):
     """pmpc_path = 1 (opt-in): the (x, y) problem without the z rows in theta / the filter and without the
     second-order correction.  Not IPOPT's iterates, but the same KKT point: at tol 1e-11 u0 within 1e-6 of

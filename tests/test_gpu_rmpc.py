@@ -248,6 +248,18 @@ def test_restoration_phase_same_path_as_oracle(dm, spread):
     for i in np.nonzero(inf)[0][:12]:
         dec, _ = rmpc_nlp.l1_stationarity(g["w"][i], D["x0"][i], D["u_prev"][i], D["theta"][i], D["prm"][i])
         assert dec <= 1e-7, (i, dec)
+    if spread == 3.0:
+        # batches of 18 (C3's size): the restoration runs in the wave that handed the instance over
+        # (rmpc_resto_tail, one launch) -- the same statuses and iterations as the oracle
+        s = dm.RmpcSolver(N=20, tol=1e-8, B_max=18)
+        parts = [s.solve_batch(*(D[k][i:i + 18] for k in ("x0", "u_prev", "theta", "Rref", "prm")))
+                 for i in range(0, 720, 18)]
+        s.close()
+        gs = {k: np.concatenate([p_[k] for p_ in parts]) for k in ("status", "iters", "u0")}
+        assert np.array_equal(gs["status"], o["status"]), np.nonzero(gs["status"] != o["status"])
+        assert np.mean(gs["iters"] == o["iters"]) >= 0.99
+        dus = np.abs(gs["u0"] - o["u0"]).max(axis=1)
+        assert np.max(dus[~inf]) <= 1e-6
 
 
 def test_restoration_off_matches_oracle_without_restoration(dm):

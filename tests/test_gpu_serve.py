@@ -45,6 +45,23 @@ def test_served_equals_launched(N):
         np.testing.assert_array_equal(again["u0"], expect[0]["u0"])
 
 
+def test_short_idle_timeout_serves_from_the_grid():
+    """An idle timeout of a few ms (the host's pre-drain margin is at most half of it): back-to-back requests
+    are answered by the resident grid -- the same results as launches -- and it is still resident after them."""
+    import dart_mpc
+    from dart_mpc.workload import pmpc_batch
+    S, T, P = pmpc_batch(1)
+    with dart_mpc.Solver(N=20, tol=1e-8, B_max=18) as s:
+        base = s.solve_batch(S, T, P)
+        s.serve_start(B_serve=18, idle_timeout=0.004)
+        for _ in range(20):
+            got = s.solve_batch(S, T, P)
+            for k in ("u0", "f", "status", "iters"):
+                np.testing.assert_array_equal(got[k], base[k])
+        assert s.serving()
+        s.serve_stop()
+
+
 def test_idle_timeout_drains_and_restarts():
     import dart_mpc
     from dart_mpc.workload import pmpc_batch
