@@ -396,6 +396,7 @@ def bench_lmpc(args, torch, dev, stream, dart_mpc):
             launch(3 + j)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    ref_out = (U0[3:].clone(), ST[3:].clone(), IT[3:].clone())
     kern_ms = _event_ms(torch, stream, lambda j: launch(3 + j), K)
     st, its = ST[3:].cpu().numpy(), IT[3:].cpu().numpy()
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -423,6 +424,31 @@ def bench_lmpc(args, torch, dev, stream, dart_mpc):
     dt_off = time.perf_counter() - t0
     st_off = ST[3:].cpu().numpy()
     s_off.close()
+    # the same K independent batches with several in flight: launch j on stream j mod S (each stream its own
+    # restoration hand-off area), so a batch held up by a restoration instance overlaps the next batches --
+    # as the reference's controllers, each with its own solver process, do not wait for one another
+    # (rlmpc2.py:494-524).  Same outputs bit for bit as one stream.
+    inflight = {}
+    for n_str in (2, 4):
+        streams = [torch.cuda.Stream(device=dev) for _ in range(n_str)]
+
+        def launch_s(i, st_):
+            s.solve_batch_dev(B, ST0[i].data_ptr(), UP[i].data_ptr(), PV[i].data_ptr(), TG[i].data_ptr(),
+                              PR.data_ptr(), U0[i].data_ptr(), FV[i].data_ptr(), ST[i].data_ptr(), IT[i].data_ptr(),
+                              stream=st_.cuda_stream)
+        for q in range(n_str):
+            launch_s(q % 3, streams[q])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for j in range(K):
+            launch_s(3 + j, streams[j % n_str])
+        torch.cuda.synchronize()
+        dt_s = time.perf_counter() - t0
+        same = bool(torch.equal(U0[3:], ref_out[0]) and torch.equal(ST[3:], ref_out[1]) and torch.equal(IT[3:], ref_out[2]))
+        inflight[f"streams_{n_str}"] = {"solves_per_s": B * K / dt_s, "ms_per_step": dt_s / K * 1e3,
+                                        "outputs_equal_to_one_stream": same}
+    inflight["note"] = ("the same K batches of 18 with 2 / 4 of them in flight on as many streams (a batch lasts as "
+                        "long as its slowest instance; in flight, the batches behind a restoration instance proceed)")
     out = {"workload": "C5 stress: LMPC batch=18, N=30, Ts=0.002, pvec~U(0.01,1.9)^34 input (SURVEY 8d; random "
                        "physical parameters, harsher than the policy's), reference IPOPT options (tol 1e-4, max_iter 50, "
                        "acceptable 1e-3 x 5), cold start, IPOPT's restoration phases on.  C5 as BASELINE.json configures "
@@ -437,6 +463,7 @@ def bench_lmpc(args, torch, dev, stream, dart_mpc):
                                "note": "the same launches, restoration=False: a failed filter line search ends the "
                                        "solve with status -2 (rounds 1-2); the difference is IPOPT's restoration tail "
                                        "(~1 % of the instances, up to max_iter 50 iterations each)"},
+           "batches_in_flight": inflight,
            "roofline": RL.roofline(float(its.sum(axis=1).mean()), RL.F_ITER["lmpc_n30"], kern_ms * 1e-3,
                                    note="sum(iters) x 3.7e5 FLOP per launch / mean kernel time"),
            "max_abs_u0_err_vs_oracle_same_options": float(np.max(np.abs(u0 - ref["u0"]))),

@@ -202,8 +202,10 @@ struct dart_mpc_handle {
         hipStream_t s;
         double* buf;
         size_t cap;
+        int xcd;                   // XCD of the stream's small batches (round robin over the streams)
     };
     std::vector<RestoArea> resto;
+    unsigned xcd_next = 0;
 };
 
 namespace {
@@ -337,14 +339,13 @@ int server_stop(dart_mpc_handle* h) {
     return e == hipSuccess ? DART_MPC_OK : fail(h, DART_MPC_EHIP, "resident server", e);
 }
 
-// settle the stream of an earlier host PMPC call that returned on its completion words (see
-// dart_mpc_handle::pending)
-// the LMPC restoration hand-off area for B instances of a launch on stream s (device memory, one area per
-// stream, stream-ordered growth: see dart_mpc_handle::resto)
-int lmpc_resto_area(dart_mpc_handle* h, int B, hipStream_t s, double** out) {
+// The per-stream state of LMPC launches on stream s: the restoration hand-off area for B instances (device
+// memory, stream-ordered growth: see dart_mpc_handle::resto) and the XCD that a small batch's working blocks
+// take -- streams get XCDs round robin, so that batches in flight on different streams of a handle run side by
+// side on different XCDs instead of queueing for the CUs of one
+int lmpc_stream_state(dart_mpc_handle* h, int B, hipStream_t s, double** out, int* xcd) {
     *out = nullptr;
-    if (!h->cfg.restoration) return DART_MPC_OK;
-    const size_t need = (size_t)B * 64 * 16;
+    const size_t need = h->cfg.restoration ? (size_t)B * 64 * 16 : 0;
     dart_mpc_handle::RestoArea* r = nullptr;
     for (auto& e : h->resto)
         if (e.s == s) r = &e;
@@ -358,7 +359,7 @@ int lmpc_resto_area(dart_mpc_handle* h, int B, hipStream_t s, double** out) {
             h->resto.erase(h->resto.begin());
             if (old.buf) HIPCHK(h, hipFree(old.buf), "hipFree (restoration hand-off)");
         }
-        h->resto.push_back({s, nullptr, 0});
+        h->resto.push_back({s, nullptr, 0, (int)(h->xcd_next++ & 7u)});
         r = &h->resto.back();
     } else if (r != &h->resto.back()) {     // most recently used last
         dart_mpc_handle::RestoArea cur = *r;
@@ -373,6 +374,7 @@ int lmpc_resto_area(dart_mpc_handle* h, int B, hipStream_t s, double** out) {
         r->cap = need;
     }
     *out = r->buf;
+    *xcd = r->xcd;
     return DART_MPC_OK;
 }
 
@@ -736,7 +738,7 @@ int dart_lmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* state, co
     a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc; a.mult_init_max = h->cfg.constr_mult_init_max;
     a.resto = h->cfg.restoration;
     a.max_ticks = (long long)(h->cfg.max_cpu_time * 1e8);     // s_memrealtime: 100 MHz
-    if (int rc = lmpc_resto_area(h, B, stream ? (hipStream_t)stream : h->stream, &a.resto_buf)) return rc;
+    if (int rc = lmpc_stream_state(h, B, stream ? (hipStream_t)stream : h->stream, &a.resto_buf, &a.xcd)) return rc;
     a.state = state; a.u_prev = u_prev; a.pvec = pvec; a.target = target; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     a.fuse_policy = 0;
@@ -884,7 +886,7 @@ int dart_lmpc_policy_solve_batch_dev(dart_mpc_handle* h, const dart_lmpc_policy_
     a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc; a.mult_init_max = h->cfg.constr_mult_init_max;
     a.resto = h->cfg.restoration;
     a.max_ticks = (long long)(h->cfg.max_cpu_time * 1e8);     // s_memrealtime: 100 MHz
-    if (int rc = lmpc_resto_area(h, B, stream ? (hipStream_t)stream : h->stream, &a.resto_buf)) return rc;
+    if (int rc = lmpc_stream_state(h, B, stream ? (hipStream_t)stream : h->stream, &a.resto_buf, &a.xcd)) return rc;
     a.state = state; a.u_prev = u_prev; a.pvec = nullptr; a.target = target; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     HIPCHK(h, dartmpc_launch_lmpc(&a, stream ? (hipStream_t)stream : h->stream), "kernel launch");

@@ -20,6 +20,7 @@ struct LmpcArgs {
     long long max_ticks;     // IPOPT max_cpu_time in ticks of the 100 MHz constant clock (s_memrealtime), 0 = off
     double* resto_buf;       // [B][64][16] hand-off of instances entering them (device workspace of the handle)
     int pack;                // blocks per instance slot (set by the launcher; 8 = one XCD for small B)
+    int xcd;                 // that XCD (0-7): the working blocks are those with blockIdx % pack == xcd % pack
     const double* state;     // [B][8]  [px, vx, py, vy, theta_x, omega_x, theta_y, omega_y]
     const double* u_prev;    // [B][2]
     const double* pvec;      // [B][34]

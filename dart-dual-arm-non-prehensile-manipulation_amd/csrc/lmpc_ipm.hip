@@ -115,7 +115,7 @@ struct LmResto {
 __device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const RiccatiSRoles& R) {
     constexpr int NXA = LmLds::NXA, NP = LmLds::NP;
     static_assert(NXA == 5 && NP == 6, "packed row 6 = [x~ (5), u, 1] names T's six columns");
-    const int h = threadIdx.x >> 5, base = h * LM_NMAXS;
+    const int h = lane_id() >> 5, base = h * LM_NMAXS;
     int zi = 0;
     while (tri(zi + 1) <= R.e) ++zi;
     const int zj = R.e - tri(zi);
@@ -438,7 +438,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
     LmResto* RL = reinterpret_cast<LmResto*>(smem + kLmRestoOff);
     const RiccatiSRoles RR = riccati_s_roles<LmLds>();
     STAMP_DECL
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int hf = lane >> 5;                  // subsystem: 0 = x [px, vx, th_y, om_y; a], 1 = y [py, vy, th_x, om_x; b]
     const int k = lane & 31;                   // shooting node
     const int sl = hf * LM_NMAXS + k;          // node slot of this lane (every lane owns one)
@@ -1914,17 +1914,14 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
 // IPOPT's restoration phases for instance b in the wave that handed it over (batches of at most 32, one
 // instance per CU): lmpc_solve<true> resumes from the parked state as lmpc_ipm_kernel<true> would behind a
 // second launch.  A call, not inlined, so that the fast kernel keeps its register allocation; the launch
-// arguments are read from the kernel's argument segment (LmpcArgs is its first argument).  The policy
+// arguments are read from the kernel's argument segment (LmpcArgs is its first argument, kernarg_addr).  The policy
 // prologue's LDS (fused C5 launches) is dead by then: the restoration state takes its place, and the policy's
 // parameter vector is read back from model_params, as by the second launch.
-__device__ __noinline__ void lmpc_resto_tail(const int b) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    typedef const LmpcArgs __attribute__((address_space(4))) KernArgs;
-    const LmpcArgs a = *(KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+__device__ __noinline__ void lmpc_resto_tail(const int b, const unsigned long long kargs) {
+    const LmpcArgs a = kernarg_load<LmpcArgs>(kargs);
     __threadfence_block();
     __syncthreads();            // the parked state and the policy's parameter vector (global stores) first
     lmpc_solve<true>(a, b);
-#endif
 }
 
 // RESTO = false: the fast kernel of every solve; an instance whose filter line search fails parks the state
@@ -1935,14 +1932,15 @@ __device__ __noinline__ void lmpc_resto_tail(const int b) {
 // instances continue in lmpc_resto_tail in the same launch.
 template <bool RESTO, bool FUSE = false>
 __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
-    if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
+    // small batches packed onto one XCD (launcher; blocks go round robin over the 8 XCDs)
+    if (blockIdx.x % a.pack != (unsigned)(a.xcd % a.pack)) return;
     const int b = blockIdx.x / a.pack;
     if constexpr (RESTO) {
         if (a.status[b] != kLmNeedResto) return;     // wave-uniform: the instance was solved by <false>
     }
     const bool handed = lmpc_solve<RESTO>(a, b);
     if constexpr (FUSE) {
-        if (__builtin_expect(handed, 0)) lmpc_resto_tail(b);
+        if (__builtin_expect(handed, 0)) lmpc_resto_tail(b, kernarg_addr());
     }
 }
 
@@ -1981,7 +1979,7 @@ extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStre
     a.pack = (a.B <= 32) ? 8 : 1;            // one XCD (and its L2) for the code of a small batch
     // the policy prologue's LDS only when the launch runs it (the opt-in above covers the maximum)
     const size_t lds_launch = a.fuse_policy ? dartmpc::kLmPolicyLdsOff + sizeof(dartmpc::PolicyLds) : sizeof(dartmpc::LmShared);
-    if (a.resto && a.pack == 8) {   // restoration in the wave that hands the instance over: one launch
+    if (a.resto && a.pack == 8 && dartmpc::resto_fuse_enabled()) {   // restoration in the solving wave: one launch
         const size_t lds_r = dartmpc::kLmRestoOff + sizeof(dartmpc::LmResto);
         hipLaunchKernelGGL((dartmpc::lmpc_ipm_kernel<false, true>), dim3(a.B * a.pack), dim3(dartmpc::kWave),
                            lds_launch > lds_r ? lds_launch : lds_r, stream, a);

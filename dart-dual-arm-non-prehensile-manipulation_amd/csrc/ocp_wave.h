@@ -72,7 +72,7 @@ __device__ __forceinline__ void compose_pairs(FA& F, F2A& F2, int N) {
     // task = RPT rows of one pair: RPT trades rounds over the wave against work per lane
     constexpr int NB = (NXA + RPT - 1) / RPT;
     const int np2 = N >> 1, per = np2 * NB;
-    for (int t = threadIdx.x; t < H * per; t += 64) {
+    for (int t = lane_id(); t < H * per; t += 64) {
         const int h = H == 1 ? 0 : t / per, rem = t - h * per, q = rem / NB, r0 = (rem - q * NB) * RPT;
         const int s0 = h * SLOTS + 2 * q;
         double b[NXA][NXA + 1];
@@ -146,7 +146,7 @@ __device__ __forceinline__ AugRoles aug_roles() {
     constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, NX = NXA - 2;
     static_assert(ND == NXA + 3 && NP <= 8 && L::NC == 8, "two inputs, value dimension <= 8, M columns padded to 8");
     AugRoles R;
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int g = lane >> 3, s = lane & 7;
     const int ge = g < NP ? g : NP - 1, se = s < NP ? s : NP - 1;          // clamped (idle lanes stay finite)
     R.cg = ge < NX ? ge : ge + 2; R.cs = se < NX ? se : se + 2;           // z columns of the groups
@@ -271,7 +271,7 @@ struct AugSoftLds {
 template <class L, int NS>
 __device__ __forceinline__ void aug_soft_init(AugSoftLds<L, NS>* RS) {
     constexpr int NXA = L::NXA;
-    for (int e = threadIdx.x; e < L::NTP; e += 64) {
+    for (int e = lane_id(); e < L::NTP; e += 64) {
         int i = 0;
         while (tri(i + 1) <= e) ++i;
         const int j = e - tri(i);
@@ -291,11 +291,11 @@ __device__ __forceinline__ void aug_soft_init(AugSoftLds<L, NS>* RS) {
 template <class L, int NS>
 __device__ __forceinline__ void aug_soften(L* S, AugSoftLds<L, NS>* RS, int j, bool surrogate, bool& ok) {
     constexpr int NXA = L::NXA, NP = L::NP, NV = tri(NP);
-    const int e0 = (int)threadIdx.x < NV ? (int)threadIdx.x : NV - 1;
+    const int e0 = lane_id() < NV ? lane_id() : NV - 1;
     int pv = 0;
     while (tri(pv + 1) <= e0) ++pv;
     const int qv = e0 - tri(pv);
-    const bool act = (int)threadIdx.x < NV;
+    const bool act = lane_id() < NV;
     const bool ps = pv < NS, qs = qv < NS;          // (qv <= pv: qs whenever ps)
     const double* Gn = S->G[j];
     const double q00 = Gn[hp(NXA, NXA)], q01 = Gn[hp(NXA + 1, NXA)], q11 = Gn[hp(NXA + 1, NXA + 1)];
@@ -416,7 +416,7 @@ template <class L>
 __device__ __forceinline__ void gen_node_step(L* S, int k, const double* Gn, double* U, bool& ok) {
     constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, NC = L::NC;
     static_assert(ND * NP <= 64 && NP <= NC, "one lane per (stage column, value index)");
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const double* Mk = &S->M[k][0][0];
     const double q00 = Gn[hp(NXA, NXA)], q01 = Gn[hp(NXA + 1, NXA)], q11 = Gn[hp(NXA + 1, NXA + 1)];
     const double det = fma(q00, q11, -q01 * q01);
@@ -482,7 +482,7 @@ template <> struct IsNoPost<NoPost> { static constexpr bool value = true; };
 template <class L, class Post = NoPost>
 __device__ void closed_loop(L* S, int N, Post post = Post()) {
     constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, RH = (NXA + 1) / 2;
-    const int k = threadIdx.x & 31, rb = threadIdx.x >= 32 ? RH : 0;
+    const int k = lane_id() & 31, rb = lane_id() >= 32 ? RH : 0;
     if (k < N) {
         // LDS reads grouped ahead of the writes (the compiler cannot prove F, KK and M disjoint and
         // would otherwise wait out each read before the next write)
@@ -516,7 +516,7 @@ __device__ void closed_loop(L* S, int N, Post post = Post()) {
     }
     __syncthreads();
     if constexpr (!IsNoPost<Post>::value) {
-        if (k < N && threadIdx.x < 32) post(k);
+        if (k < N && lane_id() < 32) post(k);
         __syncthreads();
     }
     compose_pairs<1, L::NMAXS, NXA, 1>(S->F, S->F2, N);   // NXA floor(N / 2) tasks: one round over the wave for N <= 21 (RMPC), two beyond
@@ -606,7 +606,7 @@ __device__ __forceinline__ void pair_chain(const F2A& F2, int p0, int np2, int r
 template <class L, bool PREFETCH = true>
 __device__ void forward_sweep(L* S, int N, int node, double* dxo) {
     constexpr int NXA = L::NXA;
-    const int lr = threadIdx.x & 15;
+    const int lr = lane_id() & 15;
     const int r = lr < NXA ? lr : 0;
     double d[NXA];
 #pragma unroll
@@ -684,7 +684,7 @@ struct RiccatiSRoles {
 template <class L>
 __device__ RiccatiSRoles riccati_s_roles() {
     RiccatiSRoles r{};
-    const int e0 = threadIdx.x & 31;
+    const int e0 = lane_id() & 31;
     r.on = e0 < L::NT;
     r.e = r.on ? e0 : 0;
     int i = 0;
@@ -739,7 +739,7 @@ __device__ __forceinline__ void s_node_step(L* S, int sk, const RiccatiSRoles& R
 template <class L>
 __device__ bool riccati_s_sweep(L* S, int N, const RiccatiSRoles& R) {
     constexpr int NXA = L::NXA;
-    const int base = (threadIdx.x >> 5) * L::NMAXS;
+    const int base = (lane_id() >> 5) * L::NMAXS;
     bool ok = true;
     int k = N - 1;
     for (; k >= 1; k -= 2) {
@@ -758,7 +758,7 @@ __device__ bool riccati_s_sweep(L* S, int N, const RiccatiSRoles& R) {
 template <class L, class Post = NoPost>
 __device__ void closed_loop_s(L* S, int N, Post post = Post()) {
     constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND;
-    const int k = threadIdx.x & 31, sl = (threadIdx.x >> 5) * L::NMAXS + k;
+    const int k = lane_id() & 31, sl = (lane_id() >> 5) * L::NMAXS + k;
     if (k < N) {
         // every LDS read before the first write (the compiler cannot prove F, KK and M disjoint and
         // would otherwise wait out each read before the next write)
@@ -814,8 +814,8 @@ __device__ __forceinline__ void node_multiplier_s(const L* S, int sl, const doub
 template <class L, bool PREFETCH = true>
 __device__ void forward_sweep_s(L* S, int N, int node, double* dxo) {
     constexpr int NXA = L::NXA;
-    const int h = threadIdx.x >> 5, base = h * L::NMAXS, pbase = h * (L::NMAXS / 2);
-    const int lr = threadIdx.x & 15;
+    const int h = lane_id() >> 5, base = h * L::NMAXS, pbase = h * (L::NMAXS / 2);
+    const int lr = lane_id() & 15;
     const int r = lr < NXA ? lr : 0;
     double d[NXA];
 #pragma unroll

@@ -918,19 +918,17 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
 
 // IPOPT's restoration phases for instance b in the wave that handed it over (resto mode 3, batches of at
 // most 32): a call, not inlined, so that the register kernel keeps its own register allocation; the
-// launch arguments are read from the kernel's argument segment (PmpcArgs is the kernel's first argument;
-// the resident server passes its request's sequence and w_warm / w_out flags, which its waves change).
-// The kernel takes pmpc_resto_solve's LDS (PrShared), which costs nothing at one instance per CU.
-__device__ __noinline__ void pmpc_resto_tail(const int b, const uint32_t seq, const uint32_t fl) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    typedef const PmpcArgs __attribute__((address_space(4))) KernArgs;
-    PmpcArgs a = *(KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+// launch arguments are read from the kernel's argument segment (PmpcArgs is the kernel's first argument,
+// kernarg_addr; the resident server passes its request's sequence and w_warm / w_out flags, which its waves
+// change).  The kernel takes pmpc_resto_solve's LDS (PrShared), which costs nothing at one instance per CU.
+__device__ __noinline__ void pmpc_resto_tail(const int b, const uint32_t seq, const uint32_t fl,
+                                             const unsigned long long kargs) {
+    PmpcArgs a = kernarg_load<PmpcArgs>(kargs);
     a.seq = seq;
     if (!(fl & 1u)) a.w_warm = nullptr;
     if (!(fl & 2u)) a.w_out = nullptr;
     __syncthreads();            // the hand-off's status store (lane 0) is the only prior write
     pmpc_resto_solve(a, b);
-#endif
 }
 
 // FUSE: resto mode 3, the handed-over instance continues in pmpc_resto_tail (no second launch)
@@ -944,7 +942,7 @@ void pmpc_ipm_kernel(PmpcArgs a) {
     const int b = blockIdx.x / a.pack;
     const bool handed = pmpc_solve<NAX, QSCAN, ONEROW, SHORT2, RED>(a, b);
     if constexpr (FUSE) {
-        if (PM_EXPECT(handed, 0)) pmpc_resto_tail(b, a.seq, 3u);
+        if (PM_EXPECT(handed, 0)) pmpc_resto_tail(b, a.seq, 3u, kernarg_addr());
     }
 }
 
@@ -987,7 +985,7 @@ void pmpc_serve_kernel(PmpcArgs a, PmpcServe sv) {
             r.w_out = (fl & 2u) ? a.w_out : nullptr;
             const bool handed = pmpc_solve<NAX, true, ONEROW, SHORT2, false>(r, b);
             if constexpr (FUSE) {
-                if (PM_EXPECT(handed, 0)) pmpc_resto_tail(b, sq, fl);
+                if (PM_EXPECT(handed, 0)) pmpc_resto_tail(b, sq, fl, kernarg_addr());
             }
         }
         t_last = __builtin_amdgcn_s_memrealtime();
@@ -1078,7 +1076,7 @@ extern "C" hipError_t dartmpc_launch_pmpc_serve(const dartmpc::PmpcArgs* args, c
     a.pack = (a.B <= 32) ? 8 : 1;
     // B_serve <= 32: the restoration phases run in the wave that handed the instance over (mode 3); larger
     // servers hand it to the host (mode 2: dart_mpc_abi.hip served_resto)
-    if (a.resto && a.pack == 8) a.resto = 3;
+    if (a.resto && a.pack == 8 && dartmpc::resto_fuse_enabled()) a.resto = 3;
     else if (a.resto) a.resto = 2;
     const unsigned grid = (unsigned)(a.B * a.pack);
     if (a.N <= 15) return dartmpc_launch_pmpc_serve_onerow(&a, sv, grid, stream);
@@ -1130,7 +1128,7 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
     const bool occ2 = !a.reduced && a.B >= occ2_min_b && a.B <= qscan_max_b;
     // batches of at most 32 (one XCD, one instance per CU): IPOPT's restoration phases run in the wave that
     // handed the instance over (resto mode 3, pmpc_resto_tail), so no restoration launch follows the solve
-    if (a.resto == 1 && a.pack == 8 && !a.reduced && a.N <= 31) a.resto = 3;
+    if (a.resto == 1 && a.pack == 8 && !a.reduced && a.N <= 31 && dartmpc::resto_fuse_enabled()) a.resto = 3;
     const bool fuse = a.resto == 3;
     if (a.N <= 23 && occ2) {        // (N <= 15 too: the short-scan build at two waves beats the one-row build at one)
         hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);

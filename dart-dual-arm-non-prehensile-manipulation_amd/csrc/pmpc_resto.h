@@ -89,14 +89,14 @@ struct PrFilter {
     __device__ bool hit(double t, double p) const {
         bool h = false;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h = h || ((int)threadIdx.x + 64 * r < n && t >= th[r] && p >= ph[r]);
+        for (int r = 0; r < 4; ++r) h = h || (lane_id() + 64 * r < n && t >= th[r] && p >= ph[r]);
         return wany(h);
     }
     __device__ void add(double t, double p) {
         if (n >= 256) return;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            if ((int)threadIdx.x + 64 * r == n) { th[r] = t; ph[r] = p; }
+            if (lane_id() + 64 * r == n) { th[r] = t; ph[r] = p; }
         ++n;
     }
 };
@@ -107,7 +107,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
     PrLds* S = &SH.ocp;
     PrSoft* SR = &SH.soft;
     constexpr int NC = PrLds::NC;
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int k = lane & 31;
     const bool nod = lane < 32;
     const int N = a.N;

@@ -300,7 +300,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
     STAMP_DECL
     // lane k and its mirror lane k + 32 both own node k: the node work runs on both, the slack rows are
     // split (rm_iq3), and sums over the wave count the node terms on the node lanes only
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int k = lane & 31;
     const bool mir = lane >= 32, nod = !mir;
     const int N = a.N;
@@ -2053,17 +2053,14 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
 
 // IPOPT's restoration phases for instance b in the wave that handed it over (batches of at most 32, one
 // instance per CU): a call, not inlined, so that rmpc_ipm_kernel<false>'s register allocation stays its own;
-// the launch arguments are read from the kernel's argument segment (RmpcArgs is its first argument).  The RLS
+// the launch arguments are read from the kernel's argument segment (RmpcArgs is its first argument, kernarg_addr).  The RLS
 // update of the launch has already been applied to theta / rls_P in place, and the restoration solve reads
 // the updated theta, as rmpc_ipm_kernel<true> does behind a separate launch.
-__device__ __noinline__ void rmpc_resto_tail(const int b) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    typedef const RmpcArgs __attribute__((address_space(4))) KernArgs;
-    const RmpcArgs a = *(KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+__device__ __noinline__ void rmpc_resto_tail(const int b, const unsigned long long kargs) {
+    const RmpcArgs a = kernarg_load<RmpcArgs>(kargs);
     __threadfence_block();
     __syncthreads();            // the RLS update's theta stores (any lane) before the re-solve reads them
     rmpc_solve<true>(a, b);
-#endif
 }
 
 // RESTO: the handed-over instances of a launch (queued behind rmpc_ipm_kernel<false> for batches above 32);
@@ -2077,7 +2074,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     }
     const bool handed = rmpc_solve<RESTO>(a, b);
     if constexpr (FUSE) {
-        if (__builtin_expect(handed, 0)) rmpc_resto_tail(b);
+        if (__builtin_expect(handed, 0)) rmpc_resto_tail(b, kernarg_addr());
     }
 }
 
@@ -2085,7 +2082,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
 __global__ __launch_bounds__(kWave) void rls_update_kernel(int B, double* theta, double* P, const double* phi,
                                                           const double* y, double lam) {
     __shared__ double Pphi[7], phiP[7], ph[7], th[7];
-    const int b = blockIdx.x, l = threadIdx.x;
+    const int b = blockIdx.x, l = lane_id();
     double* Pb = P + 49 * b;
     if (l < 7) { ph[l] = phi[7 * b + l]; th[l] = theta[7 * b + l]; }
     __syncthreads();
@@ -2123,7 +2120,7 @@ extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStre
     if (args->N < 1 || args->N >= dartmpc::RM_NMAXS) return hipErrorInvalidValue;
     dartmpc::RmpcArgs a = *args;
     a.pack = (a.B <= 32) ? 8 : 1;            // blocks go round-robin over the 8 XCDs: one XCD, one L2 for the code
-    if (a.resto && a.pack == 8) {   // restoration in the wave that hands the instance over: one launch
+    if (a.resto && a.pack == 8 && dartmpc::resto_fuse_enabled()) {   // restoration in the solving wave: one launch
         hipLaunchKernelGGL((dartmpc::rmpc_ipm_kernel<false, true>), dim3(a.B * a.pack), dim3(dartmpc::kWave), 0,
                            stream, a);
         return hipGetLastError();

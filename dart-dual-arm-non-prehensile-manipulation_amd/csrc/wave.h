@@ -1,9 +1,49 @@
 // wave.h -- wave64 primitives for gfx950 shared by the solver kernels: DPP lane shifts,
 // DPP row reductions, fast reciprocal, cheap log2 and small-angle sin/cos.
 #pragma once
+#include <stdlib.h>
 #include <hip/hip_runtime.h>
 
 namespace dartmpc {
+
+// The lane of the calling thread in its wave64 (= threadIdx.x in the one-wave workgroups of these kernels).
+// Code that the restoration tails call uses this instead of threadIdx.x: a non-inlined callee that reads a
+// work-item id makes its kernel keep the packed ids live in a VGPR (v31) from entry to the call -- one more live
+// register in kernels that sit at the register limit (measured: RMPC C3 -7 %).
+__device__ __forceinline__ int lane_id() {
+    return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// The launch arguments of the calling kernel for a non-inlined callee (the restoration tails): the kernel passes
+// the address of its argument segment (its first argument sits at offset 0) and the callee loads the struct
+// from it with scalar loads.  (__builtin_amdgcn_kernarg_segment_ptr is only valid in the kernel itself: in a
+// callee it reads 0.)
+__device__ __forceinline__ unsigned long long kernarg_addr() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+    return 0;
+#endif
+}
+// host: the fused restoration (restoration in the solving wave for B <= 32) unless DART_RESTO_FUSE=0 (A/B
+// experiments: the round-4 form, a queued restoration kernel behind every launch)
+inline bool resto_fuse_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DART_RESTO_FUSE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+template <class T>
+__device__ __forceinline__ T kernarg_load(unsigned long long addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const T __attribute__((address_space(4))) KernT;
+    return *(KernT*)addr;
+#else
+    (void)addr;
+    return T{};
+#endif
+}
 
 constexpr int kWave = 64;
 

@@ -284,6 +284,24 @@ def l1_model(w, x0, up, th, prm, N=20, Ts=0.002):
             g.append(X[k, j]); lb.append(-prm[8]); ub.append(prm[8]); Jg.append(row)
     return np.concatenate(c), np.vstack(Jc), np.array(g), np.array(lb), np.array(ub), np.array(Jg)
 
+def l1_violation(w, x0, up, th, prm, N=20, Ts=0.002, relax=1e-8):
+    """l1 violation V(w) of the reference NLP's rows (np_mpc...:103-127): |x0 pin| + |RK4 defects| (equalities) and
+    the du rows / velocity caps outside their bounds (relaxed by IPOPT's bound_relax_factor); the U box is kept by
+    both solvers.  IPOPT's restoration phase (MinC_1NrmRestorationPhase) minimises this quantity."""
+    nX = 4 * (N + 1)
+    X = w[:nX].reshape(N + 1, 4)
+    U = w[nX:].reshape(N, 2)
+    v = np.abs(X[0] - x0).sum()
+    for k in range(N):
+        v += np.abs(X[k + 1] - rk4(X[k], U[k], th, prm[9], Ts)).sum()
+    lo, hi = prm[6] - relax * max(1, abs(prm[6])), prm[7] + relax * max(1, abs(prm[7]))
+    du = np.diff(np.vstack([np.asarray(up)[None], U]), axis=0)
+    v += np.maximum(0, du - hi).sum() + np.maximum(0, lo - du).sum()
+    vm = prm[8] + relax * max(1, prm[8])
+    v += np.maximum(0, np.abs(X[:N][:, [1, 3]]) - vm).sum()
+    return float(v)
+
+
 def l1_stationarity(w, x0, up, th, prm, N=20, delta=1e-4, relax=1e-8):
     """decrease of the linearised l1 infeasibility within |d|_inf <= delta, U box kept; and the value at d = 0"""
     c, Jc, g, lb, ub, Jg = l1_model(w, x0, up, th, prm, N)

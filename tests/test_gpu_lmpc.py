@@ -232,3 +232,36 @@ def test_max_cpu_time(dm):
     capped = g["status"] == -4
     assert capped.sum() >= 1 and np.all(g["iters"][capped] <= full["iters"][capped])
     assert np.all((g["status"] == full["status"]) | capped)
+
+
+def test_many_caller_streams(dm):
+    """Launches on many caller streams (the _dev entry): each stream gets its own restoration hand-off area and an
+    XCD for its small batches (round robin); at most 8 streams keep an area (least recently used evicted).  Twelve
+    streams in turn, then the first again: every launch returns the host entry's outputs bit for bit, restored
+    instances included."""
+    import torch
+    from dart_mpc.workload import lmpc_batch
+    D = lmpc_batch(40, seed0=0)
+    args = (D["state"], D["u_prev"], D["pvec"], D["target"])
+    o = oracle_lib.lmpc_solve_batch(*args, N=30, nthreads=8, want_w=False, resto=False)
+    hard = np.flatnonzero(o["status"] == -2)
+    sel = np.concatenate([hard, np.flatnonzero(o["status"] == 0)])[:18]
+    sub = tuple(a[sel] for a in args)
+    s = dm.LmpcSolver(N=30, B_max=18)
+    ref = s.solve_batch(*sub)
+    assert np.sum(ref["iters"] > 25) >= 1                  # a restored instance in the batch
+    dev = torch.device("cuda:0")
+    from dart_mpc._lib import LMPC_PRM_DEFAULT
+    t = [torch.tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev) for a in sub]
+    PR = torch.tensor(np.tile(LMPC_PRM_DEFAULT, (18, 1)), dtype=torch.float64, device=dev)
+    for rep, n in enumerate(list(range(12)) + [0]):
+        st = torch.cuda.Stream(device=dev)
+        U0 = torch.empty((18, 2), dtype=torch.float64, device=dev); FV = torch.empty(18, dtype=torch.float64, device=dev)
+        ST = torch.empty(18, dtype=torch.int32, device=dev); IT = torch.empty(18, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        s.solve_batch_dev(18, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), PR.data_ptr(),
+                          U0.data_ptr(), FV.data_ptr(), ST.data_ptr(), IT.data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(ST.cpu().numpy(), ref["status"]) and np.array_equal(IT.cpu().numpy(), ref["iters"]), rep
+        assert np.array_equal(U0.cpu().numpy(), ref["u0"]), rep
+    s.close()

@@ -224,13 +224,17 @@ def test_restoration_phase_same_path_as_oracle(dm, spread):
     restoration and restoration phases (rmpc_ipm_kernel<true>, the resume launch) take the oracle's path:
     statuses equal everywhere (2 = Infeasible_Problem_Detected where the restoration converges, 0 where it
     returns to a solvable problem), iteration counts equal on >= 99 %.  Controls: |du0| <= 1e-6 where the problem
-    is solved (status 0).  At a point of local infeasibility (status 2) tol 1e-8 leaves the iterate loose --
-    the oracle's own u0 at tol 1e-8 and at tol 1e-10 differ by 2.4e-4 (median) to 6e-2 (max) on these batches --
-    so there the bounds are 99 % of |du0| <= 5e-5 and max |du0| <= 1e-3 (measured on 2x / 3x / 6x: medians
-    ~1e-13, 99 % <= 1e-5, max 1.5e-4), and the kernel's point passes the
-    solver-independent local-infeasibility certificate (rmpc_nlp.l1_stationarity: no decrease of the linearised
-    l1 violation within |d| <= 1e-4).  The returned iterate is the next control step's warm start
-    (np_mpc...:214-217)."""
+    is solved (status 0).
+    At a point of local infeasibility (status 2) the NLP does not determine the iterate (tools/rmpc_status2_analysis.py,
+    profiles/r05/rmpc_status2.txt): the restoration phase minimises the l1 violation V of the reference NLP's rows,
+    whose minimisers form a face -- V is flat to ~1e-10 on the segment between the kernel's and the oracle's
+    points -- and only its proximity term (weight sqrt(mu)) picks the point; the oracle's own tol-1e-8 point moves
+    1e-3..4e-2 in u0 when re-solved at tol 1e-10.  So on EVERY status-2 instance the kernel's point must pass the
+    solver-independent local-infeasibility certificate (rmpc_nlp.l1_stationarity: no decrease of the linearised l1
+    violation within |d| <= 1e-4, <= 2e-7) and reach the oracle's violation (V within 1e-5 relative; measured max
+    3.9e-6); where the two u0 differ by more than 1e-6 they must lie on one face (V between them flat to 1e-7
+    relative); and |du0| <= 5e-5 on 99 %, max <= 2e-4 (measured on these batches: 99 % <= 2e-5, max 1.54e-4).
+    The returned iterate is the next control step's warm start (np_mpc...:214-217)."""
     from dart_mpc.workload import rmpc_batch
     D = _spread(rmpc_batch(40, seed0=0), spread)
     s = dm.RmpcSolver(N=20, tol=1e-8, B_max=720)
@@ -244,10 +248,17 @@ def test_restoration_phase_same_path_as_oracle(dm, spread):
     assert np.mean(g["iters"] == o["iters"]) >= 0.99, np.nonzero(g["iters"] != o["iters"])
     du = np.abs(g["u0"] - o["u0"]).max(axis=1)
     assert np.max(du[~inf]) <= 1e-6
-    assert np.percentile(du[inf], 99) <= 5e-5 and np.max(du[inf]) <= 1e-3, np.percentile(du[inf], [50, 99, 100])
-    for i in np.nonzero(inf)[0][:12]:
-        dec, _ = rmpc_nlp.l1_stationarity(g["w"][i], D["x0"][i], D["u_prev"][i], D["theta"][i], D["prm"][i])
-        assert dec <= 1e-7, (i, dec)
+    assert np.percentile(du[inf], 99) <= 5e-5 and np.max(du[inf]) <= 2e-4, np.percentile(du[inf], [50, 99, 100])
+    for i in np.nonzero(inf)[0]:
+        a = (D["x0"][i], D["u_prev"][i], D["theta"][i], D["prm"][i])
+        dec, Vk = rmpc_nlp.l1_stationarity(g["w"][i], *a)
+        assert dec <= 2e-7, (i, dec)
+        Vo = rmpc_nlp.l1_violation(o["w"][i], *a)
+        Vk = rmpc_nlp.l1_violation(g["w"][i], *a)
+        assert abs(Vk - Vo) <= 1e-5 * Vo, (i, Vk, Vo)
+        if du[i] > 1e-6:
+            seg = [rmpc_nlp.l1_violation(o["w"][i] + t * (g["w"][i] - o["w"][i]), *a) for t in (0.25, 0.5, 0.75)]
+            assert max(abs(v - Vo) for v in seg) <= 1e-7 * Vo, (i, seg, Vo)
     if spread == 3.0:
         # batches of 18 (C3's size): the restoration runs in the wave that handed the instance over
         # (rmpc_resto_tail, one launch) -- the same statuses and iterations as the oracle

@@ -28,20 +28,7 @@ N = 20
 NX = 4 * (N + 1)
 
 
-def violation(w, x0, up, th, prm, relax=1e-8):
-    """l1 violation V(w) of the reference NLP's rows (equalities |c|, inequalities outside their relaxed bounds)"""
-    X = w[:NX].reshape(N + 1, 4)
-    U = w[NX:].reshape(N, 2)
-    v = np.abs(X[0] - x0).sum()
-    for k in range(N):
-        v += np.abs(X[k + 1] - rmpc_nlp.rk4(X[k], U[k], th, prm[9], 0.002)).sum()
-    lo, hi = prm[6] - relax * max(1, abs(prm[6])), prm[7] + relax * max(1, abs(prm[7]))
-    du = np.diff(np.vstack([up[None], U]), axis=0)
-    v += np.maximum(0, du - hi).sum() + np.maximum(0, lo - du).sum()
-    vm = prm[8] + relax * max(1, prm[8])
-    vel = X[:N][:, [1, 3]]
-    v += np.maximum(0, np.abs(vel) - vm).sum()
-    return v
+violation = rmpc_nlp.l1_violation
 
 
 def main():
