@@ -301,6 +301,16 @@ int host_resto(dart_mpc_handle* h, dartmpc::PmpcArgs a, const int32_t* host_stat
     return DART_MPC_OK;
 }
 
+int stream_state(dart_mpc_handle* h, int B, hipStream_t s, double** out, int* xcd);
+
+// the restoration hand-off area of a PMPC launch of B instances on stream s (when the launch can hand over)
+int pmpc_resto_buf(dart_mpc_handle* h, int B, hipStream_t s, dartmpc::PmpcArgs& a) {
+    a.resto_buf = nullptr;
+    if (!a.resto) return DART_MPC_OK;
+    int xcd = 0;
+    return stream_state(h, B, s, &a.resto_buf, &xcd);
+}
+
 // kernel arguments reading / writing the I/O area
 dartmpc::PmpcArgs io_args(dart_mpc_handle* h, int B, bool ww, bool wo, int resto_mode = 1) {
     const auto& o = h->io;
@@ -313,6 +323,7 @@ dartmpc::PmpcArgs io_args(dart_mpc_handle* h, int B, bool ww, bool wo, int resto
     a.status = (int32_t*)(o.dout + o.off_st); a.iters = (int32_t*)(o.dout + o.off_it);
     a.done = h->ddone; a.seq = h->seq;
     a.resto = pmpc_resto_mode(h, resto_mode);
+    a.resto_buf = nullptr;        // (the caller sets it for its stream: pmpc_resto_buf)
     return a;
 }
 
@@ -321,6 +332,7 @@ hipError_t server_launch(dart_mpc_handle* h, uint32_t seen) {
     auto& v = h->srv;
     dartmpc::PmpcArgs a = io_args(h, v.B, true, true, 2);  // the flags of each request select w_warm / w_out
     a.seq = seen;
+    if (pmpc_resto_buf(h, v.B, v.stream, a) != DART_MPC_OK) return hipErrorOutOfMemory;
     dartmpc::PmpcServe sv{v.dmbox, v.idle_ticks};
     const hipError_t e = dartmpc_launch_pmpc_serve(&a, &sv, v.stream);
     v.running = e == hipSuccess;
@@ -339,13 +351,15 @@ int server_stop(dart_mpc_handle* h) {
     return e == hipSuccess ? DART_MPC_OK : fail(h, DART_MPC_EHIP, "resident server", e);
 }
 
-// The per-stream state of LMPC launches on stream s: the restoration hand-off area for B instances (device
-// memory, stream-ordered growth: see dart_mpc_handle::resto) and the XCD that a small batch's working blocks
-// take -- streams get XCDs round robin, so that batches in flight on different streams of a handle run side by
-// side on different XCDs instead of queueing for the CUs of one
-int lmpc_stream_state(dart_mpc_handle* h, int B, hipStream_t s, double** out, int* xcd) {
+// The per-stream state of PMPC / LMPC launches on stream s: the restoration hand-off area for B instances
+// (device memory, stream-ordered growth: see dart_mpc_handle::resto; PMPC pmpc_model.h kPmHo doubles per
+// instance, LMPC 64 x 16) and the XCD that a small LMPC batch's working blocks take -- streams get XCDs round
+// robin, so that batches in flight on different streams of a handle run side by side on different XCDs instead
+// of queueing for the CUs of one
+int stream_state(dart_mpc_handle* h, int B, hipStream_t s, double** out, int* xcd) {
     *out = nullptr;
-    const size_t need = h->cfg.restoration ? (size_t)B * 64 * 16 : 0;
+    const size_t per = h->cfg.variant == DART_MPC_PMPC ? (size_t)dartmpc::kPmHo : (size_t)64 * 16;
+    const size_t need = h->cfg.restoration ? (size_t)B * per : 0;
     dart_mpc_handle::RestoArea* r = nullptr;
     for (auto& e : h->resto)
         if (e.s == s) r = &e;
@@ -355,8 +369,11 @@ int lmpc_stream_state(dart_mpc_handle* h, int B, hipStream_t s, double** out, in
         // area is freed with hipFree, which waits for the device's outstanding work first (this rare path only).
         constexpr size_t kMaxRestoAreas = 8;
         if (h->resto.size() >= kMaxRestoAreas) {
-            dart_mpc_handle::RestoArea old = h->resto.front();
-            h->resto.erase(h->resto.begin());
+            // (never the resident server's: its grid may hand an instance over into it at any time)
+            size_t v = 0;
+            while (v + 1 < h->resto.size() && h->srv.stream && h->resto[v].s == h->srv.stream) ++v;
+            dart_mpc_handle::RestoArea old = h->resto[v];
+            h->resto.erase(h->resto.begin() + v);
             if (old.buf) HIPCHK(h, hipFree(old.buf), "hipFree (restoration hand-off)");
         }
         h->resto.push_back({s, nullptr, 0, (int)(h->xcd_next++ & 7u)});
@@ -398,6 +415,7 @@ int launch(dart_mpc_handle* h, int B, const double* x0, const double* ref, const
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     a.done = nullptr; a.seq = 0;
     a.resto = pmpc_resto_mode(h, 1);
+    if (int rc = pmpc_resto_buf(h, B, s, a)) return rc;
     HIPCHK(h, dartmpc_launch_pmpc(&a, s), "kernel launch");
     return DART_MPC_OK;
 }
@@ -444,6 +462,7 @@ int served_resto(dart_mpc_handle* h, int B, bool ww, bool wo) {
     HIPCHK(h, hipStreamSynchronize(v.stream), "resident server");
     dartmpc::PmpcArgs a = io_args(h, B, ww, wo, 1);
     a.done = nullptr;
+    if (int rc = pmpc_resto_buf(h, v.B, v.stream, a)) return rc;      // the area the grid handed over into
     HIPCHK(h, dartmpc_launch_pmpc_resto(&a, v.stream), "restoration kernel launch");
     HIPCHK(h, hipStreamSynchronize(v.stream), "restoration kernel");
     return DART_MPC_OK;
@@ -497,6 +516,7 @@ int served_request(dart_mpc_handle* h, int B, bool ww, bool wo) {
 int bound_launch(dart_mpc_handle* h, int B, bool ww, bool wo) {
     next_seq(h);
     dartmpc::PmpcArgs a = io_args(h, B, ww, wo, B <= 32 ? 1 : 2);
+    if (int rc = pmpc_resto_buf(h, B, h->stream, a)) return rc;
     HIPCHK(h, dartmpc_launch_pmpc(&a, h->stream), "kernel launch");
     int rc = wait_done(h, h->stream, h->hdone, B, a.seq);
     if (rc == DART_MPC_OK) rc = host_resto(h, a, (const int32_t*)(h->io.hout + h->io.off_st), h->stream);
@@ -647,6 +667,7 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     a.u0 = d_u0; a.f = d_f; a.w_out = d_wo; a.status = d_st; a.iters = d_it;
     a.done = d_done; a.seq = next_seq(h);
     a.resto = host_resto_mode(h, B);
+    if (int rc = pmpc_resto_buf(h, B, s, a)) return rc;
     HIPCHK(h, dartmpc_launch_pmpc(&a, s), "kernel launch");
     int rc = wait_done(h, s, h->hdone, B, a.seq);
     if (rc == DART_MPC_OK) rc = host_resto(h, a, S.host_of(d_st), s);
@@ -738,7 +759,7 @@ int dart_lmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* state, co
     a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc; a.mult_init_max = h->cfg.constr_mult_init_max;
     a.resto = h->cfg.restoration;
     a.max_ticks = (long long)(h->cfg.max_cpu_time * 1e8);     // s_memrealtime: 100 MHz
-    if (int rc = lmpc_stream_state(h, B, stream ? (hipStream_t)stream : h->stream, &a.resto_buf, &a.xcd)) return rc;
+    if (int rc = stream_state(h, B, stream ? (hipStream_t)stream : h->stream, &a.resto_buf, &a.xcd)) return rc;
     a.state = state; a.u_prev = u_prev; a.pvec = pvec; a.target = target; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     a.fuse_policy = 0;
@@ -886,7 +907,7 @@ int dart_lmpc_policy_solve_batch_dev(dart_mpc_handle* h, const dart_lmpc_policy_
     a.acc_tol = h->cfg.acceptable_tol; a.acc_iter = h->cfg.acceptable_iter; a.max_soc = h->cfg.max_soc; a.mult_init_max = h->cfg.constr_mult_init_max;
     a.resto = h->cfg.restoration;
     a.max_ticks = (long long)(h->cfg.max_cpu_time * 1e8);     // s_memrealtime: 100 MHz
-    if (int rc = lmpc_stream_state(h, B, stream ? (hipStream_t)stream : h->stream, &a.resto_buf, &a.xcd)) return rc;
+    if (int rc = stream_state(h, B, stream ? (hipStream_t)stream : h->stream, &a.resto_buf, &a.xcd)) return rc;
     a.state = state; a.u_prev = u_prev; a.pvec = nullptr; a.target = target; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     HIPCHK(h, dartmpc_launch_lmpc(&a, stream ? (hipStream_t)stream : h->stream), "kernel launch");

@@ -18,6 +18,8 @@ struct PmpcArgs {
     // no completion word), which dartmpc_launch_pmpc queues behind the solve on the same stream; 2 the same
     // hand-off with the completion word written (the resident server: the host runs the restoration kernel)
     int resto;
+    double* resto_buf;      // [B][kPmHo] hand-off state of the instances that enter the restoration phases
+                            // (device workspace of the handle; nullptr: the restoration solve starts over)
     const double* x0;       // [B][6]   device
     const double* ref;      // [B][6]
     const double* prm;      // [B][6]  mu, Qp, Qv, R, u_lo, u_hi

@@ -852,6 +852,22 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
 
     // -------- outputs ---------------------------------------------------------------
     if (PM_EXPECT(status == kPmNeedResto, 0)) {     // handed over: pmpc_resto_solve writes the outputs
+        if constexpr (NAX == 1 && !RED) {
+            if (a.resto_buf) {      // the iterate of the failed iteration (pmpc_model.h kPmHo layout)
+                double* ho = a.resto_buf + (size_t)kPmHo * b;
+                double* row = ho + kPmHoRow * k;
+                if (xon) {
+                    row[2 * ax0] = p[0]; row[2 * ax0 + 1] = v[0]; row[4 + ax0] = zz[0];
+                    row[8 + 2 * ax0] = lp[0]; row[8 + 2 * ax0 + 1] = lv[0]; row[8 + 4 + ax0] = 0.0;
+                }
+                if (uon) { row[6 + ax0] = th[0]; row[14 + ax0] = zl[0]; row[16 + ax0] = zu[0]; }
+                if (lane < nfilt) { ho[kPmHoFilt + 2 * lane] = fth; ho[kPmHoFilt + 2 * lane + 1] = fph; }
+                if (lane == 0) {
+                    ho[kPmHoScal] = mu; ho[kPmHoScal + 1] = delta_last;
+                    ho[kPmHoScal + 2] = (double)it; ho[kPmHoScal + 3] = (double)nfilt;
+                }
+            }
+        }
         if (lane == 0) a.status[b] = status;
         if (a.done && a.resto == 2) {
             __threadfence_system();

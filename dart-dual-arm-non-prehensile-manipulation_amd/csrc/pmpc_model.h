@@ -8,6 +8,18 @@ namespace dartmpc {
 // hand-off of an instance whose filter line search failed to pmpc_resto_kernel (internal status)
 constexpr int kPmNeedResto = -100;
 
+// The state the register kernel hands over with such an instance (PmpcArgs::resto_buf, kPmHo doubles per
+// instance): the iterate of the iteration whose line search failed -- per node k (< 32) the full state
+// x[6] = [px vx py vy pz vz], the tilts u[2], the defect-row multipliers lam[6] (the z rows' are 0 on IPOPT's
+// path: cost-free states), the bound multipliers zl[2], zu[2] -- the filter entries (theta, phi) and mu, the
+// last inertia shift, the iteration and filter counters.  pmpc_resto_solve resumes from it: the failed
+// iteration is repeated (its direction up to rounding) and the restoration phases follow, instead of solving
+// the instance again from its start.
+constexpr int kPmHoRow = 18;                          // x 0..5, u 6..7, lam 8..13, zl 14..15, zu 16..17
+constexpr int kPmHoFilt = 32 * kPmHoRow;             // 64 entries (theta, phi)
+constexpr int kPmHoScal = kPmHoFilt + 2 * 64;        // mu, delta_last, it, nfilt
+constexpr int kPmHo = kPmHoScal + 4;
+
 // mpc_3d.py:87-97, one axis:  pdot = v,  vdot = g sin(theta) - mu v
 __device__ __forceinline__ void axis_rhs(double g, double mu, double s, double v, double& dp, double& dv) {
     dp = v;

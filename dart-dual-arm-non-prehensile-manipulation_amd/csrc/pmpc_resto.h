@@ -31,6 +31,7 @@
 #include "ocp_wave.h"
 #include "pmpc_ipm.h"
 #include "pmpc_model.h"
+#include "stamps.h"
 #include "wave.h"
 
 namespace dartmpc {
@@ -101,9 +102,15 @@ struct PrFilter {
     }
 };
 
+#ifdef DART_STAMPS
+// diagnostic build: per-phase s_memtime cycles of the last handed-over instance (tools/stamps_pmpc_resto.py)
+__device__ unsigned long long g_stamp_pr[32];
+#endif
+
 // the solve of handed-over instance b by the calling wave (its LDS: the caller's kernel gets PrShared)
 __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b) {
     __shared__ PrShared SH;
+    STAMP_DECL
     PrLds* S = &SH.ocp;
     PrSoft* SR = &SH.soft;
     constexpr int NC = PrLds::NC;
@@ -328,11 +335,37 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
     double phi_rs = 0.0, tau_rs = 0.99;
     int it_next = a.mult_init_max > 0.0 ? -1 : 0;
     const double zero6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    // Resume (a.resto_buf): the register kernel's iterate of the iteration whose line search failed
+    // (pmpc_model.h kPmHo), its filter, mu, last inertia shift and iteration counter.  That iteration is repeated
+    // here -- the same point, hence the same Newton system, factored at the shift the register kernel used (0, or
+    // its updated last shift: resume_first) -- and the restoration phases follow; the scaling sc and the filter's
+    // theta bounds above belong to the starting point, as in the register kernel.
+    bool resume_first = false;
+    if (a.resto_buf) {
+        const double* ho = a.resto_buf + (size_t)kPmHo * b;
+        const double* row = ho + kPmHoRow * k;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) { x[i] = xon ? row[i] : 0.0; lam[i] = xon ? row[8 + i] : 0.0; }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            u[j] = uon ? row[6 + j] : 0.0;
+            zl[j] = uon ? row[14 + j] : 0.0; zu[j] = uon ? row[16 + j] : 0.0;
+        }
+        mu = ho[kPmHoScal]; delta_last = ho[kPmHoScal + 1];
+        it_next = (int)ho[kPmHoScal + 2];
+        const int nf = (int)ho[kPmHoScal + 3];
+        F0.th[0] = lane < nf ? ho[kPmHoFilt + 2 * lane] : 0.0;
+        F0.ph[0] = lane < nf ? ho[kPmHoFilt + 2 * lane + 1] : 0.0;
+        F0.n = nf;
+        resume_first = true;
+    }
     __syncthreads();
+    STAMP(0);
 
     for (;;) {
     for (it = it_next; it < a.max_iter; ++it) {
         const bool lsm = it < 0;      // IPOPT's least-square starting multipliers (constr_mult_init_max)
+        STAMP_ADD(16, 1);
         defects(x, u, g);             // (the accepted trial's: the same bits)
         theta = wsum(l1(g));
         double ln[6], ja[8], hdu[2], gx[6];
@@ -371,6 +404,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             F0.reset(); in_soft = 0;      // BacktrackingLineSearch::Reset: the filter and the soft phase
         }
         const double tau = fmax(0.99, 1.0 - mu);
+        STAMP(1);
         write_tilt_cols(u);
         // stage QP at inertia shift d (least squares: unit weights, the box gradient -z_L + z_U, no defects)
         auto assemble = [&](double d) {
@@ -407,14 +441,18 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
         double delta = 0.0;
         bool ok = riccati_sweep_gen(S, N, SH.U);
         for (int attempt = 0; !ok && attempt < 60; ++attempt) {
-            delta = (attempt == 0) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))
+            // (the resumed iteration: the register kernel's shift, which its update left in delta_last)
+            delta = (attempt == 0) ? (resume_first && delta_last > 0.0 ? delta_last
+                                      : delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))
                                    : delta * (delta_last == 0.0 ? 100.0 : 8.0);
             assemble(delta);
             __syncthreads();
             ok = riccati_sweep_gen(S, N, SH.U);
         }
+        resume_first = false;
         if (!ok) { status = -3; break; }
         if (delta > 0.0) delta_last = delta;
+        STAMP(2);
         solve_plain(dx, dU, lp);
         // bound-multiplier steps and the fractions to the boundary
         double dzl[2], dzu[2], amax = 1.0, az = 1.0;
@@ -435,6 +473,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             amax = wmin(am); az = wmin(a2);
         };
         duals();
+        STAMP(3);
         const double amax0 = amax, az0 = az;
         // ---- filter line search with second-order correction (W&B 2006, Alg. A) ----
         const double phi = barrier(x, u, mu);
@@ -486,6 +525,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
         for (int ls = 0; ls < 80 && !accepted && !in_soft; ++ls) {
             if (alpha < amin && ls > 0) break;
             trial(alpha);
+            STAMP_ADD(17, 1);
             if (tiny) { accepted = true; ftype = true; break; }
             accepted = accept(alpha);
             if (!accepted && ls == 0 && !(th_t < theta) && a.max_soc > 0) {
@@ -534,6 +574,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             printf("it %3d mu %.2e dinf %.2e pinf %.2e c0 %.2e delta %.1e amax %.3e alpha %.3e az %.3e th %.2e\n", it, mu,
                    dinf / s_d, pinf, c0 / s_c, delta, amax0, alpha, az, theta);
 #endif
+        STAMP(4);
         bool soft = false;
         if (!accepted) {
             // ---- IPOPT's soft restoration phase (at most 10 steps; the current point enters the filter) ----
@@ -593,6 +634,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             }
             if (!accepted) { phi_rs = phi; tau_rs = tau; go_resto = true; break; }
         }
+        STAMP(5);
         if (!soft && !ftype) F0.add((1 - gam_th) * theta, phi - gam_ph * theta);
         // ---- accept the step ----
 #pragma unroll
@@ -610,9 +652,11 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             }
         }
         __syncthreads();
+        STAMP(6);
     }
     if (!go_resto) break;
     go_resto = false;
+    STAMP(5);
 
     // ---------------- IPOPT's restoration phase (MinC_1NrmRestorationPhase; oracle/pmpc_ipm.c) -----------
     // min rho sum(p + n) + eta/2 |D_R (x - x_R)|^2 s.t. c(x) + n - p = 0 on every defect row (x_0 pinning
@@ -772,7 +816,9 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
         int rit = it + 1, rstat = -2;
         bool rfirst = true, rok = false;
         double rdelta_last = 0.0;
+        STAMP(7);
         for (;; ++rit) {
+            STAMP_ADD(18, 1);
             defects(x, u, g);
             {
                 double pv[6], nv[6];
@@ -834,6 +880,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                 F1.reset();
             }
             const double taur = fmax(0.99, 1.0 - rmu);
+            STAMP(8);
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 pn[R_RP + i] = rho - rmu / pn[R_PC + i] - lam[i];
@@ -861,6 +908,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             }
             if (!okr) { rstat = -3; break; }
             if (delta > 0.0) rdelta_last = delta;
+            STAMP(9);
             // one refinement pass (PDFullSpaceSolver): the residuals of the full Newton system at the step --
             // stationarity of x and u, the soft defect rows, the p / n rows -- solved for on the same
             // factorisation and added, while they exceed 1e-12 (1 + |step|); returns false when done
@@ -921,6 +969,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                 if (wu) smax = fmax(smax, fmax(fabs(dU[0]), fabs(dU[1])));
                 emax = wmax(emax); smax = wmax(smax);
                 if (!(emax > 1e-12 * (1.0 + smax))) return false;
+                STAMP_ADD(20, 1);
                 // the correction solve: lambda = 0, the residuals as gradient and right-hand sides
                 park(SH.SV2[lane]);
                 double gsave[8];
@@ -986,6 +1035,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                 pn_steps();
             };
             rstep(cg);
+            STAMP(10);
             // barrier objective of the restoration problem and its directional derivative
             double phir, gtdr;
             {
@@ -1069,6 +1119,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             for (int ls = 0; ls < 80 && !accr; ++ls) {
                 if (alr < aminr && ls > 0) break;
                 trial_r(alr);
+                STAMP_ADD(19, 1);
                 accr = racc(alr);
                 if (!accr && ls == 0 && !(tht < thr) && a.max_soc > 0) {
                     // second-order correction on the restoration problem's constraints; the plain step parked
@@ -1102,6 +1153,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                 printf("  resto it %3d mu %.2e err %.2e dinf %.2e pinf %.2e c0 %.2e delta %.1e amax %.3e alpha %.3e th %.3e "
                        "th_t %.3e acc %d\n", rit, rmu, errr, dinf / s_d, pinf, c0r / s_c, delta, amr, alr, thr, tht, (int)accr);
 #endif
+            STAMP(11);
             if (!accr) { rstat = -2; break; }      // a failed line search in the restoration phase
             if (!ftr) F1.add((1 - gam_th) * thr, phir - gam_ph * thr);
             // ---- accept the trial point ----
@@ -1136,7 +1188,9 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             }
             thr = tht;
             __syncthreads();
+            STAMP(12);
         }
+        STAMP(13);
         if (!rok) { status = rstat; it = rit; break; }
         // back to the original problem: the u-bound multipliers take the step (mu - z s_trial) / s that
         // pretends the restoration's progress was one Newton step, cut by the fraction to the boundary (tau
@@ -1182,6 +1236,11 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
     }
 
     // ---------------- outputs (as pmpc_ipm.hip) ------------------------------------------------------
+    STAMP(14);
+#ifdef DART_STAMPS
+    if (lane == 0)
+        for (int q = 0; q < 32; ++q) g_stamp_pr[q] = t_acc_[q];
+#endif
     const double fval = wsum(node_cost(x, u));
     if (lane == 0) {
         a.u0[2 * b] = u[0]; a.u0[2 * b + 1] = u[1];

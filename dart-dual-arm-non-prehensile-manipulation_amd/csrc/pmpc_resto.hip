@@ -25,3 +25,11 @@ extern "C" hipError_t dartmpc_launch_pmpc_resto(const dartmpc::PmpcArgs* args, h
     hipLaunchKernelGGL(dartmpc::pmpc_resto_kernel, dim3(a.B * a.pack), dim3(dartmpc::kWave), 0, stream, a);
     return hipGetLastError();
 }
+
+#ifdef DART_STAMPS
+// diagnostic build only: per-phase cycles of the last instance pmpc_resto_kernel solved (32 counters)
+extern "C" hipError_t dartmpc_read_stamps_pmpc_resto(unsigned long long* host_out) {
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp_pr), sizeof(unsigned long long) * 32, 0,
+                               hipMemcpyDeviceToHost);
+}
+#endif

@@ -281,9 +281,8 @@ __device__ __forceinline__ void rm_iq3(const double* z, double vmax, bool mir, d
     c[2] = mir ? -z[3] - vmax : z[1] - vmax;
 }
 
-// The LDS of the solve (one instance per workgroup), at namespace scope so that the main solve and the
-// restoration solve of a fused launch (rmpc_resto_tail) share it: a kernel is given the blocks its code reaches
-// (70.6 KB without the restoration phases, 151.7 KB with them)
+// The LDS of the solve (one instance per workgroup), at namespace scope: a kernel is given the blocks its code
+// reaches (70.6 KB without the restoration phases, 151.7 KB with them)
 __shared__ RmShared g_rm_sh;
 __shared__ RmResto g_rm_resto;
 
@@ -2051,31 +2050,19 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
     return false;
 }
 
-// IPOPT's restoration phases for instance b in the wave that handed it over (batches of at most 32, one
-// instance per CU): a call, not inlined, so that rmpc_ipm_kernel<false>'s register allocation stays its own;
-// the launch arguments are read from the kernel's argument segment (RmpcArgs is its first argument, kernarg_addr).  The RLS
-// update of the launch has already been applied to theta / rls_P in place, and the restoration solve reads
-// the updated theta, as rmpc_ipm_kernel<true> does behind a separate launch.
-__device__ __noinline__ void rmpc_resto_tail(const int b, const unsigned long long kargs) {
-    const RmpcArgs a = kernarg_load<RmpcArgs>(kargs);
-    __threadfence_block();
-    __syncthreads();            // the RLS update's theta stores (any lane) before the re-solve reads them
-    rmpc_solve<true>(a, b);
-}
-
-// RESTO: the handed-over instances of a launch (queued behind rmpc_ipm_kernel<false> for batches above 32);
-// FUSE: rmpc_ipm_kernel<false> whose handed-over instances continue in rmpc_resto_tail (no second launch)
-template <bool RESTO, bool FUSE = false>
+// RESTO = false: every launch; RESTO = true: the handed-over instances, queued behind it on the same stream.
+// (Unlike PMPC and LMPC, RMPC does not run the restoration in the solving wave for small batches: a
+// non-inlined restoration call at the end of this kernel -- rmpc_resto_tail, round 5 -- costs it its last free
+// registers (the call ABI's SGPRs spill into a VGPR), and the spilled main loop measured C3 -4.7 % against
+// +1.7 % for the saved dispatch; profiles/r05/fuse_ab.txt)
+template <bool RESTO>
 __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
     const int b = blockIdx.x / a.pack;
     if constexpr (RESTO) {
         if (a.status[b] != kRmNeedResto) return;     // wave-uniform: solved by rmpc_ipm_kernel<false>
     }
-    const bool handed = rmpc_solve<RESTO>(a, b);
-    if constexpr (FUSE) {
-        if (__builtin_expect(handed, 0)) rmpc_resto_tail(b, kernarg_addr());
-    }
+    (void)rmpc_solve<RESTO>(a, b);
 }
 
 // Standalone batched RLS.update (np_mpc...:17-27): one p = 7 filter per workgroup, lanes as entries.
@@ -2120,11 +2107,6 @@ extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStre
     if (args->N < 1 || args->N >= dartmpc::RM_NMAXS) return hipErrorInvalidValue;
     dartmpc::RmpcArgs a = *args;
     a.pack = (a.B <= 32) ? 8 : 1;            // blocks go round-robin over the 8 XCDs: one XCD, one L2 for the code
-    if (a.resto && a.pack == 8 && dartmpc::resto_fuse_enabled()) {   // restoration in the solving wave: one launch
-        hipLaunchKernelGGL((dartmpc::rmpc_ipm_kernel<false, true>), dim3(a.B * a.pack), dim3(dartmpc::kWave), 0,
-                           stream, a);
-        return hipGetLastError();
-    }
     hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel<false>, dim3(a.B * a.pack), dim3(dartmpc::kWave), 0, stream, a);
     if (a.resto) {      // the instances whose line search failed, with IPOPT's restoration phases
         if (hipError_t e = hipGetLastError()) return e;

@@ -1,0 +1,49 @@
+"""Diagnostic: where a PMPC restoration solve spends its cycles (pmpc_resto.h with the DART_STAMPS build).
+
+Loads dart_mpc/libdartmpc_stamps.so, solves a batch of 40 (above 32, so the queued pmpc_resto_kernel runs)
+holding ONE instance whose filter line search fails (C4's instances at N = 31 with the default options, or
+N = 20 with max_soc = 0: DART_STAMPS_N / DART_STAMPS_SOC), and prints the s_memtime cycles of that instance's
+restoration solve per phase.  Stamps fence the code: read the shares.
+Usage (on the box): python tools/stamps_pmpc_resto.py"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dart-dual-arm-non-prehensile-manipulation_amd"))
+from dart_mpc import _lib  # noqa: E402
+from dart_mpc.workload import pmpc_batch  # noqa: E402
+
+N = int(os.environ.get("DART_STAMPS_N", "31"))
+SOC = int(os.environ.get("DART_STAMPS_SOC", "4"))
+S, T, P = pmpc_batch(64, seed0=300000)
+off = _lib.Solver(N=N, B_max=S.shape[0], max_soc=SOC, restoration=False).solve_batch(S, T, P)
+hard = np.flatnonzero(off["status"] == -2)
+easy = np.flatnonzero(off["status"] == 0)
+sel = np.concatenate([hard[:1], easy[:39]])
+S, T, P = S[sel], T[sel], P[sel]
+base = _lib.Solver(N=N, B_max=40, max_soc=SOC).solve_batch(S, T, P)
+
+_lib.LIB_PATH = os.path.join(_lib.PKG_DIR, "libdartmpc_stamps.so")
+_lib._lib = None
+L = _lib.lib()
+read = L.dartmpc_read_stamps_pmpc_resto
+read.argtypes = [ctypes.c_void_p]
+s = _lib.Solver(N=N, B_max=40, max_soc=SOC)
+for rep in range(2):
+    out = s.solve_batch(S, T, P)
+st = np.zeros(32, dtype=np.uint64)
+read(ctypes.c_void_p(st.ctypes.data))
+names = {0: "setup", 1: "main: eval + errors + mu", 2: "main: Riccati (inertia)", 3: "main: solve + duals",
+         4: "main: line search", 5: "main: soft restoration", 6: "main: update", 7: "resto: start (lsq mults)",
+         8: "resto: eval + errors", 9: "resto: soft Riccati (inertia)", 10: "resto: solve + refinement",
+         11: "resto: line search", 12: "resto: update", 13: "resto: return", 14: "back in main after resto"}
+tot = float(st[:15].sum())
+print(f"N={N} max_soc={SOC}: instance {sel[0]} status {out['status'][0]} iters {out['iters'][0]} (product library: "
+      f"{base['status'][0]} / {base['iters'][0]}); total {tot:.0f} cycles (~{tot / 2.4e9 * 1e3:.3f} ms at 2.4 GHz)")
+for i, n in names.items():
+    print(f"  {n:34s} {int(st[i]):10d}  {100 * st[i] / tot:5.1f}%")
+print(f"  main iterations {int(st[16])}, main line-search trials {int(st[17])}, restoration iterations {int(st[18])}, "
+      f"restoration trials {int(st[19])}, refinement solves {int(st[20])}")
