@@ -547,6 +547,16 @@ void oracle_pmpc_set_mult_init_max(double m) { g_mult_init_max = m; }
 /* IPOPT's soft restoration and restoration phases on / off (off: a failed line search ends at -2) */
 static int g_resto = 1;
 void oracle_pmpc_set_resto(int on) { g_resto = on; }
+/* diagnostic: a relative perturbation of the soft restoration step length (0 = IPOPT's; sensitivity studies) */
+static double g_soft_perturb = 0.0;
+void oracle_pmpc_set_soft_perturb(double e) { g_soft_perturb = e; }
+/* diagnostic: how many times the restoration phase proper (not the soft phase) was entered since the last reset */
+static int g_resto_entries = 0;
+int oracle_pmpc_resto_entries(int reset) {
+    const int n = __atomic_load_n(&g_resto_entries, __ATOMIC_RELAXED);
+    if (reset) __atomic_store_n(&g_resto_entries, 0, __ATOMIC_RELAXED);
+    return n;
+}
 enum { ST_INFEASIBLE = 2 };
 
 /* the dynamics Jacobians (A, Bm) and the lambda-weighted RK4 Hessians at the iterate in W */
@@ -589,7 +599,7 @@ static double soft_resto_step(const ctx_t *C, work_t *W, int nfilt, double th, d
                               double curr_pd, double *th_t, double *ph_t, int *orig) {
     const prob_t *P = C->P; const int N = C->N, nU = NU * N, ng = NX * (N + 1);
     const double gam_th = 1e-5, gam_ph = 1e-8;
-    const double a = fmin(frac_to_boundary(C, W, W->dU, tau), bound_dual_step(C, W, nU, tau));
+    const double a = fmin(frac_to_boundary(C, W, W->dU, tau), bound_dual_step(C, W, nU, tau)) * (1.0 - g_soft_perturb);
     for (int i = 0; i < ng; ++i) W->Xt[i] = W->X[i] + a * W->dX[i];
     for (int j = 0; j < nU; ++j) W->Ut[j] = W->U[j] + a * W->dU[j];
     *th_t = constraints(C, W->Xt, W->Ut, W->gt);
@@ -1170,6 +1180,7 @@ int oracle_pmpc_solve(int N, double Ts, const double *state, const double *targe
             }
             if (!accepted) {
                 /* IPOPT's restoration phase */
+                __atomic_fetch_add(&g_resto_entries, 1, __ATOMIC_RELAXED);
                 int rst = ST_LS_FAIL;
                 if (!restoration(&C, W, &it, max_iter, tol, th, phi, nfilt, tau, g, &rst)) { status = rst; break; }
                 th = constraints(&C, W->X, W->U, g);

@@ -30,9 +30,11 @@ ALGO_BYTES = {"pmpc_ipm_kernel": 18 * 176, "rmpc_ipm_kernel": 18 * (4 + 2 + 14 +
 # of the same kernel in the bench (C4, saturation runs) are left out of the per-launch figures
 GRID = {"pmpc_ipm_kernel": 18 * 8 * 64, "rmpc_ipm_kernel": 18 * 8 * 64, "lmpc_ipm_kernel": 18 * 8 * 64,
         "arm_qp_kernel": 36 * 64}
-STATS_NAME = {"pmpc_ipm_kernel": "pmpc_ipm_kernel<1, true, false, true, false, false>",   # template instance the C2 launch uses
-              "rmpc_ipm_kernel": "rmpc_ipm_kernel<false>",     # (<true> of RMPC and LMPC resumes restoration
-              "lmpc_ipm_kernel": "lmpc_ipm_kernel<false>"}     #  hand-offs only: ~4 us when empty)
+# the template instances the headline launches use: round 5, B <= 32 runs the FUSE instantiations of PMPC and
+# LMPC (restoration in the solving wave); RMPC's <false> is followed by its queued <true> (~4 us when empty)
+STATS_NAME = {"pmpc_ipm_kernel": "pmpc_ipm_kernel<1, true, false, true, false, false, true>",
+              "rmpc_ipm_kernel": "rmpc_ipm_kernel<false>",
+              "lmpc_ipm_kernel": "lmpc_ipm_kernel<false, true>"}
 
 
 def short(name):
