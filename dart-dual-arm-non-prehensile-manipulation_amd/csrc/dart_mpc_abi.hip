@@ -283,6 +283,9 @@ int pmpc_resto_mode(const dart_mpc_handle* h, int mode) {
     return (h->cfg.restoration && h->cfg.pmpc_path == 0 && h->cfg.N <= 31) ? mode : 0;
 }
 
+// IPOPT's soft restoration phase in the register kernel: with the restoration phases on, on IPOPT's path, at every N
+int pmpc_soft(const dart_mpc_handle* h) { return (h->cfg.restoration && h->cfg.pmpc_path == 0) ? 1 : 0; }
+
 // the mode of a host-entry launch of B instances: in the solving wave (small batches), else host-driven
 int host_resto_mode(const dart_mpc_handle* h, int B) { return pmpc_resto_mode(h, B <= 32 ? 1 : 2); }
 
@@ -332,6 +335,7 @@ dartmpc::PmpcArgs io_args(dart_mpc_handle* h, int B, bool ww, bool wo, int resto
     a.status = (int32_t*)(o.dout + o.off_st); a.iters = (int32_t*)(o.dout + o.off_it);
     a.done = h->ddone; a.seq = h->seq;
     a.resto = pmpc_resto_mode(h, resto_mode);
+    a.soft = pmpc_soft(h);
     a.resto_buf = nullptr;        // (the caller sets it for its stream: pmpc_resto_buf)
     return a;
 }
@@ -424,6 +428,7 @@ int launch(dart_mpc_handle* h, int B, const double* x0, const double* ref, const
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
     a.done = nullptr; a.seq = 0;
     a.resto = pmpc_resto_mode(h, 1);
+    a.soft = pmpc_soft(h);
     if (int rc = pmpc_resto_buf(h, B, s, a)) return rc;
     HIPCHK(h, dartmpc_launch_pmpc(&a, s), "kernel launch");
     return DART_MPC_OK;
@@ -676,6 +681,7 @@ int dart_mpc_solve_batch(dart_mpc_handle* h, int B, const double* x0, const doub
     a.u0 = d_u0; a.f = d_f; a.w_out = d_wo; a.status = d_st; a.iters = d_it;
     a.done = d_done; a.seq = next_seq(h);
     a.resto = host_resto_mode(h, B);
+    a.soft = pmpc_soft(h);
     if (int rc = pmpc_resto_buf(h, B, s, a)) return rc;
     HIPCHK(h, dartmpc_launch_pmpc(&a, s), "kernel launch");
     int rc = wait_done(h, s, h->hdone, B, a.seq);

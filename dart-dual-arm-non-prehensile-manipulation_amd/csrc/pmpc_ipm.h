@@ -18,6 +18,9 @@ struct PmpcArgs {
     // no completion word), which dartmpc_launch_pmpc queues behind the solve on the same stream; 2 the same
     // hand-off with the completion word written (the resident server: the host runs the restoration kernel)
     int resto;
+    // IPOPT's soft restoration phase in the register kernel (1 with the restoration phases on, at every N; the
+    // restoration phase proper follows only where resto allows the hand-off, N <= 31)
+    int soft;
     double* resto_buf;      // [B][kPmHo] hand-off state of the instances that enter the restoration phases
                             // (device workspace of the handle; nullptr: the restoration solve starts over)
     const double* x0;       // [B][6]   device

@@ -294,6 +294,8 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
     int nfilt = 0;
     double mu = 0.1, delta_last = 0.0;
     int status = -1, it = 0;
+    // IPOPT's soft restoration phase (round 5): in_soft while its steps are being taken, soft_count of them
+    int in_soft = 0, soft_count = 0;
     STAMP(0);
 
 #ifdef DART_STAMPS
@@ -351,7 +353,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
             const double cmu = fmax(c0 - mu, mu - cmin_w);
             if (fmax(dinf * is_d, fmax(pinf, cmu * is_c)) > 10.0 * mu || mu <= mu_min) break;
             mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
-            nfilt = 0;
+            nfilt = 0; in_soft = 0;       // BacktrackingLineSearch::Reset: the filter and the soft phase
         }
         const double tau = fmax(0.99, 1.0 - mu);
         STAMP(2);
@@ -781,6 +783,10 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
             }
             STAMP(5);
             bool again = false;
+            if constexpr (NAX == 2 && !RED) {
+                if (PM_EXPECT(in_soft, 0)) break;      // in the soft restoration phase: its step only (below)
+                if (PM_EXPECT(soc < 0 && alpha < amin, 0)) break;
+            }
             for (;;) {
                 trial(alpha);
                 bool ft = false;
@@ -814,8 +820,10 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                         defects(p[j], v[j], snc[j], sp[j], sv[j], g1[j], g2[j]);
                         gz[j] = RED ? 0.0 : zdefect(zz[j], w0, j);
                     }
+                    // (NAX == 2, the soft phase below: always through the loop top, so that a line search that fails
+                    // here leaves the plain step in the direction registers; alpha < amin stops it there)
                     soc = -1; ls = 1; alpha = 0.5 * amain;
-                    again = !(alpha < amin);
+                    again = (NAX == 2 && !RED) || !(alpha < amin);
                     break;
                 }
                 ++ls;
@@ -827,9 +835,90 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
         STAMP_ADD(10, ls + 1);
         STAMP_ADD(15, soc > 0 ? 1 : 0);
         STAMP(6);
-        // a failed line search: IPOPT's restoration phases in pmpc_resto_kernel (or status -2 without)
-        if (PM_EXPECT(!accepted, 0)) { status = a.resto ? kPmNeedResto : -2; break; }
-        if (!ftype && nfilt < kWave) {
+        // A failed line search: IPOPT's soft restoration phase here (BacktrackingLineSearch::TrySoftRestoStep;
+        // oracle/pmpc_ipm.c soft_resto_step), then, if it cannot proceed, the restoration phase proper in
+        // pmpc_resto_solve (or status -2 without the phases).  The soft step is the plain primal-dual step damped
+        // only by the fractions to the boundary (one length for x, lambda and z); it is taken if the original
+        // filter accepts it with alpha_primal_test = 0 (the phase ends) or if it cuts IPOPT's primal-dual system
+        // error at mu (the l1 norms of the primal and dual infeasibilities and of z s - mu, added) by 0.9999; at most
+        // 10 such steps, and a mu decrease ends the phase.  Only for N > 31 (NAX == 2), where the restoration solve
+        // on the LDS engine (pmpc_resto.h) does not fit: at the default options every PMPC line-search failure there
+        // is settled in the soft phase (N = 40: 41 of C4's 1152 instances), which round 4 ended at -2.  For N <= 31
+        // the handed-over instance is solved again on the LDS engine, whose sequential arithmetic takes the oracle's
+        // iterations exactly; run here, the soft phase measured 87-93 % equal iteration counts on the restored
+        // instances and cost C2 5 % (its register allocation; profiles/r05/pmpc_soft_in_register_kernel.txt).
+        bool soft = false;
+        if (PM_EXPECT(!accepted, 0)) {
+            if constexpr (!RED && NAX == 2) {
+                if (a.soft) {
+                    if (!in_soft) {       // PrepareRestoPhaseStart: the current point enters the filter
+                        if (nfilt < kWave) {
+                            if (lane == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
+                            ++nfilt;
+                        }
+                        soft_count = 0;
+                    }
+                    if (!(in_soft && ++soft_count > 10)) {
+                        // the fractions to the boundary of the plain step in f64 (the line search's f32 minima
+                        // are rounded down by up to 2^-20; a soft step takes them whole, so they are formed exactly)
+                        double am = 1.0, a2 = 1.0;
+#pragma unroll
+                        for (int j = 0; j < NAX; ++j) {
+                            if (uon) {
+                                const double sl = th[j] - lo, su = hi - th[j];
+                                if (dth[j] < 0) am = fmin(am, -tau * sl / dth[j]);
+                                if (dth[j] > 0) am = fmin(am, tau * su / dth[j]);
+                                if (dzl[j] < 0) a2 = fmin(a2, -tau * zl[j] / dzl[j]);
+                                if (dzu[j] < 0) a2 = fmin(a2, -tau * zu[j] / dzu[j]);
+                            }
+                        }
+                        const double as = fmin(wmin(am), wmin(a2));
+                        trial(as);
+                        bool ft_ = false;
+                        const bool orig = acceptable(0.0, ft_);
+                        bool take = orig;
+                        if (!take && isfinite(ph_t)) {
+                            // the primal-dual system error at the point (pass 0) and at the trial with every
+                            // multiplier moved by as (pass 1); one code site for both
+                            double pd[2];
+#pragma unroll 1
+                            for (int pass = 0; pass < 2; ++pass) {
+                                const double sa = pass ? as : 0.0;
+                                double t = 0.0;
+#pragma unroll
+                                for (int j = 0; j < NAX; ++j) {
+                                    const double pp = fma(sa, dp[j], p[j]), vv = fma(sa, dv[j], v[j]);
+                                    const double tt = fma(sa, dth[j], th[j]);
+                                    const double lpv = fma(sa, dlp[j], lp[j]), lvv = fma(sa, dlv[j], lv[j]);
+                                    const double zlv = uon ? fma(sa, dzl[j], zl[j]) : 0.0;
+                                    const double zuv = uon ? fma(sa, dzu[j], zu[j]) : 0.0;
+                                    const double ga = pass ? g1t[j] : g1[j], gb = pass ? g2t[j] : g2[j];
+                                    const double gc = pass ? gzt[j] : gz[j];
+                                    const double ln = from_next(lpv), vn = from_next(lvv);
+                                    const double lpn_ = uon ? ln : 0.0, lvn_ = uon ? vn : 0.0;
+                                    const double r1 = fma(qp2, pp - rp[j], lpv - lpn_);
+                                    const double r2x = fma(qv2, vv - rv[j], lvv - fma(a12, lpn_, a22 * lvn_));
+                                    const double c_ = tilt_cos_econ(poly, tt);
+                                    const double ru = fma(r2, tt, -c_ * fma(b1, lpn_, b2 * lvn_)) - zlv + zuv;
+                                    const double sl = tt - lo, su = hi - tt;
+                                    t += xon ? fabs(r1) + fabs(r2x) + fabs(ga) + fabs(gb) + fabs(gc) : 0.0;
+                                    t += uon ? fabs(ru) + fabs(zlv * sl - mu) + fabs(zuv * su - mu) : 0.0;
+                                }
+                                pd[pass] = wsum(t);
+                            }
+                            take = pd[1] <= 0.9999 * pd[0];
+                        }
+                        if (take) {
+                            accepted = true; soft = true; alpha = as; az = as;
+                            in_soft = orig ? 0 : 1;
+                            if (orig) soft_count = 0;
+                        }
+                    }
+                }
+            }
+            if (!accepted) { status = a.resto ? kPmNeedResto : -2; break; }
+        }
+        if (!soft && !ftype && nfilt < kWave) {
             if (lane == nfilt) { fth = (1 - gam_th) * theta; fph = phi - gam_ph * theta; }
             ++nfilt;
         }

@@ -191,6 +191,33 @@ def test_restoration_phases_same_path_as_oracle(dm, N, max_soc):
     assert du[~rest].max() <= 1e-6
 
 
+@pytest.mark.parametrize("N", [40, 50])
+def test_soft_restoration_long_horizons(dm, N):
+    """Horizons above 31 (mpc_3d.py:12 takes N freely): at N = 40, 41 of C4's 1152 instances (N = 50: 4) fail the
+    filter line search at the default options, and IPOPT settles every one of them in its soft restoration phase
+    (the oracle never enters the restoration phase proper there).  For N > 31 the register kernel runs that phase
+    itself (round 5; the LDS-engine restart of N <= 31 does not fit), so those instances end at the oracle's status
+    0 -- round 4 returned -2 -- with u0 within 1e-6 and iterations equal on >= 99 % of the batch.  On the restored
+    instances themselves the register kernel's arithmetic takes the oracle's iteration count on 83 % (N = 40) /
+    3 of 4 (N = 50) as measured in round 5 (the restart on the LDS engine, N <= 31, gives 100 %): the bound there is
+    that measured figure, >= 0.7."""
+    import oracle_lib
+    from dart_mpc.workload import pmpc_batch
+    S, T, P = pmpc_batch(64)
+    s = dm.Solver(N=N, Ts=0.002, tol=1e-8, B_max=S.shape[0])
+    g = s.solve_batch(S, T, P)
+    s.close()
+    kw = dict(N=N, Ts=0.002, tol=1e-8, max_iter=3000, nthreads=8, want_w=False)
+    o = oracle_lib.solve_batch(S, T, P, **kw)
+    off = oracle_lib.solve_batch(S, T, P, resto=False, **kw)
+    rest = off["status"] != 0
+    assert rest.sum() >= 4 and np.all(o["status"] == 0)
+    assert np.array_equal(g["status"], o["status"]), np.unique(g["status"], return_counts=True)
+    assert np.mean(g["iters"] == o["iters"]) >= 0.99
+    assert np.mean(g["iters"][rest] == o["iters"][rest]) >= 0.7, (g["iters"][rest], o["iters"][rest])
+    assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6
+
+
 def test_restoration_off_keeps_the_failed_line_search(dm):
     """restoration=False: an instance whose filter line search fails ends at status -2 (IPOPT with the
     restoration phases unavailable), on the oracle's instances; the others are solved as with them on."""

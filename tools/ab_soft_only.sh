@@ -1,10 +1,5 @@
 #!/bin/bash
-# round 5: the soft restoration phase in the PMPC register kernel -- PMPC GPU tests, A/B against the previous build
-# (libdartmpc_head.so) on C2 / N = 15 / C4 / saturation, and the restoration bench lines.
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_pmpc.py tests/test_gpu_serve.py tests/test_gpu_call_form.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pmpc_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/pmpc_tests.log; exit 1; }
-tail -2 gpurun_out/pmpc_tests.log
 ARGS="--steps 2000 --warmup 50 --no-cpu-baseline --saturation-batch 18432 --host-calls 0 --c4-steps 100 --n15-steps 1000 --rmpc-steps 0 --lmpc-steps 0 --lmpc-policy-steps 0 --arm-steps 0 --resto-steps 0"
 for r in 1 2 3; do
   for lib in libdartmpc_head.so libdartmpc.so; do
