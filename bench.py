@@ -67,6 +67,8 @@ def parse():
                     help="launches of the supplementary PMPC line at the driver's horizon N=15 (0 = skip)")
     ap.add_argument("--resto-steps", type=int, default=10,
                     help="launches per line of the supplementary PMPC restoration lines (0 = skip)")
+    ap.add_argument("--long-steps", type=int, default=10,
+                    help="batches per line of the supplementary long-horizon lines (N = 40, 63; 0 = skip)")
     ap.add_argument("--c4-steps", type=int, default=50,
                     help="steps of the supplementary C4 line (1152 instances sharded over the ranks + gather; 0 = skip)")
     ap.add_argument("--dist-backend", default=None,
@@ -144,6 +146,59 @@ def bench_rmpc(args, torch, dev, stream, dart_mpc):
         out["cpu_baseline"] = {"value": solved / cdt, "unit": "solves/s", "cores": nt, "kind": "port",
                                "sample": f"C oracle (oracle/rmpc_ipm.c), {solved} cold-start C3 solves in {cdt:.1f} s"}
     s.close()
+    return out
+
+
+def bench_long_horizons(args, dart_mpc):
+    """Horizons beyond the one-wave kernels (N = 40 and 63; the reference takes N as a free constructor argument,
+    mpc_3d.py:12, np_mpc...:35, rlmpc2.py): per variant a batch of 18 fresh instances per call through the host
+    entry (inputs copied in, outputs out: PCIe-inclusive), statuses and iterations of the first batch against
+    the C oracle.  PMPC N > 31 runs two registers per lane in one wave; RMPC and LMPC the two-wave builds."""
+    from dart_mpc.workload import lmpc_batch, pmpc_batch, rmpc_batch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_lib   # checker only
+    K = args.long_steps
+    out = {"note": "host entry (PCIe-inclusive), batch 18, fresh instances per call; *_equal: the first batch "
+                   "against the C oracle at the same options"}
+    for N in (40, 63):
+        P = [pmpc_batch(1, seed0=700000 + 1000 * i) for i in range(K + 1)]
+        R = [rmpc_batch(1, seed0=9500 + i, N=N) for i in range(K + 1)]
+        L = [lmpc_batch(1, seed0=7500 + i) for i in range(K + 1)]
+        line = {}
+        s = dart_mpc.Solver(N=N, Ts=0.002, tol=args.tol, B_max=18)
+        first = s.solve_batch(*P[0])
+        t0 = time.perf_counter()
+        for i in range(1, K + 1):
+            s.solve_batch(*P[i])
+        dt = time.perf_counter() - t0
+        s.close()
+        o = oracle_lib.solve_batch(*P[0], N=N, Ts=0.002, tol=args.tol, nthreads=8, want_w=False)
+        line["pmpc"] = {"solves_per_s": 18 * K / dt, "status_equal": bool(np.array_equal(first["status"], o["status"])),
+                        "iters_equal_frac": float(np.mean(first["iters"] == o["iters"]))}
+        s = dart_mpc.RmpcSolver(N=N, tol=args.tol, B_max=18)
+        k5 = ("x0", "u_prev", "theta", "Rref", "prm")
+        first = s.solve_batch(*(R[0][k] for k in k5))
+        t0 = time.perf_counter()
+        for i in range(1, K + 1):
+            s.solve_batch(*(R[i][k] for k in k5))
+        dt = time.perf_counter() - t0
+        s.close()
+        o = oracle_lib.rmpc_solve_batch(*(R[0][k] for k in k5), N=N, tol=args.tol, nthreads=8, want_w=False)
+        line["rmpc"] = {"solves_per_s": 18 * K / dt, "status_equal": bool(np.array_equal(first["status"], o["status"])),
+                        "iters_equal_frac": float(np.mean(first["iters"] == o["iters"]))}
+        s = dart_mpc.LmpcSolver(N=N, B_max=18)
+        k4 = ("state", "u_prev", "pvec", "target")
+        first = s.solve_batch(*(L[0][k] for k in k4))
+        t0 = time.perf_counter()
+        for i in range(1, K + 1):
+            s.solve_batch(*(L[i][k] for k in k4))
+        dt = time.perf_counter() - t0
+        s.close()
+        o = oracle_lib.lmpc_solve_batch(*(L[0][k] for k in k4), N=N, nthreads=8, want_w=False)
+        line["lmpc"] = {"solves_per_s": 18 * K / dt, "status_equal": bool(np.array_equal(first["status"], o["status"])),
+                        "iters_equal_frac": float(np.mean(first["iters"] == o["iters"])),
+                        "options": "reference (tol 1e-4, acceptable 1e-3 x 5, max_iter 50)"}
+        out[f"N{N}"] = line
     return out
 
 
@@ -994,6 +1049,11 @@ def main():
     if rank == 0 and args.resto_steps > 0:
         pmpc_resto = bench_pmpc_restoration(args, torch, dev, stream, dart_mpc)
 
+    # supplementary: horizons beyond 31 on all three variants
+    long_h = None
+    if rank == 0 and args.long_steps > 0:
+        long_h = bench_long_horizons(args, dart_mpc)
+
     # supplementary PMPC line at the DART driver's horizon (N = 15)
     n15 = None
     if rank == 0 and args.n15_steps > 0:
@@ -1084,6 +1144,7 @@ def main():
             "pmpc_c4": c4,
             "pmpc_restoration": pmpc_resto,
             "pmpc_n15": n15,
+            "long_horizons": long_h,
             "rmpc_c3": rmpc,
             "lmpc_c5": lmpc,
             "arm_qp": arm,

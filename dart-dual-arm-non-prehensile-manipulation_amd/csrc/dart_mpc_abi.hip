@@ -15,6 +15,7 @@
 #include "dart_mpc.h"
 #include "pmpc_ipm.h"
 #include "pmpc_model.h"
+#include "wave.h"
 #include "rmpc_ipm.h"
 #include "lmpc_ipm.h"
 #include "lmpc_policy.h"
@@ -229,7 +230,7 @@ int fail(dart_mpc_handle* h, int code, const char* what, hipError_t e = hipSucce
 int check_cfg(const dart_mpc_config* c) {
     if (!c) return 0;
     if (c->variant != DART_MPC_PMPC && c->variant != DART_MPC_RMPC && c->variant != DART_MPC_LMPC) return 0;
-    if (c->N < 1 || c->N > (c->variant == DART_MPC_PMPC ? 63 : 31)) return 0;
+    if (c->N < 1 || c->N > 63) return 0;
     if (!(c->Ts > 0.0) || !(c->tol > 0.0) || !(c->gravity == c->gravity) || c->max_iter < 1 || c->B_max < 1) return 0;
     if (c->acceptable_iter < 0 || (c->acceptable_iter > 0 && !(c->acceptable_tol > 0.0))) return 0;
     if (c->max_soc < 0 || c->max_soc > 8) return 0;
@@ -371,8 +372,15 @@ int server_stop(dart_mpc_handle* h) {
 // of queueing for the CUs of one
 int stream_state(dart_mpc_handle* h, int B, hipStream_t s, double** out, int* xcd) {
     *out = nullptr;
-    const size_t per = h->cfg.variant == DART_MPC_PMPC ? (size_t)dartmpc::kPmHo : (size_t)64 * 16;
-    const size_t need = h->cfg.restoration ? (size_t)B * per : 0;
+    // per instance: PMPC's hand-off state, LMPC's hand-off state (N > 31: and the two-wave build's second-order-
+    // correction and restoration state, needed with or without the restoration phases), RMPC's two-wave
+    // restoration state
+    const bool wg2 = h->cfg.N > 31 || dartmpc::force_wg2();
+    const size_t per = h->cfg.variant == DART_MPC_PMPC   ? (size_t)dartmpc::kPmHo
+                       : h->cfg.variant == DART_MPC_RMPC ? (dartmpc_rmpc_wg2_resto_bytes() + 7) / 8
+                       : wg2                             ? dartmpc_lmpc_wg2_area_doubles()
+                                                         : (size_t)64 * 16;
+    const size_t need = (h->cfg.restoration || (wg2 && h->cfg.variant == DART_MPC_LMPC)) ? (size_t)B * per : 0;
     dart_mpc_handle::RestoArea* r = nullptr;
     for (auto& e : h->resto)
         if (e.s == s) r = &e;
@@ -711,7 +719,13 @@ int dart_rmpc_solve_batch_dev(dart_mpc_handle* h, int B, const double* x0, const
     a.x0 = x0; a.u_prev = u_prev; a.theta = theta; a.rls_P = rls_P; a.rls_phi = rls_phi; a.rls_y = rls_y;
     a.rls_lambda = rls_lambda; a.Rref = Rref; a.prm = prm; a.w_warm = w_warm;
     a.u0 = u0; a.f = f; a.w_out = w_out; a.status = status; a.iters = iters;
-    HIPCHK(h, dartmpc_launch_rmpc(&a, stream ? (hipStream_t)stream : h->stream), "kernel launch");
+    a.resto_buf = nullptr;
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    if ((a.N > 31 || dartmpc::force_wg2()) && a.resto) {      // the two-wave build's restoration state, one area per stream
+        int xcd = 0;
+        if (int rc = stream_state(h, B, s, &a.resto_buf, &xcd)) return rc;
+    }
+    HIPCHK(h, dartmpc_launch_rmpc(&a, s), "kernel launch");
     return DART_MPC_OK;
 }
 

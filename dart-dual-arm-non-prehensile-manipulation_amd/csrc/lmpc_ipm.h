@@ -18,7 +18,8 @@ struct LmpcArgs {
     double mult_init_max;    // IPOPT constr_mult_init_max: > 0 least-square starting multipliers (default 1000)
     int resto;               // IPOPT's soft restoration and restoration phases after a failed line search (1)
     long long max_ticks;     // IPOPT max_cpu_time in ticks of the 100 MHz constant clock (s_memrealtime), 0 = off
-    double* resto_buf;       // [B][64][16] hand-off of instances entering them (device workspace of the handle)
+    double* resto_buf;       // [B][64][16] hand-off of instances entering them (device workspace of the handle);
+                             // N > 31: [B][128][16], then B x LmAux (dartmpc_lmpc_wg2_area_doubles per instance)
     int pack;                // blocks per instance slot (set by the launcher; 8 = one XCD for small B)
     int xcd;                 // that XCD (0-7): the working blocks are those with blockIdx % pack == xcd % pack
     const double* state;     // [B][8]  [px, vx, py, vy, theta_x, omega_x, theta_y, omega_y]
@@ -42,3 +43,5 @@ struct LmpcArgs {
 
 extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStream_t stream);
 extern "C" size_t dartmpc_lmpc_lds_bytes(void);
+extern "C" hipError_t dartmpc_launch_lmpc_wg2(const void* args, hipStream_t stream);
+extern "C" size_t dartmpc_lmpc_wg2_area_doubles();

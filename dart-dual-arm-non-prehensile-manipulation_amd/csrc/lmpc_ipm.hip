@@ -24,6 +24,16 @@
 // one LDS round trip per node).  Exact derivatives as IPOPT gets them from CasADi: per
 // direction of z = [x; u], the RK4 tangent (a column of the step Jacobian) and a second-order
 // adjoint sweep back through the four stages (a column of the exact Hessian of lambda^T x+).
+//
+// Horizons N = 32..63: this file built a second time with -DDART_WG=2 (Makefile: lmpc_wg2.o) -- a workgroup of two
+// waves per instance, wave w owning nodes 32 w .. 32 w + 31 of both halves (wave.h: the wave reductions and node
+// shifts combine the two waves, the Riccati and forward sweeps run in both on the shared LDS).  The 64-node stage
+// arrays fill the LDS, so that build keeps the second-order-correction scratch and the restoration-phase state in
+// a per-instance device area after the hand-off states (LmpcArgs::resto_buf), runs the policy step of a fused call
+// as its own launch, and queues the restoration kernel.  Its symbols sit in their own namespace.
+#if DART_WG == 2
+#define dartmpc dartmpc_wg2
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -36,7 +46,7 @@
 
 namespace dartmpc {
 
-constexpr int LM_NMAXS = 32;      // node slots per half (N <= 31)
+constexpr int LM_NMAXS = 32 * kWaves;      // node slots per half (N <= 31; two-wave build N <= 63)
 constexpr int LM_NSC = 5;         // stage-dependent tangent coefficients per RK stage
 constexpr double LM_G = 9.81;     // rlmpc2.py:354
 using LmLds = OcpLdsS<5, LM_NMAXS>;
@@ -64,10 +74,16 @@ struct LmSub {
     double h;               // Ts
 };
 
-struct LmShared {
-    LmLds ocp;
+struct LmSoc {
     NodeArr<double[5], 2 * LM_NMAXS> CS;     // second-order correction: c_soc rows of node k (incoming defect)
     NodeArr<double[11], 2 * LM_NMAXS> SV;    // second-order correction: the plain step (dx~, lambda+, du)
+};
+
+struct LmShared {
+    LmLds ocp;
+#if DART_WG == 1
+    LmSoc soc;                      // (two-wave build: in the device area, LmAux)
+#endif
     LmSub sub[2];                   // uniform problem data of the two halves
     double W[2][2][4], tg[2][4], st0[2][4];   // [half][stage, terminal] weights, target, x_0 (local order)
 };
@@ -215,9 +231,19 @@ __device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const Riccati
 // dynamic LDS: LmShared, then the policy step's PolicyLds (fused launches of lmpc_ipm_kernel<false>) or
 // LmResto (lmpc_ipm_kernel<true>) at the same offset
 constexpr size_t kLmPolicyLdsOff = (sizeof(LmShared) + 15) & ~size_t(15);
+#if DART_WG == 1
 constexpr size_t kLmRestoOff = kLmPolicyLdsOff;
 constexpr size_t kLmLdsBytes = kLmPolicyLdsOff + (sizeof(PolicyLds) > sizeof(LmResto) ? sizeof(PolicyLds) : sizeof(LmResto));
 static_assert(kLmLdsBytes <= 160 * 1024, "LDS of one CU");
+#else
+// two-wave build: LmShared alone (the policy step runs as its own launch; LmSoc and LmResto in the device area)
+constexpr size_t kLmLdsBytes = kLmPolicyLdsOff;
+static_assert(kLmLdsBytes + sizeof(g_wg_x) <= 160 * 1024, "LDS of one CU");
+struct LmAux {
+    LmSoc soc;
+    LmResto resto;
+};
+#endif
 // hand-off of an instance whose filter line search failed: its iteration-start state goes to HBM
 // (LmpcArgs::resto_buf, kLmNst doubles per lane) and lmpc_ipm_kernel<true> resumes it
 constexpr int kLmNeedResto = -100;
@@ -435,12 +461,20 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     LmShared& SH = *reinterpret_cast<LmShared*>(smem);
     LmLds* S = &SH.ocp;
+#if DART_WG == 1
     LmResto* RL = reinterpret_cast<LmResto*>(smem + kLmRestoOff);
+    LmSoc& SO = SH.soc;
+#else
+    LmAux* const AX = reinterpret_cast<LmAux*>(a.resto_buf + (size_t)a.B * kWave * kWaves * kLmNst) + b;
+    LmResto* RL = &AX->resto;
+    LmSoc& SO = AX->soc;
+#endif
     const RiccatiSRoles RR = riccati_s_roles<LmLds>();
     STAMP_DECL
     const int lane = lane_id();
+    const int ql = kWave * wave_idx() + lane;      // this lane's slot in the per-lane hand-off state
     const int hf = lane >> 5;                  // subsystem: 0 = x [px, vx, th_y, om_y; a], 1 = y [py, vy, th_x, om_x; b]
-    const int k = lane & 31;                   // shooting node
+    const int k = node_base() + (lane & 31);   // shooting node
     const int sl = hf * LM_NMAXS + k;          // node slot of this lane (every lane owns one)
     const int N = a.N;
     // fused policy step (C5: the learned parameter net in the same launch as the shooting defects it
@@ -457,9 +491,14 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
     // below is wave-uniform
     unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     if constexpr (RESTO)
-        t_start -= (unsigned long long)a.resto_buf[(size_t)b * kWave * kLmNst + 6 * kLmNst + kLmNst - 1];
+        t_start -= (unsigned long long)a.resto_buf[(size_t)b * kWave * kWaves * kLmNst + 6 * kLmNst + kLmNst - 1];
     auto out_of_time = [&]() {
+#if DART_WG == 1
         return a.max_ticks > 0 && (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.max_ticks;
+#else
+        // (each wave reads its own clock: the two decide together)
+        return wany(a.max_ticks > 0 && (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.max_ticks);
+#endif
     };
     const bool xon = k <= N, uon = k < N;
     constexpr int NC = LmLds::NC;
@@ -600,7 +639,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
             Hk[hp(5, 4)] = -sc * 2.0 * Rdu;
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) SH.CS[sl][i] = xn[i];       // x+ of iteration 0 (CS is free until then)
+        for (int i = 0; i < 4; ++i) SO.CS[sl][i] = xn[i];       // x+ of iteration 0 (CS is free until then)
         double rs[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -647,8 +686,8 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
     int in_soft = 0, soft_count = 0;       // IPOPT's soft restoration phase (BacktrackingLineSearch)
     int it_start = lsinit ? -1 : 0;
     if constexpr (RESTO) {      // resume a handed-off instance at the start of its failed iteration
-        const double* st = a.resto_buf + ((size_t)b * kWave + lane) * kLmNst;
-        const double* sc0 = a.resto_buf + (size_t)b * kWave * kLmNst + kLmNst - 1;
+        const double* st = a.resto_buf + ((size_t)b * kWave * kWaves + ql) * kLmNst;
+        const double* sc0 = a.resto_buf + (size_t)b * kWave * kWaves * kLmNst + kLmNst - 1;
 #pragma unroll
         for (int i = 0; i < 4; ++i) x[i] = st[i];
         up = st[4]; u = st[5];
@@ -740,7 +779,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
             double xn[4];
             if (it <= 0 && (lsm || !lsinit)) {      // the setup's derivative pass (lambda = 0: J^T lambda = 0)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) xn[i] = SH.CS[sl][i];
+                for (int i = 0; i < 4; ++i) xn[i] = SO.CS[sl][i];
 #pragma unroll
                 for (int i = 0; i < 5; ++i) jl[i] = 0.0;
             } else {
@@ -789,7 +828,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                 pl = fmax(pl, xon ? d * fabs(gi) : 0.0);
                 plu = fmax(plu, xon ? fabs(gi) : 0.0);
                 if (k == 0) S->dx0[hf][i] = -gi;
-                SH.CS[sl][i] = gi;       // c(x) for a second-order correction
+                SO.CS[sl][i] = gi;       // c(x) for a second-order correction
             }
             pinf = pl; pinf_u = plu;
         }
@@ -998,7 +1037,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
             if (soc >= 0) {
                 double cs[5];
 #pragma unroll
-                for (int i = 0; i < 5; ++i) cs[i] = xon ? SH.CS[sl][i] : 0.0;
+                for (int i = 0; i < 5; ++i) cs[i] = xon ? SO.CS[sl][i] : 0.0;
 #pragma unroll
                 for (int r = 0; r < 5; ++r) {
                     const double t = from_next(cs[r]);
@@ -1014,7 +1053,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                 for (;;) {
                     ok = riccati_s_sweep(S, N, RR);
 #ifdef DART_RESTO_TRACE
-                    if (blockIdx.x == 0 && it <= 0 && attempt < 3) {
+                    if (blockIdx.x == 0 && (it <= 0 || (RESTO && it == it_start)) && attempt < 3) {
                         bool fin = true;
                         if (uon) {
                             for (int e = 0; e < LmLds::NTP; ++e) fin = fin && isfinite(Hk[e]);
@@ -1024,10 +1063,10 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                         const bool qbad = uon && !(q > 0.0 && isfinite(q));
                         const unsigned long long nf = __ballot(!fin), nq = __ballot(qbad);
                         if (lane == 0)
-                            printf("  it %d attempt %d delta %.2e ok %d  lanes with non-finite H/M %llx  lanes with Quu<=0 %llx\n",
-                                   it, attempt, delta, (int)ok, nf, nq);
+                            printf("  wave %d it %d attempt %d delta %.2e ok %d  lanes with non-finite H/M %llx  lanes with Quu<=0 %llx\n",
+                                   wave_idx(), it, attempt, delta, (int)ok, nf, nq);
                         if (qbad && (nq & ((1ull << lane) - 1)) == 0)
-                            printf("    first bad lane %d (node %d half %d) Quu %.3e  H diag %.3e %.3e %.3e %.3e %.3e %.3e\n", lane, k,
+                            printf("    wave %d first bad lane %d (node %d half %d) Quu %.3e  H diag %.3e %.3e %.3e %.3e %.3e %.3e\n", wave_idx(), lane, k,
                                    hf, q, Hk[hp(0, 0)], Hk[hp(1, 1)], Hk[hp(2, 2)], Hk[hp(3, 3)], Hk[hp(4, 4)], Hk[hp(5, 5)]);
                     }
 #endif
@@ -1102,10 +1141,10 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                         if (xon) {      // c_soc = alpha c(x) + c(x_trial); keep the plain step
 #pragma unroll
                             for (int i = 0; i < 5; ++i) {
-                                SH.CS[sl][i] = fma(alpha, SH.CS[sl][i], gt[i]);
-                                SH.SV[sl][i] = dx[i]; SH.SV[sl][5 + i] = lamp[i];
+                                SO.CS[sl][i] = fma(alpha, SO.CS[sl][i], gt[i]);
+                                SO.SV[sl][i] = dx[i]; SO.SV[sl][5 + i] = lamp[i];
                             }
-                            SH.SV[sl][10] = dU;
+                            SO.SV[sl][10] = dU;
                         }
                         th_prev = th_t; soc = 0; resolve = true;
                         break;
@@ -1120,15 +1159,15 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                     if (soc + 1 < a.max_soc && th_t <= 0.99 * th_prev) {
                         if (xon) {      // c_soc <- alpha_soc c_soc + c(x_soc trial)
 #pragma unroll
-                            for (int i = 0; i < 5; ++i) SH.CS[sl][i] = fma(al_try, SH.CS[sl][i], gt[i]);
+                            for (int i = 0; i < 5; ++i) SO.CS[sl][i] = fma(al_try, SO.CS[sl][i], gt[i]);
                         }
                         th_prev = th_t; ++soc; resolve = true;
                         break;
                     }
                     if (xon) {      // corrections failed: back to the plain step, backtrack
 #pragma unroll
-                        for (int i = 0; i < 5; ++i) { dx[i] = SH.SV[sl][i]; lamp[i] = SH.SV[sl][5 + i]; }
-                        dU = SH.SV[sl][10];
+                        for (int i = 0; i < 5; ++i) { dx[i] = SO.SV[sl][i]; lamp[i] = SO.SV[sl][5 + i]; }
+                        dU = SO.SV[sl][10];
                     }
                     soc = -1;
                 }
@@ -1150,7 +1189,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
         if constexpr (!RESTO) {
             if (!accepted && a.resto) {
                 // hand-off to lmpc_ipm_kernel<true>: the state of this iteration's start to HBM
-                double* st = a.resto_buf + ((size_t)b * kWave + lane) * kLmNst;
+                double* st = a.resto_buf + ((size_t)b * kWave * kWaves + ql) * kLmNst;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) st[i] = x[i];
                 st[4] = up; st[5] = u;
@@ -1897,7 +1936,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
 
     // ---------------- outputs -------------------------------------------------------------
     const double fval = wsum(cost_val(x, u, up));
-    if (lane == 0) { a.f[b] = fval; a.status[b] = status; a.iters[b] = it; }
+    if (lane == 0 && wave_idx() == 0) { a.f[b] = fval; a.status[b] = status; a.iters[b] = it; }
     if (k == 0) a.u0[2 * b + hf] = u;
     if (a.w_out) {
         double* wo = a.w_out + (size_t)nw * b;
@@ -1931,7 +1970,7 @@ __device__ __noinline__ void lmpc_resto_tail(const int b, const unsigned long lo
 // reload the parked state and continue from the failed iteration.  FUSE (batches of at most 32): the flagged
 // instances continue in lmpc_resto_tail in the same launch.
 template <bool RESTO, bool FUSE = false>
-__global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
+__global__ __launch_bounds__(kWave * kWaves) void lmpc_ipm_kernel(LmpcArgs a) {
     // small batches packed onto one XCD (launcher; blocks go round robin over the 8 XCDs)
     if (blockIdx.x % a.pack != (unsigned)(a.xcd % a.pack)) return;
     const int b = blockIdx.x / a.pack;
@@ -1946,10 +1985,58 @@ __global__ __launch_bounds__(kWave) void lmpc_ipm_kernel(LmpcArgs a) {
 
 }  // namespace dartmpc
 
+#if DART_WG == 2
+// N = 32..63 (dartmpc_launch_lmpc forwards here): one instance per two-wave workgroup.  Device area per instance:
+// the hand-off state of its 128 lanes, then LmAux (second-order-correction scratch, restoration state).
+extern "C" size_t dartmpc_lmpc_wg2_area_doubles() {
+    return (size_t)dartmpc::kWave * dartmpc::kWaves * dartmpc::kLmNst + (sizeof(dartmpc::LmAux) + 7) / 8;
+}
+extern "C" hipError_t dartmpc_launch_lmpc_wg2(const void* args, hipStream_t stream) {
+    dartmpc::LmpcArgs a = *static_cast<const dartmpc::LmpcArgs*>(args);
+    if (a.N < (dartmpc::force_wg2() ? 1 : 32) || a.N >= dartmpc::LM_NMAXS) return hipErrorInvalidValue;
+    if (!a.resto_buf) return hipErrorInvalidValue;          // the device area is needed with or without resto
+    static std::mutex mu;
+    static bool attr_set[64] = {};
+    const size_t lds = dartmpc::kLmLdsBytes;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (!attr_set[dev]) {
+            e = hipFuncSetAttribute((const void*)dartmpc::lmpc_ipm_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)dartmpc::lmpc_ipm_kernel<true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+            attr_set[dev] = true;
+        }
+    }
+    if (a.fuse_policy) {        // the policy step of every instance first (its own launch, same stream)
+        e = dartmpc_launch_policy(&a.pol, stream);
+        if (e != hipSuccess) return e;
+        a.pvec = a.pol.model_params;
+        a.fuse_policy = 0;
+    }
+    a.pack = 1; a.xcd = 0;
+    const dim3 block(dartmpc::kWave * dartmpc::kWaves);
+    hipLaunchKernelGGL(dartmpc::lmpc_ipm_kernel<false>, dim3(a.B), block, lds, stream, a);
+    if (a.resto) {
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(dartmpc::lmpc_ipm_kernel<true>, dim3(a.B), block, lds, stream, a);
+    }
+    return hipGetLastError();
+}
+#else
+
 extern "C" size_t dartmpc_lmpc_lds_bytes(void) { return dartmpc::kLmLdsBytes; }
 
 extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStream_t stream) {
     if (args->B <= 0) return hipSuccess;
+    if ((args->N >= dartmpc::LM_NMAXS || dartmpc::force_wg2()) && args->N < 2 * dartmpc::LM_NMAXS)
+        return dartmpc_launch_lmpc_wg2(args, stream);
     if (args->N < 1 || args->N >= dartmpc::LM_NMAXS) return hipErrorInvalidValue;
     if (args->resto && !args->resto_buf) return hipErrorInvalidValue;
     // the dynamic-LDS opt-in is per device: set once for every device a launch goes to (thread-safe)
@@ -1999,3 +2086,4 @@ extern "C" hipError_t dartmpc_read_stamps_lmpc(unsigned long long* host_out) {
                                hipMemcpyDeviceToHost);
 }
 #endif
+#endif  // DART_WG

@@ -474,7 +474,7 @@ struct NoPost {
 template <class P> struct IsNoPost { static constexpr bool value = false; };
 template <> struct IsNoPost<NoPost> { static constexpr bool value = true; };
 
-// Gains and closed-loop matrices for the forward sweep, lanes k and k + 32 per node (N <= 32): both
+// Gains and closed-loop matrices for the forward sweep, lanes k and k + 32 per node (of the calling wave): both
 // form [K | k] = -Quu^-1 Guz, lane k writes it, and the rows of Phi_k = A_k + B_k K_k, f_k = c_k + B_k k_k
 // split between them.  Ends with a barrier.
 // post(k) (restoration phase: the rows mapped through node k+1's soft rows) runs on the node lanes k < N
@@ -482,7 +482,7 @@ template <> struct IsNoPost<NoPost> { static constexpr bool value = true; };
 template <class L, class Post = NoPost>
 __device__ void closed_loop(L* S, int N, Post post = Post()) {
     constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, RH = (NXA + 1) / 2;
-    const int k = lane_id() & 31, rb = lane_id() >= 32 ? RH : 0;
+    const int k = node_base() + (lane_id() & 31), rb = lane_id() >= 32 ? RH : 0;
     if (k < N) {
         // LDS reads grouped ahead of the writes (the compiler cannot prove F, KK and M disjoint and
         // would otherwise wait out each read before the next write)
@@ -758,7 +758,7 @@ __device__ bool riccati_s_sweep(L* S, int N, const RiccatiSRoles& R) {
 template <class L, class Post = NoPost>
 __device__ void closed_loop_s(L* S, int N, Post post = Post()) {
     constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND;
-    const int k = lane_id() & 31, sl = (lane_id() >> 5) * L::NMAXS + k;
+    const int k = node_base() + (lane_id() & 31), sl = (lane_id() >> 5) * L::NMAXS + k;
     if (k < N) {
         // every LDS read before the first write (the compiler cannot prove F, KK and M disjoint and
         // would otherwise wait out each read before the next write)

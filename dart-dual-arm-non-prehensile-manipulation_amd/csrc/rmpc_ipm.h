@@ -28,10 +28,14 @@ struct RmpcArgs {
     double* w_out;           // [B][4(N+1)+2N] nullable
     int32_t* status;         // [B]
     int32_t* iters;          // [B]
+    double* resto_buf;       // N > 31 with resto: B x dartmpc_rmpc_wg2_resto_bytes() of device memory (the
+                             // two-wave build's restoration state), else unused
 };
 
 }  // namespace dartmpc
 
 extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStream_t stream);
+extern "C" hipError_t dartmpc_launch_rmpc_wg2(const void* args, hipStream_t stream);
+extern "C" size_t dartmpc_rmpc_wg2_resto_bytes();
 extern "C" hipError_t dartmpc_launch_rls(int B, double* theta, double* P, const double* phi, const double* y,
                                          double lam, hipStream_t stream);

@@ -32,6 +32,15 @@
 // their instance was handed over, the others solve the instance again from its start (the same iterates up
 // to the failure) with both phases available, to the end of the solve.  No state crosses the hand-off but
 // the status word in the caller's output array, so launches on different streams cannot interfere.
+// Horizons N = 32..63: this file built a second time with -DDART_WG=2 (Makefile: rmpc_wg2.o) -- a workgroup of
+// two waves per instance, wave w owning nodes 32 w .. 32 w + 31 with the lane roles above (wave.h: the wave
+// reductions and node shifts combine the two waves, the Riccati and forward sweeps run in both on the shared
+// LDS); its restoration-phase state lives in a per-instance global-memory area instead of LDS (RmpcArgs::
+// resto_buf), which the 64-node arrays of the solve leave no room for.  The build's symbols sit in their own
+// namespace.
+#if DART_WG == 2
+#define dartmpc dartmpc_wg2
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -44,7 +53,7 @@
 
 namespace dartmpc {
 
-constexpr int RM_NMAXS = 32;      // max shooting nodes (N <= 31)
+constexpr int RM_NMAXS = 32 * kWaves;      // max shooting nodes (N <= 31, two-wave build N <= 63)
 constexpr int RM_NIQ = 6;         // inequality rows per node: du_x, du_y, vx-vmax, -vx-vmax, vy-vmax, -vy-vmax
 constexpr int RM_NQ = 3;          // of them per lane: rows 0..2 on lane k, rows 3..5 on its mirror lane k + 32
 static_assert(2 * RM_NQ == RM_NIQ, "the node and mirror lanes split the rows evenly");
@@ -82,8 +91,8 @@ enum { V_DX = 0, V_LP = 6, V_DU = 12, V_DY = 14, V_DS = 17, V_DQP = 20, V_DQN = 
 struct RmResto {
     RmSoft soft;
     NodeArr<double[P_N], RM_NMAXS + 1> PN;
-    NodeArr<double[Q_N], kWave> Q;
-    NodeArr<double[V_N], kWave> SV, SV2;
+    NodeArr<double[Q_N], kWave * kWaves> Q;
+    NodeArr<double[V_N], kWave * kWaves> SV, SV2;
 };
 
 // closed-loop rows of node k mapped through node k+1's soft rows: [Phi | f](r) <- Y(r, :) [[Phi | f]; 0 1]
@@ -284,7 +293,11 @@ __device__ __forceinline__ void rm_iq3(const double* z, double vmax, bool mir, d
 // The LDS of the solve (one instance per workgroup), at namespace scope: a kernel is given the blocks its code
 // reaches (70.6 KB without the restoration phases, 151.7 KB with them)
 __shared__ RmShared g_rm_sh;
+#if DART_WG == 1
 __shared__ RmResto g_rm_resto;
+#else
+static_assert(sizeof(RmShared) + sizeof(g_wg_x) <= 160 * 1024, "the two-wave solve fits the LDS of a CU");
+#endif
 
 // The solve of instance b by the calling wave.  RESTO = false: the kernel of every launch, without IPOPT's
 // restoration phases; an instance whose filter line search fails is handed over (status kRmNeedResto, no other
@@ -295,13 +308,18 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
     RmShared& SH = g_rm_sh;
     RmLds* S = &SH.ocp;
     RmResto* RL = nullptr;
+#if DART_WG == 1
     if constexpr (RESTO) RL = &g_rm_resto;
+#else
+    if constexpr (RESTO) RL = reinterpret_cast<RmResto*>(a.resto_buf) + b;
+#endif
     STAMP_DECL
     // lane k and its mirror lane k + 32 both own node k: the node work runs on both, the slack rows are
     // split (rm_iq3), and sums over the wave count the node terms on the node lanes only
     const int lane = lane_id();
-    const int k = lane & 31;
+    const int k = node_base() + (lane & 31);
     const bool mir = lane >= 32, nod = !mir;
+    const int ql = kWave * wave_idx() + lane;      // this lane's slot in the per-lane restoration arrays
     const int N = a.N;
     const bool xon = k <= N, uon = k < N;
     const double* pr = a.prm + 10 * b;
@@ -345,9 +363,12 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
             thn = a.theta[14 * b + lane] + SH.rls_Pphi[ax][i] / den[ax] * err[ax];
         }
         __syncthreads();          // every lane has read P, theta before anyone writes
+        if (wave_idx() == 0) {
 #pragma unroll
-        for (int r = 0; r < 2; ++r) if (idx[r] < 98) Pg[idx[r]] = pnew[r];
-        if (lane < 14) { a.theta[14 * b + lane] = thn; SH.theta[lane] = thn; }
+            for (int r = 0; r < 2; ++r) if (idx[r] < 98) Pg[idx[r]] = pnew[r];
+            if (lane < 14) a.theta[14 * b + lane] = thn;
+        }
+        if (lane < 14) SH.theta[lane] = thn;
     } else if (lane < 14) {
         SH.theta[lane] = a.theta[14 * b + lane];
     }
@@ -1065,7 +1086,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
         RmResto& RS = *RL;
         RmSoft* const SR = &RS.soft;
         double* const pn = RS.PN[xon ? k : RM_NMAXS];      // node k's physical rows (written by the node lane)
-        double* const q = RS.Q[lane];                      // this lane's three inequality rows
+        double* const q = RS.Q[ql];                        // this lane's three inequality rows
         const double mu0 = mu, th0 = theta, phi0 = phi_rs, tau0 = fmax(0.99, 1.0 - mu0), rho = 1000.0;
         const double nbr = 24.0 * N + 8.0 * (N + 1);       // bound-multiplier count of the restoration problem
         aug_soft_init<RmLds, 4>(SR);
@@ -1692,7 +1713,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
 #endif
                 if (!(emax > 1e-12 * (1.0 + smax))) return false;
                 // the correction solve: lambda = y = 0, the residuals as gradient and right-hand sides
-                park(RS.SV2[lane]);
+                park(RS.SV2[ql]);
                 double gsave[8], offc[RM_NQ];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) gsave[j] = (uon && nod) ? Hk[hp(8, j)] : (k == N && nod && j < 6 ? S->G[N][hp(8, j)] : 0.0);
@@ -1705,7 +1726,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                 (void)riccati_sweep_aug_soft<RmLds, 4>(S, SR, N);
                 rstep();
                 rdirs(eq, offc, es, eqp, eqn, zero6, zero6, ep, en);
-                unpark(RS.SV2[lane], true);
+                unpark(RS.SV2[ql], true);
                 if (uon && nod) {
 #pragma unroll
                     for (int j = 0; j < 8; ++j) Hk[hp(8, j)] = gsave[j];
@@ -1863,7 +1884,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                         if (ls == 0 && a.max_soc > 0 && !(tht < thr)) {
                             // second-order correction on the restoration problem's constraints; the plain step
                             // is parked in LDS
-                            park(RS.SV[lane]);
+                            park(RS.SV[ql]);
 #pragma unroll
                             for (int i = 0; i < 6; ++i) csg[i] = fma(alr, cg[i], cgt[i]);
 #pragma unroll
@@ -1883,7 +1904,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                             break;
                         }
                         // the corrections failed: back to the plain step and its multiplier steps
-                        unpark(RS.SV[lane], false);
+                        unpark(RS.SV[ql], false);
                         const double amr_keep = amr;
                         pn_steps();
                         amr = amr_keep;
@@ -2030,11 +2051,11 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
 
     // ---------------- outputs -------------------------------------------------------------
     if (!RESTO && status == kRmNeedResto) {     // handed over: rmpc_solve<true> writes the outputs
-        if (lane == 0) a.status[b] = status;
+        if (lane == 0 && wave_idx() == 0) a.status[b] = status;
         return true;
     }
     const double fval = wsum_rl(nod ? cost_val(x, u, up) : 0.0);
-    if (lane == 0) {
+    if (lane == 0 && wave_idx() == 0) {
         a.u0[2 * b] = u[0]; a.u0[2 * b + 1] = u[1];
         a.f[b] = fval; a.status[b] = status; a.iters[b] = it;
     }
@@ -2056,7 +2077,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
 // registers (the call ABI's SGPRs spill into a VGPR), and the spilled main loop measured C3 -4.7 % against
 // +1.7 % for the saved dispatch; profiles/r05/fuse_ab.txt)
 template <bool RESTO>
-__global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
+__global__ __launch_bounds__(kWave * kWaves) void rmpc_ipm_kernel(RmpcArgs a) {
     if (blockIdx.x % a.pack) return;          // small batches packed onto one XCD (launcher)
     const int b = blockIdx.x / a.pack;
     if constexpr (RESTO) {
@@ -2065,6 +2086,7 @@ __global__ __launch_bounds__(kWave) void rmpc_ipm_kernel(RmpcArgs a) {
     (void)rmpc_solve<RESTO>(a, b);
 }
 
+#if DART_WG == 1
 // Standalone batched RLS.update (np_mpc...:17-27): one p = 7 filter per workgroup, lanes as entries.
 __global__ __launch_bounds__(kWave) void rls_update_kernel(int B, double* theta, double* P, const double* phi,
                                                           const double* y, double lam) {
@@ -2092,8 +2114,27 @@ __global__ __launch_bounds__(kWave) void rls_update_kernel(int B, double* theta,
     if (l < 49) Pb[l] = pn;
     if (l < 7) theta[7 * b + l] = th[l] + Pphi[l] / den * err;
 }
+#endif
 
 }  // namespace dartmpc
+
+#if DART_WG == 2
+// N = 32..63 (dartmpc_launch_rmpc forwards here): one instance per two-wave workgroup
+extern "C" size_t dartmpc_rmpc_wg2_resto_bytes() { return sizeof(dartmpc::RmResto); }
+extern "C" hipError_t dartmpc_launch_rmpc_wg2(const void* args, hipStream_t stream) {
+    dartmpc::RmpcArgs a = *static_cast<const dartmpc::RmpcArgs*>(args);
+    if (a.N < (dartmpc::force_wg2() ? 1 : 32) || a.N >= dartmpc::RM_NMAXS) return hipErrorInvalidValue;
+    if (a.resto && !a.resto_buf) return hipErrorInvalidValue;
+    a.pack = 1;
+    const dim3 block(dartmpc::kWave * dartmpc::kWaves);
+    hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel<false>, dim3(a.B), block, 0, stream, a);
+    if (a.resto) {
+        if (hipError_t e = hipGetLastError()) return e;
+        hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel<true>, dim3(a.B), block, 0, stream, a);
+    }
+    return hipGetLastError();
+}
+#else
 
 extern "C" hipError_t dartmpc_launch_rls(int B, double* theta, double* P, const double* phi, const double* y,
                                          double lam, hipStream_t stream) {
@@ -2104,13 +2145,19 @@ extern "C" hipError_t dartmpc_launch_rls(int B, double* theta, double* P, const 
 
 extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStream_t stream) {
     if (args->B <= 0) return hipSuccess;
+    if ((args->N >= dartmpc::RM_NMAXS || dartmpc::force_wg2()) && args->N < 2 * dartmpc::RM_NMAXS)
+        return dartmpc_launch_rmpc_wg2(args, stream);
     if (args->N < 1 || args->N >= dartmpc::RM_NMAXS) return hipErrorInvalidValue;
     dartmpc::RmpcArgs a = *args;
     a.pack = (a.B <= 32) ? 8 : 1;            // blocks go round-robin over the 8 XCDs: one XCD, one L2 for the code
     hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel<false>, dim3(a.B * a.pack), dim3(dartmpc::kWave), 0, stream, a);
     if (a.resto) {      // the instances whose line search failed, with IPOPT's restoration phases
         if (hipError_t e = hipGetLastError()) return e;
-        hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel<true>, dim3(a.B * a.pack), dim3(dartmpc::kWave), 0, stream, a);
+        // one block per instance (not B x pack): the blocks of the instances that were not handed over return at
+        // once, and fewer of them make the queued kernel cheaper on the launches that need no restoration
+        dartmpc::RmpcArgs r = a;
+        r.pack = 1;
+        hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel<true>, dim3(r.B), dim3(dartmpc::kWave), 0, stream, r);
     }
     return hipGetLastError();
 }
@@ -2121,3 +2168,4 @@ extern "C" hipError_t dartmpc_read_stamps_rmpc(unsigned long long* host_out) {
                                hipMemcpyDeviceToHost);
 }
 #endif
+#endif  // DART_WG

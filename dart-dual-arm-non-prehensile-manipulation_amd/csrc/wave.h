@@ -34,6 +34,15 @@ inline bool resto_fuse_enabled() {
     }();
     return on;
 }
+// host, diagnostic: DART_FORCE_WG2=1 runs RMPC and LMPC on their two-wave builds at every N (A/B of the two-wave
+// machinery against the one-wave kernels on the same instances; tools/wg2_ab.py)
+inline bool force_wg2() {
+    static const bool on = [] {
+        const char* e = getenv("DART_FORCE_WG2");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 template <class T>
 __device__ __forceinline__ T kernarg_load(unsigned long long addr) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -46,6 +55,47 @@ __device__ __forceinline__ T kernarg_load(unsigned long long addr) {
 }
 
 constexpr int kWave = 64;
+
+// Waves per instance.  1: the kernels as written (one wave64 per instance, lane k and k + 32 own node k, N <= 31).
+// 2: the DART_WG=2 builds of the RMPC and LMPC kernels for N = 32..63 -- a workgroup of two waves, wave w owns
+// nodes 32 w .. 32 w + 31 with the one-wave lane roles.  There every wave reduction below and the node shifts
+// from_prev / from_next combine the two waves through LDS (two barriers each), and the node-coupled sweeps of
+// ocp_wave.h run redundantly in both waves on the shared LDS data (equal values written twice), so the solver
+// code above these primitives is the one-wave code.
+#ifndef DART_WG
+#define DART_WG 1
+#endif
+constexpr int kWaves = DART_WG;
+static_assert(kWaves == 1 || kWaves == 2, "one or two waves per instance");
+
+__device__ __forceinline__ int wave_idx() {
+#if DART_WG == 2
+    return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#else
+    return 0;
+#endif
+}
+// the first node of the calling wave
+__device__ __forceinline__ int node_base() { return 32 * wave_idx(); }
+
+#if DART_WG == 2
+__shared__ double g_wg_x[2][8];
+// wave-uniform values of both waves, o[w][i] = v[i] of wave w; every wave then combines them in wave order (the
+// same result in both).  The second barrier keeps the next exchange from overwriting a slot still to be read.
+template <int NV>
+__device__ __forceinline__ void wg_both(const double (&v)[NV], double (&o)[2][NV]) {
+    static_assert(NV <= 8, "eight slots");
+    const int w = wave_idx();
+    if (lane_id() == 0) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) g_wg_x[w][i] = v[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) { o[0][i] = g_wg_x[0][i]; o[1][i] = g_wg_x[1][i]; }
+    __syncthreads();
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // wave primitives (every call site is at wave-uniform control flow: EXEC full)
@@ -157,8 +207,34 @@ __device__ __forceinline__ void half_pair(double x, double& lo, double& hi) {
 }
 constexpr int kWaveShl1 = 0x130;   // lane k <- lane k+1 (lane 63 <- 0)
 constexpr int kWaveShr1 = 0x138;   // lane k <- lane k-1 (lane 0 <- 0)
+#if DART_WG == 1
 __device__ __forceinline__ double from_next(double x) { return dpp<kWaveShl1>(x); }
 __device__ __forceinline__ double from_prev(double x) { return dpp<kWaveShr1>(x); }
+#else
+// two waves: lanes 0 / 32 of wave 1 take lanes 31 / 63 of wave 0 (node 31 of either lane half), and back
+__device__ __forceinline__ double from_next(double x) {
+    double v = dpp<kWaveShl1>(x);
+    const int l = lane_id(), w = wave_idx();
+    if (l == 0 || l == 32) g_wg_x[w][l >> 5] = x;
+    __syncthreads();
+    const double b0 = g_wg_x[1][0], b1 = g_wg_x[1][1];
+    __syncthreads();
+    if (w == 0 && l == 31) v = b0;
+    if (w == 0 && l == 63) v = b1;
+    return v;
+}
+__device__ __forceinline__ double from_prev(double x) {
+    double v = dpp<kWaveShr1>(x);
+    const int l = lane_id(), w = wave_idx();
+    if (l == 31 || l == 63) g_wg_x[w][l >> 5] = x;
+    __syncthreads();
+    const double b0 = g_wg_x[0][0], b1 = g_wg_x[0][1];
+    __syncthreads();
+    if (w == 1 && l == 0) v = b0;
+    if (w == 1 && l == 32) v = b1;
+    return v;
+}
+#endif
 
 struct OpSum { __device__ double operator()(double a, double b) const { return a + b; } };
 struct OpMax { __device__ double operator()(double a, double b) const { return fmax(a, b); } };
@@ -175,10 +251,18 @@ __device__ __forceinline__ double wreduce(double x, Op op) {
     x = op(x, dpp<0x4E>(x));     // quad_perm [2,3,0,1]
     x = op(x, dpp<0x124>(x));    // row_ror:4
     x = op(x, dpp<0x128>(x));    // row_ror:8
-    if constexpr (!BCAST) return op(op(readlane(x, 0), readlane(x, 16)), op(readlane(x, 32), readlane(x, 48)));
-    x = op(x, dpp<0x142, 0xa>(x));   // row_bcast:15
-    x = op(x, dpp<0x143, 0xc>(x));   // row_bcast:31
-    return readlane(x, 63);
+    double r;
+    if constexpr (!BCAST) {
+        r = op(op(readlane(x, 0), readlane(x, 16)), op(readlane(x, 32), readlane(x, 48)));
+    } else {
+        x = op(x, dpp<0x142, 0xa>(x));   // row_bcast:15
+        x = op(x, dpp<0x143, 0xc>(x));   // row_bcast:31
+        r = readlane(x, 63);
+    }
+#if DART_WG == 2
+    { const double v[1] = {r}; double o[2][1]; wg_both(v, o); r = op(o[0][0], o[1][0]); }
+#endif
+    return r;
 }
 // f32 variant for error measures, scalings and step-length minima (half the DPP traffic):
 // their consumers only compare against tolerances or fractions-to-the-boundary with >= 1 % slack
@@ -201,7 +285,11 @@ __device__ __forceinline__ float wreducef(float x, Op op) {
     x = op(x, dppf<0x128>(x));
     x = op(x, dppf<0x142, 0xa>(x));
     x = op(x, dppf<0x143, 0xc>(x));
-    return readlanef(x, 63);
+    float r = readlanef(x, 63);
+#if DART_WG == 2
+    { const double v[1] = {(double)r}; double o[2][1]; wg_both(v, o); r = op((float)o[0][0], (float)o[1][0]); }
+#endif
+    return r;
 }
 struct OpSumF { __device__ float operator()(float a, float b) const { return a + b; } };
 struct OpMaxF { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
@@ -221,7 +309,11 @@ __device__ __forceinline__ float wreduce_nn(float xf, Op op) {
     x = op(x, dppu<0x128>(x));
     x = op(x, dppu<0x142, 0xa>(x));
     x = op(x, dppu<0x143, 0xc>(x));
-    return __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)x, 63));
+    unsigned r = (unsigned)__builtin_amdgcn_readlane((int)x, 63);
+#if DART_WG == 2
+    { const double v[1] = {(double)r}; double o[2][1]; wg_both(v, o); r = op((unsigned)o[0][0], (unsigned)o[1][0]); }
+#endif
+    return __builtin_bit_cast(float, r);
 }
 __device__ __forceinline__ float wmaxf(float x) { return wreduce_nn(x, OpMaxU()); }
 __device__ __forceinline__ float wminf(float x) { return wreduce_nn(x, OpMinU()); }
@@ -246,6 +338,9 @@ __device__ __forceinline__ void wsum2(double& a, double& b) {
     DART_LEVELS(DART_L)
 #undef DART_L
     a = readlane(a, 63); b = readlane(b, 63);
+#if DART_WG == 2
+    { const double v[2] = {a, b}; double o[2][2]; wg_both(v, o); a = o[0][0] + o[1][0]; b = o[0][1] + o[1][1]; }
+#endif
 }
 // two f32 minima of non-negative values (see wreduce_nn)
 __device__ __forceinline__ void wmin2f(float& a, float& b) {
@@ -253,9 +348,34 @@ __device__ __forceinline__ void wmin2f(float& a, float& b) {
 #define DART_L(C, R) lvl_minu<C, R>(x); lvl_minu<C, R>(y);
     DART_LEVELS(DART_L)
 #undef DART_L
+#if DART_WG == 2
+    x = (unsigned)__builtin_amdgcn_readlane((int)x, 63); y = (unsigned)__builtin_amdgcn_readlane((int)y, 63);
+    {
+        const double v[2] = {(double)x, (double)y};
+        double o[2][2];
+        wg_both(v, o);
+        x = (unsigned)fmin(o[0][0], o[1][0]); y = (unsigned)fmin(o[0][1], o[1][1]);
+    }
+    a = __builtin_bit_cast(float, x); b = __builtin_bit_cast(float, y);
+#else
     a = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)x, 63));
     b = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)y, 63));
+#endif
 }
+#if DART_WG == 2
+// the two waves' error measures combined (maxima / minimum of non-negative floats by their bit patterns)
+__device__ __forceinline__ void wg_errors(float& mx0, float& mx1, float& mx2, float* mx3, float& mn, float& s0, float& s1) {
+    auto u = [](float f) { return (double)__builtin_bit_cast(unsigned, f); };
+    auto f = [](double d) { return __builtin_bit_cast(float, (unsigned)d); };
+    const double v[7] = {u(mx0), u(mx1), u(mx2), mx3 ? u(*mx3) : 0.0, u(mn), (double)s0, (double)s1};
+    double o[2][7];
+    wg_both(v, o);
+    mx0 = f(fmax(o[0][0], o[1][0])); mx1 = f(fmax(o[0][1], o[1][1])); mx2 = f(fmax(o[0][2], o[1][2]));
+    if (mx3) *mx3 = f(fmax(o[0][3], o[1][3]));
+    mn = f(fmin(o[0][4], o[1][4]));
+    s0 = (float)o[0][5] + (float)o[1][5]; s1 = (float)o[0][6] + (float)o[1][6];
+}
+#endif
 // the error-measure reductions of an IPM iteration: four maxima and one minimum of non-negative
 // values, two f32 sums
 __device__ __forceinline__ void wred_errors4(float& mx0, float& mx1, float& mx2, float& mx3, float& mn, float& s0,
@@ -273,6 +393,9 @@ __device__ __forceinline__ void wred_errors4(float& mx0, float& mx1, float& mx2,
     mx3 = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)e, 63));
     mn = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)d, 63));
     s0 = readlanef(s0, 63); s1 = readlanef(s1, 63);
+#if DART_WG == 2
+    wg_errors(mx0, mx1, mx2, &mx3, mn, s0, s1);
+#endif
 }
 // the error-measure reductions of an IPM iteration: three maxima and one minimum of non-negative
 // values, two f32 sums
@@ -288,13 +411,22 @@ __device__ __forceinline__ void wred_errors(float& mx0, float& mx1, float& mx2, 
     mx2 = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)c, 63));
     mn = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)d, 63));
     s0 = readlanef(s0, 63); s1 = readlanef(s1, 63);
+#if DART_WG == 2
+    wg_errors(mx0, mx1, mx2, nullptr, mn, s0, s1);
+#endif
 }
 
 __device__ __forceinline__ double wsum(double x) { return wreduce(x, OpSum()); }
 __device__ __forceinline__ double wsum_rl(double x) { return wreduce<OpSum, false>(x, OpSum()); }
 __device__ __forceinline__ double wmax(double x) { return wreduce(x, OpMax()); }
 __device__ __forceinline__ double wmin(double x) { return wreduce(x, OpMin()); }
-__device__ __forceinline__ bool wany(bool p) { return __ballot(p) != 0ull; }
+__device__ __forceinline__ bool wany(bool p) {
+    bool r = __ballot(p) != 0ull;
+#if DART_WG == 2
+    { const double v[1] = {r ? 1.0 : 0.0}; double o[2][1]; wg_both(v, o); r = o[0][0] + o[1][0] > 0.0; }
+#endif
+    return r;
+}
 
 // reciprocal: v_rcp_f64 (measured max relative error 2e-8 on gfx950, tests/test_gpu_pmpc.py
 // selftest) + one Newton step -> ~4e-16 relative; operands are well scaled, no denormals

@@ -394,7 +394,7 @@ class Bound:
 
 
 class RmpcSolver(Solver):
-    """``dart_mpc_handle`` of variant RMPC (regressor NMPC + fused RLS), N <= 31.  Defaults are the
+    """``dart_mpc_handle`` of variant RMPC (regressor NMPC + fused RLS), N <= 63 (N > 31: the two-wave build).  Defaults are the
     reference's options (np_mpc...:158-162: max_iter 200) and IPOPT's: constr_mult_init_max 1000, its soft
     restoration / restoration phases after a failed line search (restoration=False: status -2 there; a measured
     |v| above vmax at the pinned node 0 ends at status 2 with them) and max_soc 4 in the restoration phase."""
@@ -451,7 +451,7 @@ LMPC_PRM_DEFAULT = np.array([200.0, 2.0, 200.0, 2.0, 0.0, 0.0, 0.0, 0.0,     # Q
 
 
 class LmpcSolver(Solver):
-    """``dart_mpc_handle`` of variant LMPC, N <= 31.  Defaults are the reference's IPOPT options
+    """``dart_mpc_handle`` of variant LMPC, N <= 63 (N > 31: the two-wave build).  Defaults are the reference's IPOPT options
     (LMPC/src/controller/rlmpc2.py:480-489): max_iter 50, tol 1e-4, acceptable_tol 1e-3,
     acceptable_iter 5, and IPOPT's defaults max_soc 4 (second-order correction; 0 = off),
     constr_mult_init_max 1000 (least-square starting multipliers; 0 = start from 0) and its soft

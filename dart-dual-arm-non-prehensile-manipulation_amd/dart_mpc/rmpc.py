@@ -67,8 +67,8 @@ class AdaptiveNPMPCSmooth:
                  *, device=0, tol=1e-8, max_iter=200):
         if nx != 4 or nu != 2:
             raise ValueError("the regressor model is defined for nx=4, nu=2 (np_mpc...:178-186)")
-        if not (1 <= int(N) <= 31):
-            raise ValueError("horizon N must be in [1, 31]")
+        if not (1 <= int(N) <= 63):
+            raise ValueError("horizon N must be in [1, 63]")
         self.model, self.data = model, data
         self.Ts = float(Ts)
         self.nx, self.nu, self.N = nx, nu, int(N)

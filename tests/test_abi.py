@@ -45,7 +45,7 @@ def test_create_rejects_bad_config_without_touching_a_gpu():
                  dict(max_cpu_time=-1.0)):
         c = _lib.default_config(**over)
         assert _lib.lib().dart_mpc_create(ctypes.byref(c), 0, ctypes.byref(h)) == -1
-    for over in (dict(variant=1, N=32), dict(variant=1, N=0), dict(variant=2, N=32),   # RMPC/LMPC: N <= 31
+    for over in (dict(variant=1, N=64), dict(variant=1, N=0), dict(variant=2, N=64),   # RMPC, LMPC: N <= 63
                  dict(variant=2, acceptable_iter=-1), dict(variant=2, acceptable_iter=5, acceptable_tol=0.0)):
         c = _lib.default_config(**over)
         assert _lib.lib().dart_mpc_create(ctypes.byref(c), 0, ctypes.byref(h)) == -1
@@ -63,7 +63,7 @@ def test_rmpc_shim_validates_like_reference():
     with pytest.raises(ValueError):
         dart_mpc.AdaptiveNPMPCSmooth(None, None, nx=6)
     with pytest.raises(ValueError):
-        dart_mpc.AdaptiveNPMPCSmooth(None, None, N=32)
+        dart_mpc.AdaptiveNPMPCSmooth(None, None, N=64)
     c = dart_mpc.AdaptiveNPMPCSmooth(None, None, Ts=0.002, N=20, Qp=80.0, Qv=2.0, Ru=0.02, Rdu=1.0,
                                      u_bounds=(-0.6, 0.6), du_bounds=(-0.06, 0.06), vmax=0.2, v_eps=0.1)
     assert c.w0.shape == (124,) and c.gz == -9.81

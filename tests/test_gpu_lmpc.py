@@ -100,8 +100,9 @@ def test_reference_options(dm, lmpc_goldens):
     assert np.all(warm["status"] >= 0) and warm["iters"].mean() <= out["iters"].mean()
 
 
-@pytest.mark.parametrize("N", [1, 2, 15, 31])
+@pytest.mark.parametrize("N", [1, 2, 15, 31, 32, 40, 63])
 def test_horizons(dm, N):
+    """N <= 31: one wave per instance; N = 32..63: the two-wave build (lmpc_ipm.hip with DART_WG=2)."""
     from dart_mpc.workload import lmpc_batch
     D = lmpc_batch(1, seed0=3)
     s = dm.LmpcSolver(N=N, tol=1e-10, max_iter=500, acceptable_iter=0, B_max=32)
@@ -116,6 +117,47 @@ def test_horizons(dm, N):
     ok = ref["status"] == 0
     nX = 8 * (N + 1)
     assert np.max(np.abs(out["w"][ok][:, nX:] - ref["w"][ok][:, nX:])) <= 1e-6
+
+
+@pytest.mark.parametrize("N", [40, 63])
+def test_long_horizons_reference_options_same_path(dm, N):
+    """The two-wave build on 180 C5 instances with the reference's options (tol 1e-4, acceptable 1e-3 x 5,
+    max_iter 50): the oracle's path -- same statuses and iterations, |du0| <= 1e-6 -- including the instances
+    whose filter line search fails (3 at N = 40, 4 at N = 63: IPOPT's restoration phases, their state in the
+    per-stream device area) and whose second-order corrections run from that area too."""
+    from dart_mpc.workload import lmpc_batch
+    D = lmpc_batch(10, seed0=7000)
+    args = (D["state"], D["u_prev"], D["pvec"], D["target"])
+    s = dm.LmpcSolver(N=N, B_max=256)
+    g = s.solve_batch(*args)
+    s.close()
+    o = oracle_lib.lmpc_solve_batch(*args, N=N, nthreads=8, want_w=False)
+    off = oracle_lib.lmpc_solve_batch(*args, N=N, nthreads=8, want_w=False, resto=False)
+    assert np.sum(off["status"] == -2) >= 3          # the batch reaches the restoration phases
+    _same_outcome(g, o, min_conv=170)
+
+
+def test_long_horizon_fused_policy_call(dm):
+    """dart_lmpc_policy_solve_batch at N = 40 (the two-wave build runs the policy step as its own launch
+    before the solve): every output and the policy state equal to the two-call chain, over 4 steps."""
+    B, T, N = 6, 4, 40
+    rng = np.random.default_rng(22)
+    fa, fb = dm.LmpcPolicy(B, seed=3), dm.LmpcPolicy(B, seed=3)
+    sa, sb = dm.LmpcSolver(N=N, B_max=B), dm.LmpcSolver(N=N, B_max=B)
+    wa = wb = None
+    up = np.zeros((B, 2))
+    for t in range(T):
+        state = np.concatenate([rng.uniform(-0.1, 0.1, (B, 4)), rng.uniform(-0.05, 0.05, (B, 4))], axis=1)
+        target = np.zeros((B, 8)); target[:, 0] = rng.uniform(-0.1, 0.1, B); target[:, 2] = rng.uniform(-0.1, 0.1, B)
+        eps = rng.standard_normal((B, 34)).astype(np.float32)
+        oa = dm.policy_solve_batch(sa, fa, state, up, target, w_warm=wa, want_w=True, noise=eps)
+        act = fb.step(state, target, up, noise=eps)
+        ob = sb.solve_batch(state, up, fb.model_params, target, w_warm=wb, want_w=True)
+        for k in ("u0", "f", "w", "status", "iters"):
+            assert np.array_equal(oa[k], ob[k]), (t, k)
+        assert np.array_equal(oa["action"], act), t
+        wa, wb, up = oa["w"], ob["w"], oa["u0"]
+    sa.close(); sb.close()
 
 
 def test_edge_batches(dm):

@@ -75,8 +75,9 @@ def test_wide_tilt_box_library_trig_path(dm):
     assert np.allclose(out["f"], ref["f"], rtol=1e-6, atol=1e-10)
 
 
-@pytest.mark.parametrize("N", [1, 2, 15, 21, 22, 31])
+@pytest.mark.parametrize("N", [1, 2, 15, 21, 22, 31, 32, 40, 63])
 def test_horizons(dm, N):
+    """N <= 31: one wave per instance; N = 32..63: the two-wave build (rmpc_ipm.hip with DART_WG=2)."""
     from dart_mpc.workload import rmpc_batch
     D = rmpc_batch(1, seed0=3, N=N)
     s = dm.RmpcSolver(N=N, tol=1e-11, max_iter=500, B_max=32)
@@ -211,6 +212,51 @@ def test_same_path_as_oracle(dm, soc):
     assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6
 
 
+@pytest.mark.parametrize("N", [40, 63])
+def test_long_horizons_same_path_as_oracle(dm, N):
+    """The two-wave build (N = 32..63) on the C3 workload at the reference's tol 1e-8: IPOPT's path as the oracle's --
+    statuses equal, iteration counts equal on >= 95 % and never more than one apart (at N = 63 the longer sums
+    shift convergence by one iteration on 2 of 72 instances), u0 within 1e-6."""
+    from dart_mpc.workload import rmpc_batch
+    D = rmpc_batch(4, seed0=60, N=N)
+    s = dm.RmpcSolver(N=N, tol=1e-8, B_max=128)
+    g = s.solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
+    s.close()
+    o = oracle_lib.rmpc_solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"], N=N, tol=1e-8, nthreads=8)
+    assert np.array_equal(g["status"], o["status"]), (g["status"], o["status"])
+    d = np.abs(g["iters"] - o["iters"])
+    assert np.mean(d == 0) >= 0.95 and d.max() <= 1, (g["iters"], o["iters"])
+    ok = np.isin(o["status"], (0, 1))
+    assert ok.all()
+    assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6
+
+
+@pytest.mark.parametrize("N", [40, 63])
+def test_long_horizons_restoration(dm, N):
+    """Measured velocities 3x the C3 spread at N = 40 / 63: IPOPT's soft restoration and restoration phases in the
+    two-wave build (their state in a per-stream device area instead of LDS) take the oracle's path -- statuses
+    equal (2 where the restoration converges to local infeasibility, 0 where it returns), iterations equal on
+    >= 95 %, u0 within 1e-6 where solved; every status-2 point passes the l1 local-infeasibility certificate."""
+    from dart_mpc.workload import rmpc_batch
+    D = _spread(rmpc_batch(2, seed0=70, N=N), 3.0)
+    s = dm.RmpcSolver(N=N, tol=1e-8, B_max=64)
+    g = s.solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"], want_w=True)
+    s.close()
+    o = oracle_lib.rmpc_solve_batch(D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"], N=N, tol=1e-8,
+                                    nthreads=8)
+    inf = o["status"] == 2
+    assert inf.sum() >= 5
+    assert np.array_equal(g["status"], o["status"]), (g["status"], o["status"])
+    assert np.mean(g["iters"] == o["iters"]) >= 0.95, (g["iters"], o["iters"])
+    du = np.abs(g["u0"] - o["u0"]).max(axis=1)
+    if (~inf).any():
+        assert np.max(du[~inf]) <= 1e-6
+    for i in np.nonzero(inf)[0]:
+        a = (D["x0"][i], D["u_prev"][i], D["theta"][i], D["prm"][i])
+        dec, _ = rmpc_nlp.l1_stationarity(g["w"][i], *a, N=N)
+        assert dec <= 2e-7, (i, dec)
+
+
 def _spread(D, factor):
     D["x0"] = D["x0"].copy()
     D["x0"][:, [1, 3]] *= factor
@@ -260,8 +306,8 @@ def test_restoration_phase_same_path_as_oracle(dm, spread):
             seg = [rmpc_nlp.l1_violation(o["w"][i] + t * (g["w"][i] - o["w"][i]), *a) for t in (0.25, 0.5, 0.75)]
             assert max(abs(v - Vo) for v in seg) <= 1e-7 * Vo, (i, seg, Vo)
     if spread == 3.0:
-        # batches of 18 (C3's size): the restoration runs in the wave that handed the instance over
-        # (rmpc_resto_tail, one launch) -- the same statuses and iterations as the oracle
+        # batches of 18 (C3's size, one launch and its queued restoration kernel) -- the same statuses and
+        # iterations as the oracle
         s = dm.RmpcSolver(N=20, tol=1e-8, B_max=18)
         parts = [s.solve_batch(*(D[k][i:i + 18] for k in ("x0", "u_prev", "theta", "Rref", "prm")))
                  for i in range(0, 720, 18)]
