@@ -696,6 +696,11 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
         zl = st[11]; zu = st[12]; fth = st[13]; fph = st[14];
         mu = sc0[0]; theta = sc0[kLmNst]; delta_last = sc0[2 * kLmNst];
         it_start = (int)sc0[3 * kLmNst]; nfilt = (int)sc0[4 * kLmNst]; acc_count = (int)sc0[5 * kLmNst];
+#ifdef DART_RESTO_TRACE
+        if (lane == 0)
+            printf("resume wave %d: mu %.6e theta %.6e delta_last %.6e it %d nfilt %d acc %d\n", wave_idx(), mu, theta,
+                   delta_last, it_start, nfilt, acc_count);
+#endif
     }
 
     // ---- helpers of the restoration phases (cold path) -----------------------------------------
@@ -1053,7 +1058,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                 for (;;) {
                     ok = riccati_s_sweep(S, N, RR);
 #ifdef DART_RESTO_TRACE
-                    if (blockIdx.x == 0 && (it <= 0 || (RESTO && it == it_start)) && attempt < 3) {
+                    if (blockIdx.x == 0 && (it <= 0 || N > 31) && attempt < 3) {
                         bool fin = true;
                         if (uon) {
                             for (int e = 0; e < LmLds::NTP; ++e) fin = fin && isfinite(Hk[e]);
@@ -1196,6 +1201,11 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
 #pragma unroll
                 for (int i = 0; i < 5; ++i) st[6 + i] = lam[i];
                 st[11] = zl; st[12] = zu; st[13] = fth; st[14] = fph;
+#ifdef DART_RESTO_TRACE
+                if (lane == 0)
+                    printf("hand-off wave %d: mu %.6e theta %.6e delta_last %.6e it %d nfilt %d acc %d\n", wave_idx(), mu_it,
+                           theta, dl_it, it, nfilt_it, acc_it);
+#endif
                 st[15] = lane == 0 ? mu_it : lane == 1 ? theta : lane == 2 ? dl_it : lane == 3 ? (double)it
                        : lane == 4 ? (double)nfilt_it : lane == 5 ? (double)acc_it
                        : (double)(__builtin_amdgcn_s_memrealtime() - t_start);     // elapsed ticks

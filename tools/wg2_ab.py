@@ -31,6 +31,12 @@ def run(mode):
     s.close()
     for k in ("status", "iters", "u0", "w"):
         res[f"lmpc_ref/{k}"] = g[k]
+    D = lmpc_batch(40, seed0=0)         # 720 instances, 5 of them through IPOPT's restoration phases
+    s = dart_mpc.LmpcSolver(N=30, B_max=1024, max_cpu_time=0.0)
+    g = s.solve_batch(*(D[k] for k in k4), want_w=True)
+    s.close()
+    for k in ("status", "iters", "u0", "w"):
+        res[f"lmpc_resto/{k}"] = g[k]
     k5 = ("x0", "u_prev", "theta", "Rref", "prm")
     D = rmpc_batch(4, seed0=60)
     s = dart_mpc.RmpcSolver(N=20, tol=1e-8, B_max=128)
