@@ -86,6 +86,7 @@ struct LmShared {
 #endif
     LmSub sub[2];                   // uniform problem data of the two halves
     double W[2][2][4], tg[2][4], st0[2][4];   // [half][stage, terminal] weights, target, x_0 (local order)
+    alignas(16) double Ps[2][LmLds::NTP];     // the explicit value function of riccati_s_sweep_p
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -684,6 +685,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
     // defect column; y = the step's new multipliers.  Mirrors ls_multipliers in oracle/lmpc_ipm.c.
     const bool lsinit = a.mult_init_max > 0.0;
     int in_soft = 0, soft_count = 0;       // IPOPT's soft restoration phase (BacktrackingLineSearch)
+    bool pformed = false;                  // the inertia tests run on riccati_s_sweep_p (set once, see there)
     int it_start = lsinit ? -1 : 0;
     if constexpr (RESTO) {      // resume a handed-off instance at the start of its failed iteration
         const double* st = a.resto_buf + ((size_t)b * kWave * kWaves + ql) * kLmNst;
@@ -696,6 +698,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
         zl = st[11]; zu = st[12]; fth = st[13]; fph = st[14];
         mu = sc0[0]; theta = sc0[kLmNst]; delta_last = sc0[2 * kLmNst];
         it_start = (int)sc0[3 * kLmNst]; nfilt = (int)sc0[4 * kLmNst]; acc_count = (int)sc0[5 * kLmNst];
+        pformed = sc0[7 * kLmNst] != 0.0;
 #ifdef DART_RESTO_TRACE
         if (lane == 0)
             printf("resume wave %d: mu %.6e theta %.6e delta_last %.6e it %d nfilt %d acc %d\n", wave_idx(), mu, theta,
@@ -773,6 +776,28 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
         // the iteration-start values a hand-off parks (the rest of the state changes only on acceptance)
         const double mu_it = mu, dl_it = delta_last;
         const int nfilt_it = nfilt, acc_it = acc_count;
+        // hand-off to lmpc_ipm_kernel<true> (<false> only): the state of this iteration's start to HBM; pf = the
+        // inertia tests of the resumed iteration run on the explicit value function (riccati_s_sweep_p)
+        auto handoff = [&](bool pf) {
+            double* st = a.resto_buf + ((size_t)b * kWave * kWaves + ql) * kLmNst;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) st[i] = x[i];
+            st[4] = up; st[5] = u;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) st[6 + i] = lam[i];
+            st[11] = zl; st[12] = zu; st[13] = fth; st[14] = fph;
+#ifdef DART_RESTO_TRACE
+            if (lane == 0)
+                printf("hand-off wave %d: mu %.6e theta %.6e delta_last %.6e it %d nfilt %d acc %d pformed %d\n", wave_idx(),
+                       mu_it, theta, dl_it, it, nfilt_it, acc_it, (int)pf);
+#endif
+            st[15] = lane == 0 ? mu_it : lane == 1 ? theta : lane == 2 ? dl_it : lane == 3 ? (double)it
+                   : lane == 4 ? (double)nfilt_it : lane == 5 ? (double)acc_it
+                   : lane == 7 ? (pf ? 1.0 : 0.0)
+                   : (double)(__builtin_amdgcn_s_memrealtime() - t_start);     // elapsed ticks (lane 6)
+            status = kLmNeedResto;
+        };
+        (void)handoff;
         // ---------------- derivatives, residuals, optimality error ---------------------------
         const double isl = uon ? frcp(u - lo) : 0.0, isu = uon ? frcp(hi - u) : 0.0;
         double lamn[5];
@@ -1056,7 +1081,8 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                 double delta = 0.0, dapplied = 0.0;
                 int attempt = 0;
                 for (;;) {
-                    ok = riccati_s_sweep(S, N, RR);
+                    if constexpr (RESTO) ok = pformed ? riccati_s_sweep_p(S, SH.Ps, N, RR) : riccati_s_sweep(S, N, RR);
+                    else ok = riccati_s_sweep(S, N, RR);
 #ifdef DART_RESTO_TRACE
                     if (blockIdx.x == 0 && (it <= 0 || N > 31) && attempt < 3) {
                         bool fin = true;
@@ -1075,9 +1101,19 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                                    hf, q, Hk[hp(0, 0)], Hk[hp(1, 1)], Hk[hp(2, 2)], Hk[hp(3, 3)], Hk[hp(4, 4)], Hk[hp(5, 5)]);
                     }
 #endif
-                    if (ok || soc >= 0 || ++attempt >= 60) break;
-                    delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))   // IPOPT perturb_dec_fact 1/3
-                                           : delta * (delta_last == 0.0 ? 100.0 : 8.0);
+                    if (ok || soc >= 0) break;
+                    if (++attempt >= 60) {
+                        // the folded recursion fails the inertia test at every perturbation: where the value function
+                        // reaches ~1e18 its sign decisions part from the explicit form IPOPT-style recursions (and
+                        // the oracle) take -- the whole perturbation sequence again with P formed, for the rest of
+                        // the solve (profiles/r04/lmpc_riccati_probe_*.txt; 2 of 28,800 C5 stress instances).  That
+                        // form lives in <true> only (the fast kernel keeps its registers): <false> hands over.
+                        if (!RESTO || pformed) break;
+                        pformed = true; attempt = 0; delta = 0.0;
+                    } else {
+                        delta = (attempt == 1) ? (delta_last == 0.0 ? 1e-4 : fmax(1e-20, delta_last * (1.0 / 3.0)))   // IPOPT perturb_dec_fact 1/3
+                                               : delta * (delta_last == 0.0 ? 100.0 : 8.0);
+                    }
                     const double dd = delta - dapplied;
                     if (uon) {
 #pragma unroll
@@ -1183,7 +1219,13 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
             }
             if (!resolve) break;
         }
-        if (!ok) { status = -3; break; }
+        if (!ok) {
+            if constexpr (!RESTO) {
+                if (a.resto) { handoff(true); break; }
+            }
+            status = -3;
+            break;
+        }
         STAMP_ADD(10, ls + 1);
         STAMP(7);
         // ---------------- IPOPT's soft restoration phase (BacktrackingLineSearch::TrySoftRestoStep) ------
@@ -1193,23 +1235,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
         // error at mu by the factor 0.9999; at most max_soft_resto_iters = 10 steps
         if constexpr (!RESTO) {
             if (!accepted && a.resto) {
-                // hand-off to lmpc_ipm_kernel<true>: the state of this iteration's start to HBM
-                double* st = a.resto_buf + ((size_t)b * kWave * kWaves + ql) * kLmNst;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) st[i] = x[i];
-                st[4] = up; st[5] = u;
-#pragma unroll
-                for (int i = 0; i < 5; ++i) st[6 + i] = lam[i];
-                st[11] = zl; st[12] = zu; st[13] = fth; st[14] = fph;
-#ifdef DART_RESTO_TRACE
-                if (lane == 0)
-                    printf("hand-off wave %d: mu %.6e theta %.6e delta_last %.6e it %d nfilt %d acc %d\n", wave_idx(), mu_it,
-                           theta, dl_it, it, nfilt_it, acc_it);
-#endif
-                st[15] = lane == 0 ? mu_it : lane == 1 ? theta : lane == 2 ? dl_it : lane == 3 ? (double)it
-                       : lane == 4 ? (double)nfilt_it : lane == 5 ? (double)acc_it
-                       : (double)(__builtin_amdgcn_s_memrealtime() - t_start);     // elapsed ticks
-                status = kLmNeedResto;
+                handoff(pformed);
                 break;
             }
         }

@@ -752,6 +752,56 @@ __device__ bool riccati_s_sweep(L* S, int N, const RiccatiSRoles& R) {
     return !wany(!ok);
 }
 
+// The same backward sweep with the value function formed explicitly at every node (the order of IPOPT-style
+// dense recursions and of the C oracle, oracle/lmpc_ipm.c riccati_factor): phase 1, lane e of each half forms the
+// packed entry e of P_{k+1} = Gzz - Gzu Guz / Quu from G_{k+1} into Ps[h] (u entries: 0, Quu: 1), one barrier;
+// phase 2, the node step on that surrogate.  Where the value function reaches ~1e18 (LMPC stress instances with
+// an unstable open loop) the two orders can decide Quu's sign differently (profiles/r04/lmpc_riccati_probe_*.txt);
+// the LMPC kernel takes this form when the folded one fails the inertia test at every perturbation.  Returns
+// false (wave-uniform) if some Quu is not positive.
+template <class L>
+__device__ bool riccati_s_sweep_p(L* S, double (*Ps)[L::NTP], int N, const RiccatiSRoles& R) {
+    constexpr int NXA = L::NXA;
+    const int h = lane_id() >> 5, base = h * L::NMAXS;
+    int zi = 0;
+    while (tri(zi + 1) <= R.e) ++zi;
+    const int zj = R.e - tri(zi);
+    const bool uent = zi == NXA || zj == NXA;
+    bool ok = true;
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Gn = S->G[base + k + 1];
+        const double q = Gn[hp(NXA, NXA)];
+        ok = ok && q > 0.0 && isfinite(q);
+        const double gi = Gn[hp(zi, NXA)], gj = Gn[hp(zj, NXA)];
+        const double pv = Gn[R.e] - gi * gj / q;
+        Ps[h][R.e] = uent ? ((zi == NXA && zj == NXA) ? 1.0 : 0.0) : pv;
+        __syncthreads();
+        // node step on the surrogate (s_node_step with Gn = Ps[h]: Gzu = 0, Quu = 1)
+        const double hk = S->H[base + k][R.e];
+        const double* Mk = &S->M[base + k][0][0];
+        constexpr int NP = L::NP;
+        double vi[NP], vj[NP];
+#pragma unroll
+        for (int m = 0; m < NP; ++m) { vi[m] = Mk[R.ci + m]; vj[m] = Mk[R.cj + m]; }
+        const double* P = Ps[h];
+        double t[NP];
+#pragma unroll
+        for (int m = 0; m < NP; ++m) t[m] = 0.0;
+#pragma unroll
+        for (int n = 0; n < NP; ++n)
+#pragma unroll
+            for (int m = 0; m < NP; ++m) t[m] = fma(P[gszz<NXA>(m, n)], vj[n], t[m]);
+        double g = hk;
+#pragma unroll
+        for (int m = 0; m < NP; ++m) g = fma(vi[m], t[m], g);
+        S->G[base + k][R.e] = g;
+        __syncthreads();
+    }
+    const double q0 = S->G[base][hp(NXA, NXA)];
+    ok = ok && q0 > 0.0 && isfinite(q0);
+    return !wany(!ok);
+}
+
 // [K | k] = -Guz / Quu and [Phi | f] of every node, lane 32 h + k per node (k < N); post(slot, k) then
 // runs on each node's lane before the pair maps are composed (the LMPC restoration phase maps the rows
 // through its soft defect rows there).  Ends with a barrier.

@@ -117,12 +117,12 @@ def test_horizons(dm, N):
     if N <= 31:
         assert np.array_equal(out["iters"], ref["iters"]), (out["iters"], ref["iters"])
     else:
-        # N > 31 (the two-wave build): the restoration phase's start (IPOPT's closed-form p, n of each row, which
-        # cancels where c >> mu / rho) turns rounding of the defects into ~1e-7 of its barrier objective -- at
-        # every N, in the oracle as in the kernel (tools/wg2_trace.py beside the oracle's ORACLE_DEBUG trace) --
-        # and the tight-tolerance restoration solve of #15 ends 57 / 59 iterations apart at N = 32 (same status,
-        # same point).  The two-wave machinery itself is bit-identical to the one-wave kernels
-        # (tools/wg2_ab.py).  Every other instance takes the oracle's iterations exactly.
+        # N > 31 (the two-wave build): the restoration phase's barrier objective differs from the oracle's by ~1e-7
+        # relative at its first iteration -- at N = 30 on the one-wave kernel too (profiles/r05/wg2_trace_30r.txt
+        # beside the oracle's ORACLE_DEBUG trace; cause not isolated) -- and the tight-tolerance restoration
+        # solve of #15 ends 57 / 59 iterations apart at N = 32 (same status, same point).  The two-wave machinery
+        # itself is bit-identical to the one-wave kernels (tools/wg2_ab.py, profiles/r05/wg2_ab.txt).  Every other
+        # instance takes the oracle's iterations exactly.
         other = np.arange(len(ref["iters"])) != 15
         assert np.array_equal(out["iters"][other], ref["iters"][other]), (out["iters"], ref["iters"])
     ok = ref["status"] == 0
@@ -178,6 +178,30 @@ def test_long_horizon_fused_policy_call(dm):
         assert np.array_equal(oa["action"], act), t
         wa, wb, up = oa["w"], ob["w"], oa["u0"]
     sa.close(); sb.close()
+
+
+def test_inertia_blowups_take_the_explicit_value_function(dm):
+    """The two C5 stress instances of the 28,800-instance sweep (#18257, #18351: lmpc_batch(1, 101014)[5],
+    lmpc_batch(1, 101019)[9]) whose value function reaches ~1e18 at iteration 0: the kernel's folded Riccati
+    recursion fails the inertia test at every perturbation there, while the explicit form the oracle (and any
+    IPOPT-style dense recursion) takes is positive definite (profiles/r04/lmpc_riccati_probe_*.txt).  The kernel
+    hands such an iteration to lmpc_ipm_kernel<true>, which repeats it on riccati_s_sweep_p: no status -3 at
+    iteration 0 any more, and the oracle's statuses and iteration counts (max_iter -1 after 50, and -2 after 33)."""
+    from dart_mpc.workload import lmpc_batch
+    rows = []
+    for seed, i in ((101014, 5), (101019, 9)):
+        D = lmpc_batch(1, seed0=seed)
+        rows.append({k: D[k][i] for k in ("state", "u_prev", "pvec", "target")})
+    args = tuple(np.stack([r[k] for r in rows]) for k in ("state", "u_prev", "pvec", "target"))
+    for B in (2, 40):       # in the solving wave (B <= 32) and through the queued restoration kernel
+        rep = tuple(np.concatenate([a] * (B // 2)) for a in args)
+        s = dm.LmpcSolver(N=30, B_max=64, max_cpu_time=0.0)
+        g = s.solve_batch(*rep)
+        s.close()
+        o = oracle_lib.lmpc_solve_batch(*rep, N=30, nthreads=8, want_w=False)
+        assert not np.any(g["status"] == -3), (B, g["status"], g["iters"])
+        assert np.array_equal(g["status"], o["status"]), (B, g["status"], o["status"], g["iters"], o["iters"])
+        assert np.array_equal(g["iters"], o["iters"]), (B, g["iters"], o["iters"])
 
 
 def test_edge_batches(dm):
