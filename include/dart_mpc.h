@@ -70,8 +70,8 @@ extern "C" {
 
 enum dart_mpc_variant {
     DART_MPC_PMPC = 0,      /* PMPC/src/controller/mpc_3d.py, N <= 63 */
-    DART_MPC_RMPC = 1,      /* RMPC/dev_dual/controller/np_mpc_adaptive_with_linear_regressor.py, N <= 31 */
-    DART_MPC_LMPC = 2       /* LMPC/src/controller/rlmpc2.py, N <= 31 */
+    DART_MPC_RMPC = 1,      /* RMPC/dev_dual/controller/np_mpc_adaptive_with_linear_regressor.py, N <= 63 */
+    DART_MPC_LMPC = 2       /* LMPC/src/controller/rlmpc2.py, N <= 63 */
 };
 
 enum dart_mpc_status {
@@ -115,9 +115,11 @@ typedef struct dart_mpc_config {
     int32_t restoration;  /* LMPC (ABI 6), RMPC and PMPC (ABI 8): 1 = IPOPT's soft restoration and
                            restoration phases after a failed filter line search (default;
                            MinC_1NrmRestorationPhase, the fallback of every nlpsol call, mpc_3d.py:82,
-                           np_mpc...:158-162, rlmpc2.py:480-489); 0 = stop with status -2 there.  RMPC and
-                           PMPC: the failed instances of a launch are re-solved by a second kernel queued on
-                           the same stream (PMPC: IPOPT's path, N <= 31; the reduced path and N > 31 keep -2) */
+                           np_mpc...:158-162, rlmpc2.py:480-489); 0 = stop with status -2 there.  PMPC and
+                           LMPC batches of at most 32 run them in the solving wave; larger batches and RMPC
+                           hand the failed instances to a second kernel queued on the same stream.  PMPC: on
+                           IPOPT's path; for N > 31 the soft phase only (the restoration phase proper and the
+                           reduced path keep -2).  RMPC / LMPC: at every N */
     double constr_mult_init_max;  /* IPOPT constr_mult_init_max (default 1000): the starting equality
                            multipliers are IPOPT's least-square estimate unless its max norm exceeds this
                            (then 0); 0 = always start from 0.  Used by PMPC, RMPC and LMPC */
