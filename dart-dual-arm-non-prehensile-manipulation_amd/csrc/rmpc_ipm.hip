@@ -2153,8 +2153,9 @@ extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStre
     hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel<false>, dim3(a.B * a.pack), dim3(dartmpc::kWave), 0, stream, a);
     if (a.resto) {      // the instances whose line search failed, with IPOPT's restoration phases
         if (hipError_t e = hipGetLastError()) return e;
-        // one block per instance (not B x pack): the blocks of the instances that were not handed over return at
-        // once, and fewer of them make the queued kernel cheaper on the launches that need no restoration
+        // one block per instance (not B x pack; the blocks of the instances that were not handed over return at
+        // once): 4.39 -> 4.40 us per launch, the dispatch itself.  Inlining the restoration behind the solve instead
+        // costs C3 10.5 % (profiles/r05/rmpc_inline_ab.txt), a non-inlined call 4.7 % (fuse_ab.txt).
         dartmpc::RmpcArgs r = a;
         r.pack = 1;
         hipLaunchKernelGGL(dartmpc::rmpc_ipm_kernel<true>, dim3(r.B), dim3(dartmpc::kWave), 0, stream, r);

@@ -4,6 +4,7 @@ at the reference's options -- PMPC tol 1e-8 (C2/C4 workload), RMPC tol 1e-8 (C3)
 agreement, iteration agreement, max |du0| over the instances the oracle solves (status 0 / 1) and the
 status counts of both.  Round 4 adds the restoration phases: RMPC with the C3 velocities spread 3x (infeasible starts) and PMPC at
 N = 31 and with max_soc = 0 (instances whose filter line search fails).
+Round 5 adds horizons 40 and 63 on all three variants (DART_SWEEP_LONG=0 skips them).
 Usage: python tools/parity_sweep.py [pmpc_seeds rmpc_seeds lmpc_seeds [rmpc_spread_seeds]]"""
 import os
 import sys
@@ -88,4 +89,27 @@ if len(ns) > 3 or len(sys.argv) <= 4:
                                      resto=False)
         report(f"PMPC N={N} max_soc={soc} (seeds 300000+; {int(np.sum(off['status'] != 0))} need restoration)", g, o,
                lambda st: st == 0)
+# horizons beyond 31 (round 5): PMPC two registers per lane, RMPC / LMPC the two-wave builds
+if os.environ.get("DART_SWEEP_LONG", "1") == "1":
+    for N in (40, 63):
+        S, T, P = pmpc_batch(80, seed0=400000)
+        s = dart_mpc.Solver(N=N, Ts=0.002, tol=1e-8, B_max=S.shape[0])
+        g = s.solve_batch(S, T, P)
+        s.close()
+        o = oracle_lib.solve_batch(S, T, P, N=N, Ts=0.002, tol=1e-8, max_iter=3000, nthreads=NT, want_w=False)
+        report(f"PMPC N={N} (seeds 400000+)", g, o, lambda st: st == 0)
+        D = rmpc_batch(80, seed0=400000, N=N)
+        args = (D["x0"], D["u_prev"], D["theta"], D["Rref"], D["prm"])
+        s = dart_mpc.RmpcSolver(N=N, tol=1e-8, B_max=len(D["x0"]))
+        g = s.solve_batch(*args)
+        s.close()
+        o = oracle_lib.rmpc_solve_batch(*args, N=N, tol=1e-8, nthreads=NT)
+        report(f"RMPC N={N} (seeds 400000+)", g, o, lambda st: st == 0)
+        D = lmpc_batch(80, seed0=400000)
+        args = (D["state"], D["u_prev"], D["pvec"], D["target"])
+        s = dart_mpc.LmpcSolver(N=N, B_max=len(D["state"]), max_cpu_time=0.0)
+        g = s.solve_batch(*args)
+        s.close()
+        o = oracle_lib.lmpc_solve_batch(*args, N=N, nthreads=NT, want_w=False)
+        report(f"LMPC stress N={N} (seeds 400000+, restoration on)", g, o, lambda st: np.isin(st, (0, 1)))
 print(f"({time.time() - t0:.0f} s, oracle on {NT} threads)")
