@@ -90,11 +90,14 @@ def test_horizons(dm, N):
     assert np.max(np.abs(out["w"][:, nX:] - ref["w"][:, nX:])) <= 1e-6
 
 
-def test_fused_rls_matches_oracle_and_unfused(dm):
+@pytest.mark.parametrize("N", [20, 40])
+def test_fused_rls_matches_oracle_and_unfused(dm, N):
+    """The RLS update fused into the solve launch (one wave; at N = 40 the two-wave build, whose first wave writes
+    theta and P back) against the oracle's RLS and against the unfused solve with the updated estimate."""
     from dart_mpc.workload import rmpc_batch
-    D = rmpc_batch(1, seed0=5)
+    D = rmpc_batch(1, seed0=5, N=N)
     B = D["x0"].shape[0]
-    s = dm.RmpcSolver(N=20, tol=1e-10, max_iter=500, B_max=32)
+    s = dm.RmpcSolver(N=N, tol=1e-10, max_iter=500, B_max=32)
     fused = s.solve_batch(D["x0"], D["u_prev"], D["rls_theta"], D["Rref"], D["prm"], want_w=True,
                           rls_P=D["rls_P"], rls_phi=D["phi_prev"], rls_y=D["y"], rls_lambda=0.995)
     th_ref = np.zeros((B, 14)); P_ref = np.zeros((B, 2, 7, 7))
