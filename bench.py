@@ -153,7 +153,7 @@ def bench_long_horizons(args, dart_mpc):
     """Horizons beyond the one-wave kernels (N = 40 and 63; the reference takes N as a free constructor argument,
     mpc_3d.py:12, np_mpc...:35, rlmpc2.py): per variant a batch of 18 fresh instances per call through the host
     entry (inputs copied in, outputs out: PCIe-inclusive), statuses and iterations of the first batch against
-    the C oracle.  PMPC N > 31 runs two registers per lane in one wave; RMPC and LMPC the two-wave builds."""
+    the C oracle.  N > 31 runs the two-wave builds of all three variants (PMPC: the scan build, pmpc_wg2.o)."""
     from dart_mpc.workload import lmpc_batch, pmpc_batch, rmpc_batch
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_lib   # checker only

@@ -24,6 +24,15 @@
 // blocks to the neighbouring lane with DPP wave shifts (no LDS); norms and
 // inner products are DPP row reductions.  No LDS and no global traffic inside
 // the iteration loop.
+// Horizons N = 32..63: this file built a third time with -DDART_WG=2 (Makefile: pmpc_wg2.o) -- the scan build
+// (NAX = 1) on a workgroup of two waves per instance, wave w owning nodes 32 w .. 32 w + 31 with the one-wave lane
+// roles (wave.h: the wave reductions and node shifts combine the two waves).  Every scan runs in both waves and is
+// continued across the wave boundary by one LDS hand-over (pm_pass): the suffix scans of wave 0 start from the
+// values of node 32 (wave 1), the prefix scans of wave 1 from those of node 31 (wave 0).  IPOPT's soft restoration
+// phase runs in the kernel as in the sequential N > 31 build.  The build's symbols sit in their own namespace.
+#if DART_WG == 2
+#define dartmpc dartmpc_wg2
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -51,6 +60,32 @@ __device__ unsigned long long g_stamp_seq[16];
 #else
 #define STAMP_FLUSH(b) STAMP_FLUSH_TO(g_stamp, b)
 #endif
+
+// values of node `src_node` of wave `src_wave` (lane src_node: axis x, lane src_node + 32: axis y) in every lane of
+// the same axis half of both waves; two barriers (the second keeps the next hand-over from overwriting a slot
+// still to be read).  Two-wave build only (the one-wave build names it in discarded branches).
+#if DART_WG == 2
+__shared__ double g_pm_x[2][4];
+#endif
+template <int NV>
+__device__ __forceinline__ void pm_pass(int src_wave, int src_node, const double (&v)[NV], double (&o)[NV]) {
+    static_assert(NV <= 4, "four slots");
+#if DART_WG == 1
+    (void)src_wave; (void)src_node;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) o[i] = v[i];
+#else
+    const int l = lane_id();
+    if (wave_idx() == src_wave && (l & 31) == src_node) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) g_pm_x[l >> 5][i] = v[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) o[i] = g_pm_x[l >> 5][i];
+    __syncthreads();
+#endif
+}
 
 // DPP move with an identity fill (FILL = 0.0 or 1.0) for lanes whose source is outside the row or
 // masked out.  With every row enabled a zero half comes from bound_ctrl (the DPP writes 0 where the
@@ -167,8 +202,8 @@ __device__ __forceinline__ void mat4_scan_level(double* T) {
 template <int NAX, bool QSCAN, bool ONEROW, bool SHORT2, bool RED>
 __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
     STAMP_DECL
-    const int lane = threadIdx.x;
-    const int k = NAX == 1 ? (lane & 31) : lane;            // shooting node of this lane
+    const int lane = kWaves == 1 ? (int)threadIdx.x : lane_id();
+    const int k = NAX == 1 ? node_base() + (lane & 31) : lane;      // shooting node of this lane
     const int ax0 = NAX == 1 ? (lane >> 5) : 0;               // axis of slot 0 (NAX == 1)
     const int N = a.N;
     const bool xon = k <= N, uon = k < N;
@@ -444,7 +479,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                                 W[2 * i + jj] = fma(T[4 * i], F[jj], fma(T[4 * i + 1], F[2 + jj],
                                                     fma(T[4 * i + 2], F[4 + jj], T[4 * i + 3] * F[6 + jj])));
                     }
-                } else if constexpr (!one_row) {
+                } else if constexpr (!one_row && kWaves == 1) {
                     // rows 0 and 2 of each half: [U; Y]_k = T_k(row) [U; Y]_16, the 4 x 2 of lane 16 (48)
                     // fetched by ds_swizzle (bitmask mode, or_mask 16: no address, no LDS access)
                     double F[8];
@@ -457,6 +492,41 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                             for (int jj = 0; jj < 2; ++jj)
                                 W[2 * i + jj] = fma(T[4 * i], F[jj], fma(T[4 * i + 1], F[2 + jj],
                                                     fma(T[4 * i + 2], F[4 + jj], T[4 * i + 3] * F[6 + jj])));
+                    }
+                }
+                if constexpr (kWaves == 2) {
+                    // two waves (N >= 32, rows as above): wave 1's suffixes reach the terminal; wave 0's continue
+                    // from the value function of node 32, [U; Y]_k = T_k(..31) [I; P_32] (exact in the reals, as the
+                    // scan itself)
+                    auto rows = [&]() {
+                        double F[8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) F[e] = half_bcast_c<16>(W[e]);
+                        if ((lane & 16) == 0) {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                                for (int jj = 0; jj < 2; ++jj)
+                                    W[2 * i + jj] = fma(T[4 * i], F[jj], fma(T[4 * i + 1], F[2 + jj],
+                                                        fma(T[4 * i + 2], F[4 + jj], T[4 * i + 3] * F[6 + jj])));
+                        }
+                    };
+                    double v[3] = {0.0, 0.0, 0.0}, pn[3];
+                    if (wave_idx() == 1) {
+                        rows();
+                        const double idet = frcp(fma(W[0], W[3], -W[1] * W[2]));
+                        v[0] = fma(W[4], W[3], -W[5] * W[2]) * idet;
+                        v[1] = 0.5 * (fma(W[5], W[0], -W[4] * W[1]) * idet + fma(W[6], W[3], -W[7] * W[2]) * idet);
+                        v[2] = fma(W[7], W[0], -W[6] * W[1]) * idet;
+                    }
+                    pm_pass(1, 0, v, pn);
+                    if (wave_idx() == 0) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            W[2 * i] = fma(T[4 * i + 3], pn[1], fma(T[4 * i + 2], pn[0], T[4 * i]));
+                            W[2 * i + 1] = fma(T[4 * i + 3], pn[2], fma(T[4 * i + 2], pn[1], T[4 * i + 1]));
+                        }
+                        rows();
                     }
                 }
                 // P = Y U^-1 (symmetrised)
@@ -562,10 +632,31 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                     affine_scan_level<0x108, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:8
                     // rows 0 and 2 compose with the suffix held by the first lane of rows 1 and 3
                     const bool lo_row = (lane & 16) == 0;
-                    const double r1 = half_bcast_c<16>(c1), r2 = half_bcast_c<16>(c2);   // only the constant is needed now
-                    if (lo_row) {
-                        c1 = fma(m11, r1, fma(m12, r2, c1));
-                        c2 = fma(m21, r1, fma(m22, r2, c2));
+                    if constexpr (kWaves == 1) {
+                        const double r1 = half_bcast_c<16>(c1), r2 = half_bcast_c<16>(c2);   // only the constant is needed now
+                        if (lo_row) {
+                            c1 = fma(m11, r1, fma(m12, r2, c1));
+                            c2 = fma(m21, r1, fma(m22, r2, c2));
+                        }
+                    } else {
+                        auto rows = [&]() {
+                            const double r1 = half_bcast_c<16>(c1), r2 = half_bcast_c<16>(c2);
+                            if (lo_row) {
+                                c1 = fma(m11, r1, fma(m12, r2, c1));
+                                c2 = fma(m21, r1, fma(m22, r2, c2));
+                            }
+                        };
+                        // two waves: wave 0's rows 1 / 3 (their maps span nodes k..31) continue from p_32 of wave 1
+                        if (wave_idx() == 1) rows();
+                        double r[2];
+                        { const double v[2] = {c1, c2}; pm_pass(1, 0, v, r); }
+                        if (wave_idx() == 0) {
+                            if (!lo_row) {
+                                c1 = fma(m11, r[0], fma(m12, r[1], c1));
+                                c2 = fma(m21, r[0], fma(m22, r[1], c2));
+                            }
+                            rows();
+                        }
                     }
                 }
                 p1[0] = c1; p2[0] = c2;
@@ -590,7 +681,21 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                 // a constant once row 0 is done, so the row_bcast:15 level into rows 1 / 3 is one too
                 if constexpr (one_row || short2) affine_scan_const<0x118, 0xf>(f11_, f12_, f21_, f22_, d1, d2);
                 else affine_scan_level<0x118, 0xf>(f11_, f12_, f21_, f22_, d1, d2);   // row_shr:8
-                if constexpr (!one_row) affine_scan_const<0x142, 0xa>(f11_, f12_, f21_, f22_, d1, d2);   // row_bcast:15 -> rows 1, 3
+                if constexpr (kWaves == 1) {
+                    if constexpr (!one_row) affine_scan_const<0x142, 0xa>(f11_, f12_, f21_, f22_, d1, d2);   // row_bcast:15 -> rows 1, 3
+                } else {
+                    // two waves: wave 1's rows 0 / 2 (their maps span nodes 32..k) continue from dx_31 of wave 0
+                    if (wave_idx() == 0) affine_scan_const<0x142, 0xa>(f11_, f12_, f21_, f22_, d1, d2);
+                    double r[2];
+                    { const double v[2] = {d1, d2}; pm_pass(0, 31, v, r); }
+                    if (wave_idx() == 1) {
+                        if ((lane & 16) == 0) {
+                            d1 = fma(f11_, r[0], fma(f12_, r[1], d1));
+                            d2 = fma(f21_, r[0], fma(f22_, r[1], d2));
+                        }
+                        affine_scan_const<0x142, 0xa>(f11_, f12_, f21_, f22_, d1, d2);
+                    }
+                }
                 dp[0] = d1; dv[0] = d2;
             } else {
                 // linear part of the value function (sequential): p_k = q_k + A_k^T h - w_k (e^T h + rt)
@@ -669,7 +774,17 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                 affine1_scan_level<0x114, 0xf>(m, c);   // row_shr:4
                 if constexpr (one_row || short2) affine1_scan_const<0x118, 0xf>(m, c);
                 else affine1_scan_level<0x118, 0xf>(m, c);   // row_shr:8
-                if constexpr (!one_row) affine1_scan_const<0x142, 0xa>(m, c);   // row_bcast:15 -> rows 1, 3
+                if constexpr (kWaves == 1) {
+                    if constexpr (!one_row) affine1_scan_const<0x142, 0xa>(m, c);   // row_bcast:15 -> rows 1, 3
+                } else {       // two waves: as the state sweep
+                    if (wave_idx() == 0) affine1_scan_const<0x142, 0xa>(m, c);
+                    double r[1];
+                    { const double v[1] = {c}; pm_pass(0, 31, v, r); }
+                    if (wave_idx() == 1) {
+                        if ((lane & 16) == 0) c = fma(m, r[0], c);
+                        affine1_scan_const<0x142, 0xa>(m, c);
+                    }
+                }
                 dz[0] = c;
             } else {
 #pragma unroll
@@ -783,7 +898,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
             }
             STAMP(5);
             bool again = false;
-            if constexpr (NAX == 2 && !RED) {
+            if constexpr ((NAX == 2 || kWaves == 2) && !RED) {
                 if (PM_EXPECT(in_soft, 0)) break;      // in the soft restoration phase: its step only (below)
                 if (PM_EXPECT(soc < 0 && alpha < amin, 0)) break;
             }
@@ -820,10 +935,10 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                         defects(p[j], v[j], snc[j], sp[j], sv[j], g1[j], g2[j]);
                         gz[j] = RED ? 0.0 : zdefect(zz[j], w0, j);
                     }
-                    // (NAX == 2, the soft phase below: always through the loop top, so that a line search that fails
+                    // (NAX == 2 or two waves, the soft phase below: always through the loop top, so that a line search that fails
                     // here leaves the plain step in the direction registers; alpha < amin stops it there)
                     soc = -1; ls = 1; alpha = 0.5 * amain;
-                    again = (NAX == 2 && !RED) || !(alpha < amin);
+                    again = ((NAX == 2 || kWaves == 2) && !RED) || !(alpha < amin);
                     break;
                 }
                 ++ls;
@@ -841,7 +956,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
         // only by the fractions to the boundary (one length for x, lambda and z); it is taken if the original
         // filter accepts it with alpha_primal_test = 0 (the phase ends) or if it cuts IPOPT's primal-dual system
         // error at mu (the l1 norms of the primal and dual infeasibilities and of z s - mu, added) by 0.9999; at most
-        // 10 such steps, and a mu decrease ends the phase.  Only for N > 31 (NAX == 2), where the restoration solve
+        // 10 such steps, and a mu decrease ends the phase.  Only for N > 31 (NAX == 2, two waves), where the restoration solve
         // on the LDS engine (pmpc_resto.h) does not fit: at the default options every PMPC line-search failure there
         // is settled in the soft phase (N = 40: 41 of C4's 1152 instances), which round 4 ended at -2.  For N <= 31
         // the handed-over instance is solved again on the LDS engine, whose sequential arithmetic takes the oracle's
@@ -849,7 +964,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
         // instances and cost C2 5 % (its register allocation; profiles/r05/pmpc_soft_in_register_kernel.txt).
         bool soft = false;
         if (PM_EXPECT(!accepted, 0)) {
-            if constexpr (!RED && NAX == 2) {
+            if constexpr (!RED && (NAX == 2 || kWaves == 2)) {
                 if (a.soft) {
                     if (!in_soft) {       // PrepareRestoPhaseStart: the current point enters the filter
                         if (nfilt < kWave) {
@@ -941,7 +1056,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
 
     // -------- outputs ---------------------------------------------------------------
     if (PM_EXPECT(status == kPmNeedResto, 0)) {     // handed over: pmpc_resto_solve writes the outputs
-        if constexpr (NAX == 1 && !RED) {
+        if constexpr (NAX == 1 && kWaves == 1 && !RED) {
             if (a.resto_buf) {      // the iterate of the failed iteration (pmpc_model.h kPmHo layout)
                 double* ho = a.resto_buf + (size_t)kPmHo * b;
                 double* row = ho + kPmHoRow * k;
@@ -957,7 +1072,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                 }
             }
         }
-        if (lane == 0) a.status[b] = status;
+        if (lane == 0 && wave_idx() == 0) a.status[b] = status;
         if (a.done && a.resto == 2) {
             __threadfence_system();
             if (lane == 0) __hip_atomic_store(a.done + b, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -982,7 +1097,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
     } else {
         tx = th[0]; ty = th[NAX - 1];
     }
-    if (lane == 0) {
+    if (lane == 0 && wave_idx() == 0) {
         a.u0[2 * b] = tx;
         a.u0[2 * b + 1] = ty;
         a.f[b] = fval;
@@ -1014,7 +1129,8 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
     if (a.done) {
         // release at system scope: the wave's output stores (any lane) are visible before the word
         __threadfence_system();
-        if (lane == 0) __hip_atomic_store(a.done + b, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if constexpr (kWaves == 2) __syncthreads();       // and those of the other wave
+        if (lane == 0 && wave_idx() == 0) __hip_atomic_store(a.done + b, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     STAMP(8);
     STAMP_FLUSH(b);
@@ -1039,7 +1155,7 @@ __device__ __noinline__ void pmpc_resto_tail(const int b, const uint32_t seq, co
 // FUSE: resto mode 3, the handed-over instance continues in pmpc_resto_tail (no second launch)
 template <int NAX, bool QSCAN, bool ONEROW = false, bool SHORT2 = false, bool RED = false, bool OCC2 = false,
           bool FUSE = false>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(OCC2 ? 2 : ((QSCAN || NAX == 2) ? 1 : 2))))
+__global__ __launch_bounds__(kWave * kWaves) __attribute__((amdgpu_waves_per_eu(OCC2 ? 2 : ((QSCAN || NAX == 2) ? 1 : 2))))
 void pmpc_ipm_kernel(PmpcArgs a) {
     // small batches: the launcher deals 8 blocks per instance and only every 8th works, so all
     // instances land on one XCD (blocks go round-robin over the 8 XCDs) and share its L2 for the code
@@ -1097,7 +1213,7 @@ void pmpc_serve_kernel(PmpcArgs a, PmpcServe sv) {
     }
 }
 
-#ifndef PMPC_SEQ
+#if !defined(PMPC_SEQ) && DART_WG == 1
 // self-test of the wave primitives: out[0..63] = from_next(lane), out[64..127] = from_prev(lane),
 // out[128] = wsum(lane), out[129] = wmax(lane), out[130] = wmin(lane + 1),
 // out[131..194] = relative error of the raw v_rcp_f64 on x_i = 1.37^(i-32)*pi (diagnostic),
@@ -1126,7 +1242,17 @@ __global__ __launch_bounds__(kWave) void wave_selftest_kernel(double* out) {
 
 }  // namespace dartmpc
 
-#ifdef PMPC_SEQ
+#if DART_WG == 2
+// N = 32..63 on IPOPT's path (dartmpc_launch_pmpc forwards here): the scan build, one instance per two-wave
+// workgroup; grid = B x pack blocks as for the one-wave builds
+extern "C" hipError_t dartmpc_launch_pmpc_wg2(const void* args, unsigned grid, hipStream_t stream) {
+    const dartmpc::PmpcArgs& a = *static_cast<const dartmpc::PmpcArgs*>(args);
+    if (a.N < 32 || a.N > 63 || a.reduced || a.resto) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true>), dim3(grid), dim3(dartmpc::kWave * dartmpc::kWaves), 0,
+                       stream, a);
+    return hipGetLastError();
+}
+#elif defined(PMPC_SEQ)
 // one-row scan build (onerow != 0, N <= 15), else the sequential (throughput) builds: two waves per
 // SIMD, used once B exceeds the scan limit or N > 31
 template <bool RED>
@@ -1172,6 +1298,7 @@ extern "C" hipError_t dartmpc_launch_pmpc_seq(const dartmpc::PmpcArgs* a, unsign
                                               int onerow);
 extern "C" hipError_t dartmpc_launch_pmpc_serve_onerow(const dartmpc::PmpcArgs* a, const dartmpc::PmpcServe* sv,
                                                       unsigned grid, hipStream_t stream);
+extern "C" hipError_t dartmpc_launch_pmpc_wg2(const void* args, unsigned grid, hipStream_t stream);
 
 // the resident server for B_serve slots (IPOPT's path, N <= 31): one wave per slot, one XCD when it fits
 extern "C" hipError_t dartmpc_launch_pmpc_serve(const dartmpc::PmpcArgs* args, const dartmpc::PmpcServe* sv,
@@ -1231,6 +1358,12 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
         return 2 * 4 * cus;
     }();
     const bool occ2 = !a.reduced && a.B >= occ2_min_b && a.B <= qscan_max_b;
+    // N = 32..63 on IPOPT's path: the scan build on two waves per instance (DART_PMPC_SEQ_LONG=1: the one-wave
+    // sequential build, NAX = 2, for A/B)
+    static const bool long_wg2 = [] {
+        const char* e = getenv("DART_PMPC_SEQ_LONG");
+        return !(e && e[0] == '1');
+    }();
     // batches of at most 32 (one XCD, one instance per CU): IPOPT's restoration phases run in the wave that
     // handed the instance over (resto mode 3, pmpc_resto_tail), so no restoration launch follows the solve
     if (a.resto == 1 && a.pack == 8 && !a.reduced && a.N <= 31 && dartmpc::resto_fuse_enabled()) a.resto = 3;
@@ -1255,6 +1388,8 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
         else
             hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true>), grid, dim3(dartmpc::kWave), 0, stream, a);
+    } else if (a.N > 31 && !a.reduced && !a.resto && long_wg2) {
+        if (hipError_t e = dartmpc_launch_pmpc_wg2(&a, grid.x, stream)) return e;
     } else {
         if (hipError_t e = dartmpc_launch_pmpc_seq(&a, grid.x, stream, 0)) return e;
     }
