@@ -281,7 +281,15 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
     auto defects = [&](double pj, double vj, double sj, double spj, double svj, double& g1, double& g2) {
         const double fp = fma(a12, vj, fma(b1, sj, pj));
         const double fv = fma(a22, vj, b2 * sj);
-        const double ip = from_prev(fp), iv = from_prev(fv);
+        double ip, iv;
+        if constexpr (kWaves == 1) {
+            ip = from_prev(fp); iv = from_prev(fv);
+        } else {       // two waves: one exchange for both shifts
+            const double x2[2] = {fp, fv};
+            double o2[2];
+            from_prev_n(x2, o2);
+            ip = o2[0]; iv = o2[1];
+        }
         g1 = (k == 0) ? pj - spj : pj - ip;
         g2 = (k == 0) ? vj - svj : vj - iv;
     };
@@ -355,7 +363,15 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
             sn[j] = snc[j];
             const double c_ = tilt_cos_econ(poly, th[j]);
             cs[j] = uon ? c_ : 0.0;
-            const double ln = from_next(lp[j]), vn = from_next(lv[j]);   // unconditional: EXEC stays full
+            double ln, vn;       // unconditional: EXEC stays full
+            if constexpr (kWaves == 1) {
+                ln = from_next(lp[j]); vn = from_next(lv[j]);
+            } else {
+                const double x2[2] = {lp[j], lv[j]};
+                double o2[2];
+                from_next_n(x2, o2);
+                ln = o2[0]; vn = o2[1];
+            }
             lpn[j] = uon ? ln : 0.0; lvn[j] = uon ? vn : 0.0;
             const double sl = th[j] - lo, su = hi - th[j];
             isl[j] = uon ? frcp(sl) : 0.0; isu[j] = uon ? frcp(su) : 0.0;
@@ -494,6 +510,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                                                     fma(T[4 * i + 2], F[4 + jj], T[4 * i + 3] * F[6 + jj])));
                     }
                 }
+                double pnx[3] = {0.0, 0.0, 0.0};      // two waves: P_32 (wave 1's node 32) in wave 0
                 if constexpr (kWaves == 2) {
                     // two waves (N >= 32, rows as above): wave 1's suffixes reach the terminal; wave 0's continue
                     // from the value function of node 32, [U; Y]_k = T_k(..31) [I; P_32] (exact in the reals, as the
@@ -520,6 +537,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                         v[2] = fma(W[7], W[0], -W[6] * W[1]) * idet;
                     }
                     pm_pass(1, 0, v, pn);
+                    pnx[0] = pn[0]; pnx[1] = pn[1]; pnx[2] = pn[2];
                     if (wave_idx() == 0) {
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
@@ -537,7 +555,14 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                 const double q21 = fma(Y21, U22, -Y22 * U21) * idet, q22 = fma(Y22, U11, -Y21 * U12) * idet;
                 P11[0] = q11; P12[0] = 0.5 * (q12 + q21); P22[0] = q22;
                 // the stage quantities of node k from P_{k+1}
-                const double n11 = from_next(P11[0]), n12 = from_next(P12[0]), n22 = from_next(P22[0]);
+                double n11, n12, n22;
+                if constexpr (kWaves == 1) {
+                    n11 = from_next(P11[0]); n12 = from_next(P12[0]); n22 = from_next(P22[0]);
+                } else {
+                    // two waves: node 32's value function is already in wave 0 (pnx), no exchange
+                    n11 = dpp<kWaveShl1>(P11[0]); n12 = dpp<kWaveShl1>(P12[0]); n22 = dpp<kWaveShl1>(P22[0]);
+                    if (wave_idx() == 0 && (lane & 31) == 31) { n11 = pnx[0]; n12 = pnx[1]; n22 = pnx[2]; }
+                }
                 const double e1 = be1[0], e2 = be2[0];
                 const double Q = fma(E11[0], n11, fma(E12[0], n12, fma(E22[0], n22, Rt[0])));
                 const double PB1 = fma(n11, e1, n12 * e2), PB2 = fma(n12, e1, n22 * e2);
@@ -595,20 +620,32 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
             for (int j = 0; j < NAX; ++j) {      // right-hand side: the defects (0 for the multiplier estimate)
                 g1[j] = lsm ? 0.0 : g1o[j]; g2[j] = lsm ? 0.0 : g2o[j]; gz[j] = lsm ? 0.0 : gzo[j];
             }
+            double nPw[3];       // two waves: P_{k+1} fetched with g_{k+1} in one exchange
+            if constexpr (kWaves == 1) {
 #pragma unroll
-            for (int j = 0; j < NAX; ++j) { gn1[j] = from_next(g1[j]); gn2[j] = from_next(g2[j]); }
+                for (int j = 0; j < NAX; ++j) { gn1[j] = from_next(g1[j]); gn2[j] = from_next(g2[j]); }
+            } else {
+                const double x5[5] = {g1[0], g2[0], P11[0], P12[0], P22[0]};
+                double o5[5];
+                from_next_n(x5, o5);
+                gn1[0] = o5[0]; gn2[0] = o5[1]; nPw[0] = o5[2]; nPw[1] = o5[3]; nPw[2] = o5[4];
+            }
             if constexpr (NAX == 1) {
                 // linear part of the value function, p_k = M_k p_{k+1} + m_k with M_k = A_k^T - w_k e_k^T
                 // and m_k = q_k - w_k rt_k - M_k P_{k+1} g_{k+1}: a suffix scan of affine maps (row_shl
                 // 1/2/4/8 inside the rows, then row 1 -> row 0 of each half by a lane shuffle); the
                 // terminal/idle lanes carry M = 0, so each suffix stops at node N
                 const double e1 = be1[0], e2 = be2[0], w1 = W1[0], w2 = W2[0];
-                const double nP11 = from_next(P11[0]), nP12 = from_next(P12[0]), nP22 = from_next(P22[0]);
+                const double nP11 = kWaves == 1 ? from_next(P11[0]) : nPw[0];
+                const double nP12 = kWaves == 1 ? from_next(P12[0]) : nPw[1];
+                const double nP22 = kWaves == 1 ? from_next(P22[0]) : nPw[2];
                 const double t1 = fma(nP11, gn1[0], nP12 * gn2[0]), t2 = fma(nP12, gn1[0], nP22 * gn2[0]);
                 double m11 = fma(-w1, e1, f11), m12 = -w1 * e2, m21 = fma(-w2, e1, a12k), m22 = fma(-w2, e2, a22k);
                 const double rtk = rt[0];
                 double c1 = fma(-w1, rtk, q1[0]) - fma(m11, t1, m12 * t2);
                 double c2 = fma(-w2, rtk, q2[0]) - fma(m21, t1, m22 * t2);
+                double p32[2] = {0.0, 0.0};      // two waves: p of node 32 (wave 1) in wave 0
+                (void)p32;
                 affine_scan_level<0x101, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:1
                 affine_scan_level<0x102, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:2
                 affine_scan_level<0x104, 0xf>(m11, m12, m21, m22, c1, c2);   // row_shl:4
@@ -650,6 +687,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                         if (wave_idx() == 1) rows();
                         double r[2];
                         { const double v[2] = {c1, c2}; pm_pass(1, 0, v, r); }
+                        p32[0] = r[0]; p32[1] = r[1];
                         if (wave_idx() == 0) {
                             if (!lo_row) {
                                 c1 = fma(m11, r[0], fma(m12, r[1], c1));
@@ -661,15 +699,30 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                 }
                 p1[0] = c1; p2[0] = c2;
                 // feed-forward k_k = -(e^T h + rt) / Q with h = p_{k+1} - P_{k+1} g_{k+1}
-                const double np1 = from_next(c1), np2 = from_next(c2);
+                double np1, np2;
+                if constexpr (kWaves == 1) {
+                    np1 = from_next(c1); np2 = from_next(c2);
+                } else {
+                    // two waves: node 32's p is already in wave 0 (p32), no exchange
+                    np1 = dpp<kWaveShl1>(c1); np2 = dpp<kWaveShl1>(c2);
+                    if (wave_idx() == 0 && (lane & 31) == 31) { np1 = p32[0]; np2 = p32[1]; }
+                }
                 const double h1 = np1 - t1, h2 = np2 - t2;
                 kff[0] = -iQs[0] * fma(e1, h1, fma(e2, h2, rtk));
 
                 // forward sweep of the state step: dx_k = F_{k-1} dx_{k-1} + f_{k-1} - g_k as an
                 // inclusive scan of affine maps within each 32-lane axis half (DPP row_shr 1/2/4/8 inside
                 // the 16-lane rows, then row_bcast:15 into the second row of each half)
-                const double pw1 = from_prev(W1[0]), pw2 = from_prev(W2[0]), pkf = from_prev(kff[0]);
-                const double pb1 = from_prev(be1[0]), pb2 = from_prev(be2[0]);
+                double pw1, pw2, pkf, pb1, pb2;
+                if constexpr (kWaves == 1) {
+                    pw1 = from_prev(W1[0]); pw2 = from_prev(W2[0]); pkf = from_prev(kff[0]);
+                    pb1 = from_prev(be1[0]); pb2 = from_prev(be2[0]);
+                } else {
+                    const double x5[5] = {W1[0], W2[0], kff[0], be1[0], be2[0]};
+                    double o5[5];
+                    from_prev_n(x5, o5);
+                    pw1 = o5[0]; pw2 = o5[1]; pkf = o5[2]; pb1 = o5[3]; pb2 = o5[4];
+                }
                 double f11_ = 1.0 - pb1 * pw1, f12_ = fma(-pb1, pw2, a12), f21_ = -pb2 * pw1, f22_ = fma(-pb2, pw2, a22);
                 double d1 = fma(pb1, pkf, -g1[0]), d2 = fma(pb2, pkf, -g2[0]);
                 if (k == 0) { f11_ = 0.0; f12_ = 0.0; f21_ = 0.0; f22_ = 0.0; d1 = -g1[0]; d2 = -g2[0]; }
@@ -808,6 +861,31 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
         // trial point x + al d: defects, wave-summed theta and barrier objective
         auto trial = [&](double al) {
             double thl = 0.0, phl = 0.0, tt[NAX];
+            if constexpr (kWaves == 2 && NAX == 1 && !RED) {
+                // two waves: the three node shifts of the trial's defects (defects, zdefect) in one exchange
+                const double pt = fma(al, dp[0], p[0]), vt = fma(al, dv[0], v[0]);
+                tt[0] = fma(al, dth[0], th[0]);
+                double s_, c_;
+                tilt_sincos(poly, tt[0], s_, c_);
+                snt[0] = uon ? s_ : 0.0;
+                const double wt = vz_new(tt);
+                const double zt = fma(al, dz[0], zz[0]);
+                const double x3[3] = {fma(a12, vt, fma(b1, snt[0], pt)), fma(a22, vt, b2 * snt[0]),
+                                      fma(zA[0], zt, zC[0] * wt)};
+                double o3[3];
+                from_prev_n(x3, o3);
+                g1t[0] = (k == 0) ? pt - sp[0] : pt - o3[0];
+                g2t[0] = (k == 0) ? vt - sv[0] : vt - o3[1];
+                gzt[0] = (k == 0) ? zt - zs[0] : zt - o3[2];
+                const double ep = pt - rp[0], ev = vt - rv[0];
+                thl += xon ? fabs(g1t[0]) + fabs(g2t[0]) : 0.0;
+                phl += xon ? fma(scQp * ep, ep, scQv * ev * ev) : 0.0;
+                phl += uon ? fma(scR * tt[0], tt[0], -mu * log_fast((tt[0] - lo) * (hi - tt[0]))) : 0.0;
+                thl += xon ? fabs(gzt[0]) : 0.0;
+                wsum2(thl, phl);
+                th_t = thl; ph_t = phl;
+                return;
+            }
 #pragma unroll
             for (int j = 0; j < NAX; ++j) {
                 const double pt = fma(al, dp[j], p[j]), vt = fma(al, dv[j], v[j]);

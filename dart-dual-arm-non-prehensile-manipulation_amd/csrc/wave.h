@@ -236,6 +236,56 @@ __device__ __forceinline__ double from_prev(double x) {
 }
 #endif
 
+// NV node shifts at once: one wave, the DPP shifts of from_next / from_prev; two waves, one LDS exchange for all
+// NV values (two barriers) instead of one per value
+#if DART_WG == 2
+__shared__ double g_wg_s[2][2][8];        // [wave][lane half][value]
+#endif
+template <int NV>
+__device__ __forceinline__ void from_next_n(const double (&x)[NV], double (&o)[NV]) {
+#if DART_WG == 1
+#pragma unroll
+    for (int i = 0; i < NV; ++i) o[i] = from_next(x[i]);
+#else
+    static_assert(NV <= 8, "eight slots");
+    const int l = lane_id(), w = wave_idx();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) o[i] = dpp<kWaveShl1>(x[i]);
+    if (l == 0 || l == 32) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) g_wg_s[w][l >> 5][i] = x[i];
+    }
+    __syncthreads();
+    if (w == 0 && (l == 31 || l == 63)) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) o[i] = g_wg_s[1][l >> 5][i];
+    }
+    __syncthreads();
+#endif
+}
+template <int NV>
+__device__ __forceinline__ void from_prev_n(const double (&x)[NV], double (&o)[NV]) {
+#if DART_WG == 1
+#pragma unroll
+    for (int i = 0; i < NV; ++i) o[i] = from_prev(x[i]);
+#else
+    static_assert(NV <= 8, "eight slots");
+    const int l = lane_id(), w = wave_idx();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) o[i] = dpp<kWaveShr1>(x[i]);
+    if (l == 31 || l == 63) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) g_wg_s[w][l >> 5][i] = x[i];
+    }
+    __syncthreads();
+    if (w == 1 && (l == 0 || l == 32)) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) o[i] = g_wg_s[0][l >> 5][i];
+    }
+    __syncthreads();
+#endif
+}
+
 struct OpSum { __device__ double operator()(double a, double b) const { return a + b; } };
 struct OpMax { __device__ double operator()(double a, double b) const { return fmax(a, b); } };
 struct OpMin { __device__ double operator()(double a, double b) const { return fmin(a, b); } };
