@@ -600,9 +600,14 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
         tilt_sincos_econ(poly, uu, sa, ca);
         sub_rk4(m, xx, sa, xn);
         double f[5];
+        if constexpr (kWaves == 1) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) f[i] = from_prev(xn[i]);
-        f[4] = from_prev(uu);
+            for (int i = 0; i < 4; ++i) f[i] = from_prev(xn[i]);
+            f[4] = from_prev(uu);
+        } else {       // two waves: one exchange for the five shifts
+            const double x5[5] = {xn[0], xn[1], xn[2], xn[3], uu};
+            from_prev_n(x5, f);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) g[i] = k == 0 ? xx[i] - st0[i] : xx[i] - f[i];
         g[4] = k == 0 ? pp - upv : pp - f[4];
@@ -651,7 +656,16 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
             rs[i] = uon ? (mx > 100.0 ? 100.0 / mx : 1.0) : 1.0;
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { const double t = from_prev(rs[i]); dsc[i] = k == 0 ? 1.0 : t; }
+        for (int i = 0; i < 4; ++i) {
+            const double t = kWaves == 1 ? from_prev(rs[i]) : 0.0;
+            dsc[i] = k == 0 ? 1.0 : t;
+        }
+        if constexpr (kWaves == 2) {
+            double t4[4];
+            from_prev_n(rs, t4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dsc[i] = k == 0 ? 1.0 : t4[i];
+        }
     }
 
     const double tol = a.tol, mu_min = tol / 10;
@@ -728,13 +742,24 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
     // incoming augmented defects g_k of node k from x+ of every node (as at the top of the loop)
     auto incoming = [&](const double* xx, double ppv, double uu, const double* xn_, double* g) {
         double cdef[5];
+        if constexpr (kWaves == 1) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { const double t = from_next(xx[i]); cdef[i] = xn_[i] - t; }
-        { const double t0 = from_next(ppv); cdef[4] = uu - t0; }
+            for (int i = 0; i < 4; ++i) { const double t = from_next(xx[i]); cdef[i] = xn_[i] - t; }
+            { const double t0 = from_next(ppv); cdef[4] = uu - t0; }
 #pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const double t = from_prev(cdef[i]);
-            g[i] = k == 0 ? (i < 4 ? xx[i] - st0[i] : ppv - upv) : -t;
+            for (int i = 0; i < 5; ++i) {
+                const double t = from_prev(cdef[i]);
+                g[i] = k == 0 ? (i < 4 ? xx[i] - st0[i] : ppv - upv) : -t;
+            }
+        } else {       // two waves: two exchanges
+            double t5[5], pcd[5];
+            { const double x5[5] = {xx[0], xx[1], xx[2], xx[3], ppv}; from_next_n(x5, t5); }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cdef[i] = xn_[i] - t5[i];
+            cdef[4] = uu - t5[4];
+            from_prev_n(cdef, pcd);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) g[i] = k == 0 ? (i < 4 ? xx[i] - st0[i] : ppv - upv) : -pcd[i];
         }
     };
     // IPOPT's primal-dual system error at mu (l1 norms of the scaled primal infeasibility, the dual
@@ -743,8 +768,16 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
     auto pd_l1 = [&](const double* xx, double ppv, double uu, const double* lm, double zlv, double zuv) {
         double lmn[5], jl_[5], xn_[4], g[5], gl[6];
         const double c0z[4] = {0.0, 0.0, 0.0, 0.0};
+        if constexpr (kWaves == 1) {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) { const double t = from_next(lm[i]); lmn[i] = uon ? t : 0.0; }
+            for (int i = 0; i < 5; ++i) { const double t = from_next(lm[i]); lmn[i] = uon ? t : 0.0; }
+        } else {
+            const double x5[5] = {lm[0], lm[1], lm[2], lm[3], lm[4]};
+            double t5[5];
+            from_next_n(x5, t5);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) lmn[i] = uon ? t5[i] : 0.0;
+        }
         deriv_pass(xx, uu, lmn, c0z, 0.0, jl_, xn_);
         incoming(xx, ppv, uu, xn_, g);
         double tot = 0.0;
@@ -801,8 +834,15 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
         // ---------------- derivatives, residuals, optimality error ---------------------------
         const double isl = uon ? frcp(u - lo) : 0.0, isu = uon ? frcp(hi - u) : 0.0;
         double lamn[5];
+        if constexpr (kWaves == 1) {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) { const double t = from_next(lam[i]); lamn[i] = uon ? t : 0.0; }
+            for (int i = 0; i < 5; ++i) { const double t = from_next(lam[i]); lamn[i] = uon ? t : 0.0; }
+        } else {
+            double t5[5];
+            from_next_n(lam, t5);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) lamn[i] = uon ? t5[i] : 0.0;
+        }
         double jl[5];       // J^T lambda_{k+1} (x columns 0..3, tilt 4)
         double pinf, pinf_u;  // primal residual maxima
         {
@@ -840,9 +880,20 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
             }
             // outgoing augmented defect c_k = [F(z_k); u_k] - x~_{k+1} -> defect column of M~
             double cdef[5];
+            double pcd[5];       // (two waves: the shifts in two exchanges, the incoming ones here)
+            if constexpr (kWaves == 1) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { const double t = from_next(x[i]); cdef[i] = xn[i] - t; }
-            { const double t0 = from_next(up); cdef[4] = u - t0; }
+                for (int i = 0; i < 4; ++i) { const double t = from_next(x[i]); cdef[i] = xn[i] - t; }
+                { const double t0 = from_next(up); cdef[4] = u - t0; }
+            } else {
+                const double x5[5] = {x[0], x[1], x[2], x[3], up};
+                double t5[5];
+                from_next_n(x5, t5);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cdef[i] = xn[i] - t5[i];
+                cdef[4] = u - t5[4];
+                from_prev_n(cdef, pcd);
+            }
             if (uon) {
 #pragma unroll
                 for (int r = 0; r < 5; ++r) Mk[6 * NC + r] = cdef[r];
@@ -851,7 +902,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
             double pl = 0.0, plu = 0.0;
 #pragma unroll
             for (int i = 0; i < 5; ++i) {
-                const double t = from_prev(cdef[i]);
+                const double t = kWaves == 1 ? from_prev(cdef[i]) : pcd[i];
                 double gi = -t;
                 if (k == 0) gi = i < 4 ? x[i] - st0[i] : up - upv;
                 const double d = i < 4 ? dsc[i] : 1.0;

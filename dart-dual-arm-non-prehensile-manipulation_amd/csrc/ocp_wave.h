@@ -628,8 +628,15 @@ __device__ void forward_sweep(L* S, int N, int node, double* dxo) {
 #pragma unroll
     for (int i = 0; i < NXA; ++i) dxo[i] = (even_n || odd_end) ? S->dxs[slot][i] : S->dx0[i];
     double pv[NXA];
+    if constexpr (kWaves == 1) {
 #pragma unroll
-    for (int i = 0; i < NXA; ++i) pv[i] = from_prev(dxo[i]);
+        for (int i = 0; i < NXA; ++i) pv[i] = from_prev(dxo[i]);
+    } else {       // two waves: one exchange
+        double xo[NXA];
+#pragma unroll
+        for (int i = 0; i < NXA; ++i) xo[i] = dxo[i];
+        from_prev_n(xo, pv);
+    }
     if ((node & 1) && node < 2 * np2) {
 #pragma unroll
         for (int rr = 0; rr < NXA; ++rr) {
@@ -886,8 +893,15 @@ __device__ void forward_sweep_s(L* S, int N, int node, double* dxo) {
 #pragma unroll
     for (int i = 0; i < NXA; ++i) dxo[i] = (even_n || odd_end) ? S->dxs[h][slot][i] : S->dx0[h][i];
     double pv[NXA];
+    if constexpr (kWaves == 1) {
 #pragma unroll
-    for (int i = 0; i < NXA; ++i) pv[i] = from_prev(dxo[i]);
+        for (int i = 0; i < NXA; ++i) pv[i] = from_prev(dxo[i]);
+    } else {       // two waves: one exchange
+        double xo[NXA];
+#pragma unroll
+        for (int i = 0; i < NXA; ++i) xo[i] = dxo[i];
+        from_prev_n(xo, pv);
+    }
     if ((node & 1) && node < 2 * np2) {
 #pragma unroll
         for (int rr = 0; rr < NXA; ++rr) {

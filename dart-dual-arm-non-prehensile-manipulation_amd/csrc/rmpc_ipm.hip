@@ -471,9 +471,14 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
         rm_sincos2(uu, sa, ca, sb, cb);
         rm_rk4(m, xx, sa, sb, xn, mir);
         double f[6];
+        if constexpr (kWaves == 1) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) f[i] = from_prev(xn[i]);
-        f[4] = from_prev(uu[0]); f[5] = from_prev(uu[1]);
+            for (int i = 0; i < 4; ++i) f[i] = from_prev(xn[i]);
+            f[4] = from_prev(uu[0]); f[5] = from_prev(uu[1]);
+        } else {       // two waves: one exchange for the six shifts
+            const double x6[6] = {xn[0], xn[1], xn[2], xn[3], uu[0], uu[1]};
+            from_prev_n(x6, f);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) g[i] = k == 0 ? xx[i] - x0[i] : xx[i] - f[i];
         g[4] = k == 0 ? pp[0] - upv[0] : pp[0] - f[4];
@@ -531,8 +536,15 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
         // stage data go to LDS as soon as they exist (Jacobian columns, dynamics Hessian, defect
         // column, dx~_0) to keep the register working set small
         double lamn[6];
+        if constexpr (kWaves == 1) {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) { const double t = from_next(lam[i]); lamn[i] = uon ? t : 0.0; }
+            for (int i = 0; i < 6; ++i) { const double t = from_next(lam[i]); lamn[i] = uon ? t : 0.0; }
+        } else {
+            double t6[6];
+            from_next_n(lam, t6);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) lamn[i] = uon ? t6[i] : 0.0;
+        }
         double jl[6];            // J^T lambda_{k+1} (x columns 0..3, tilt 4..5)
         {
             double sa, ca, sb, cb;
@@ -550,9 +562,20 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) jl[i] = uon ? SH.JL[sr][i] : 0.0;
             double cdef[6];      // outgoing defect c_k = F(z_k) - x~_{k+1} -> defect column of M~
+            double pcd[6];       // (two waves: the shifts in two exchanges, the incoming ones here)
+            if constexpr (kWaves == 1) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { const double t = from_next(x[i]); cdef[i] = xn[i] - t; }
-            { const double t0 = from_next(up[0]), t1 = from_next(up[1]); cdef[4] = u[0] - t0; cdef[5] = u[1] - t1; }
+                for (int i = 0; i < 4; ++i) { const double t = from_next(x[i]); cdef[i] = xn[i] - t; }
+                { const double t0 = from_next(up[0]), t1 = from_next(up[1]); cdef[4] = u[0] - t0; cdef[5] = u[1] - t1; }
+            } else {
+                const double x6[6] = {x[0], x[1], x[2], x[3], up[0], up[1]};
+                double t6[6];
+                from_next_n(x6, t6);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cdef[i] = xn[i] - t6[i];
+                cdef[4] = u[0] - t6[4]; cdef[5] = u[1] - t6[5];
+                from_prev_n(cdef, pcd);
+            }
             if (uon) {
 #pragma unroll
                 for (int r = 0; r < 6; ++r) Mk[8 * RmLds::NC + r] = lsm ? 0.0 : cdef[r];
@@ -560,7 +583,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
             double pl = 0.0;     // incoming defect g_k: primal residual, -g_0 = dx~_0
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                const double t = from_prev(cdef[i]);
+                const double t = kWaves == 1 ? from_prev(cdef[i]) : pcd[i];
                 double gi = -t;
                 if (k == 0) gi = i < 4 ? x[i] - x0[i] : up[i - 4] - upv[i - 4];
                 pl = fmax(pl, xon ? fabs(gi) : 0.0);
@@ -1143,8 +1166,15 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
         // M~, the dynamics Hessian into H~, jl = J^T lmn (x columns 0..3, tilts 4..5), xn = x+ of node k
         double lmn[6], jl[6], xn[4], hd[6];
         auto rderiv = [&]() {
+            if constexpr (kWaves == 1) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) { const double t = from_next(lam[i]); lmn[i] = uon ? t : 0.0; }
+                for (int i = 0; i < 6; ++i) { const double t = from_next(lam[i]); lmn[i] = uon ? t : 0.0; }
+            } else {
+                double t6[6];
+                from_next_n(lam, t6);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) lmn[i] = uon ? t6[i] : 0.0;
+            }
             double sa, ca, sb, cb, huu[2], scr[4][4], sdr[4][2];
             rm_sincos2(u, sa, ca, sb, cb);
             rm_rk4_lin(m, x, sa, sb, xn, scr, sdr, mir);
@@ -1161,13 +1191,24 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
         // incoming defects of node k (6 rows) from x+ of every node
         auto incoming = [&](double* g) {
             double cdef[6];
+            if constexpr (kWaves == 1) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { const double t = from_next(x[i]); cdef[i] = xn[i] - t; }
-            { const double t0 = from_next(up[0]), t1 = from_next(up[1]); cdef[4] = u[0] - t0; cdef[5] = u[1] - t1; }
+                for (int i = 0; i < 4; ++i) { const double t = from_next(x[i]); cdef[i] = xn[i] - t; }
+                { const double t0 = from_next(up[0]), t1 = from_next(up[1]); cdef[4] = u[0] - t0; cdef[5] = u[1] - t1; }
 #pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const double t = from_prev(cdef[i]);
-                g[i] = k == 0 ? (i < 4 ? x[i] - x0[i] : up[i - 4] - upv[i - 4]) : -t;
+                for (int i = 0; i < 6; ++i) {
+                    const double t = from_prev(cdef[i]);
+                    g[i] = k == 0 ? (i < 4 ? x[i] - x0[i] : up[i - 4] - upv[i - 4]) : -t;
+                }
+            } else {       // two waves: two exchanges
+                double t6[6], pcd[6];
+                { const double x6[6] = {x[0], x[1], x[2], x[3], up[0], up[1]}; from_next_n(x6, t6); }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cdef[i] = xn[i] - t6[i];
+                cdef[4] = u[0] - t6[4]; cdef[5] = u[1] - t6[5];
+                from_prev_n(cdef, pcd);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) g[i] = k == 0 ? (i < 4 ? x[i] - x0[i] : up[i - 4] - upv[i - 4]) : -pcd[i];
             }
         };
         // the inequality rows (shift delta; lsq: the least-square multipliers' unit weights): Sigma's, sigma,

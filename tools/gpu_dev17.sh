@@ -1,0 +1,12 @@
+# Two-wave RMPC / LMPC with batched node shifts: A/B identity against the one-wave kernels, speed, tests, timings
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u tools/wg2_ab.py > gpurun_out/wg2_ab3.txt 2>&1; rc=$?
+tail -8 gpurun_out/wg2_ab3.txt; [ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python -u tools/wg2_speed.py > gpurun_out/wg2_speed3.txt 2>&1; rc=$?
+cat gpurun_out/wg2_speed3.txt; [ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python -u tools/long_diag.py 40 > gpurun_out/long_diag3.txt 2>&1; rc=$?
+cat gpurun_out/long_diag3.txt; [ $rc -eq 0 ] || exit 1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_rmpc.py tests/test_gpu_lmpc.py -q --timeout 300 --timeout-method thread > gpurun_out/wg2_tests3.log 2>&1; rc=$?
+tail -4 gpurun_out/wg2_tests3.log; [ $rc -eq 0 ] || exit 1
+echo DEV17_OK
