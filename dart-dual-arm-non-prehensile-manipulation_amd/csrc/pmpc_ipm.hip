@@ -62,14 +62,16 @@ __device__ unsigned long long g_stamp_seq[16];
 #endif
 
 // values of node `src_node` of wave `src_wave` (lane src_node: axis x, lane src_node + 32: axis y) in every lane of
-// the same axis half of both waves; two barriers (the second keeps the next hand-over from overwriting a slot
-// still to be read).  Two-wave build only (the one-wave build names it in discarded branches).
+// the same axis half of both waves.  One barrier: every call site SITE has its own slots, and between two passes
+// of one site both waves cross other barriers (the reductions and shifts of an iteration), each after its reads
+// of the slot have completed (__syncthreads waits for the wave's LDS accesses), so no pass overwrites a slot that
+// is still to be read.  Two-wave build only (the one-wave build names it in discarded branches).
 #if DART_WG == 2
-__shared__ double g_pm_x[2][4];
+__shared__ double g_pm_x[4][2][4];
 #endif
-template <int NV>
+template <int SITE, int NV>
 __device__ __forceinline__ void pm_pass(int src_wave, int src_node, const double (&v)[NV], double (&o)[NV]) {
-    static_assert(NV <= 4, "four slots");
+    static_assert(NV <= 4 && SITE < 4, "four slots, four sites");
 #if DART_WG == 1
     (void)src_wave; (void)src_node;
 #pragma unroll
@@ -78,12 +80,11 @@ __device__ __forceinline__ void pm_pass(int src_wave, int src_node, const double
     const int l = lane_id();
     if (wave_idx() == src_wave && (l & 31) == src_node) {
 #pragma unroll
-        for (int i = 0; i < NV; ++i) g_pm_x[l >> 5][i] = v[i];
+        for (int i = 0; i < NV; ++i) g_pm_x[SITE][l >> 5][i] = v[i];
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < NV; ++i) o[i] = g_pm_x[l >> 5][i];
-    __syncthreads();
+    for (int i = 0; i < NV; ++i) o[i] = g_pm_x[SITE][l >> 5][i];
 #endif
 }
 
@@ -536,7 +537,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                         v[1] = 0.5 * (fma(W[5], W[0], -W[4] * W[1]) * idet + fma(W[6], W[3], -W[7] * W[2]) * idet);
                         v[2] = fma(W[7], W[0], -W[6] * W[1]) * idet;
                     }
-                    pm_pass(1, 0, v, pn);
+                    pm_pass<0>(1, 0, v, pn);
                     pnx[0] = pn[0]; pnx[1] = pn[1]; pnx[2] = pn[2];
                     if (wave_idx() == 0) {
 #pragma unroll
@@ -686,7 +687,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                         // two waves: wave 0's rows 1 / 3 (their maps span nodes k..31) continue from p_32 of wave 1
                         if (wave_idx() == 1) rows();
                         double r[2];
-                        { const double v[2] = {c1, c2}; pm_pass(1, 0, v, r); }
+                        { const double v[2] = {c1, c2}; pm_pass<1>(1, 0, v, r); }
                         p32[0] = r[0]; p32[1] = r[1];
                         if (wave_idx() == 0) {
                             if (!lo_row) {
@@ -740,7 +741,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                     // two waves: wave 1's rows 0 / 2 (their maps span nodes 32..k) continue from dx_31 of wave 0
                     if (wave_idx() == 0) affine_scan_const<0x142, 0xa>(f11_, f12_, f21_, f22_, d1, d2);
                     double r[2];
-                    { const double v[2] = {d1, d2}; pm_pass(0, 31, v, r); }
+                    { const double v[2] = {d1, d2}; pm_pass<2>(0, 31, v, r); }
                     if (wave_idx() == 1) {
                         if ((lane & 16) == 0) {
                             d1 = fma(f11_, r[0], fma(f12_, r[1], d1));
@@ -832,7 +833,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                 } else {       // two waves: as the state sweep
                     if (wave_idx() == 0) affine1_scan_const<0x142, 0xa>(m, c);
                     double r[1];
-                    { const double v[1] = {c}; pm_pass(0, 31, v, r); }
+                    { const double v[1] = {c}; pm_pass<3>(0, 31, v, r); }
                     if (wave_idx() == 1) {
                         if ((lane & 16) == 0) c = fma(m, r[0], c);
                         affine1_scan_const<0x142, 0xa>(m, c);
@@ -916,7 +917,9 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
         // filter acceptance of (th_t, ph_t) for the step size al_test (IPOPT alpha_primal_test)
         auto acceptable = [&](double al_test, bool& ft) {
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
-            in_filter = in_filter || wany(lane < nfilt && th_t >= fth && ph_t >= fph);
+            // (two waves: both hold the same filter entries, so the wave's own ballot decides)
+            if constexpr (kWaves == 1) in_filter = in_filter || wany(lane < nfilt && th_t >= fth && ph_t >= fph);
+            else in_filter = in_filter || __ballot(lane < nfilt && th_t >= fth && ph_t >= fph) != 0ull;
             if (in_filter) return false;
             const bool sw = gTd < 0.0 && lg2(al_test) > lg_sw;
             if (theta <= th_min && sw) {
@@ -951,7 +954,19 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                     phil += uon ? fma(scR * th[j], th[j], -mu * log_fast(sl * su)) : 0.0;
                     gtdl += uon ? rt[j] * dth[j] : 0.0;
                 }
-                wsum2(phil, gtdl);
+                float tn_w = 0.0f;      // two waves: the tiny-step maximum (below) rides with the two sums
+                if constexpr (kWaves == 1) {
+                    wsum2(phil, gtdl);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < NAX; ++j) {
+                        tn_w = fmaxf(tn_w, xon ? fabsf((float)dp[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)p[j])) : 0.0f);
+                        tn_w = fmaxf(tn_w, xon ? fabsf((float)dv[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)v[j])) : 0.0f);
+                        tn_w = fmaxf(tn_w, xon ? fabsf((float)dz[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)zz[j])) : 0.0f);
+                        tn_w = fmaxf(tn_w, uon ? fabsf((float)dth[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)th[j])) : 0.0f);
+                    }
+                    wsum2_maxf(phil, gtdl, tn_w);
+                }
                 phi = phil; gTd = gtdl;
                 // switching condition alpha (-gTd)^s_ph > delta theta^s_th, compared in log2 space
                 const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
@@ -961,15 +976,19 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                 if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta * frcp(-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
                 amin *= gam_al;
                 // IPOPT's tiny-step test: max |d|/(1+|x|) < 10 eps_mach accepts the full step unfiltered
-                float tnl = 0.0f;
+                if constexpr (kWaves == 1) {
+                    float tnl = 0.0f;
 #pragma unroll
-                for (int j = 0; j < NAX; ++j) {
-                    tnl = fmaxf(tnl, xon ? fabsf((float)dp[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)p[j])) : 0.0f);
-                    tnl = fmaxf(tnl, xon ? fabsf((float)dv[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)v[j])) : 0.0f);
-                    tnl = fmaxf(tnl, xon ? fabsf((float)dz[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)zz[j])) : 0.0f);
-                    tnl = fmaxf(tnl, uon ? fabsf((float)dth[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)th[j])) : 0.0f);
+                    for (int j = 0; j < NAX; ++j) {
+                        tnl = fmaxf(tnl, xon ? fabsf((float)dp[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)p[j])) : 0.0f);
+                        tnl = fmaxf(tnl, xon ? fabsf((float)dv[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)v[j])) : 0.0f);
+                        tnl = fmaxf(tnl, xon ? fabsf((float)dz[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)zz[j])) : 0.0f);
+                        tnl = fmaxf(tnl, uon ? fabsf((float)dth[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)th[j])) : 0.0f);
+                    }
+                    tiny = wmaxf(tnl) < 2.2e-15f;
+                } else {
+                    tiny = tn_w < 2.2e-15f;
                 }
-                tiny = wmaxf(tnl) < 2.2e-15f;
                 alpha = amax; amain = amax;
             } else if (soc > 0) {
                 alpha = amax;                 // alpha_soc: fraction to the boundary of the corrected step

@@ -392,6 +392,25 @@ __device__ __forceinline__ void wsum2(double& a, double& b) {
     { const double v[2] = {a, b}; double o[2][2]; wg_both(v, o); a = o[0][0] + o[1][0]; b = o[0][1] + o[1][1]; }
 #endif
 }
+// two f64 sums and one f32 maximum of non-negative values (wreduce_nn) together: two waves, one exchange
+__device__ __forceinline__ void wsum2_maxf(double& a, double& b, float& m) {
+#if DART_WG == 1
+    wsum2(a, b);
+    m = wmaxf(m);
+#else
+    unsigned x = __builtin_bit_cast(unsigned, m);
+#define DART_L(C, R) lvl_sum<C, R>(a); lvl_sum<C, R>(b); lvl_maxu<C, R>(x);
+    DART_LEVELS(DART_L)
+#undef DART_L
+    a = readlane(a, 63); b = readlane(b, 63);
+    x = (unsigned)__builtin_amdgcn_readlane((int)x, 63);
+    const double v[3] = {a, b, (double)x};
+    double o[2][3];
+    wg_both(v, o);
+    a = o[0][0] + o[1][0]; b = o[0][1] + o[1][1];
+    m = __builtin_bit_cast(float, (unsigned)fmax(o[0][2], o[1][2]));
+#endif
+}
 // two f32 minima of non-negative values (see wreduce_nn)
 __device__ __forceinline__ void wmin2f(float& a, float& b) {
     unsigned x = __builtin_bit_cast(unsigned, a), y = __builtin_bit_cast(unsigned, b);
