@@ -1103,7 +1103,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
         // filter acceptance of (th_t, ph_t) for the step size al_test (IPOPT alpha_primal_test)
         auto acceptable = [&](double al_test, bool& ft) {
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
-            in_filter = in_filter || wany(lane < nfilt && th_t >= fth && ph_t >= fph);
+            in_filter = in_filter || wany_rep(lane < nfilt && th_t >= fth && ph_t >= fph);
             if (in_filter) return false;
             const bool sw = gTd < 0.0 && lg2(al_test) > lg_sw;
             if (theta <= th_min && sw) {
@@ -1543,7 +1543,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                         double pl = sc * cost_val(x, u, up);
                         if (uon) pl -= mu0 * log_fast((u - lo) * (hi - u));
                         const double pho = wsum(pl);
-                        bool accp = isfinite(pho) && !wany(lane < nfilt && tho >= fth && pho >= fph);
+                        bool accp = isfinite(pho) && !wany_rep(lane < nfilt && tho >= fth && pho >= fph);
                         accp = accp && (cmp_le(tho, (1 - gam_th) * th0, th0) || cmp_le(pho - phi0, -gam_ph * th0, phi0));
                         if (accp) { rok = true; theta = tho; break; }
                     }
@@ -1834,7 +1834,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                     tht = thl; pht = phl;
                 };
                 auto racc = [&](double al_test, bool& ft) {
-                    const bool in_f = !(tht < rth_max) || !isfinite(pht) || wany(lane < rnf && tht >= rfth && pht >= rfph);
+                    const bool in_f = !(tht < rth_max) || !isfinite(pht) || wany_rep(lane < rnf && tht >= rfth && pht >= rfph);
                     if (in_f) return false;
                     const bool sw = gtdr < 0.0 && al_test * pow(-gtdr, s_ph) > pow(thr, s_th);
                     if (thr <= rth_min && sw) {

@@ -917,9 +917,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
         // filter acceptance of (th_t, ph_t) for the step size al_test (IPOPT alpha_primal_test)
         auto acceptable = [&](double al_test, bool& ft) {
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
-            // (two waves: both hold the same filter entries, so the wave's own ballot decides)
-            if constexpr (kWaves == 1) in_filter = in_filter || wany(lane < nfilt && th_t >= fth && ph_t >= fph);
-            else in_filter = in_filter || __ballot(lane < nfilt && th_t >= fth && ph_t >= fph) != 0ull;
+            in_filter = in_filter || wany_rep(lane < nfilt && th_t >= fth && ph_t >= fph);   // (replicated filter)
             if (in_filter) return false;
             const bool sw = gTd < 0.0 && lg2(al_test) > lg_sw;
             if (theta <= th_min && sw) {

@@ -902,7 +902,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
             th_t = wsum_rl(thl); ph_t = wsum_rl(phl);
             if (tiny) { accepted = true; ftype = true; break; }
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
-            in_filter = in_filter || wany(lane < nfilt && th_t >= fth && ph_t >= fph);
+            in_filter = in_filter || wany_rep(lane < nfilt && th_t >= fth && ph_t >= fph);
             if (!in_filter) {
                 const bool sw = gTd < 0.0 && lg2(alpha) > lg_sw;
                 if (theta <= th_min && sw) {
@@ -964,7 +964,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                         phl -= uon ? mu * log_fast(barrier_args(ut, st_)) : 0.0;
                         th_s = wsum_rl(thl); ph_s = wsum_rl(phl);
                     }
-                    bool orig = th_s < th_max && isfinite(ph_s) && !wany(lane < nfilt && th_s >= fth && ph_s >= fph);
+                    bool orig = th_s < th_max && isfinite(ph_s) && !wany_rep(lane < nfilt && th_s >= fth && ph_s >= fph);
                     orig = orig && (cmp_le(th_s, (1 - gam_th) * theta, theta) || cmp_le(ph_s - phi, -gam_ph * theta, phi));
                     bool take = orig;
                     if (!take && isfinite(ph_s)) {
@@ -1504,7 +1504,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                         }
                         pl -= uon ? mu0 * log_fast(pa) : 0.0;
                         const double pho = wsum_rl(pl);
-                        bool accp = isfinite(pho) && !wany(lane < nfilt && tho >= fth && pho >= fph);
+                        bool accp = isfinite(pho) && !wany_rep(lane < nfilt && tho >= fth && pho >= fph);
                         accp = accp && (cmp_le(tho, (1 - gam_th) * th0, th0) || cmp_le(pho - phi0, -gam_ph * th0, phi0));
                         if (accp) { rok = true; theta = tho; break; }
                     }
@@ -1838,7 +1838,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                 tht = wsum_rl(thl); pht = wsum_rl(phl);
             };
             auto racc = [&](double al_test, bool& ft) {
-                const bool in_f = !(tht < rth_max) || !isfinite(pht) || wany(lane < rnf && tht >= rfth && pht >= rfph);
+                const bool in_f = !(tht < rth_max) || !isfinite(pht) || wany_rep(lane < rnf && tht >= rfth && pht >= rfph);
                 if (in_f) return false;
                 const bool sw = gtdr < 0.0 && al_test * pow(-gtdr, s_ph) > pow(thr, s_th);
                 if (thr <= rth_min && sw) {

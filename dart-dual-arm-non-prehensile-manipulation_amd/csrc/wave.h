@@ -497,6 +497,10 @@ __device__ __forceinline__ bool wany(bool p) {
     return r;
 }
 
+// any over the wave of a predicate on state that both waves of a two-wave instance hold alike (the filter
+// entries, one per lane, set from wave-uniform values): the wave's own ballot decides, no exchange
+__device__ __forceinline__ bool wany_rep(bool p) { return __ballot(p) != 0ull; }
+
 // reciprocal: v_rcp_f64 (measured max relative error 2e-8 on gfx950, tests/test_gpu_pmpc.py
 // selftest) + one Newton step -> ~4e-16 relative; operands are well scaled, no denormals
 __device__ __forceinline__ double frcp(double x) {
