@@ -242,6 +242,27 @@ def test_long_horizons_two_wave_scan_same_path(dm, N):
     assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6
 
 
+@pytest.mark.parametrize("N", [40, 63])
+def test_long_horizon_decision_vector_and_warm_start(dm, N):
+    """The two-wave build writes w (mpc_3d.py:69 layout: x_0..x_N, then u_0..u_{N-1}) from both waves -- nodes 0..31
+    from wave 0, 32..N from wave 1 -- and reads a warm start the same way: w against the oracle's at the same
+    tolerance, then a warm start from the kernel's own w returns the same u0 in fewer iterations."""
+    import oracle_lib
+    from dart_mpc.workload import pmpc_batch
+    S, T, P = pmpc_batch(1)
+    s = dm.Solver(N=N, Ts=0.002, tol=1e-10, B_max=64)
+    cold = s.solve_batch(S, T, P, want_w=True)
+    o = oracle_lib.solve_batch(S, T, P, N=N, Ts=0.002, tol=1e-10, nthreads=8, want_w=True)
+    assert np.all(cold["status"] == 0) and np.array_equal(cold["status"], o["status"])
+    assert cold["w"].shape == (S.shape[0], _nw(N))
+    assert np.max(np.abs(cold["w"] - o["w"])) <= 1e-6
+    warm = s.solve_batch(S, T, P, w_warm=np.ascontiguousarray(cold["w"]), want_w=True)
+    s.close()
+    assert np.all(warm["status"] == 0)
+    assert np.max(np.abs(warm["u0"] - cold["u0"])) <= 1e-8
+    assert warm["iters"].mean() < cold["iters"].mean()
+
+
 def test_restoration_off_keeps_the_failed_line_search(dm):
     """restoration=False: an instance whose filter line search fails ends at status -2 (IPOPT with the
     restoration phases unavailable), on the oracle's instances; the others are solved as with them on."""
