@@ -411,9 +411,26 @@ __device__ bool riccati_sweep_aug_soft(L* S, AugSoftLds<L, NS>* RS, int N) {
 // x~ = the six states, no u_prev block).  Two LDS phases: lane NP i + s (i < ND, s < NP) forms
 // u_i[s] = (Pt_{k+1} a_i)[s] = (Gzz a_i)[s] - Gzu(s, :) Quu^-1 (Guz a_i), a_i column i of M_k, parked in U
 // (ND rows of stride NC); then lane e < NT forms the packed entry G_k(i, j) = H_k(i, j) + a_j^T u_i.
-// ok &= Quu of Gn positive definite.  Two barriers.
+// ok &= Quu of Gn positive definite.  Two barriers.  R: the lane roles (gen_roles), the same at every node.
+struct GenRoles {
+    int i1, s1;          // phase 1: stage column i, value index s of lane NP i + s (clamped)
+    int i2, j2;          // phase 2: the packed entry (i, j) of lane e < NT
+};
 template <class L>
-__device__ __forceinline__ void gen_node_step(L* S, int k, const double* Gn, double* U, bool& ok) {
+__device__ __forceinline__ GenRoles gen_roles() {
+    constexpr int NP = L::NP, ND = L::ND;
+    GenRoles R;
+    const int lane = lane_id();
+    const int l = lane < ND * NP ? lane : ND * NP - 1;
+    R.i1 = l / NP; R.s1 = l - R.i1 * NP;
+    const int e = lane < L::NT ? lane : 0;
+    int i = 0;
+    while (tri(i + 1) <= e) ++i;
+    R.i2 = i; R.j2 = e - tri(i);
+    return R;
+}
+template <class L>
+__device__ __forceinline__ void gen_node_step(L* S, int k, const double* Gn, double* U, const GenRoles& R, bool& ok) {
     constexpr int NXA = L::NXA, NP = L::NP, ND = L::ND, NC = L::NC;
     static_assert(ND * NP <= 64 && NP <= NC, "one lane per (stage column, value index)");
     const int lane = lane_id();
@@ -422,8 +439,7 @@ __device__ __forceinline__ void gen_node_step(L* S, int k, const double* Gn, dou
     const double det = fma(q00, q11, -q01 * q01);
     ok = ok && (q00 > 0.0) && (det > 0.0) && isfinite(det);
     {
-        const int l = lane < ND * NP ? lane : ND * NP - 1;
-        const int i = l / NP, s = l - i * NP;
+        const int i = R.i1, s = R.s1;
         double t = 0.0, w0 = 0.0, w1 = 0.0;
 #pragma unroll
         for (int n = 0; n < NP; ++n) {
@@ -438,9 +454,7 @@ __device__ __forceinline__ void gen_node_step(L* S, int k, const double* Gn, dou
     }
     __syncthreads();
     if (lane < L::NT) {
-        int i = 0;
-        while (tri(i + 1) <= lane) ++i;
-        const int j = lane - tri(i);
+        const int i = R.i2, j = R.j2;
         double gv = S->H[k][lane];
 #pragma unroll
         for (int m = 0; m < NP; ++m) gv = fma(Mk[j * NC + m], U[i * NC + m], gv);
@@ -452,17 +466,19 @@ __device__ __forceinline__ void gen_node_step(L* S, int k, const double* Gn, dou
 // backward sweeps with gen_node_step: plain, and with the soft rows of every node (as riccati_sweep_aug[_soft])
 template <class L>
 __device__ bool riccati_sweep_gen(L* S, int N, double* U) {
+    const GenRoles R = gen_roles<L>();
     bool ok = true;
-    for (int k = N - 1; k >= 0; --k) gen_node_step<L>(S, k, S->G[k + 1], U, ok);
+    for (int k = N - 1; k >= 0; --k) gen_node_step<L>(S, k, S->G[k + 1], U, R, ok);
     double i00, i01, i11;
     return quu_inverse<L::NXA>(S->G[0], i00, i01, i11) && ok;
 }
 template <class L, int NS>
 __device__ bool riccati_sweep_gen_soft(L* S, AugSoftLds<L, NS>* RS, int N, double* U) {
+    const GenRoles R = gen_roles<L>();
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
         aug_soften<L, NS>(S, RS, k + 1, true, ok);
-        gen_node_step<L>(S, k, RS->Gs, U, ok);
+        gen_node_step<L>(S, k, RS->Gs, U, R, ok);
     }
     aug_soften<L, NS>(S, RS, 0, false, ok);
     return !wany(!ok);

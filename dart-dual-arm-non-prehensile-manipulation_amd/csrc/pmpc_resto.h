@@ -232,7 +232,9 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             }
         }
         if (wany(out)) return (double)INFINITY;
-        return sc * wsum(node_cost(xx, uu)) - m * wsum(lb);
+        double nc = node_cost(xx, uu);
+        wsum2(nc, lb);            // (the same bits as two wsum: the same reduction tree, in lock step)
+        return sc * nc - m * lb;
     };
 
     // constant structure of M_k: zeroed once, then only the tilt and defect columns are written
@@ -487,8 +489,10 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             for (int j = 0; j < 2; ++j) gtd += (sc * 2 * R * u[j] - mu / (u[j] - lo) + mu / (hi - u[j])) * dU[j];
         }
         const double gTd = wsum(gtd);
+        // theta^s_th and (-gTd)^s_ph are fixed through the line search: formed once here, not at every trial
+        const double pw_th = gTd < 0 ? pow(theta, s_th) : 0.0, pw_gd = gTd < 0 ? pow(-gTd, s_ph) : 0.0;
         double amin = gam_th;
-        if (gTd < 0) amin = fmin(gam_th, fmin(gam_ph * theta / (-gTd), pow(theta, s_th) / pow(-gTd, s_ph)));
+        if (gTd < 0) amin = fmin(gam_th, fmin(gam_ph * theta / (-gTd), pw_th / pw_gd));
         if (theta == 0.0 && gTd < 0) amin = 0.0;
         amin *= gam_al;
         double tn = 0.0;
@@ -513,7 +517,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
         auto accept = [&](double al) -> bool {
             if (!(th_t < th_max) || !isfinite(ph_t)) return false;
             if (F0.hit(th_t, ph_t)) return false;
-            const bool sw = gTd < 0 && al * pow(-gTd, s_ph) > pow(theta, s_th);
+            const bool sw = gTd < 0 && al * pw_gd > pw_th;
             if (theta <= th_min && sw) {
                 if (cmp_le(ph_t, phi + eta_ph * al * gTd, phi)) { ftype = true; return true; }
                 return false;
@@ -1064,8 +1068,9 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                 phir = wsum(pl) - rmu * wsum(lb);
                 gtdr = wsum(gd);
             }
+            const double pw_thr = gtdr < 0 ? pow(thr, s_th) : 0.0, pw_gdr = gtdr < 0 ? pow(-gtdr, s_ph) : 0.0;
             double aminr = gam_th;
-            if (gtdr < 0) aminr = fmin(gam_th, fmin(gam_ph * thr / (-gtdr), pow(thr, s_th) / pow(-gtdr, s_ph)));
+            if (gtdr < 0) aminr = fmin(gam_th, fmin(gam_ph * thr / (-gtdr), pw_thr / pw_gdr));
             aminr *= gam_al;
             double xt[6], ut[2], gt[6], tht = 0.0, pht = 0.0;
             // trial point of the restoration problem at step al: constraint values cgt, theta, barrier
@@ -1107,7 +1112,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             bool ftr = false;
             auto racc = [&](double al) -> bool {
                 if (!(tht < rth_max) || !isfinite(pht) || F1.hit(tht, pht)) return false;
-                const bool sw = gtdr < 0.0 && al * pow(-gtdr, s_ph) > pow(thr, s_th);
+                const bool sw = gtdr < 0.0 && al * pw_gdr > pw_thr;
                 if (thr <= rth_min && sw) {
                     if (cmp_le(pht, phir + eta_ph * al * gtdr, phir)) { ftr = true; return true; }
                     return false;
