@@ -145,6 +145,42 @@ def bench_rmpc(args, torch, dev, stream, dart_mpc):
         cdt = time.perf_counter() - c0
         out["cpu_baseline"] = {"value": solved / cdt, "unit": "solves/s", "cores": nt, "kind": "port",
                                "sample": f"C oracle (oracle/rmpc_ipm.c), {solved} cold-start C3 solves in {cdt:.1f} s"}
+    # the infeasible-start regime: measured velocities 3x the C3 spread put |v| above vmax at the pinned node 0 on
+    # most instances, and IPOPT's restoration phases end those at status 2 (the oracle's), whose point the next
+    # step warm-starts from (np_mpc...:214-217).  Same shape as C3 (batch 18, N = 20), without the RLS update.
+    K2 = max(1, min(K, 100))
+    Dv = [rmpc_batch(1, seed0=200000 + i) for i in range(K2 + 1)]
+    for d in Dv:
+        d["x0"] = d["x0"].copy()
+        d["x0"][:, [1, 3]] *= 3.0
+    Tv = lambda k: torch.tensor(np.stack([d[k] for d in Dv]), dtype=torch.float64, device=dev).contiguous()
+    VX0, VUP, VTH, VRR, VPR = Tv("x0"), Tv("u_prev"), Tv("theta"), Tv("Rref"), Tv("prm")
+
+    def vlaunch(i):
+        s.solve_batch_dev(B, VX0[i].data_ptr(), VUP[i].data_ptr(), VTH[i].data_ptr(), VRR[i].data_ptr(),
+                          VPR[i].data_ptr(), U0[i].data_ptr(), FV[i].data_ptr(), ST[i].data_ptr(), IT[i].data_ptr(),
+                          stream=sp)
+
+    vlaunch(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for i in range(1, K2 + 1):
+            vlaunch(i)
+    torch.cuda.synchronize()
+    dtv = time.perf_counter() - t0
+    stv, u0v = ST[1:K2 + 1].cpu().numpy(), U0[1].cpu().numpy()
+    d = Dv[1]
+    ov = oracle_lib.rmpc_solve_batch(d["x0"], d["u_prev"], d["theta"], d["Rref"], d["prm"], N=N, tol=args.tol,
+                                     nthreads=4, want_w=False)
+    out["infeasible_start"] = {
+        "workload": "C3 shape with measured velocities x3 (|v| > vmax at node 0), restoration phases on, no RLS",
+        "solves_per_s": B * K2 / dtv, "ms_per_step": dtv / K2 * 1e3,
+        "status_infeasible_frac": float(np.mean(stv == 2)), "status_ok_frac": float(np.mean(stv == 0)),
+        "iters_mean": float(IT[1:K2 + 1].float().mean().item()), "batch_max_iters_mean":
+            float(IT[1:K2 + 1].max(dim=1).values.float().mean().item()),
+        "first_batch_status_equal_to_oracle": bool(np.array_equal(stv[0], ov["status"])),
+        "first_batch_max_abs_u0_err_vs_oracle": float(np.max(np.abs(u0v - ov["u0"])))}
     s.close()
     return out
 
