@@ -288,13 +288,25 @@ __device__ __forceinline__ void aug_soft_init(AugSoftLds<L, NS>* RS) {
 // diagonal soft lanes store Y's column qv (D^-1_qv t), the lanes of the homogeneous row with qv not soft store
 // -t.  With `surrogate` every lane stores Pt'(pv, qv) into Gs.  ok &= (Quu of G_j and S positive definite).
 // Ends with a barrier.
-template <class L, int NS>
-__device__ __forceinline__ void aug_soften(L* S, AugSoftLds<L, NS>* RS, int j, bool surrogate, bool& ok) {
-    constexpr int NXA = L::NXA, NP = L::NP, NV = tri(NP);
+// The lane's packed value entry (pv, qv) of aug_soften, the same at every node: formed once per sweep.
+struct SoftenRoles {
+    int pv, qv;
+};
+template <class L>
+__device__ __forceinline__ SoftenRoles soften_roles() {
+    constexpr int NV = tri(L::NP);
     const int e0 = lane_id() < NV ? lane_id() : NV - 1;
-    int pv = 0;
-    while (tri(pv + 1) <= e0) ++pv;
-    const int qv = e0 - tri(pv);
+    SoftenRoles R;
+    R.pv = 0;
+    while (tri(R.pv + 1) <= e0) ++R.pv;
+    R.qv = e0 - tri(R.pv);
+    return R;
+}
+template <class L, int NS>
+__device__ __forceinline__ void aug_soften(L* S, AugSoftLds<L, NS>* RS, int j, bool surrogate, const SoftenRoles& SR,
+                                           bool& ok) {
+    constexpr int NXA = L::NXA, NP = L::NP, NV = tri(NP);
+    const int pv = SR.pv, qv = SR.qv;
     const bool act = lane_id() < NV;
     const bool ps = pv < NS, qs = qv < NS;          // (qv <= pv: qs whenever ps)
     const double* Gn = S->G[j];
@@ -397,12 +409,13 @@ __device__ __forceinline__ void aug_soften(L* S, AugSoftLds<L, NS>* RS, int j, b
 template <class L, int NS>
 __device__ bool riccati_sweep_aug_soft(L* S, AugSoftLds<L, NS>* RS, int N) {
     const AugRoles R = aug_roles<L>();
+    const SoftenRoles SR = soften_roles<L>();
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
-        aug_soften<L, NS>(S, RS, k + 1, true, ok);
+        aug_soften<L, NS>(S, RS, k + 1, true, SR, ok);
         aug_node_step<L>(S, k, RS->Gs, R, ok);
     }
-    aug_soften<L, NS>(S, RS, 0, false, ok);
+    aug_soften<L, NS>(S, RS, 0, false, SR, ok);
     return !wany(!ok);
 }
 
@@ -475,12 +488,13 @@ __device__ bool riccati_sweep_gen(L* S, int N, double* U) {
 template <class L, int NS>
 __device__ bool riccati_sweep_gen_soft(L* S, AugSoftLds<L, NS>* RS, int N, double* U) {
     const GenRoles R = gen_roles<L>();
+    const SoftenRoles SR = soften_roles<L>();
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
-        aug_soften<L, NS>(S, RS, k + 1, true, ok);
+        aug_soften<L, NS>(S, RS, k + 1, true, SR, ok);
         gen_node_step<L>(S, k, RS->Gs, U, R, ok);
     }
-    aug_soften<L, NS>(S, RS, 0, false, ok);
+    aug_soften<L, NS>(S, RS, 0, false, SR, ok);
     return !wany(!ok);
 }
 
