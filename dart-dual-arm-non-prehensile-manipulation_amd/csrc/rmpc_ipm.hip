@@ -62,7 +62,7 @@ using RmSoft = AugSoftLds<RmLds, 4>;     // restoration: the four physical rows 
 constexpr int kRmNeedResto = -100;      // hand-off of an instance to rmpc_ipm_kernel<true>
 
 #ifdef DART_STAMPS
-__device__ unsigned long long g_stamp_rm[16];
+__device__ unsigned long long g_stamp_rm[32];
 #endif
 
 struct RmModel {
@@ -1422,6 +1422,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
         const double zero6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 
         // ---- least-square equality multipliers of the restoration problem (unit weights on x, u, s, p, n) ----
+        STAMP(7);               // (diagnostic stamps: 16.. the restoration phase proper)
         {
             if (nod) {
 #pragma unroll
@@ -1466,7 +1467,9 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
         bool rfirst = true, rok = false;
         double rfth = 0.0, rfph = 0.0, rdelta_last = 0.0, thr = 0.0, rth_max = 0.0, rth_min = 0.0;
         double cg[6], cr[RM_NQ];
+        STAMP(16);
         for (;; ++rit) {
+            STAMP_ADD(27, 1);
             rderiv();
             {
                 double g[6], cz[RM_NQ];
@@ -1598,6 +1601,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                 q[Q_RQP + i] = uon ? rho - rmu / q[Q_QP + i] - yq[i] : 0.0;
                 q[Q_RQN + i] = uon ? rho - rmu / q[Q_QN + i] + yq[i] : 0.0;
             }
+            STAMP(17);
             // ---- the step: plain (with inertia correction) or a second-order correction pass, one solve site;
             //      each solve refined iteratively (IPOPT's PDFullSpaceSolver) ----
             double delta = 0.0, amr = 1.0, azr = 1.0, phir = 0.0, gtdr = 0.0, aminr = 0.0, alr = 1.0;
@@ -1858,6 +1862,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                         soft_rhs(cg, lam, pn + P_RP, pn + P_RN);
                         __syncthreads();
                         okr = riccati_sweep_aug_soft<RmLds, 4>(S, SR, N);
+                        STAMP_ADD(24, 1);
                         if (okr || ++attempt >= 60) break;
                         delta = (attempt == 1) ? (rdelta_last == 0.0 ? 1e-4 : fmax(1e-20, rdelta_last * (1.0 / 3.0)))
                                                : delta * (rdelta_last == 0.0 ? 100.0 : 8.0);
@@ -1869,11 +1874,14 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                     soft_rhs(csg, lam, pn + P_RP, pn + P_RN);
                     __syncthreads();
                     (void)riccati_sweep_aug_soft<RmLds, 4>(S, SR, N);
+                    STAMP_ADD(24, 1);
                 }
+                STAMP(18);
                 rstep();
                 rdirs(soc < 0 ? cr : csr, q + Q_OFF, q + Q_PSI, q + Q_RQP, q + Q_RQN, yq, lam, pn + P_RP, pn + P_RN);
-                for (int rr = 0; rr < 3 && refine(soc < 0 ? cg : csg, soc < 0 ? cr : csr); ++rr) {}
+                for (int rr = 0; rr < 3 && refine(soc < 0 ? cg : csg, soc < 0 ? cr : csr); ++rr) { STAMP_ADD(25, 1); }
                 pn_steps();
+                STAMP(19);
                 double al_try;
                 if (soc < 0) {
                     // barrier objective of the restoration problem and its directional derivative
@@ -1920,6 +1928,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                 bool resolve = false;
                 for (;;) {
                     trial_r(al_try);
+                    STAMP_ADD(26, 1);
                     if (soc < 0) {
                         if (racc(alr, ftr)) { accr = true; break; }
                         if (ls == 0 && a.max_soc > 0 && !(tht < thr)) {
@@ -1958,6 +1967,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                 }
                 if (!resolve) break;
             }
+            STAMP(20);
 #ifdef DART_RESTO_TRACE
             if (blockIdx.x == 0 && lane == 0)
                 printf("  resto it %3d mu %.2e err %.2e dinf %.2e pinf %.2e c0 %.2e delta %.1e amax %.3e alpha %.3e th %.3e "
@@ -2019,6 +2029,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
             }
             thr = tht;
             __syncthreads();
+            STAMP(22);
         }
         if (!rok) { status = rstat; it = rit; break; }
         // back to the original problem: the bound multipliers take the step (mu - z s_trial) / s that pretends
@@ -2087,6 +2098,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
         in_soft = 0; soft_count = 0;
         it_next = rit;
         __syncthreads();
+        STAMP(21);
     }
     }
 
@@ -2108,7 +2120,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
         }
         if (nod && uon) { wo[4 * (N + 1) + 2 * k] = u[0]; wo[4 * (N + 1) + 2 * k + 1] = u[1]; }
     }
-    STAMP_FLUSH_TO(g_stamp_rm, b);
+    STAMP_FLUSH32_TO(g_stamp_rm, b);
     return false;
 }
 
@@ -2206,7 +2218,7 @@ extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStre
 
 #ifdef DART_STAMPS
 extern "C" hipError_t dartmpc_read_stamps_rmpc(unsigned long long* host_out) {
-    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp_rm), sizeof(unsigned long long) * 16, 0,
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(dartmpc::g_stamp_rm), sizeof(unsigned long long) * 32, 0,
                                hipMemcpyDeviceToHost);
 }
 #endif
