@@ -224,8 +224,14 @@ __device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const Riccati
         for (int m = 0; m < NP; ++m) ga = fma(vi[m], t[m], ga);
         S->G[base + k][R.e] = ga;
         __syncthreads();
+        // a failed inertia test (Quu or a soft block's pivot of either half) ends the sweep: the caller discards it
+        // and factors again with a new perturbation.  Every lane of a half tests the same LDS values, and the two
+        // waves of a two-wave build run the sweep alike, so the wave's own ballot decides uniformly; the return
+        // value is the full sweep's (ok only accumulates).  (Restoration tails: ~2 soft sweeps per iteration on
+        // the C5 stress instances, profiles/r05/stamps_lmpc_resto.txt.)
+        if (__ballot(!ok) != 0ull) break;
     }
-    soften(base, false);
+    if (__ballot(!ok) == 0ull) soften(base, false);
     return !wany(!ok);
 }
 
