@@ -181,6 +181,57 @@ def bench_rmpc(args, torch, dev, stream, dart_mpc):
             float(IT[1:K2 + 1].max(dim=1).values.float().mean().item()),
         "first_batch_status_equal_to_oracle": bool(np.array_equal(stv[0], ov["status"])),
         "first_batch_max_abs_u0_err_vs_oracle": float(np.max(np.abs(u0v - ov["u0"])))}
+    if not args.no_cpu_baseline:
+        # the same infeasible-start batches on the C oracle (restoration phases included), bounded sample
+        nt = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
+        solved, c0, i = 0, time.perf_counter(), 1
+        while time.perf_counter() - c0 < min(6.0, args.cpu_seconds) and i <= K2:
+            dd = Dv[i]
+            oracle_lib.rmpc_solve_batch(dd["x0"], dd["u_prev"], dd["theta"], dd["Rref"], dd["prm"], N=N, tol=args.tol,
+                                        nthreads=nt, want_w=False)
+            solved += B
+            i += 1
+        cdt = time.perf_counter() - c0
+        out["infeasible_start"]["cpu_baseline"] = {
+            "value": solved / cdt, "unit": "solves/s", "cores": nt, "kind": "port",
+            "sample": f"C oracle (oracle/rmpc_ipm.c, IPOPT's restoration phases), {solved} solves of the bench's own "
+                      f"infeasible-start batches in {cdt:.1f} s"}
+    # SURVEY 8(d), host to host: the reference's RMPC step is synchronous (rob_ctrl.py:351-352) -- host arrays in,
+    # the fused RLS update and the solve, theta / P / u0 back in host memory, per call
+    if args.host_calls > 0:
+        Kh = max(20, min(args.host_calls, K))
+        hs = dart_mpc.RmpcSolver(N=N, tol=args.tol, B_max=B, device=dev.index)
+
+        def hcall(i):
+            d = D[i % len(D)]
+            th, Pm = d["rls_theta"].copy(), d["rls_P"].copy()
+            hs.solve_batch(d["x0"], d["u_prev"], th, d["Rref"], d["prm"], rls_P=Pm, rls_phi=d["phi_prev"], rls_y=d["y"],
+                           rls_lambda=0.995)
+        h = _host_line(hcall, Kh)
+        hs.close()
+        out["host_inclusive_8d"] = {"value": B / (h["median_ms_per_call"] * 1e-3), "unit": "solves/s", **h,
+                                    "note": "dart_rmpc_solve_batch from Python: host inputs (x0, u_prev, theta, Rref, prm, "
+                                            "RLS P / phi / y) in, RLS update + solve, theta, P, u0, f back in host "
+                                            "memory; median call"}
+    # saturated lines: C3-type batches of 18 x 64 and 18 x 1024 in one launch each (the object-config sweep x
+    # Monte-Carlo seeds of north_star, np_mpc...:212-222)
+    sat = {}
+    for ns in (64, 1024):
+        Dd = rmpc_batch(ns, seed0=600000)
+        Bs = 18 * ns
+        t_ = lambda k: torch.tensor(Dd[k], dtype=torch.float64, device=dev).contiguous()
+        a_ = [t_(k) for k in ("x0", "u_prev", "theta", "Rref", "prm")]
+        su = torch.empty((Bs, 2), dtype=torch.float64, device=dev); sf = torch.empty(Bs, dtype=torch.float64, device=dev)
+        ss = torch.empty(Bs, dtype=torch.int32, device=dev); si = torch.empty(Bs, dtype=torch.int32, device=dev)
+        big = dart_mpc.RmpcSolver(N=N, tol=args.tol, B_max=Bs, device=dev.index)
+        line = _saturated(torch, stream, lambda: big.solve_batch_dev(
+            Bs, *[x.data_ptr() for x in a_], su.data_ptr(), sf.data_ptr(), ss.data_ptr(), si.data_ptr(), stream=sp),
+            Bs, ss, si, RL.F_ITER["rmpc_n20"], int(dart_mpc._lib.lib().dartmpc_rmpc_blocks_per_cu()))
+        big.close()
+        sat[f"b{Bs}"] = line
+    sat["note"] = ("C3-type inputs (no RLS update), cold start, tol 1e-8, one launch per batch; rmpc_ipm_kernel<false> "
+                   "takes 70.6 KB of LDS and 256 VGPRs + 240 AGPRs per instance")
+    out["saturation"] = sat
     s.close()
     return out
 
@@ -289,6 +340,48 @@ def _event_ms(torch, stream, launch, K):
             ev[j][1].record(stream)
     torch.cuda.synchronize()
     return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+
+def _host_line(call, n_calls, warm=3):
+    """SURVEY 8(d) host-to-host rate of one batch per call: host arrays in, results back in host memory, blocking;
+    median of n_calls timed calls (fresh inputs each) after `warm` untimed ones.  call(i) runs call i."""
+    for i in range(warm):
+        call(i)
+    per = np.empty(n_calls)
+    t0 = time.perf_counter()
+    for j in range(n_calls):
+        c0 = time.perf_counter()
+        call(warm + j)
+        per[j] = time.perf_counter() - c0
+    tot = time.perf_counter() - t0
+    return {"calls": n_calls, "ms_per_call": tot / n_calls * 1e3, "median_ms_per_call": float(np.median(per)) * 1e3}
+
+
+def _saturated(torch, stream, launch, B, ST, IT, f_iter, blocks_per_cu, reps=3):
+    """One launch over a large batch (inputs resident in HBM), timed by HIP events on the launch stream: the
+    median of `reps` launches after one untimed.  Residency: instances of the kernel the runtime keeps per CU."""
+    launch()
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        launch()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    m = float(np.median(ms))
+    st, it = ST.cpu().numpy(), IT.cpu().numpy()
+    ncu = torch.cuda.get_device_properties(stream.device).multi_processor_count
+    return {"batch": B, "ms_per_launch": m, "solves_per_s": B / (m * 1e-3), "iters_mean": float(it.mean()),
+            "status_ok_frac": float(np.mean(np.isin(st, (0, 1)))),
+            "residency": {"instances_per_cu": blocks_per_cu, "cus": ncu,
+                          "instances_in_flight": blocks_per_cu * ncu if blocks_per_cu > 0 else None,
+                          "source": "hipOccupancyMaxActiveBlocksPerMultiprocessor of the solve kernel (one wave per "
+                                    "instance; its registers and LDS)"},
+            "roofline": RL.roofline(float(it.sum()), f_iter, m * 1e-3,
+                                    note=f"sum(iters) x {f_iter:.1e} FLOP / launch time; the chip holds "
+                                         f"{blocks_per_cu} instance(s) per CU")}
 
 
 def _max_over_ranks(vals, dev, host_coll):
@@ -575,6 +668,38 @@ def bench_lmpc(args, torch, dev, stream, dart_mpc):
         out["cpu_baseline"] = {"value": solved / cdt, "unit": "solves/s", "cores": nt, "kind": "port",
                                "sample": f"C oracle (oracle/lmpc_ipm.c, exact jet Hessian), {solved} cold-start C5 "
                                          f"solves in {cdt:.1f} s"}
+    # SURVEY 8(d), host to host: one C5 batch per call from host arrays (the solver worker's shared-memory inputs,
+    # rlmpc2.py:508-515), u0 / f / status back in host memory
+    if args.host_calls > 0:
+        Kh = max(20, min(args.host_calls, K))
+        hs = dart_mpc.LmpcSolver(N=N, B_max=B, device=dev.index)
+
+        def hcall(i):
+            d = D[i % len(D)]
+            hs.solve_batch(d["state"], d["u_prev"], d["pvec"], d["target"])
+        h = _host_line(hcall, Kh)
+        hs.close()
+        out["host_inclusive_8d"] = {"value": B / (h["median_ms_per_call"] * 1e-3), "unit": "solves/s", **h,
+                                    "note": "dart_lmpc_solve_batch from Python: host inputs in, u0, f, status back in "
+                                            "host memory; median call (restoration tails included)"}
+    sat = {}
+    for ns in (64, 1024):
+        Dd = lmpc_batch(ns, seed0=600000)
+        Bs = 18 * ns
+        t_ = lambda k: torch.tensor(Dd[k], dtype=torch.float64, device=dev).contiguous()
+        a_ = [t_(k) for k in ("state", "u_prev", "pvec", "target")]
+        pr_ = torch.tensor(np.tile(LMPC_PRM_DEFAULT, (Bs, 1)), dtype=torch.float64, device=dev)
+        su = torch.empty((Bs, 2), dtype=torch.float64, device=dev); sf = torch.empty(Bs, dtype=torch.float64, device=dev)
+        ss = torch.empty(Bs, dtype=torch.int32, device=dev); si = torch.empty(Bs, dtype=torch.int32, device=dev)
+        big = dart_mpc.LmpcSolver(N=N, B_max=Bs, device=dev.index)
+        line = _saturated(torch, stream, lambda: big.solve_batch_dev(
+            Bs, *[x.data_ptr() for x in a_], pr_.data_ptr(), su.data_ptr(), sf.data_ptr(), ss.data_ptr(), si.data_ptr(),
+            stream=sp), Bs, ss, si, RL.F_ITER["lmpc_n30"], int(dart_mpc._lib.lib().dartmpc_lmpc_blocks_per_cu()))
+        big.close()
+        sat[f"b{Bs}"] = line
+    sat["note"] = ("C5 stress inputs, reference options, restoration phases on (queued kernel for batches above 32), "
+                   "one launch per batch; lmpc_ipm_kernel<false> takes LmShared of LDS per instance")
+    out["saturation"] = sat
     s.close()
     return out
 

@@ -501,8 +501,13 @@ int served_request(dart_mpc_handle* h, int B, bool ww, bool wo) {
     // relaunches it before posting.  Before that point no wave can have left (each wave's last request is no
     // older than the host's last post).
     const double since = std::chrono::duration<double>(std::chrono::steady_clock::now() - v.t_post).count();
-    // (the 2 ms margin is capped at half the idle timeout, so that short timeouts still serve from the grid)
-    if (v.running && since > std::fmax(0.9 * v.idle_s - 0.002, 0.5 * v.idle_s)) {
+    // The margin between this check and a wave's own timeout is 10 % of the timeout + 2 ms, capped at half the
+    // timeout (so that short timeouts still serve from the grid), but never below 2 ms: a host stall between the
+    // check and the post longer than the margin could let part of the grid leave, and the request would then
+    // wait out a further idle period.  Timeouts of 4 ms and less therefore pre-drain (relaunch) whenever more
+    // than idle - 2 ms has passed: a latency cost, never a stall.
+    const double margin = std::fmax(0.002, std::fmin(0.1 * v.idle_s + 0.002, 0.5 * v.idle_s));
+    if (v.running && since > v.idle_s - margin) {
         __atomic_store_n((unsigned long long*)v.mbox, (unsigned long long)v.mbox[0] | (1ull << 56), __ATOMIC_RELEASE);
         v.running = false;
     }
@@ -575,6 +580,19 @@ int dart_rmpc_nw(int N) { return 4 * (N + 1) + 2 * N; }
 int dart_lmpc_nw(int N) { return 8 * (N + 1) + 2 * N; }
 
 int dart_mpc_abi_version(void) { return DART_MPC_ABI_VERSION; }
+#ifndef DART_BUILD_ID
+#define DART_BUILD_ID "unknown"
+#endif
+const char* dart_mpc_build_id(void) { return DART_BUILD_ID; }
+const char* dart_mpc_build_flavor(void) {
+#if defined(DART_STAMPS)
+    return "stamps";
+#elif defined(DART_RESTO_TRACE)
+    return "trace";
+#else
+    return "";
+#endif
+}
 
 int dart_mpc_create(const dart_mpc_config* cfg, int device, dart_mpc_handle** out) {
     if (!out || !check_cfg(cfg)) return DART_MPC_EINVAL;

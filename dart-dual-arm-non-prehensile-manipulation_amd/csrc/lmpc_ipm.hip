@@ -129,7 +129,7 @@ struct LmResto {
 // results are the same bits, with one barrier per node instead of three.)  G[slot N] must hold the
 // terminal surrogate, RL->Dinv every node's 1 / D.  Returns false (wave-uniform) if some S or Quu is
 // not positive definite.
-__device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const RiccatiSRoles& R) {
+__device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const RiccatiSRoles& R, bool early) {
     constexpr int NXA = LmLds::NXA, NP = LmLds::NP;
     static_assert(NXA == 5 && NP == 6, "packed row 6 = [x~ (5), u, 1] names T's six columns");
     const int h = lane_id() >> 5, base = h * LM_NMAXS;
@@ -224,14 +224,16 @@ __device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const Riccati
         for (int m = 0; m < NP; ++m) ga = fma(vi[m], t[m], ga);
         S->G[base + k][R.e] = ga;
         __syncthreads();
-        // a failed inertia test (Quu or a soft block's pivot of either half) ends the sweep: the caller discards it
-        // and factors again with a new perturbation.  Every lane of a half tests the same LDS values, and the two
-        // waves of a two-wave build run the sweep alike, so the wave's own ballot decides uniformly; the return
-        // value is the full sweep's (ok only accumulates).  (Restoration tails: ~2 soft sweeps per iteration on
-        // the C5 stress instances, profiles/r05/stamps_lmpc_resto.txt.)
-        if (__ballot(!ok) != 0ull) break;
+        // early: a failed inertia test (Quu or a soft block's pivot of either half) ends the sweep -- only for the
+        // perturbation loop, whose caller discards a failed sweep and factors again with a new perturbation.  Every
+        // lane of a half tests the same LDS values, and the two waves of a two-wave build run the sweep alike, so
+        // the wave's own ballot decides uniformly; the return value is the full sweep's (ok only accumulates).
+        // (Restoration tails: ~2 soft sweeps per iteration on the C5 stress instances,
+        // profiles/r05/stamps_lmpc_resto.txt.)  The callers that use the sweep whatever it returns (least-square
+        // multipliers, refinement, second-order correction) run it whole, so no node keeps a stale factorisation.
+        if (early && __ballot(!ok) != 0ull) break;
     }
-    if (__ballot(!ok) == 0ull) soften(base, false);
+    if (!early || __ballot(!ok) == 0ull) soften(base, false);
     return !wany(!ok);
 }
 
@@ -1278,6 +1280,8 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
         }
         if (!ok) {
             if constexpr (!RESTO) {
+                // (ok is false here only after 60 failed perturbations: a second-order-correction pass keeps its
+                // sweep whatever the inertia test says, `if (soc >= 0) ok = true` above)
                 if (a.resto) { handoff(true); break; }
             }
             status = -3;
@@ -1511,7 +1515,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                 const double cz[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
                 soft_rows(0.0, true, cz);
                 __syncthreads();
-                (void)riccati_s_sweep_soft(S, RL, N, RR);
+                (void)riccati_s_sweep_soft(S, RL, N, RR, false);
                 resto_step();
                 double ym = 0.0;
                 bool fin = true;
@@ -1630,7 +1634,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                 for (;;) {
                     soft_rows(delta, false, cres);
                     __syncthreads();
-                    okr = riccati_s_sweep_soft(S, RL, N, RR);
+                    okr = riccati_s_sweep_soft(S, RL, N, RR, true);
                     if (okr || ++attempt >= 60) break;
                     delta = (attempt == 1) ? (rdelta_last == 0.0 ? 1e-4 : fmax(1e-20, rdelta_last * (1.0 / 3.0)))
                                            : delta * (rdelta_last == 0.0 ? 100.0 : 8.0);
@@ -1761,7 +1765,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                         if (k == 0) S->dx0[hf][r] = -rg[r];
                     }
                     __syncthreads();
-                    (void)riccati_s_sweep_soft(S, RL, N, RR);
+                    (void)riccati_s_sweep_soft(S, RL, N, RR, false);
                     double dx0_[5], lp0_[5];
                     const double du0_ = dUr;
 #pragma unroll
@@ -1878,7 +1882,7 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                             for (int i = 0; i < 5; ++i) csoc[i] = fma(asoc, csoc[i], ct[i]);
                             soft_rows(delta, false, csoc);
                             __syncthreads();
-                            (void)riccati_s_sweep_soft(S, RL, N, RR);
+                            (void)riccati_s_sweep_soft(S, RL, N, RR, false);
                             resto_step();
 #if DART_RESTO_REFINE
                             for (int rr = 0; rr < DART_RESTO_REFINE && refine(csoc); ++rr) {}
@@ -2125,6 +2129,18 @@ extern "C" hipError_t dartmpc_launch_lmpc_wg2(const void* args, hipStream_t stre
 #else
 
 extern "C" size_t dartmpc_lmpc_lds_bytes(void) { return dartmpc::kLmLdsBytes; }
+
+// internal (bench.py's saturated lines): instances of lmpc_ipm_kernel<false> resident per CU in a batch of more than
+// 32 (its LDS: LmShared alone), by the runtime's occupancy calculation; -1 on error (call after a launch, which
+// sets the dynamic-LDS opt-in)
+extern "C" int dartmpc_lmpc_blocks_per_cu(void) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dartmpc::lmpc_ipm_kernel<false>, dartmpc::kWave,
+                                                     sizeof(dartmpc::LmShared)) != hipSuccess)
+        return -1;
+    return n;
+}
+extern "C" size_t dartmpc_lmpc_shared_bytes(void) { return sizeof(dartmpc::LmShared); }
 
 extern "C" hipError_t dartmpc_launch_lmpc(const dartmpc::LmpcArgs* args, hipStream_t stream) {
     if (args->B <= 0) return hipSuccess;

@@ -1460,8 +1460,12 @@ extern "C" hipError_t dartmpc_launch_pmpc(const dartmpc::PmpcArgs* args, hipStre
         return !(e && e[0] == '1');
     }();
     // batches of at most 32 (one XCD, one instance per CU): IPOPT's restoration phases run in the wave that
-    // handed the instance over (resto mode 3, pmpc_resto_tail), so no restoration launch follows the solve
-    if (a.resto == 1 && a.pack == 8 && !a.reduced && a.N <= 31 && dartmpc::resto_fuse_enabled()) a.resto = 3;
+    // handed the instance over (resto mode 3, pmpc_resto_tail), so no restoration launch follows the solve.
+    // Only the branches below that launch a FUSE instantiation take mode 3 (not the two-waves-per-SIMD build, not
+    // the sequential builds past DART_PMPC_QSCAN_MAX_B): everywhere else the queued pmpc_resto_kernel (mode 1) stays
+    if (a.resto == 1 && a.pack == 8 && !a.reduced && a.N <= 31 && !occ2 && a.B <= qscan_max_b &&
+        dartmpc::resto_fuse_enabled())
+        a.resto = 3;
     const bool fuse = a.resto == 3;
     if (a.N <= 23 && occ2) {        // (N <= 15 too: the short-scan build at two waves beats the one-row build at one)
         hipLaunchKernelGGL((dartmpc::pmpc_ipm_kernel<1, true, false, true, false, true>), grid, dim3(dartmpc::kWave), 0, stream, a);

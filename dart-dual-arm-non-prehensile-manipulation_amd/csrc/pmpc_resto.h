@@ -5,8 +5,13 @@
 // handed over to pmpc_resto_solve below, which solves it again from its start on the full 6-state NLP of
 // mpc_3d.py:28-85, with IPOPT's soft restoration phase (BacktrackingLineSearch::TrySoftRestoStep) and
 // restoration phase (MinC_1NrmRestorationPhase) available, to the end of the solve: oracle/pmpc_ipm.c
-// `soft_resto_step`, `restoration`, whose commentary applies.  No state crosses the hand-off but the
-// instance index.  Two callers:
+// `soft_resto_step`, `restoration`, whose commentary applies.  By default no state crosses the hand-off but the
+// instance index (the restart repeats the oracle's arithmetic order from the first iteration).  Opt-in
+// (DART_PMPC_RESUME=1): the register kernel also hands over the iterate of the iteration whose line search
+// failed -- per node x, u, lambda, z_L, z_U, then its filter, mu, the last inertia shift, the iteration and filter
+// counters (pmpc_model.h kPmHo layout, PmpcArgs::resto_buf) -- and the solve repeats that iteration at the same
+// shift instead of starting over (faster, but not the oracle's path on every restored instance).
+// Two callers:
 //  * small batches (B <= 32, the latency regime): the register kernel's own wave calls it right after the
 //    failed line search (pmpc_ipm.hip `pmpc_resto_tail`, a non-inlined call, so the register kernel's
 //    allocation is untouched): no second dispatch on any launch;

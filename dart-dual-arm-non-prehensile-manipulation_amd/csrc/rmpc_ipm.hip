@@ -2196,6 +2196,15 @@ extern "C" hipError_t dartmpc_launch_rls(int B, double* theta, double* P, const 
     return hipGetLastError();
 }
 
+// internal (bench.py's saturated lines): instances of rmpc_ipm_kernel<false> resident per CU, by the runtime's own
+// occupancy calculation (registers, LDS, waves); -1 on error
+extern "C" int dartmpc_rmpc_blocks_per_cu(void) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dartmpc::rmpc_ipm_kernel<false>, dartmpc::kWave, 0) != hipSuccess)
+        return -1;
+    return n;
+}
+
 extern "C" hipError_t dartmpc_launch_rmpc(const dartmpc::RmpcArgs* args, hipStream_t stream) {
     if (args->B <= 0) return hipSuccess;
     if ((args->N >= dartmpc::RM_NMAXS || dartmpc::force_wg2()) && args->N < 2 * dartmpc::RM_NMAXS)

@@ -15,8 +15,12 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
-# DART_MPC_LIB: file name of an alternative in-tree build (A/B timing of two builds, tools/ab_lib.sh)
-LIB_PATH = os.path.join(PKG_DIR, os.path.basename(os.environ.get("DART_MPC_LIB", "libdartmpc.so")))
+# DART_MPC_LIB: file name of an alternative in-tree build.  The product path loads only a library built from the
+# sources beside it (build_id below): the product library itself, or a diagnostic build of the same sources
+# (phase stamps, restoration trace).  A/B timing of two different builds (tools/ab_lib.sh) must say so with
+# DART_MPC_AB=1, which only the A/B tools set.
+LIB_NAME = os.path.basename(os.environ.get("DART_MPC_LIB", "libdartmpc.so"))
+LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
 
 SOLVED, ACCEPTABLE, INFEASIBLE, MAXITER, LS_FAIL, INERTIA_FAIL, MAXTIME = 0, 1, 2, -1, -2, -3, -4
 STATUS_NAMES = {SOLVED: "Solve_Succeeded", ACCEPTABLE: "Solved_To_Acceptable_Level", INFEASIBLE: "Infeasible_Problem_Detected",
@@ -33,7 +37,8 @@ EXPORTS = ("dart_mpc_config_default", "dart_mpc_create", "dart_mpc_solve_batch",
            "dart_lmpc_policy_solve_batch", "dart_lmpc_policy_solve_batch_dev",
            "dart_arm_config_default", "dart_arm_snapshot_len", "dart_arm_param_len", "dart_arm_solve_batch",
            "dart_arm_solve_batch_dev", "dart_set_device", "dart_mpc_serve_start", "dart_mpc_serve_stop",
-           "dart_mpc_serve_running", "dart_mpc_bind", "dart_mpc_solve_bound")
+           "dart_mpc_serve_running", "dart_mpc_bind", "dart_mpc_solve_bound", "dart_mpc_build_id",
+           "dart_mpc_build_flavor")
 VARIANT_PMPC, VARIANT_RMPC, VARIANT_LMPC = 0, 1, 2
 ABI_VERSION = 8
 
@@ -65,8 +70,41 @@ def build(verbose: bool = False) -> str:
     return LIB_PATH
 
 
+def source_build_id() -> str:
+    """SHA-1 (first 16 hex digits) of the library's sources as the Makefile computes it: the SRC then HDR files."""
+    import hashlib
+    import re
+    mk = open(os.path.join(CSRC_DIR, "Makefile")).read()
+    files = []
+    for var in ("SRC", "HDR"):
+        m = re.search(r"^%s := (.*)$" % var, mk, re.M)
+        files += m.group(1).split()
+    h = hashlib.sha1()
+    for f in files:
+        with open(os.path.join(CSRC_DIR, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _check_build(L):
+    """Refuse a library that was not built from the sources beside it (unless an A/B run says otherwise)."""
+    if not hasattr(L, "dart_mpc_build_id"):
+        if os.environ.get("DART_MPC_AB") == "1":
+            return
+        raise DartMPCError(f"{LIB_PATH} predates the build identity: rebuild it (make -C {CSRC_DIR})")
+    L.dart_mpc_build_id.restype = ctypes.c_char_p
+    L.dart_mpc_build_flavor.restype = ctypes.c_char_p
+    got, want = L.dart_mpc_build_id().decode(), source_build_id()
+    flavor = L.dart_mpc_build_flavor().decode()
+    if os.path.basename(LIB_PATH) == "libdartmpc.so" and flavor:
+        raise DartMPCError(f"{LIB_PATH} is a diagnostic ({flavor}) build, not the product library")
+    if got != want and os.environ.get("DART_MPC_AB") != "1":
+        raise DartMPCError(f"{LIB_PATH} was built from other sources (build id {got}, sources {want}): "
+                           f"stale build, run __graft_entry__.build() or `make -C {CSRC_DIR}`")
+
+
 def lib():
-    """Load the library (no compute).  Raises if it is missing."""
+    """Load the library (no compute).  Raises if it is missing or stale."""
     global _lib
     if _lib is not None:
         return _lib
@@ -161,6 +199,7 @@ def lib():
         L.dart_set_device.restype = ctypes.c_int
     if L.dart_mpc_abi_version() != ABI_VERSION:
         raise DartMPCError("libdartmpc.so ABI version mismatch")
+    _check_build(L)
     _lib = L
     return L
 

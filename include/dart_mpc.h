@@ -116,8 +116,10 @@ typedef struct dart_mpc_config {
                            restoration phases after a failed filter line search (default;
                            MinC_1NrmRestorationPhase, the fallback of every nlpsol call, mpc_3d.py:82,
                            np_mpc...:158-162, rlmpc2.py:480-489); 0 = stop with status -2 there.  PMPC and
-                           LMPC batches of at most 32 run them in the solving wave; larger batches and RMPC
-                           hand the failed instances to a second kernel queued on the same stream.  PMPC: on
+                           LMPC batches of at most 32 with N <= 31 run them in the solving wave (unless the
+                           environment sets DART_RESTO_FUSE=0); larger batches, N > 31 (the two-wave builds)
+                           and RMPC hand the failed instances to a second kernel queued on the same stream.
+                           PMPC: on
                            IPOPT's path; for N > 31 the soft phase only (the restoration phase proper and the
                            reduced path keep -2).  RMPC / LMPC: at every N */
     double constr_mult_init_max;  /* IPOPT constr_mult_init_max (default 1000): the starting equality
@@ -381,6 +383,13 @@ int dart_mpc_nw(int N);
 
 /* ABI version (DART_MPC_ABI_VERSION) of the loaded library. */
 int dart_mpc_abi_version(void);
+
+/* Build identity (round 6): the first 16 hex digits of the SHA-1 of the sources the library was compiled from
+ * (the Makefile's SRC then HDR lists, concatenated), and the diagnostic flavour of the build: "" for the product
+ * library, "stamps" / "trace" for the phase-stamp and restoration-trace builds.  The Python binding refuses a
+ * library whose identity is not that of the sources beside it (a stale build). */
+const char *dart_mpc_build_id(void);
+const char *dart_mpc_build_flavor(void);
 
 #ifdef __cplusplus
 }

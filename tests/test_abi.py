@@ -117,3 +117,19 @@ def test_arm_qp_abi_lengths_and_validation():
     bad = ArmConfig(tol=1e-6, acceptable_tol=1e-8, max_iter=60)              # acceptable < tol
     assert L.dart_arm_solve_batch(*args(bad, 0, 7, 0)) == -1
     assert L.dart_arm_solve_batch_dev(*(args(c, 0, 7, 262) + (z,))) == 0
+
+
+def test_library_is_built_from_the_sources_beside_it(monkeypatch):
+    """The product path refuses a stale library (hygiene): the build identity compiled into
+    libdartmpc.so equals the SHA-1 of the sources, and a mismatch -- or an A/B library name without
+    DART_MPC_AB=1 -- raises instead of loading."""
+    from dart_mpc import _lib
+    L = _lib.lib()
+    assert L.dart_mpc_build_id().decode() == _lib.source_build_id()
+    assert L.dart_mpc_build_flavor().decode() == ""
+    monkeypatch.setattr(_lib, "source_build_id", lambda: "0" * 16)
+    monkeypatch.delenv("DART_MPC_AB", raising=False)
+    with pytest.raises(_lib.DartMPCError, match="stale build"):
+        _lib._check_build(L)
+    monkeypatch.setenv("DART_MPC_AB", "1")
+    _lib._check_build(L)            # the A/B tools' explicit escape hatch

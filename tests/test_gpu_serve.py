@@ -62,6 +62,29 @@ def test_short_idle_timeout_serves_from_the_grid():
         s.serve_stop()
 
 
+def test_requests_spaced_near_half_a_short_idle_timeout():
+    """Requests spaced ~0.45 of a short idle timeout apart: the host's pre-drain margin is at
+    least 2 ms, so whether a request is served from the grid or after a host-side drain and relaunch, its
+    results equal a launch's and it never waits out a further idle period."""
+    import dart_mpc
+    from dart_mpc.workload import pmpc_batch
+    S, T, P = pmpc_batch(1)
+    with dart_mpc.Solver(N=20, tol=1e-8, B_max=18) as s:
+        base = s.solve_batch(S, T, P)
+        for idle in (0.004, 0.01):
+            s.serve_start(B_serve=18, idle_timeout=idle)
+            worst = 0.0
+            for _ in range(12):
+                time.sleep(0.45 * idle)
+                t0 = time.perf_counter()
+                got = s.solve_batch(S, T, P)
+                worst = max(worst, time.perf_counter() - t0)
+                for k in ("u0", "f", "status", "iters"):
+                    np.testing.assert_array_equal(got[k], base[k])
+            assert worst < 0.05, (idle, worst)
+            s.serve_stop()
+
+
 def test_idle_timeout_drains_and_restarts():
     import dart_mpc
     from dart_mpc.workload import pmpc_batch

@@ -6,7 +6,7 @@ LIBS=${1:?libs}
 REPS=${2:-3}
 mkdir -p gpurun_out
 for lib in $LIBS; do
-  DART_MPC_LIB=$lib timeout -k 10 400 python -u -m pytest tests/test_gpu_pmpc.py tests/test_gpu_rmpc.py tests/test_gpu_lmpc.py \
+  DART_MPC_AB=1 DART_MPC_LIB=$lib timeout -k 10 400 python -u -m pytest tests/test_gpu_pmpc.py tests/test_gpu_rmpc.py tests/test_gpu_lmpc.py \
     -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/ab_tests_$lib.log 2>&1 || { echo "TESTS_FAILED $lib"; tail -30 gpurun_out/ab_tests_$lib.log; exit 1; }
   echo "$lib $(tail -1 gpurun_out/ab_tests_$lib.log)"
 done

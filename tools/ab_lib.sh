@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 ARGS="--steps 2000 --warmup 50 --no-cpu-baseline --saturation-batch 0 --host-calls 0 --c4-steps 0 --n15-steps 0 --lmpc-policy-steps 0 $EXTRA"
 for r in $(seq 1 $REPS); do
   for lib in $LIBS; do
-    DART_MPC_LIB=$lib timeout -k 10 180 python bench.py $ARGS > gpurun_out/ab.json 2>gpurun_out/ab.err || exit $?
+    DART_MPC_AB=1 DART_MPC_LIB=$lib timeout -k 10 180 python bench.py $ARGS > gpurun_out/ab.json 2>gpurun_out/ab.err || exit $?
     python - "$lib" <<'PY'
 import json, sys
 d = json.load(open("gpurun_out/ab.json"))
