@@ -181,32 +181,44 @@ __device__ __forceinline__ AugRoles aug_roles() {
     return R;
 }
 
+// The end of a node step of a backward sweep (the next node reads what this one wrote).  One wave: the LDS
+// instructions of a wave execute in the order they are issued, so the next node's reads of G_k follow this
+// node's write without a wait for it -- only the compiler must keep program order (the empty asm with a
+// memory clobber: no LDS access moves across it).  Two waves (DART_WG = 2): a workgroup barrier.
+__device__ __forceinline__ void chain_sync() {
+#if DART_WG == 1
+    asm volatile("" ::: "memory");
+#else
+    __syncthreads();
+#endif
+}
+
 // One node step: G_k from M_k, H_k and the value function held in Gn (G_{k+1}, or its soft-row
-// surrogate); ok &= Quu of Gn positive definite.  Ends with a barrier.
+// surrogate); ok &= Quu of Gn positive definite.  Ends with chain_sync().
+// Every LDS read of the step is issued before the first product, with no wait in between (the sched_barrier
+// keeps the scheduler from sinking reads behind the arithmetic, where their latency would sit on the node
+// chain): the M_k column of phase 1 first, then G_{k+1} -- the read that waits on the previous node's write --
+// then the phase-2 column of M_k and the H entry, which are needed last.
 template <class L>
 __device__ __forceinline__ void aug_node_step(L* S, int k, const double* Gn, const AugRoles& R, bool& ok) {
     constexpr int NXA = L::NXA, NP = L::NP, NC = L::NC;
-    // off the chain: the two M columns and the H entry of this lane
     const double* Mk = &S->M[k][0][0];
     double a[NP], b[8];
 #pragma unroll
     for (int m = 0; m < NP; ++m) a[m] = Mk[R.cg * NC + m];
-#pragma unroll
-    for (int x = 0; x < 8; ++x) b[x] = Mk[R.cs * NC + (R.s ^ x)];
-    const double hk = S->H[k][R.e];
-    // the phase-2 column of M_k issued with the G_{k+1} reads (an empty asm use keeps the scheduler from
-    // sinking these loads behind phase 1, where their latency would sit on the node chain; C3 -1.7% kernel
-    // time, profiles/r04/pin_b_ab.txt)
-#pragma unroll
-    for (int x = 0; x < 8; ++x) asm volatile("" : "+v"(b[x]));
-    // phase 1: every read of G_{k+1} issued before the first product
+    __builtin_amdgcn_sched_barrier(0);
     double gz[NP], gu0[NP], gu1[NP];
 #pragma unroll
     for (int n = 0; n < NP; ++n) { gu0[n] = Gn[gzu<NXA>(n, 0)]; gu1[n] = Gn[gzu<NXA>(n, 1)]; }
+    const double q00 = Gn[hp(NXA, NXA)], q01 = Gn[hp(NXA + 1, NXA)], q11 = Gn[hp(NXA + 1, NXA + 1)];
 #pragma unroll
     for (int n = 0; n < NP; ++n) gz[n] = Gn[R.goff[n]];
     const double gs0 = Gn[R.gsu0], gs1 = Gn[R.gsu1];
-    const double q00 = Gn[hp(NXA, NXA)], q01 = Gn[hp(NXA + 1, NXA)], q11 = Gn[hp(NXA + 1, NXA + 1)];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int x = 0; x < 8; ++x) b[x] = Mk[R.cs * NC + (R.s ^ x)];
+    const double hk = S->H[k][R.e];
+    __builtin_amdgcn_sched_barrier(0);
     double t0 = 0.0, t1 = 0.0, w0 = 0.0, w1 = 0.0;
 #pragma unroll
     for (int n = 0; n < NP; ++n) {
@@ -233,7 +245,7 @@ __device__ __forceinline__ void aug_node_step(L* S, int k, const double* Gn, con
     for (int x = 0; x < 8; x += 2) { p0 = fma(b[x], ux[x], p0); p1 = fma(b[x + 1], ux[x + 1], p1); }
     // all reads of G_{k+1} and M_k precede the write of G_k (distinct rows: no hazard)
     S->G[k][R.e] = R.prod ? p0 + p1 : hk;
-    __syncthreads();
+    chain_sync();
 }
 
 template <class L>
