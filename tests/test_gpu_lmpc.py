@@ -124,8 +124,13 @@ def test_horizons(dm, N):
         # status, same point).  The two-wave machinery
         # itself is bit-identical to the one-wave kernels (tools/wg2_ab.py, profiles/r05/wg2_ab.txt).  Every other
         # instance takes the oracle's iterations exactly.
+        # #15 itself: the same status and end point (the w check below) and at most two iterations apart
+        # (measured 57 / 59 at N = 32; the oracle keeps its 59 under 1e-11 relative input perturbations, so the
+        # path difference is the two-wave kernel's arithmetic order in the restoration solve, not an
+        # ill-determined NLP)
         other = np.arange(len(ref["iters"])) != 15
         assert np.array_equal(out["iters"][other], ref["iters"][other]), (out["iters"], ref["iters"])
+        assert abs(int(out["iters"][15]) - int(ref["iters"][15])) <= 2, (out["iters"][15], ref["iters"][15])
     ok = ref["status"] == 0
     nX = 8 * (N + 1)
     assert np.max(np.abs(out["w"][ok][:, nX:] - ref["w"][ok][:, nX:])) <= 1e-6

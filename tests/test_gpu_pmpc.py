@@ -196,26 +196,44 @@ def test_soft_restoration_long_horizons(dm, N):
     """Horizons above 31 (mpc_3d.py:12 takes N freely): at N = 40, 41 of C4's 1152 instances (N = 50: 4) fail the
     filter line search at the default options, and IPOPT settles every one of them in its soft restoration phase
     (the oracle never enters the restoration phase proper there).  For N > 31 the register kernel runs that phase
-    itself (round 5; the LDS-engine restart of N <= 31 does not fit), so those instances end at the oracle's status
-    0 -- round 4 returned -2 -- with u0 within 1e-6 and iterations equal on >= 99 % of the batch.  On the restored
-    instances themselves the register kernel's arithmetic takes the oracle's iteration count on 83 % (N = 40) /
-    3 of 4 (N = 50) as measured in round 5 (the restart on the LDS engine, N <= 31, gives 100 %): the bound there is
-    that measured figure, >= 0.7."""
+    itself (the LDS-engine restart of N <= 31 does not fit), so those instances end at the oracle's status 0.
+
+    The bar on the restored instances is the end point, certified solver-independently (round 6, VERDICT r05 item
+    5), not the iteration fraction: the kernel's and the oracle's end points are the same KKT point of the
+    reference NLP -- u0 within 1e-9 (measured <= 3.3e-11 on 143 restored instances, N = 40 / 50 x three seed
+    sets of 1152, profiles/r06/pmpc_long_resto_cert.txt) and the numpy restatement's certificate (primal <= tol, the
+    stationarity of free and active tilts) equal for both -- while the soft phase's damped steps amplify the
+    register kernel's rounding (scan-form recursions, f32 error reductions) into a path that may take up
+    to three iterations more or fewer (measured: |diff| <= 3, 78 % equal).  The oracle itself keeps its iteration count
+    under 1e-11 relative input perturbations (it is the kernel's different arithmetic order, not an
+    ill-determined NLP, that moves the path), so the bound is on what the restart cannot give here: the point."""
     import oracle_lib
+    from pmpc_nlp import PMPCProblem, kkt_certificate
     from dart_mpc.workload import pmpc_batch
     S, T, P = pmpc_batch(64)
     s = dm.Solver(N=N, Ts=0.002, tol=1e-8, B_max=S.shape[0])
-    g = s.solve_batch(S, T, P)
+    g = s.solve_batch(S, T, P, want_w=True)
     s.close()
-    kw = dict(N=N, Ts=0.002, tol=1e-8, max_iter=3000, nthreads=8, want_w=False)
-    o = oracle_lib.solve_batch(S, T, P, **kw)
-    off = oracle_lib.solve_batch(S, T, P, resto=False, **kw)
+    kw = dict(N=N, Ts=0.002, tol=1e-8, max_iter=3000, nthreads=8)
+    o = oracle_lib.solve_batch(S, T, P, want_w=True, **kw)
+    off = oracle_lib.solve_batch(S, T, P, resto=False, want_w=False, **kw)
     rest = off["status"] != 0
     assert rest.sum() >= 4 and np.all(o["status"] == 0)
     assert np.array_equal(g["status"], o["status"]), np.unique(g["status"], return_counts=True)
     assert np.mean(g["iters"] == o["iters"]) >= 0.99
-    assert np.mean(g["iters"][rest] == o["iters"][rest]) >= 0.7, (g["iters"][rest], o["iters"][rest])
     assert np.max(np.abs(g["u0"] - o["u0"])) <= 1e-6
+    idx = np.flatnonzero(rest)
+    assert np.max(np.abs(g["u0"][idx] - o["u0"][idx])) <= 1e-9
+    assert np.max(np.abs(g["iters"][idx] - o["iters"][idx])) <= 3, (g["iters"][idx], o["iters"][idx])
+    for i in idx:
+        mu, qp, qv, r, lo, hi = P[i]
+        prob = PMPCProblem(N=N, Ts=0.002, Qp=qp, Qv=qv, R=r, mu=mu, u_bounds=(lo, hi))
+        p = np.concatenate([S[i], T[i]])
+        cg, co = kkt_certificate(prob, g["w"][i], p, act_tol=1e-6), kkt_certificate(prob, o["w"][i], p, act_tol=1e-6)
+        assert cg["primal"] <= 1e-8 and cg["bound"] == 0.0, (i, cg["primal"])
+        assert abs(cg["primal"] - co["primal"]) <= 1e-10, (i, cg["primal"], co["primal"])
+        sg, so = max(cg["stat_free"], cg["stat_sign"]), max(co["stat_free"], co["stat_sign"])
+        assert abs(sg - so) <= 1e-8 * max(1.0, cg["grad_scale"]), (i, sg, so)
 
 
 @pytest.mark.parametrize("N", [32, 40, 63])
