@@ -1046,6 +1046,11 @@ def main():
         for j in range(K):
             launch(W + j)
         ev1.record(stream)
+    # the host notices the end of the last launch by polling its event (hipEventQuery) rather than by the blocking
+    # wait alone, whose wake-up latency (tens of us) would otherwise count against a 20-step run; the
+    # synchronize that brackets the timed region follows and returns at once
+    while not ev1.query():
+        pass
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

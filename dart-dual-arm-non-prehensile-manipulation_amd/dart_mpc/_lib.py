@@ -6,10 +6,12 @@ every solve raises ``DartMPCError``.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import subprocess
 import threading
+import weakref
 
 import numpy as np
 
@@ -235,6 +237,20 @@ def _ptr(a):
     return None if a is None else ctypes.c_void_p(a.ctypes.data)
 
 
+# Handles still open at interpreter exit are destroyed by an atexit hook, before the HIP runtime's own teardown:
+# a handle freed later, from a finaliser, would free device memory through a runtime that is already gone.
+_LIVE = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live_handles():
+    for s in list(_LIVE):
+        try:
+            s.close()
+        except Exception:
+            pass
+
+
 class Solver:
     """Owns one ``dart_mpc_handle`` (device workspace + stream) for a fixed N/Ts/tol.  ``max_soc`` is
     IPOPT's second-order-correction count (default 4, as ``mpc_3d.py:82`` leaves it; 0 = off).
@@ -256,6 +272,7 @@ class Solver:
                                   constr_mult_init_max=float(constr_mult_init_max),
                                   restoration=int(bool(restoration)))
         rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
+        _LIVE.add(self)
         if rc != 0:
             raise DartMPCError(f"dart_mpc_create failed with code {rc} (no gfx950 device or bad config)")
         self.N = int(N)
@@ -446,6 +463,7 @@ class RmpcSolver(Solver):
                                   constr_mult_init_max=float(constr_mult_init_max),
                                   restoration=int(bool(restoration)), max_soc=int(max_soc))
         rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
+        _LIVE.add(self)
         if rc != 0:
             raise DartMPCError(f"dart_mpc_create(RMPC) failed with code {rc} (no gfx950 device or bad config)")
         self.N = int(N)
@@ -506,6 +524,7 @@ class LmpcSolver(Solver):
                                   constr_mult_init_max=float(constr_mult_init_max),
                                   restoration=int(bool(restoration)), max_cpu_time=float(max_cpu_time))
         rc = lib().dart_mpc_create(ctypes.byref(self.cfg), int(device), ctypes.byref(self._h))
+        _LIVE.add(self)
         if rc != 0:
             raise DartMPCError(f"dart_mpc_create(LMPC) failed with code {rc} (no gfx950 device or bad config)")
         self.N = int(N)
