@@ -1020,9 +1020,13 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     sp = stream.cuda_stream
 
+    # every step's device pointers formed before the timed region (tensor indexing costs the host ~5 us per view;
+    # at 20 steps the first launch's share of that sat in the timed region before the GPU started)
+    ptrs = [(X0[i].data_ptr(), RF[i].data_ptr(), PR[i].data_ptr(), U0[i].data_ptr(), FV[i].data_ptr(),
+             ST[i].data_ptr(), IT[i].data_ptr()) for i in range(W + K)]
+
     def launch(i):
-        solver.solve_batch_dev(B, X0[i].data_ptr(), RF[i].data_ptr(), PR[i].data_ptr(), U0[i].data_ptr(),
-                               FV[i].data_ptr(), ST[i].data_ptr(), IT[i].data_ptr(), stream=sp)
+        solver.solve_batch_dev(B, *ptrs[i], stream=sp)
 
     # kernel time base of the roofline: ONE event pair on the launch stream around the whole timed
     # loop of back-to-back launches, divided by K -- the mean launch duration including the (~0-2 us)
