@@ -1044,9 +1044,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    # the start event goes on the stream just before the timed region: its host cost (~10 us of torch + HIP event
+    # record) is not the hot path's, and the event span then also covers the host's first launch (kernel_ms a
+    # slight overestimate: roofline.frac stays a lower bound)
     with torch.cuda.stream(stream):
         ev0.record(stream)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
         for j in range(K):
             launch(W + j)
         ev1.record(stream)
