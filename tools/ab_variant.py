@@ -35,6 +35,15 @@ elif kind == "lmpc":
     PR = f64(np.tile(LMPC_PRM_DEFAULT, (B, 1)))
     s = dart_mpc.LmpcSolver(N=30, B_max=B, device=0)
     call = lambda i, o: s.solve_batch_dev(B, *[x[i % nb].data_ptr() for x in X], PR.data_ptr(), *o, stream=sp)
+elif kind in ("pmpc_resto", "pmpc_soc0"):
+    # C4's 1152 instances with IPOPT's restoration phases in play: N = 31 (a few restored), or N = 20 with
+    # max_soc = 0 (about one in ten restored); one launch per call, the same inputs every call
+    B, nb = 1152, 1
+    S_, T_, P_ = W.pmpc_batch(64, seed0=300000)
+    X = [f64(a)[None] for a in (S_, T_, P_)]
+    s = dart_mpc.Solver(N=31 if kind == "pmpc_resto" else 20, tol=1e-8, B_max=B, device=0,
+                        max_soc=4 if kind == "pmpc_resto" else 0)
+    call = lambda i, o: s.solve_batch_dev(B, *[x[0].data_ptr() for x in X], *o, stream=sp)
 else:
     Ds = [W.pmpc_batch(1, seed0=i) for i in range(nb)]
     X = [f64(np.stack([d[j] for d in Ds])) for j in range(3)]
