@@ -202,7 +202,7 @@ __device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const Riccati
             for (int a = 0; a < 4; ++a) v -= rp[a] * t4[a];
             RL->Gs[h][R.e] = uent ? ((zi == NXA && zj == NXA) ? 1.0 : 0.0) : v;
         }
-        __syncthreads();
+        chain_sync();
     };
     for (int k = N - 1; k >= 0; --k) {
         soften(base + k + 1, true);
@@ -223,7 +223,7 @@ __device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const Riccati
 #pragma unroll
         for (int m = 0; m < NP; ++m) ga = fma(vi[m], t[m], ga);
         S->G[base + k][R.e] = ga;
-        __syncthreads();
+        chain_sync();
         // early: a failed inertia test (Quu or a soft block's pivot of either half) ends the sweep -- only for the
         // perturbation loop, whose caller discards a failed sweep and factors again with a new perturbation.  Every
         // lane of a half tests the same LDS values, and the two waves of a two-wave build run the sweep alike, so

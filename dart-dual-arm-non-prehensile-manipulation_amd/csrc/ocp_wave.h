@@ -25,6 +25,18 @@
 
 namespace dartmpc {
 
+// The end of a node step of a backward sweep (the next node reads what this one wrote).  One wave: the LDS
+// instructions of a wave execute in the order they are issued, so the next node's reads of G_k follow this
+// node's write without a wait for it -- only the compiler must keep program order (the empty asm with a
+// memory clobber: no LDS access moves across it).  Two waves (DART_WG = 2): a workgroup barrier.
+__device__ __forceinline__ void chain_sync() {
+#if DART_WG == 1
+    asm volatile("" ::: "memory");
+#else
+    __syncthreads();
+#endif
+}
+
 __host__ __device__ constexpr int tri(int n) { return n * (n + 1) / 2; }
 __host__ __device__ constexpr int hp(int i, int j) { return i >= j ? tri(i) + j : tri(j) + i; }
 __host__ __device__ constexpr int even(int n) { return (n + 1) & ~1; }
@@ -179,18 +191,6 @@ __device__ __forceinline__ AugRoles aug_roles() {
     }
     R.gsu0 = hp(NXA, zs); R.gsu1 = hp(NXA + 1, zs);
     return R;
-}
-
-// The end of a node step of a backward sweep (the next node reads what this one wrote).  One wave: the LDS
-// instructions of a wave execute in the order they are issued, so the next node's reads of G_k follow this
-// node's write without a wait for it -- only the compiler must keep program order (the empty asm with a
-// memory clobber: no LDS access moves across it).  Two waves (DART_WG = 2): a workgroup barrier.
-__device__ __forceinline__ void chain_sync() {
-#if DART_WG == 1
-    asm volatile("" ::: "memory");
-#else
-    __syncthreads();
-#endif
 }
 
 // One node step: G_k from M_k, H_k and the value function held in Gn (G_{k+1}, or its soft-row
@@ -410,7 +410,7 @@ __device__ __forceinline__ void aug_soften(L* S, AugSoftLds<L, NS>* RS, int j, b
         }
         RS->Gs[gzz<NXA>(pv, qv)] = v;
     }
-    __syncthreads();
+    chain_sync();
 }
 
 // Backward sweep with the soft rows of every node (restoration phase): before the step of node k the
@@ -477,7 +477,7 @@ __device__ __forceinline__ void gen_node_step(L* S, int k, const double* Gn, dou
         const double r0 = fma(q11, gs0, -q01 * gs1) / det, r1 = fma(q00, gs1, -q01 * gs0) / det;
         if (lane < ND * NP) U[i * NC + s] = t - fma(r0, w0, r1 * w1);
     }
-    __syncthreads();
+    chain_sync();
     if (lane < L::NT) {
         const int i = R.i2, j = R.j2;
         double gv = S->H[k][lane];
@@ -485,7 +485,7 @@ __device__ __forceinline__ void gen_node_step(L* S, int k, const double* Gn, dou
         for (int m = 0; m < NP; ++m) gv = fma(Mk[j * NC + m], U[i * NC + m], gv);
         S->G[k][lane] = gv;
     }
-    __syncthreads();
+    chain_sync();
 }
 
 // backward sweeps with gen_node_step: plain, and with the soft rows of every node (as riccati_sweep_aug[_soft])
@@ -751,21 +751,38 @@ __device__ RiccatiSRoles riccati_s_roles() {
 template <class L>
 __device__ __forceinline__ void s_node_step(L* S, int sk, const RiccatiSRoles& R, bool& ok) {
     constexpr int NXA = L::NXA, NP = L::NP;
-    const double hk = S->H[sk][R.e];
+    // every LDS read of the step issued before the first product (sched_barrier), the column of M_k that the
+    // first products need first, then G_{k+1} -- whose reads follow the previous node's write in the wave's LDS
+    // order (chain_sync) -- then the other column and the H entry: one LDS latency on the chain, where the
+    // compiler's own schedule re-used registers across the G_{k+1} reads and waited out several
     const double* Mk = &S->M[sk][0][0];
     double vi[NP], vj[NP];
 #pragma unroll
-    for (int m = 0; m < NP; ++m) { vi[m] = Mk[R.ci + m]; vj[m] = Mk[R.cj + m]; }
+    for (int m = 0; m < NP; ++m) vj[m] = Mk[R.cj + m];
+    __builtin_amdgcn_sched_barrier(0);
     const double* Gn = S->G[sk + 1];
+    double gzz_[NP][NP], gzu_[NP];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+#pragma unroll
+        for (int m = 0; m <= n; ++m) gzz_[m][n] = Gn[gszz<NXA>(m, n)];
+        gzu_[n] = Gn[gszu<NXA>(n)];
+    }
+    const double q = Gn[hp(NXA, NXA)];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < NP; ++m) vi[m] = Mk[R.ci + m];
+    const double hk = S->H[sk][R.e];
+    __builtin_amdgcn_sched_barrier(0);
     double t[NP], b = 0.0, c = 0.0;
 #pragma unroll
     for (int m = 0; m < NP; ++m) t[m] = 0.0;
 #pragma unroll
     for (int n = 0; n < NP; ++n) {
 #pragma unroll
-        for (int m = 0; m < NP; ++m) t[m] = fma(Gn[gszz<NXA>(m, n)], vj[n], t[m]);
-        b = fma(vi[n], Gn[gszu<NXA>(n)], b);
-        c = fma(vj[n], Gn[gszu<NXA>(n)], c);
+        for (int m = 0; m < NP; ++m) t[m] = fma(m <= n ? gzz_[m][n] : gzz_[n][m], vj[n], t[m]);
+        b = fma(vi[n], gzu_[n], b);
+        c = fma(vj[n], gzu_[n], c);
     }
     double ga = hk, gb = 0.0;
 #pragma unroll
@@ -773,12 +790,11 @@ __device__ __forceinline__ void s_node_step(L* S, int sk, const RiccatiSRoles& R
         ga = fma(vi[m], t[m], ga);
         if (m + 1 < NP) gb = fma(vi[m + 1], t[m + 1], gb);
     }
-    const double q = Gn[hp(NXA, NXA)];
     ok = ok && q > 0.0 && isfinite(q);
     const double g = (ga + gb) - b * c * frcp(q);
     // all reads of G_{k+1} and M_k precede the write of G_k (distinct slots: no hazard)
     S->G[sk][R.e] = g;
-    __syncthreads();
+    chain_sync();
 }
 
 // Backward sweep of both halves over nodes N-1 .. 0; G[slot N] must hold each half's terminal
@@ -824,7 +840,7 @@ __device__ bool riccati_s_sweep_p(L* S, double (*Ps)[L::NTP], int N, const Ricca
         const double gi = Gn[hp(zi, NXA)], gj = Gn[hp(zj, NXA)];
         const double pv = Gn[R.e] - gi * gj / q;
         Ps[h][R.e] = uent ? ((zi == NXA && zj == NXA) ? 1.0 : 0.0) : pv;
-        __syncthreads();
+        chain_sync();
         // node step on the surrogate (s_node_step with Gn = Ps[h]: Gzu = 0, Quu = 1)
         const double hk = S->H[base + k][R.e];
         const double* Mk = &S->M[base + k][0][0];
@@ -844,7 +860,7 @@ __device__ bool riccati_s_sweep_p(L* S, double (*Ps)[L::NTP], int N, const Ricca
 #pragma unroll
         for (int m = 0; m < NP; ++m) g = fma(vi[m], t[m], g);
         S->G[base + k][R.e] = g;
-        __syncthreads();
+        chain_sync();
     }
     const double q0 = S->G[base][hp(NXA, NXA)];
     ok = ok && q0 > 0.0 && isfinite(q0);
