@@ -460,29 +460,42 @@ __device__ __forceinline__ void gen_node_step(L* S, int k, const double* Gn, dou
     static_assert(ND * NP <= 64 && NP <= NC, "one lane per (stage column, value index)");
     const int lane = lane_id();
     const double* Mk = &S->M[k][0][0];
+    const int i = R.i1, s = R.s1;
+    // every read that does not depend on this step's own products is issued up front, in three groups (as
+    // aug_node_step): column i of M_k, then G_{k+1} (the read that follows the previous node's write), then
+    // the phase-2 column j of M_k and the H entry; the three accumulations below keep their order
+    double an[NP];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) an[n] = Mk[i * NC + n];
+    __builtin_amdgcn_sched_barrier(0);
     const double q00 = Gn[hp(NXA, NXA)], q01 = Gn[hp(NXA + 1, NXA)], q11 = Gn[hp(NXA + 1, NXA + 1)];
+    double gsn[NP], g0n[NP], g1n[NP];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) { gsn[n] = Gn[gzz<NXA>(s, n)]; g0n[n] = Gn[gzu<NXA>(n, 0)]; g1n[n] = Gn[gzu<NXA>(n, 1)]; }
+    const double gs0 = Gn[gzu<NXA>(s, 0)], gs1 = Gn[gzu<NXA>(s, 1)];
+    __builtin_amdgcn_sched_barrier(0);
+    const int i2 = R.i2, j2 = R.j2;
+    double mj[NP];
+#pragma unroll
+    for (int m = 0; m < NP; ++m) mj[m] = Mk[j2 * NC + m];
+    const double hk = S->H[k][lane < L::NT ? lane : 0];
+    __builtin_amdgcn_sched_barrier(0);
     const double det = fma(q00, q11, -q01 * q01);
     ok = ok && (q00 > 0.0) && (det > 0.0) && isfinite(det);
-    {
-        const int i = R.i1, s = R.s1;
-        double t = 0.0, w0 = 0.0, w1 = 0.0;
+    double t = 0.0, w0 = 0.0, w1 = 0.0;
 #pragma unroll
-        for (int n = 0; n < NP; ++n) {
-            const double an = Mk[i * NC + n];
-            t = fma(Gn[gzz<NXA>(s, n)], an, t);
-            w0 = fma(Gn[gzu<NXA>(n, 0)], an, w0);
-            w1 = fma(Gn[gzu<NXA>(n, 1)], an, w1);
-        }
-        const double gs0 = Gn[gzu<NXA>(s, 0)], gs1 = Gn[gzu<NXA>(s, 1)];
-        const double r0 = fma(q11, gs0, -q01 * gs1) / det, r1 = fma(q00, gs1, -q01 * gs0) / det;
-        if (lane < ND * NP) U[i * NC + s] = t - fma(r0, w0, r1 * w1);
+    for (int n = 0; n < NP; ++n) {
+        t = fma(gsn[n], an[n], t);
+        w0 = fma(g0n[n], an[n], w0);
+        w1 = fma(g1n[n], an[n], w1);
     }
+    const double r0 = fma(q11, gs0, -q01 * gs1) / det, r1 = fma(q00, gs1, -q01 * gs0) / det;
+    if (lane < ND * NP) U[i * NC + s] = t - fma(r0, w0, r1 * w1);
     chain_sync();
     if (lane < L::NT) {
-        const int i = R.i2, j = R.j2;
-        double gv = S->H[k][lane];
+        double gv = hk;
 #pragma unroll
-        for (int m = 0; m < NP; ++m) gv = fma(Mk[j * NC + m], U[i * NC + m], gv);
+        for (int m = 0; m < NP; ++m) gv = fma(mj[m], U[i2 * NC + m], gv);
         S->G[k][lane] = gv;
     }
     chain_sync();

@@ -87,18 +87,18 @@ struct PrSoftPost {
 struct PrFilter {
     double th[4], ph[4];
     int n;
-    __device__ void reset() {
+    __device__ __forceinline__ void reset() {
         n = 0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) { th[r] = 0.0; ph[r] = 0.0; }
     }
-    __device__ bool hit(double t, double p) const {
+    __device__ __forceinline__ bool hit(double t, double p) const {
         bool h = false;
 #pragma unroll
         for (int r = 0; r < 4; ++r) h = h || (lane_id() + 64 * r < n && t >= th[r] && p >= ph[r]);
         return wany(h);
     }
-    __device__ void add(double t, double p) {
+    __device__ __forceinline__ void add(double t, double p) {
         if (n >= 256) return;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -106,6 +106,11 @@ struct PrFilter {
         ++n;
     }
 };
+
+// Transcendental pairs: a node's lanes k and k + 32 hold the same operands, so lanes 0-31 evaluate the first
+// of a pair and lanes 32-63 the second, and v_permlane32_swap hands each half the other's result (half_pair):
+// the same function on the same operand -- the same bits -- at half the evaluations per lane.  EXEC full.
+__device__ __forceinline__ bool pr_low_half() { return lane_id() < 32; }
 
 #ifdef DART_STAMPS
 // diagnostic build: per-phase s_memtime cycles of the last handed-over instance (tools/stamps_pmpc_resto.py)
@@ -170,7 +175,8 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
 
     // ---------------- model and NLP pieces of node k -------------------------------------------------
     auto fwd = [&](const double* xx, const double* uu, double* xn) {          // f(x_k, u_k), mpc_3d.py:87-104
-        const double sx = sin(uu[0]), sy = sin(uu[1]);
+        double sx, sy;
+        half_pair(sin(pr_low_half() ? uu[0] : uu[1]), sx, sy);
         const double w = -gz * (uu[0] * uu[0] + uu[1] * uu[1]);
         xn[0] = fma(a12, xx[1], fma(b1, sx, xx[0])); xn[1] = fma(a22, xx[1], b2 * sx);
         xn[2] = fma(a12, xx[3], fma(b1, sy, xx[2])); xn[3] = fma(a22, xx[3], b2 * sy);
@@ -193,9 +199,10 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
     // J^T ln of node k at controls uu: A^T ln (ja[0..5]) and B^T ln (ja[6..7]), and the curvature
     // ln^T d2 f / d theta_a^2 of the tilt diagonal (hu) -- d2 of -ln^T f, the lambda-weighted dynamics Hessian
     auto jac_t = [&](const double* uu, const double* ln, double* ja, double* hu) {
-        double sx, cx, sy, cy;
-        sincos(uu[0], &sx, &cx);
-        sincos(uu[1], &sy, &cy);
+        double sx, cx, sy, cy, sh, ch;
+        sincos(pr_low_half() ? uu[0] : uu[1], &sh, &ch);
+        half_pair(sh, sx, sy);
+        half_pair(ch, cx, cy);
         const double lz = fma(zcp, ln[4], zcv * ln[5]);
         const double lx = fma(b1, ln[0], b2 * ln[1]), ly = fma(b1, ln[2], b2 * ln[3]);
         ja[0] = ln[0]; ja[1] = fma(a12, ln[0], a22 * ln[1]);
@@ -228,12 +235,18 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
     auto barrier = [&](const double* xx, const double* uu, double m) {
         double lb = 0.0;
         bool out = false;
+        double lsl[2], lsu[2];
+        {
+            const double uh = pr_low_half() ? uu[0] : uu[1];
+            half_pair(log(uh - lo), lsl[0], lsl[1]);
+            half_pair(log(hi - uh), lsu[0], lsu[1]);
+        }
         if (wu) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const double sl = uu[j] - lo, su = hi - uu[j];
                 out = out || !(sl > 0) || !(su > 0);
-                lb += log(sl) + log(su);
+                lb += lsl[j] + lsu[j];
             }
         }
         if (wany(out)) return (double)INFINITY;
@@ -257,7 +270,8 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
     }
     // the tilt columns of M_k at controls uu
     auto write_tilt_cols = [&](const double* uu) {
-        const double cx = cos(uu[0]), cy = cos(uu[1]);
+        double cx, cy;
+        half_pair(cos(pr_low_half() ? uu[0] : uu[1]), cx, cy);
         if (wu) {
             Mk[6 * NC + 0] = b1 * cx; Mk[6 * NC + 1] = b2 * cx;
             Mk[6 * NC + 4] = zcp * (-2.0 * gz * uu[0]); Mk[6 * NC + 5] = zcv * (-2.0 * gz * uu[0]);
@@ -446,7 +460,10 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
         }
         // ---- Newton step: Riccati with inertia correction ----
         double delta = 0.0;
+        SPAN_BEGIN(sp_ric);
         bool ok = riccati_sweep_gen(S, N, SH.U);
+        SPAN_END(21, sp_ric);
+        STAMP_ADD(22, 1);
         for (int attempt = 0; !ok && attempt < 60; ++attempt) {
             // (the resumed iteration: the register kernel's shift, which its update left in delta_last)
             delta = (attempt == 0) ? (resume_first && delta_last > 0.0 ? delta_last
@@ -495,7 +512,8 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
         }
         const double gTd = wsum(gtd);
         // theta^s_th and (-gTd)^s_ph are fixed through the line search: formed once here, not at every trial
-        const double pw_th = gTd < 0 ? pow(theta, s_th) : 0.0, pw_gd = gTd < 0 ? pow(-gTd, s_ph) : 0.0;
+        double pw_th = 0.0, pw_gd = 0.0;
+        if (gTd < 0) half_pair(pr_low_half() ? pow(theta, s_th) : pow(-gTd, s_ph), pw_th, pw_gd);
         double amin = gam_th;
         if (gTd < 0) amin = fmin(gam_th, fmin(gam_ph * theta / (-gTd), pw_th / pw_gd));
         if (theta == 0.0 && gTd < 0) amin = 0.0;
@@ -509,13 +527,17 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
         const bool tiny = wmax(tn) < 10.0 * 2.220446049250313e-16;
         double xt[6], ut[2], gt[6], th_t = 0.0, ph_t = 0.0;
         auto trial = [&](double al) {
+            SPAN_BEGIN(sp_tr);
 #pragma unroll
             for (int i = 0; i < 6; ++i) xt[i] = xon ? fma(al, dx[i], x[i]) : x[i];
 #pragma unroll
             for (int j = 0; j < 2; ++j) ut[j] = uon ? fma(al, dU[j], u[j]) : u[j];
             defects(xt, ut, gt);
             th_t = wsum(l1(gt));
+            SPAN_END(23, sp_tr);
+            SPAN_BEGIN(sp_ph);
             ph_t = barrier(xt, ut, mu);
+            SPAN_END(24, sp_ph);
         };
         bool ftype = false;
         // FilterLSAcceptor::CheckAcceptabilityOfTrialPoint with alpha_primal_test = al
@@ -536,7 +558,9 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             trial(alpha);
             STAMP_ADD(17, 1);
             if (tiny) { accepted = true; ftype = true; break; }
+            SPAN_BEGIN(sp_acc);
             accepted = accept(alpha);
+            SPAN_END(27, sp_acc);
             if (!accepted && ls == 0 && !(th_t < theta) && a.max_soc > 0) {
                 // FilterLSAcceptor::TrySecondOrderCorrection on the plain step's factorisation
                 double sdx[6], sdU[2], slp[6], cs[6];
@@ -549,10 +573,13 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                     th_old = th_t;
 #pragma unroll
                     for (int i = 0; i < 6; ++i) cs[i] = fma(asoc, cs[i], gt[i]);
+                    SPAN_BEGIN(sp_soc);
                     write_rhs(cs);
                     __syncthreads();
                     (void)riccati_sweep_gen(S, N, SH.U);
                     solve_plain(dx, dU, lp);
+                    SPAN_END(25, sp_soc);
+                    STAMP_ADD(26, 1);
                     double am = 1.0;
                     if (wu) {
 #pragma unroll
@@ -1049,6 +1076,15 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             double phir, gtdr;
             {
                 double pl = 0.0, gd = 0.0, lb = 0.0;
+                double lgp[6], lgn[6], lgl[2], lgu[2];
+#pragma unroll
+                for (int i = 0; i < 6; ++i)
+                    half_pair(log(pr_low_half() ? pn[R_PC + i] : pn[R_NC + i]), lgp[i], lgn[i]);
+                {
+                    const double uh = pr_low_half() ? u[0] : u[1];
+                    half_pair(log(uh - lo), lgl[0], lgl[1]);
+                    half_pair(log(hi - uh), lgu[0], lgu[1]);
+                }
                 if (wx) {
 #pragma unroll
                     for (int i = 0; i < 6; ++i) {
@@ -1056,7 +1092,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                         const double w = eta * pn[R_DRX + i] * pn[R_DRX + i];
                         const double e = pn[R_DRX + i] * (x[i] - pn[R_XR + i]);
                         pl += rho * (p + n) + 0.5 * eta * e * e;
-                        lb += log(p) + log(n);
+                        lb += lgp[i] + lgn[i];
                         gd += w * (x[i] - pn[R_XR + i]) * dx[i] + (rho - rmu / p) * dpc[i] + (rho - rmu / n) * dnc[i];
                     }
                 }
@@ -1066,14 +1102,15 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                         const double w = eta * pn[R_DRU + j] * pn[R_DRU + j];
                         const double e = pn[R_DRU + j] * (u[j] - pn[R_UR + j]);
                         pl += 0.5 * eta * e * e;
-                        lb += log(u[j] - lo) + log(hi - u[j]);
+                        lb += lgl[j] + lgu[j];
                         gd += (w * (u[j] - pn[R_UR + j]) - rmu / (u[j] - lo) + rmu / (hi - u[j])) * dU[j];
                     }
                 }
                 phir = wsum(pl) - rmu * wsum(lb);
                 gtdr = wsum(gd);
             }
-            const double pw_thr = gtdr < 0 ? pow(thr, s_th) : 0.0, pw_gdr = gtdr < 0 ? pow(-gtdr, s_ph) : 0.0;
+            double pw_thr = 0.0, pw_gdr = 0.0;
+            if (gtdr < 0) half_pair(pr_low_half() ? pow(thr, s_th) : pow(-gtdr, s_ph), pw_thr, pw_gdr);
             double aminr = gam_th;
             if (gtdr < 0) aminr = fmin(gam_th, fmin(gam_ph * thr / (-gtdr), pw_thr / pw_gdr));
             aminr *= gam_al;
@@ -1087,6 +1124,17 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                 defects(xt, ut, gt);
                 double thl = 0.0, phl = 0.0, lb = 0.0;
                 bool out = false;
+                double lgp[6], lgn[6], lgl[2], lgu[2];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    const double p = fma(al, dpc[i], pn[R_PC + i]), n = fma(al, dnc[i], pn[R_NC + i]);
+                    half_pair(log(pr_low_half() ? p : n), lgp[i], lgn[i]);
+                }
+                {
+                    const double uh = pr_low_half() ? ut[0] : ut[1];
+                    half_pair(log(uh - lo), lgl[0], lgl[1]);
+                    half_pair(log(hi - uh), lgu[0], lgu[1]);
+                }
                 if (wx) {
 #pragma unroll
                     for (int i = 0; i < 6; ++i) {
@@ -1096,7 +1144,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                         const double e = pn[R_DRX + i] * (xt[i] - pn[R_XR + i]);
                         phl += rho * (p + n) + 0.5 * eta * e * e;
                         out = out || !(p > 0.0) || !(n > 0.0);
-                        lb += log(p) + log(n);
+                        lb += lgp[i] + lgn[i];
                     }
                 } else {
 #pragma unroll
@@ -1108,7 +1156,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                         const double e = pn[R_DRU + j] * (ut[j] - pn[R_UR + j]);
                         phl += 0.5 * eta * e * e;
                         out = out || !(ut[j] > lo) || !(ut[j] < hi);
-                        lb += log(ut[j] - lo) + log(hi - ut[j]);
+                        lb += lgl[j] + lgu[j];
                     }
                 }
                 tht = wsum(thl);

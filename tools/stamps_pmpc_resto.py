@@ -47,3 +47,8 @@ for i, n in names.items():
     print(f"  {n:34s} {int(st[i]):10d}  {100 * st[i] / tot:5.1f}%")
 print(f"  main iterations {int(st[16])}, main line-search trials {int(st[17])}, restoration iterations {int(st[18])}, "
       f"restoration trials {int(st[19])}, refinement solves {int(st[20])}")
+print(f"  main: plain Riccati sweeps {int(st[22])} take {int(st[21])} cycles ({st[21] / max(1, st[22]):.0f} per sweep); "
+      f"trials: defects + theta {int(st[23])}, barrier {int(st[24])}, filter test {int(st[27])} cycles; "
+      f"second-order corrections {int(st[26])} take {int(st[25])} cycles")
+sys.stdout.flush()
+os._exit(0)      # (two libraries in one process: skip the runtime teardown)
