@@ -205,12 +205,14 @@ __device__ bool riccati_s_sweep_soft(LmLds* S, LmResto* RL, int N, const Riccati
         chain_sync();
     };
     for (int k = N - 1; k >= 0; --k) {
-        soften(base + k + 1, true);
+        // node k's M and H entries do not depend on the chain: read before the soft-row transform of node k+1
+        // (whose closing fence no LDS access crosses), so their latency is off the chain
         const double hk = S->H[base + k][R.e];
         const double* Mk = &S->M[base + k][0][0];
         double vi[NP], vj[NP];
 #pragma unroll
         for (int m = 0; m < NP; ++m) { vi[m] = Mk[R.ci + m]; vj[m] = Mk[R.cj + m]; }
+        soften(base + k + 1, true);
         const double* Gn = RL->Gs[h];
         double t[NP];
 #pragma unroll
