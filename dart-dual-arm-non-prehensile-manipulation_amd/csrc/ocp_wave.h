@@ -199,13 +199,35 @@ __device__ __forceinline__ AugRoles aug_roles() {
 // keeps the scheduler from sinking reads behind the arithmetic, where their latency would sit on the node
 // chain): the M_k column of phase 1 first, then G_{k+1} -- the read that waits on the previous node's write --
 // then the phase-2 column of M_k and the H entry, which are needed last.
+// The step's operands that do not depend on the chain: the phase-1 and phase-2 columns of M_k and the H entry.
+// The soft sweep reads them before the soft-row transform of node k+1 (aug_node_in), off the chain.
 template <class L>
-__device__ __forceinline__ void aug_node_step(L* S, int k, const double* Gn, const AugRoles& R, bool& ok) {
+struct AugNodeIn {
+    double a[L::NP], b[8], hk;
+};
+template <class L>
+__device__ __forceinline__ void aug_node_in(const L* S, int k, const AugRoles& R, AugNodeIn<L>& in) {
+    constexpr int NP = L::NP, NC = L::NC;
+    const double* Mk = &S->M[k][0][0];
+#pragma unroll
+    for (int m = 0; m < NP; ++m) in.a[m] = Mk[R.cg * NC + m];
+#pragma unroll
+    for (int x = 0; x < 8; ++x) in.b[x] = Mk[R.cs * NC + (R.s ^ x)];
+    in.hk = S->H[k][R.e];
+}
+template <class L, bool PRE = false>
+__device__ __forceinline__ void aug_node_step(L* S, int k, const double* Gn, const AugRoles& R, bool& ok,
+                                              const AugNodeIn<L>* pre = nullptr) {
     constexpr int NXA = L::NXA, NP = L::NP, NC = L::NC;
     const double* Mk = &S->M[k][0][0];
     double a[NP], b[8];
+    if constexpr (PRE) {
 #pragma unroll
-    for (int m = 0; m < NP; ++m) a[m] = Mk[R.cg * NC + m];
+        for (int m = 0; m < NP; ++m) a[m] = pre->a[m];
+    } else {
+#pragma unroll
+        for (int m = 0; m < NP; ++m) a[m] = Mk[R.cg * NC + m];
+    }
     __builtin_amdgcn_sched_barrier(0);
     double gz[NP], gu0[NP], gu1[NP];
 #pragma unroll
@@ -215,9 +237,16 @@ __device__ __forceinline__ void aug_node_step(L* S, int k, const double* Gn, con
     for (int n = 0; n < NP; ++n) gz[n] = Gn[R.goff[n]];
     const double gs0 = Gn[R.gsu0], gs1 = Gn[R.gsu1];
     __builtin_amdgcn_sched_barrier(0);
+    double hk;
+    if constexpr (PRE) {
 #pragma unroll
-    for (int x = 0; x < 8; ++x) b[x] = Mk[R.cs * NC + (R.s ^ x)];
-    const double hk = S->H[k][R.e];
+        for (int x = 0; x < 8; ++x) b[x] = pre->b[x];
+        hk = pre->hk;
+    } else {
+#pragma unroll
+        for (int x = 0; x < 8; ++x) b[x] = Mk[R.cs * NC + (R.s ^ x)];
+        hk = S->H[k][R.e];
+    }
     __builtin_amdgcn_sched_barrier(0);
     double t0 = 0.0, t1 = 0.0, w0 = 0.0, w1 = 0.0;
 #pragma unroll
@@ -424,8 +453,10 @@ __device__ bool riccati_sweep_aug_soft(L* S, AugSoftLds<L, NS>* RS, int N) {
     const SoftenRoles SR = soften_roles<L>();
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
+        AugNodeIn<L> in;
+        aug_node_in<L>(S, k, R, in);          // off the chain: issued before the transform's closing fence
         aug_soften<L, NS>(S, RS, k + 1, true, SR, ok);
-        aug_node_step<L>(S, k, RS->Gs, R, ok);
+        aug_node_step<L, true>(S, k, RS->Gs, R, ok, &in);
     }
     aug_soften<L, NS>(S, RS, 0, false, SR, ok);
     return !wany(!ok);
@@ -515,6 +546,7 @@ __device__ bool riccati_sweep_gen_soft(L* S, AugSoftLds<L, NS>* RS, int N, doubl
     const GenRoles R = gen_roles<L>();
     const SoftenRoles SR = soften_roles<L>();
     bool ok = true;
+    // (the operands off the chain stay in the node step here: read ahead of the NS = 6 transform they spill)
     for (int k = N - 1; k >= 0; --k) {
         aug_soften<L, NS>(S, RS, k + 1, true, SR, ok);
         gen_node_step<L>(S, k, RS->Gs, U, R, ok);
