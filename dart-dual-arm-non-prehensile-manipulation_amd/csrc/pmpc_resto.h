@@ -413,8 +413,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                 sumz += zl[j] + zu[j];
             }
         }
-        dinf = wmax(dinf); pinf = wmax(pinf); c0 = wmax(c0); cmin = wmin(cmin);
-        suml = wsum(suml); sumz = wsum(sumz);
+        wred_errors_f64(dinf, pinf, c0, cmin, suml, sumz);
         const double s_d = fmax(100.0, (suml + sumz) / (ng + 2 * nU)) / 100.0;
         const double s_c = fmax(100.0, sumz / (2 * nU)) / 100.0;
         if (!lsm && fmax(dinf / s_d, fmax(pinf, c0 / s_c)) <= tol) { status = 0; break; }
@@ -533,10 +532,29 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
 #pragma unroll
             for (int j = 0; j < 2; ++j) ut[j] = uon ? fma(al, dU[j], u[j]) : u[j];
             defects(xt, ut, gt);
-            th_t = wsum(l1(gt));
             SPAN_END(23, sp_tr);
             SPAN_BEGIN(sp_ph);
-            ph_t = barrier(xt, ut, mu);
+            // theta and the barrier objective's two sums in one lock-step reduction (barrier(): the same bits)
+            double thl = l1(gt), lb = 0.0;
+            bool out = false;
+            double lsl[2], lsu[2];
+            {
+                const double uh = pr_low_half() ? ut[0] : ut[1];
+                half_pair(log(uh - lo), lsl[0], lsl[1]);
+                half_pair(log(hi - uh), lsu[0], lsu[1]);
+            }
+            if (wu) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const double sl = ut[j] - lo, su = hi - ut[j];
+                    out = out || !(sl > 0) || !(su > 0);
+                    lb += lsl[j] + lsu[j];
+                }
+            }
+            double nc = node_cost(xt, ut);
+            wsum3(thl, nc, lb);
+            th_t = thl;
+            ph_t = wany(out) ? (double)INFINITY : sc * nc - mu * lb;
             SPAN_END(24, sp_ph);
         };
         bool ftype = false;
@@ -900,8 +918,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                     sumz += zl[j] + zu[j];
                 }
             }
-            dinf = wmax(dinf); pinf = wmax(pinf); c0r = wmax(c0r); cminr = wmin(cminr);
-            suml = wsum(suml); sumz = wsum(sumz);
+            wred_errors_f64(dinf, pinf, c0r, cminr, suml, sumz);
             const double s_d = fmax(100.0, (suml + sumz) / (ng + nb)) / 100.0;
             const double s_c = fmax(100.0, sumz / nb) / 100.0;
             const double errr = fmax(dinf / s_d, fmax(pinf, c0r / s_c));
@@ -1106,8 +1123,9 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                         gd += (w * (u[j] - pn[R_UR + j]) - rmu / (u[j] - lo) + rmu / (hi - u[j])) * dU[j];
                     }
                 }
-                phir = wsum(pl) - rmu * wsum(lb);
-                gtdr = wsum(gd);
+                wsum3(pl, lb, gd);
+                phir = pl - rmu * lb;
+                gtdr = gd;
             }
             double pw_thr = 0.0, pw_gdr = 0.0;
             if (gtdr < 0) half_pair(pr_low_half() ? pow(thr, s_th) : pow(-gtdr, s_ph), pw_thr, pw_gdr);
@@ -1159,8 +1177,9 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                         lb += lgl[j] + lgu[j];
                     }
                 }
-                tht = wsum(thl);
-                pht = wany(out) ? (double)INFINITY : wsum(phl) - rmu * wsum(lb);
+                wsum3(thl, phl, lb);
+                tht = thl;
+                pht = wany(out) ? (double)INFINITY : phl - rmu * lb;
             };
             bool ftr = false;
             auto racc = [&](double al) -> bool {

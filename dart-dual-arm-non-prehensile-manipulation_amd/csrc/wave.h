@@ -486,9 +486,38 @@ __device__ __forceinline__ void wred_errors(float& mx0, float& mx1, float& mx2, 
 }
 
 __device__ __forceinline__ double wsum(double x) { return wreduce(x, OpSum()); }
-__device__ __forceinline__ double wsum_rl(double x) { return wreduce<OpSum, false>(x, OpSum()); }
 __device__ __forceinline__ double wmax(double x) { return wreduce(x, OpMax()); }
 __device__ __forceinline__ double wmin(double x) { return wreduce(x, OpMin()); }
+// f64 reductions advanced level by level together (the chains interleave): each value takes exactly the steps of
+// its own wsum / wmax / wmin, so the results are the same bits.  The two-wave builds take them one by one.
+template <int CTRL, int RM>
+__device__ __forceinline__ void lvl_maxd(double& x) { x = fmax(x, dpp<CTRL, RM>(x)); }
+template <int CTRL, int RM>
+__device__ __forceinline__ void lvl_mind(double& x) { x = fmin(x, dpp<CTRL, RM>(x)); }
+__device__ __forceinline__ void wsum3(double& a, double& b, double& c) {
+#if DART_WG == 1
+#define DART_L(C, R) lvl_sum<C, R>(a); lvl_sum<C, R>(b); lvl_sum<C, R>(c);
+    DART_LEVELS(DART_L)
+#undef DART_L
+    a = readlane(a, 63); b = readlane(b, 63); c = readlane(c, 63);
+#else
+    a = wsum(a); b = wsum(b); c = wsum(c);
+#endif
+}
+// three maxima, one minimum, two sums (IPOPT's optimality error and its scalings)
+__device__ __forceinline__ void wred_errors_f64(double& mx0, double& mx1, double& mx2, double& mn, double& s0, double& s1) {
+#if DART_WG == 1
+#define DART_L(C, R) lvl_maxd<C, R>(mx0); lvl_maxd<C, R>(mx1); lvl_maxd<C, R>(mx2); lvl_mind<C, R>(mn); \
+    lvl_sum<C, R>(s0); lvl_sum<C, R>(s1);
+    DART_LEVELS(DART_L)
+#undef DART_L
+    mx0 = readlane(mx0, 63); mx1 = readlane(mx1, 63); mx2 = readlane(mx2, 63); mn = readlane(mn, 63);
+    s0 = readlane(s0, 63); s1 = readlane(s1, 63);
+#else
+    mx0 = wmax(mx0); mx1 = wmax(mx1); mx2 = wmax(mx2); mn = wmin(mn); s0 = wsum(s0); s1 = wsum(s1);
+#endif
+}
+__device__ __forceinline__ double wsum_rl(double x) { return wreduce<OpSum, false>(x, OpSum()); }
 __device__ __forceinline__ bool wany(bool p) {
     bool r = __ballot(p) != 0ull;
 #if DART_WG == 2
