@@ -774,6 +774,33 @@ def bench_lmpc_policy(args, torch, dev, stream, dart_mpc):
     same = bool(torch.equal(out["u0_f"], out["u0_s"])) and all(torch.equal(A[k], Bst[k]) for k in A)
     kern_ms = _event_ms(torch, stream, lambda j: fused(3 + j), min(K, 50))
     s.close()
+    cpu = None
+    if not args.no_cpu_baseline:
+        # the same step on the host: the numpy restatement of the policy step per controller, then the C oracle's
+        # solves of the 18 NLPs with the parameters it wrote (fresh states every step, as the timed GPU loop)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_lib   # CPU baseline only
+        import lmpc_policy as lp
+        try:
+            ncores = len(os.sched_getaffinity(0))
+        except AttributeError:
+            ncores = os.cpu_count() or 1
+        nt = max(1, min(16, ncores))
+        wts = init_policy_weights(0)
+        orc = [lp.PolicyState(k0[b]) for b in range(B)]
+        nzh = NZ.cpu().numpy()
+        steps, c0 = 0, time.perf_counter()
+        while time.perf_counter() - c0 < min(6.0, args.cpu_seconds):
+            d = D[steps % len(D)]
+            for b in range(B):
+                lp.policy_step(orc[b], wts, d["state"][b], d["target"][b], d["u_prev"][b], nzh[steps % len(D), b])
+            mp = np.stack([o.model_params for o in orc])
+            oracle_lib.lmpc_solve_batch(d["state"], d["u_prev"], mp, d["target"], N=N, nthreads=nt, want_w=False)
+            steps += 1
+        cdt = time.perf_counter() - c0
+        cpu = {"value": steps * B / cdt, "unit": "solves/s", "cores": nt, "kind": "port",
+               "sample": f"{steps} steps of 18 controllers in {cdt:.1f} s: oracle/lmpc_policy.py policy step per "
+                         f"controller (numpy, one core) + the C oracle's 18 solves (oracle/lmpc_ipm.c, {nt} threads)"}
     return {"workload": "C5 with the parameter policy in the launch: 18 LMPC controllers, N=30, reference IPOPT "
                         "options, policy step (MLP 520-64-64-34 fp32, logit update every 8th step) as the prologue "
                         "of the solve kernel, fresh states every step, weights = Policy._init_weights (checkpoints "
@@ -781,7 +808,7 @@ def bench_lmpc_policy(args, torch, dev, stream, dart_mpc):
             "solves_per_s": B / res["fused"], "ms_per_step": res["fused"] * 1e3, "kernel_ms": kern_ms,
             "two_launch_ms_per_step": res["two_launch"] * 1e3,
             "status_ok_frac": float(((SS[3:] == 0) | (SS[3:] == 1)).float().mean()), "iters_mean": float(IT[3:].double().mean()),
-            "fused_equals_two_launch": same,
+            "fused_equals_two_launch": same, "cpu_baseline": cpu,
             "note": "pvec comes from the policy (current_k mid-range +-5 %, then logit updates), not from the "
                     "U(0.01, 1.9) draws of the plain C5 line, so these NLPs are easier (fewer iterations)"}
 
