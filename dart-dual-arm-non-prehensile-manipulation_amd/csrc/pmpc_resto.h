@@ -387,12 +387,17 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
     for (it = it_next; it < a.max_iter; ++it) {
         const bool lsm = it < 0;      // IPOPT's least-square starting multipliers (constr_mult_init_max)
         STAMP_ADD(16, 1);
+        SPAN_BEGIN(sp_e0);
         defects(x, u, g);             // (the accepted trial's: the same bits)
         theta = wsum(l1(g));
+        SPAN_END(28, sp_e0);
+        SPAN_BEGIN(sp_e1);
         double ln[6], ja[8], hdu[2], gx[6];
         next_of(lam, ln);
         jac_t(u, ln, ja, hdu);
         cost_grad(x, gx);
+        SPAN_END(29, sp_e1);
+        SPAN_BEGIN(sp_e2);
         // ---- optimality error, IPOPT eq. (5) ----
         double dinf = 0.0, pinf = 0.0, c0 = 0.0, cmin = 1e300, suml = 0.0, sumz = 0.0;
         if (wx) {
@@ -414,6 +419,8 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             }
         }
         wred_errors_f64(dinf, pinf, c0, cmin, suml, sumz);
+        SPAN_END(30, sp_e2);
+        SPAN_BEGIN(sp_e3);
         const double s_d = fmax(100.0, (suml + sumz) / (ng + 2 * nU)) / 100.0;
         const double s_c = fmax(100.0, sumz / (2 * nU)) / 100.0;
         if (!lsm && fmax(dinf / s_d, fmax(pinf, c0 / s_c)) <= tol) { status = 0; break; }
@@ -424,6 +431,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             F0.reset(); in_soft = 0;      // BacktrackingLineSearch::Reset: the filter and the soft phase
         }
         const double tau = fmax(0.99, 1.0 - mu);
+        SPAN_END(31, sp_e3);
         STAMP(1);
         write_tilt_cols(u);
         // stage QP at inertia shift d (least squares: unit weights, the box gradient -z_L + z_U, no defects)
@@ -498,6 +506,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
         duals();
         STAMP(3);
         const double amax0 = amax, az0 = az;
+        SPAN_BEGIN(sp_lsp);
         // ---- filter line search with second-order correction (W&B 2006, Alg. A) ----
         const double phi = barrier(x, u, mu);
         double gtd = 0.0;
@@ -569,6 +578,7 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
             }
             return cmp_le(th_t, (1 - gam_th) * theta, theta) || cmp_le(ph_t - phi, -gam_ph * theta, phi);
         };
+        SPAN_END(15, sp_lsp);
         double alpha = amax;
         bool accepted = false;
         for (int ls = 0; ls < 80 && !accepted && !in_soft; ++ls) {

@@ -50,5 +50,7 @@ print(f"  main iterations {int(st[16])}, main line-search trials {int(st[17])}, 
 print(f"  main: plain Riccati sweeps {int(st[22])} take {int(st[21])} cycles ({st[21] / max(1, st[22]):.0f} per sweep); "
       f"trials: defects + theta {int(st[23])}, barrier {int(st[24])}, filter test {int(st[27])} cycles; "
       f"second-order corrections {int(st[26])} take {int(st[25])} cycles")
+print(f"  main eval: defects + theta {int(st[28])}, multipliers / Jacobian / gradient {int(st[29])}, error terms + "
+      f"reductions {int(st[30])}, tests + mu update {int(st[31])} cycles; line-search preparation {int(st[15])} cycles")
 sys.stdout.flush()
 os._exit(0)      # (two libraries in one process: skip the runtime teardown)
