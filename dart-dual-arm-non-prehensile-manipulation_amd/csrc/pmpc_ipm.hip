@@ -952,19 +952,17 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                     phil += uon ? fma(scR * th[j], th[j], -mu * log_fast(sl * su)) : 0.0;
                     gtdl += uon ? rt[j] * dth[j] : 0.0;
                 }
-                float tn_w = 0.0f;      // two waves: the tiny-step maximum (below) rides with the two sums
-                if constexpr (kWaves == 1) {
-                    wsum2(phil, gtdl);
-                } else {
+                // IPOPT's tiny-step test (max |d|/(1+|x|) < 10 eps_mach accepts the full step unfiltered): its maximum
+                // rides with the two sums (one lock-step reduction; two waves: one exchange)
+                float tn_w = 0.0f;
 #pragma unroll
-                    for (int j = 0; j < NAX; ++j) {
-                        tn_w = fmaxf(tn_w, xon ? fabsf((float)dp[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)p[j])) : 0.0f);
-                        tn_w = fmaxf(tn_w, xon ? fabsf((float)dv[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)v[j])) : 0.0f);
-                        tn_w = fmaxf(tn_w, xon ? fabsf((float)dz[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)zz[j])) : 0.0f);
-                        tn_w = fmaxf(tn_w, uon ? fabsf((float)dth[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)th[j])) : 0.0f);
-                    }
-                    wsum2_maxf(phil, gtdl, tn_w);
+                for (int j = 0; j < NAX; ++j) {
+                    tn_w = fmaxf(tn_w, xon ? fabsf((float)dp[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)p[j])) : 0.0f);
+                    tn_w = fmaxf(tn_w, xon ? fabsf((float)dv[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)v[j])) : 0.0f);
+                    tn_w = fmaxf(tn_w, xon ? fabsf((float)dz[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)zz[j])) : 0.0f);
+                    tn_w = fmaxf(tn_w, uon ? fabsf((float)dth[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)th[j])) : 0.0f);
                 }
+                wsum2_maxf(phil, gtdl, tn_w);
                 phi = phil; gTd = gtdl;
                 // switching condition alpha (-gTd)^s_ph > delta theta^s_th, compared in log2 space
                 const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
@@ -973,20 +971,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                 amin = gam_th;
                 if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta * frcp(-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
                 amin *= gam_al;
-                // IPOPT's tiny-step test: max |d|/(1+|x|) < 10 eps_mach accepts the full step unfiltered
-                if constexpr (kWaves == 1) {
-                    float tnl = 0.0f;
-#pragma unroll
-                    for (int j = 0; j < NAX; ++j) {
-                        tnl = fmaxf(tnl, xon ? fabsf((float)dp[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)p[j])) : 0.0f);
-                        tnl = fmaxf(tnl, xon ? fabsf((float)dv[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)v[j])) : 0.0f);
-                        tnl = fmaxf(tnl, xon ? fabsf((float)dz[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)zz[j])) : 0.0f);
-                        tnl = fmaxf(tnl, uon ? fabsf((float)dth[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)th[j])) : 0.0f);
-                    }
-                    tiny = wmaxf(tnl) < 2.2e-15f;
-                } else {
-                    tiny = tn_w < 2.2e-15f;
-                }
+                tiny = tn_w < 2.2e-15f;
                 alpha = amax; amain = amax;
             } else if (soc > 0) {
                 alpha = amax;                 // alpha_soc: fraction to the boundary of the corrected step

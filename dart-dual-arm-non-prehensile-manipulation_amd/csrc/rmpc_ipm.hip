@@ -858,16 +858,8 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                 for (int i = 0; i < RM_NQ; ++i) gtdl += psi[i] * dS[i];
             }
         }
-        const double phi = wsum_rl(phil), gTd = wsum_rl(gtdl);
-        const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
-        const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
-        const float lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;
-        double amin = gam_th;
-        if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta * frcp(-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
-        amin *= gam_al;
-        double alpha = amax, th_t = 0.0, ph_t = 0.0;
-        bool accepted = false, ftype = false;
-        // IPOPT's tiny-step test: max |d|/(1+|x|) < 10 eps_mach accepts the full step unfiltered
+        // IPOPT's tiny-step test: max |d|/(1+|x|) < 10 eps_mach accepts the full step unfiltered; its maximum rides with
+        // the two sums (one lock-step reduction)
         float tnl = 0.0f;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -878,7 +870,17 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
 #pragma unroll
             for (int i = 0; i < RM_NQ; ++i) tnl = fmaxf(tnl, fabsf((float)dS[i]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)s[i])));
         }
-        const bool tiny = wmaxf(tnl) < 2.2e-15f;
+        wsum2_rl_maxf(phil, gtdl, tnl);
+        const double phi = phil, gTd = gtdl;
+        const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
+        const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
+        const float lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;
+        double amin = gam_th;
+        if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta * frcp(-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
+        amin *= gam_al;
+        double alpha = amax, th_t = 0.0, ph_t = 0.0;
+        bool accepted = false, ftype = false;
+        const bool tiny = tnl < 2.2e-15f;
         STAMP(6);
         int ls = 0;
         for (; ls < 80 && !in_soft; ++ls) {
@@ -899,7 +901,8 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
             for (int i = 0; i < RM_NQ; ++i) thl += uon ? fabs(ct[i] - st_[i]) : 0.0;
             double phl = nod ? sc * cost_val(xt, ut, pt) : 0.0;
             phl -= uon ? mu * log_fast(barrier_args(ut, st_)) : 0.0;
-            th_t = wsum_rl(thl); ph_t = wsum_rl(phl);
+            wsum2_rl(thl, phl);
+            th_t = thl; ph_t = phl;
             if (tiny) { accepted = true; ftype = true; break; }
             bool in_filter = !(th_t < th_max) || !isfinite(ph_t);
             in_filter = in_filter || wany_rep(lane < nfilt && th_t >= fth && ph_t >= fph);
@@ -962,7 +965,8 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                         for (int i = 0; i < RM_NQ; ++i) thl += uon ? fabs(ct[i] - st_[i]) : 0.0;
                         double phl = nod ? sc * cost_val(xt, ut, pt) : 0.0;
                         phl -= uon ? mu * log_fast(barrier_args(ut, st_)) : 0.0;
-                        th_s = wsum_rl(thl); ph_s = wsum_rl(phl);
+                        wsum2_rl(thl, phl);
+                        th_s = thl; ph_s = phl;
                     }
                     bool orig = th_s < th_max && isfinite(ph_s) && !wany_rep(lane < nfilt && th_s >= fth && ph_s >= fph);
                     orig = orig && (cmp_le(th_s, (1 - gam_th) * theta, theta) || cmp_le(ph_s - phi, -gam_ph * theta, phi));
@@ -1572,8 +1576,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                         sumz += pn[P_ZP + i] + pn[P_ZN + i];
                     }
                 }
-                dinf = wmax(dinf); pinf = wmax(pinf); c0r = wmax(c0r); cminr = wmin(cminr);
-                suml = wsum_rl(suml); sumz = wsum_rl(sumz);
+                wred_errors_f64_rl(dinf, pinf, c0r, cminr, suml, sumz);
             }
             const double s_d = fmax(100.0, (suml + sumz) / (nA + nI + nbr)) / 100.0;
             const double s_c = fmax(100.0, sumz / nbr) / 100.0;
@@ -1839,7 +1842,8 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                     for (int i = 0; i < RM_NQ; ++i) crt[i] = 0.0;
                 }
                 phl = inside ? phl - rmu * lb : __builtin_inf();
-                tht = wsum_rl(thl); pht = wsum_rl(phl);
+                wsum2_rl(thl, phl);
+                tht = thl; pht = phl;
             };
             auto racc = [&](double al_test, bool& ft) {
                 const bool in_f = !(tht < rth_max) || !isfinite(pht) || wany_rep(lane < rnf && tht >= rfth && pht >= rfph);

@@ -395,8 +395,13 @@ __device__ __forceinline__ void wsum2(double& a, double& b) {
 // two f64 sums and one f32 maximum of non-negative values (wreduce_nn) together: two waves, one exchange
 __device__ __forceinline__ void wsum2_maxf(double& a, double& b, float& m) {
 #if DART_WG == 1
-    wsum2(a, b);
-    m = wmaxf(m);
+    // one wave: the three chains in lock step (each takes its own wsum / wmaxf steps: the same bits)
+    unsigned x = __builtin_bit_cast(unsigned, m);
+#define DART_L(C, R) lvl_sum<C, R>(a); lvl_sum<C, R>(b); lvl_maxu<C, R>(x);
+    DART_LEVELS(DART_L)
+#undef DART_L
+    a = readlane(a, 63); b = readlane(b, 63);
+    m = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)x, 63));
 #else
     unsigned x = __builtin_bit_cast(unsigned, m);
 #define DART_L(C, R) lvl_sum<C, R>(a); lvl_sum<C, R>(b); lvl_maxu<C, R>(x);
@@ -518,6 +523,49 @@ __device__ __forceinline__ void wred_errors_f64(double& mx0, double& mx1, double
 #endif
 }
 __device__ __forceinline__ double wsum_rl(double x) { return wreduce<OpSum, false>(x, OpSum()); }
+// two wsum_rl (and a wmaxf) in lock step, one wave: each value takes its own reduction's steps (the same bits)
+__device__ __forceinline__ void wsum2_rl(double& a, double& b) {
+#if DART_WG == 1
+#define DART_L(C, R) lvl_sum<C, R>(a); lvl_sum<C, R>(b);
+    DART_L(0xB1, 0xf) DART_L(0x4E, 0xf) DART_L(0x124, 0xf) DART_L(0x128, 0xf)
+#undef DART_L
+    a = (readlane(a, 0) + readlane(a, 16)) + (readlane(a, 32) + readlane(a, 48));
+    b = (readlane(b, 0) + readlane(b, 16)) + (readlane(b, 32) + readlane(b, 48));
+#else
+    a = wsum_rl(a); b = wsum_rl(b);
+#endif
+}
+// wmax x3, wmin and wsum_rl x2 in lock step (RMPC's restoration errors): the same bits as the six calls
+__device__ __forceinline__ void wred_errors_f64_rl(double& mx0, double& mx1, double& mx2, double& mn, double& s0, double& s1) {
+#if DART_WG == 1
+#define DART_L(C, R) lvl_maxd<C, R>(mx0); lvl_maxd<C, R>(mx1); lvl_maxd<C, R>(mx2); lvl_mind<C, R>(mn); \
+    lvl_sum<C, R>(s0); lvl_sum<C, R>(s1);
+    DART_L(0xB1, 0xf) DART_L(0x4E, 0xf) DART_L(0x124, 0xf) DART_L(0x128, 0xf)
+#undef DART_L
+#define DART_L(C, R) lvl_maxd<C, R>(mx0); lvl_maxd<C, R>(mx1); lvl_maxd<C, R>(mx2); lvl_mind<C, R>(mn);
+    DART_L(0x142, 0xa) DART_L(0x143, 0xc)
+#undef DART_L
+    mx0 = readlane(mx0, 63); mx1 = readlane(mx1, 63); mx2 = readlane(mx2, 63); mn = readlane(mn, 63);
+    s0 = (readlane(s0, 0) + readlane(s0, 16)) + (readlane(s0, 32) + readlane(s0, 48));
+    s1 = (readlane(s1, 0) + readlane(s1, 16)) + (readlane(s1, 32) + readlane(s1, 48));
+#else
+    mx0 = wmax(mx0); mx1 = wmax(mx1); mx2 = wmax(mx2); mn = wmin(mn); s0 = wsum_rl(s0); s1 = wsum_rl(s1);
+#endif
+}
+__device__ __forceinline__ void wsum2_rl_maxf(double& a, double& b, float& m) {
+#if DART_WG == 1
+    unsigned x = __builtin_bit_cast(unsigned, m);
+#define DART_L(C, R) lvl_sum<C, R>(a); lvl_sum<C, R>(b); lvl_maxu<C, R>(x);
+    DART_L(0xB1, 0xf) DART_L(0x4E, 0xf) DART_L(0x124, 0xf) DART_L(0x128, 0xf)
+#undef DART_L
+    lvl_maxu<0x142, 0xa>(x); lvl_maxu<0x143, 0xc>(x);
+    a = (readlane(a, 0) + readlane(a, 16)) + (readlane(a, 32) + readlane(a, 48));
+    b = (readlane(b, 0) + readlane(b, 16)) + (readlane(b, 32) + readlane(b, 48));
+    m = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)x, 63));
+#else
+    a = wsum_rl(a); b = wsum_rl(b); m = wmaxf(m);
+#endif
+}
 __device__ __forceinline__ bool wany(bool p) {
     bool r = __ballot(p) != 0ull;
 #if DART_WG == 2
