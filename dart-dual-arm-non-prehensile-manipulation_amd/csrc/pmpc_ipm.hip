@@ -614,6 +614,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
         // in place of the defects, so while it runs g1 / g2 / gz hold c_soc.
         double dp[NAX], dv[NAX], dth[NAX], dlp[NAX], dlv[NAX], dzl[NAX], dzu[NAX], dz[NAX];
         double amax = 1.0, az = 1.0;
+        float am_lf = 1.0f, az_lf = 1.0f;     // this lane's fractions to the boundary (the wave minima: amax, az)
         const double (&g1o)[NAX] = g1, (&g2o)[NAX] = g2, (&gzo)[NAX] = gz;
         auto direction = [&]() {
             double p1[NAX], p2[NAX], kff[NAX], gn1[NAX], gn2[NAX], g1[NAX], g2[NAX], gz[NAX];
@@ -810,11 +811,9 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                 az_ = fmin(az_, uon ? fmin(czl, czu) : 1.0);
                 twd[j] = 2.0 * th[j] * dth[j];
             }
-            // f32 minima rounded down: tau <= 0.99 leaves far more slack than the f32 rounding
-            float amax_f = (float)am, az_f = (float)az_;
-            wmin2f(amax_f, az_f);
-            amax = (double)amax_f * (1.0 - 1.0 / 1048576.0);
-            az = (double)az_f * (1.0 - 1.0 / 1048576.0);
+            // f32 minima rounded down (tau <= 0.99 leaves far more slack than the f32 rounding); reduced by the
+            // caller (frac_minima, or with the line search's sums)
+            am_lf = (float)am; az_lf = (float)az_;
             // z step: dz_k = zA dz_{k-1} + zC dw_{k-1} - gz_k, dw = -g (2 theta_x dtheta_x + 2 theta_y dtheta_y)
             const double wd = RED ? 0.0 : -a.g * axes_sum(twd);
             if constexpr (RED) {
@@ -851,6 +850,12 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                     }
                 }
             }
+        };
+
+        // amax, az from this lane's fractions (f32 minima rounded down)
+        auto frac_set = [&]() {
+            amax = (double)am_lf * (1.0 - 1.0 / 1048576.0);
+            az = (double)az_lf * (1.0 - 1.0 / 1048576.0);
         };
 
         // -------- filter line search (Waechter & Biegler 2006, Alg. A) with second-order correction
@@ -940,6 +945,7 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
         }
         for (;;) {
             direction();
+            if (PM_EXPECT(soc != 0, 0)) { wmin2f(am_lf, az_lf); frac_set(); }
             STAMP(4);
             if (PM_EXPECT(soc == 0, 1)) {
                 double phil = 0.0, gtdl = 0.0;
@@ -962,7 +968,8 @@ __device__ __forceinline__ bool pmpc_solve(const PmpcArgs& a, const int b) {
                     tn_w = fmaxf(tn_w, xon ? fabsf((float)dz[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)zz[j])) : 0.0f);
                     tn_w = fmaxf(tn_w, uon ? fabsf((float)dth[j]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)th[j])) : 0.0f);
                 }
-                wsum2_maxf(phil, gtdl, tn_w);
+                wsum2_maxf_min2f(phil, gtdl, tn_w, am_lf, az_lf);      // (the fraction minima ride along)
+                frac_set();
                 phi = phil; gTd = gtdl;
                 // switching condition alpha (-gTd)^s_ph > delta theta^s_th, compared in log2 space
                 const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;

@@ -416,6 +416,25 @@ __device__ __forceinline__ void wsum2_maxf(double& a, double& b, float& m) {
     m = __builtin_bit_cast(float, (unsigned)fmax(o[0][2], o[1][2]));
 #endif
 }
+// wsum2_maxf with two f32 minima of non-negative values (wmin2f) in the same lock step (one wave); two waves: the
+// minima first, then wsum2_maxf's exchange
+__device__ __forceinline__ void wmin2f(float& a, float& b);
+__device__ __forceinline__ void wsum2_maxf_min2f(double& a, double& b, float& m, float& n0, float& n1) {
+#if DART_WG == 1
+    unsigned x = __builtin_bit_cast(unsigned, m);
+    unsigned y0 = __builtin_bit_cast(unsigned, n0), y1 = __builtin_bit_cast(unsigned, n1);
+#define DART_L(C, R) lvl_sum<C, R>(a); lvl_sum<C, R>(b); lvl_maxu<C, R>(x); lvl_minu<C, R>(y0); lvl_minu<C, R>(y1);
+    DART_LEVELS(DART_L)
+#undef DART_L
+    a = readlane(a, 63); b = readlane(b, 63);
+    m = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)x, 63));
+    n0 = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)y0, 63));
+    n1 = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_readlane((int)y1, 63));
+#else
+    wmin2f(n0, n1);
+    wsum2_maxf(a, b, m);
+#endif
+}
 // two f32 minima of non-negative values (see wreduce_nn)
 __device__ __forceinline__ void wmin2f(float& a, float& b) {
     unsigned x = __builtin_bit_cast(unsigned, a), y = __builtin_bit_cast(unsigned, b);
