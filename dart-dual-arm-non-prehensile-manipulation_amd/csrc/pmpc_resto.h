@@ -501,7 +501,8 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                     if (dzu[j] < 0) a2 = fmin(a2, -tau * zu[j] / dzu[j]);
                 }
             }
-            amax = wmin(am); az = wmin(a2);
+            wmin2d(am, a2);
+            amax = am; az = a2;
         };
         duals();
         STAMP(3);
@@ -1088,7 +1089,8 @@ __device__ __forceinline__ void pmpc_resto_solve(const PmpcArgs& a, const int b)
                         if (dzu_ < 0) a2 = fmin(a2, -taur * zu[j] / dzu_);
                     }
                 }
-                amr = wmin(am); azr = wmin(a2);
+                wmin2d(am, a2);
+                amr = am; azr = a2;
             };
             // the step of the right-hand side cgv: solve, p / n steps, refinement, fractions to the boundary
             auto rstep = [&](const double* cgv) {
