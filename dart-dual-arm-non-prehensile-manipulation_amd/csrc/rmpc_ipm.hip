@@ -1609,6 +1609,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
             // ---- the step: plain (with inertia correction) or a second-order correction pass, one solve site;
             //      each solve refined iteratively (IPOPT's PDFullSpaceSolver) ----
             double delta = 0.0, amr = 1.0, azr = 1.0, phir = 0.0, gtdr = 0.0, aminr = 0.0, alr = 1.0;
+            double pw_thr = 0.0, pw_gdr = 0.0;      // theta^s_th, (-gTd)^s_ph of the line search (gTd < 0)
             double csg[6], csr[RM_NQ], cgt[6], crt[RM_NQ], tht = 0.0, pht = 0.0, th_prev = 0.0;
             bool accr = false, ftr = false, okr = true;
             int soc = -1, ls = 0;
@@ -1850,7 +1851,7 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
             auto racc = [&](double al_test, bool& ft) {
                 const bool in_f = !(tht < rth_max) || !isfinite(pht) || wany_rep(lane < rnf && tht >= rfth && pht >= rfph);
                 if (in_f) return false;
-                const bool sw = gtdr < 0.0 && al_test * pow(-gtdr, s_ph) > pow(thr, s_th);
+                const bool sw = gtdr < 0.0 && al_test * pw_gdr > pw_thr;
                 if (thr <= rth_min && sw) {
                     if (cmp_le(pht, phir + eta_ph * al_test * gtdr, phir)) { ft = true; return true; }
                     return false;
@@ -1922,9 +1923,14 @@ __device__ __forceinline__ bool rmpc_solve(const RmpcArgs& a, const int b) {
                             }
                         }
                     }
-                    phir = wsum_rl(pl - rmu * lb); gtdr = wsum_rl(gd);
+                    double plb = pl - rmu * lb;
+                    wsum2_rl(plb, gd);
+                    phir = plb; gtdr = gd;
+                    // theta^s_th and (-gTd)^s_ph, fixed through the line search: once here, one on each half of the wave
+                    pw_thr = 0.0; pw_gdr = 0.0;
+                    if (gtdr < 0) half_pair(lane < 32 ? pow(thr, s_th) : pow(-gtdr, s_ph), pw_thr, pw_gdr);
                     aminr = gam_th;
-                    if (gtdr < 0) aminr = fmin(gam_th, fmin(gam_ph * thr / (-gtdr), pow(thr, s_th) / pow(-gtdr, s_ph)));
+                    if (gtdr < 0) aminr = fmin(gam_th, fmin(gam_ph * thr / (-gtdr), pw_thr / pw_gdr));
                     aminr *= gam_al;
                     alr = amr;
                     al_try = alr;
