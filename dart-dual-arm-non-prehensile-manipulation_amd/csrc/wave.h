@@ -518,17 +518,6 @@ template <int CTRL, int RM>
 __device__ __forceinline__ void lvl_maxd(double& x) { x = fmax(x, dpp<CTRL, RM>(x)); }
 template <int CTRL, int RM>
 __device__ __forceinline__ void lvl_mind(double& x) { x = fmin(x, dpp<CTRL, RM>(x)); }
-// two f64 maxima in lock step (the same bits as two wmax)
-__device__ __forceinline__ void wmax2d(double& a, double& b) {
-#if DART_WG == 1
-#define DART_L(C, R) lvl_maxd<C, R>(a); lvl_maxd<C, R>(b);
-    DART_LEVELS(DART_L)
-#undef DART_L
-    a = readlane(a, 63); b = readlane(b, 63);
-#else
-    a = wmax(a); b = wmax(b);
-#endif
-}
 // two f64 minima in lock step (the same bits as two wmin)
 __device__ __forceinline__ void wmin2d(double& a, double& b) {
 #if DART_WG == 1
