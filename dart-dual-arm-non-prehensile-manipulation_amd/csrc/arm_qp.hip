@@ -72,6 +72,14 @@ __device__ __forceinline__ double red8(double x, Op op) {
     return op(readlane(x, 0), readlane(x, 4));
 }
 
+// three maxima and one sum over lanes 0..7 in lock step (each takes red8's steps: the same bits)
+__device__ __forceinline__ void red8_max3_sum(double& m0, double& m1, double& m2, double& s0) {
+    m0 = fmax(m0, dpp<0xB1>(m0)); m1 = fmax(m1, dpp<0xB1>(m1)); m2 = fmax(m2, dpp<0xB1>(m2)); s0 = s0 + dpp<0xB1>(s0);
+    m0 = fmax(m0, dpp<0x4E>(m0)); m1 = fmax(m1, dpp<0x4E>(m1)); m2 = fmax(m2, dpp<0x4E>(m2)); s0 = s0 + dpp<0x4E>(s0);
+    m0 = fmax(readlane(m0, 0), readlane(m0, 4)); m1 = fmax(readlane(m1, 0), readlane(m1, 4));
+    m2 = fmax(readlane(m2, 0), readlane(m2, 4)); s0 = readlane(s0, 0) + readlane(s0, 4);
+}
+
 // round-robin pairing of 8 indices, round r = 0..6 (index 7 fixed)
 __device__ __forceinline__ int jpartner(int i, int r) {
     if (i == 7) return r;
@@ -132,8 +140,11 @@ __global__ __launch_bounds__(kWave) void arm_qp_kernel(ArmArgs a) {
     int cur = 0;
     for (int sweep = 0; sweep < 16; ++sweep) {
         const double a0 = SH.A[cur][0][l], a1 = SH.A[cur][1][l];
-        const double off0 = wsum(ei != ej ? a0 * a0 : 0.0), dg0 = wsum(ei == ej ? a0 * a0 : 0.0);
-        const double off1 = wsum(ei != ej ? a1 * a1 : 0.0), dg1 = wsum(ei == ej ? a1 * a1 : 0.0);
+        // the four sums in lock step (wsum2: each the same bits as its wsum)
+        double off0 = ei != ej ? a0 * a0 : 0.0, dg0 = ei == ej ? a0 * a0 : 0.0;
+        double off1 = ei != ej ? a1 * a1 : 0.0, dg1 = ei == ej ? a1 * a1 : 0.0;
+        wsum2(off0, dg0);
+        wsum2(off1, dg1);
         if (off0 <= 1e-32 * dg0 && off1 <= 1e-32 * dg1) break;
         STAMP_ADD(9, 1);
         for (int r = 0; r < 7; ++r) {
@@ -388,10 +399,10 @@ __global__ __launch_bounds__(kWave) void arm_qp_kernel(ArmArgs a) {
 #pragma unroll
         for (int k = 0; k < n; ++k) rd = fma(Hrow[k], xs[k], rd);
         rd = jl ? rd : 0.0;
-        const double rdm = red8(fabs(rd), OpMax());
-        rpm = red8(rpm, OpMax());
-        const double mu = red8(szl, OpSum()) * inact;
-        const double zmax = red8(zmx, OpMax());
+        double rdm = fabs(rd);
+        red8_max3_sum(rdm, rpm, zmx, szl);          // (four red8 in lock step)
+        const double mu = szl * inact;
+        const double zmax = zmx;
         const double err = fmax(rdm * isd, fmax(rpm * isp, mu * isd));
         if (err <= tol) { status = 0; break; }
         if (zmax > 1e14 * sd) { status = -3; break; }

@@ -35,6 +35,20 @@ elif kind == "lmpc":
     PR = f64(np.tile(LMPC_PRM_DEFAULT, (B, 1)))
     s = dart_mpc.LmpcSolver(N=30, B_max=B, device=0)
     call = lambda i, o: s.solve_batch_dev(B, *[x[i % nb].data_ptr() for x in X], PR.data_ptr(), *o, stream=sp)
+elif kind == "arm":
+    # the bench's arm QP line: 36 arm snapshots per launch (18 configs x 2 arms), n = 7, reference parameters
+    from dart_mpc.arm import pack_params, pack_snapshot
+    from dart_mpc.workload import arm_batch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import arm_qp   # (the reference parameters only)
+    snaps = [arm_batch(1, seed0=5000 + i)[0] for i in range(nb)]
+    B = snaps[0]["q"].shape[0]
+    SR = f64(np.stack([pack_snapshot(x) for x in snaps]))
+    PR = f64(pack_params(arm_qp.default_params()))
+    s = dart_mpc.ArmSolver(7)
+    TQ = torch.empty((K, B, 7), dtype=torch.float64, device=dev)
+    call = lambda i, o: s.solve_batch_dev(B, SR[i % nb].data_ptr(), PR.data_ptr(), True, o[0], TQ[i].data_ptr(),
+                                          o[1], o[2], o[3], stream=sp)
 elif kind in ("pmpc_resto", "pmpc_soc0"):
     # C4's 1152 instances with IPOPT's restoration phases in play: N = 31 (a few restored), or N = 20 with
     # max_soc = 0 (about one in ten restored); one launch per call, the same inputs every call
@@ -51,7 +65,7 @@ else:
     call = lambda i, o: s.solve_batch_dev(B, *[x[i % nb].data_ptr() for x in X], *o, stream=sp)
 stream = torch.cuda.Stream(device=dev)
 sp = stream.cuda_stream
-U0 = torch.empty((K, B, 2), dtype=torch.float64, device=dev)
+U0 = torch.empty((K, B, 7 if kind == "arm" else 2), dtype=torch.float64, device=dev)
 ST = torch.empty((K, B), dtype=torch.int32, device=dev)
 IT = torch.empty((K, B), dtype=torch.int32, device=dev)
 FV = torch.empty((K, B), dtype=torch.float64, device=dev)
