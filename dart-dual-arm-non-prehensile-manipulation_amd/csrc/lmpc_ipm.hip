@@ -1077,17 +1077,18 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
             dU = uon ? d0 : 0.0;
             node_multiplier_s(S, xon ? sl : hf * LM_NMAXS, dx, dU, lamp);
         };
-        // primal fraction to the boundary of dU (wave-uniform)
-        auto primal_ftb = [&]() {
+        // primal fraction to the boundary of dU: this lane's, and the wave's (reduced in f32 with a 2^-20 margin)
+        auto primal_ftb_l = [&]() {
             double am = 1.0;
             if (uon) {
-                if (dU < 0) am = fmin(am, -tau * (u - lo) * frcp(dU));     // reduced in f32 with a 2^-20 margin
+                if (dU < 0) am = fmin(am, -tau * (u - lo) * frcp(dU));
                 if (dU > 0) am = fmin(am, tau * (hi - u) * frcp(dU));
             }
-            return (double)wminf((float)am) * (1.0 - 1.0 / 1048576.0);
+            return (float)am;
         };
-        // bound-multiplier directions of dU and their fraction to the boundary (wave-uniform)
-        auto dual_step = [&]() {
+        auto primal_ftb = [&]() { return (double)wminf(primal_ftb_l()) * (1.0 - 1.0 / 1048576.0); };
+        // bound-multiplier directions of dU and their fraction to the boundary: this lane's, and the wave's
+        auto dual_step_l = [&]() {
             dzl = uon ? mu * isl - zl - zl * isl * dU : 0.0;
             dzu = uon ? mu * isu - zu + zu * isu * dU : 0.0;
             double az_ = 1.0;
@@ -1095,8 +1096,9 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                 if (dzl < 0) az_ = fmin(az_, -tau * zl * frcp(dzl));
                 if (dzu < 0) az_ = fmin(az_, -tau * zu * frcp(dzu));
             }
-            return (double)wminf((float)az_) * (1.0 - 1.0 / 1048576.0);
+            return (float)az_;
         };
+        auto dual_step = [&]() { return (double)wminf(dual_step_l()) * (1.0 - 1.0 / 1048576.0); };
         // trial point x + al d: incoming defects gt of node k, wave-summed theta and barrier objective
         auto trial = [&](double al) {
             double xt[4];
@@ -1199,8 +1201,9 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
             STAMP(4);
             double al_try;
             if (soc < 0) {
-                amax = primal_ftb();
-                az = dual_step();
+                // the two fraction minima, the line search's two sums and the tiny-step maximum: one lock-step
+                // reduction (each value takes its own reduction's steps: the same bits)
+                float amf = primal_ftb_l(), azf = dual_step_l();
                 STAMP(5);
                 double phil = sc * cost_val(x, u, up), gtdl = 0.0;
                 if (uon) phil -= mu * log_fast((u - lo) * (hi - u));
@@ -1211,14 +1214,6 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                     for (int i = 0; i < 5; ++i) gtdl += xon ? sc * gz_[i] * dx[i] : 0.0;
                     if (uon) gtdl += (sc * gz_[5] - mu * isl + mu * isu) * dU;
                 }
-                wsum2(phil, gtdl);
-                phi = phil; gTd = gtdl;
-                const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
-                const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
-                lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;
-                amin = gam_th;
-                if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta * frcp(-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
-                amin *= gam_al;
                 float tnl = 0.0f;
 #pragma unroll
                 for (int i = 0; i < 5; ++i) {
@@ -1226,7 +1221,17 @@ __device__ __forceinline__ bool lmpc_solve(const LmpcArgs& a, const int b) {
                     tnl = fmaxf(tnl, xon ? fabsf((float)dx[i]) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)xi)) : 0.0f);
                 }
                 if (uon) tnl = fmaxf(tnl, fabsf((float)dU) * __builtin_amdgcn_rcpf(1.0f + fabsf((float)u)));
-                tiny = wmaxf(tnl) < 2.2e-15f;
+                wsum2_maxf_min2f(phil, gtdl, tnl, amf, azf);
+                amax = (double)amf * (1.0 - 1.0 / 1048576.0);
+                az = (double)azf * (1.0 - 1.0 / 1048576.0);
+                tiny = tnl < 2.2e-15f;
+                phi = phil; gTd = gtdl;
+                const float lg_th = theta > 0.0 ? lg2(theta) : -3.0e38f;
+                const float lg_gd = gTd < 0.0 ? lg2(-gTd) : 3.0e38f;
+                lg_sw = (float)s_th * lg_th - (float)s_ph * lg_gd;
+                amin = gam_th;
+                if (gTd < 0.0) amin = fmin(gam_th, fmin(gam_ph * theta * frcp(-gTd), (double)__builtin_amdgcn_exp2f(fmaxf(lg_sw, -126.0f))));
+                amin *= gam_al;
                 alpha = amax;
                 al_try = alpha;
                 STAMP(6);
