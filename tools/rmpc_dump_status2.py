@@ -4,7 +4,7 @@ spread 2x / 3x / 6x, tests/test_gpu_rmpc.py) and on the parity sweep's batch (rm
 tools/parity_sweep.py), each solved as one launch (the queued restoration kernel) and in batches of 18 (the
 restoration in the solving wave).  Saved to gpurun_out/rmpc_status2_kernel.npz; tools/rmpc_status2_analysis.py
 compares them with the oracle on the CPU.
-Usage (on the box): python tools/rmpc_dump_status2.py"""
+Usage (on the box): [DART_S2_CASES=sweep4_x3] python tools/rmpc_dump_status2.py"""
 import os
 import sys
 
@@ -15,7 +15,11 @@ sys.path[:0] = [os.path.join(ROOT, "dart-dual-arm-non-prehensile-manipulation_am
 import dart_mpc  # noqa: E402
 from dart_mpc.workload import rmpc_batch  # noqa: E402
 
-CASES = {"test_x2": (40, 0, 2.0), "test_x3": (40, 0, 3.0), "test_x6": (40, 0, 6.0), "sweep_x3": (80, 200000, 3.0)}
+CASES = {"test_x2": (40, 0, 2.0), "test_x3": (40, 0, 3.0), "test_x6": (40, 0, 6.0), "sweep_x3": (80, 200000, 3.0),
+         "sweep4_x3": (320, 200000, 3.0)}
+# DART_S2_CASES=name,name selects cases (default: the round-5 set, without the 4x sweep batch)
+_sel = os.environ.get("DART_S2_CASES", "test_x2,test_x3,test_x6,sweep_x3").split(",")
+CASES = {k: v for k, v in CASES.items() if k in _sel}
 
 
 def batch(n, seed0, spread):

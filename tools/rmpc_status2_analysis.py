@@ -11,7 +11,7 @@ instance both solvers end at status 2 it computes, solver-independently (oracle/
     restoration problem fixes the point only through its proximity term eta/2 |D_R (x - x_R)|^2, eta = sqrt(mu);
   * both points re-solved by the oracle at tol 1e-10 from their own w (IPOPT warm start), and the oracle cold at
     tol 1e-10: which of the two tol-1e-8 points is nearer the tighter answers.
-Usage: python tools/rmpc_status2_analysis.py [top_k]  (writes profiles/r05/rmpc_status2.txt)"""
+Usage: [DART_S2_CASES=... DART_S2_OUT=...] python tools/rmpc_status2_analysis.py [top_k]  (default profiles/r05/rmpc_status2.txt)"""
 import os
 import sys
 
@@ -82,8 +82,9 @@ def main():
                f"from the oracle's w: status {ro['status'][j]}, u0 moves {d_res(ro['w'][j], wo[j]):.2e}; "
                f"cold tol 1e-10: status {rc['status'][j]}, u0 from kernel {d_res(rc['w'][j], wk[j]):.2e} / from oracle "
                f"{d_res(rc['w'][j], wo[j]):.2e}; the two re-solved points {d_res(rk['w'][j], ro['w'][j]):.2e} apart")
-    os.makedirs(os.path.join(ROOT, "profiles", "r05"), exist_ok=True)
-    with open(os.path.join(ROOT, "profiles", "r05", "rmpc_status2.txt"), "w") as fh:
+    out = os.environ.get("DART_S2_OUT", os.path.join(ROOT, "profiles", "r05", "rmpc_status2.txt"))
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as fh:
         fh.write("\n".join(lines) + "\n")
 
 
